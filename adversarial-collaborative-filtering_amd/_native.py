@@ -1,0 +1,117 @@
+"""ctypes binding of ``libacf_apr.so`` (C-ABI declared in ``include/acf_apr.h``).
+
+This is the only route from Python to the HIP kernels.  There is no CPU fallback:
+if the library is missing or the machine has no HIP device, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libacf_apr.so")
+
+ACF_OK, ACF_E_INVALID, ACF_E_RANGE, ACF_E_HIP, ACF_E_NOMEM, ACF_E_STATE = range(6)
+ABI_VERSION = 1
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_F = ctypes.c_float
+
+
+class Tables(ctypes.Structure):
+    """acf_apr_tables: embedding_P, embedding_Q and their Adagrad slots."""
+    _fields_ = [("P", _P), ("Q", _P), ("accP", _P), ("accQ", _P)]
+
+
+class HParams(ctypes.Structure):
+    """acf_apr_hparams (APR.py:86-97 + graph constants)."""
+    _fields_ = [
+        ("lr", _F), ("eps", _F), ("reg", _F), ("reg_adv", _F), ("clip_lo", _F), ("clip_hi", _F),
+        ("adver", _I32), ("adv_mode", _I32), ("seed", _U64), ("zero_delta", _I32),
+        ("reserved", _I32),
+    ]
+
+
+# (name, restype, argtypes) for every function declared in include/acf_apr.h
+SIGNATURES = {
+    "acf_apr_abi_version": (ctypes.c_int, []),
+    "acf_apr_last_error": (ctypes.c_char_p, []),
+    "acf_apr_create": (ctypes.c_int, [ctypes.POINTER(_P), _I64, _I64, _I32, _I32, _I32]),
+    "acf_apr_destroy": (ctypes.c_int, [_P]),
+    "acf_apr_plan": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P]),
+    "acf_apr_delta_update": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _P]),
+    "acf_apr_optimizer_step": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _P]),
+    "acf_apr_train_planned": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _I32,
+                                             _I32, _P]),
+    "acf_apr_time_kernels": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _I32,
+                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I32), _P]),
+    "acf_apr_copy_losses": (ctypes.c_int, [_P, _P, _P, _P]),
+    "acf_apr_delta_scatter": (ctypes.c_int, [_P, _P, _P, _P]),
+    "acf_bpr_forward": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _P, _I32, _I32, _F, _F, _P, _P,
+                                       _P, _P, _P]),
+    "acf_eval_positions_all": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I32, _I32, _P, _P, _P,
+                                              _P]),
+    "acf_eval_positions_list": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P]),
+    "acf_sample_epoch": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P, _U64, _I32, _I32, _P, _P,
+                                        _P, _P]),
+    "acf_dns_select": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I64, _I32, _P, _P]),
+}
+
+
+class NativeError(RuntimeError):
+    """A C-ABI call returned an error code."""
+
+    def __init__(self, code: int, func: str, msg: str):
+        self.code = code
+        super().__init__(f"{func} failed (code {code}): {msg}")
+
+
+class NativeIndexError(NativeError, IndexError):
+    """ACF_E_RANGE: an index outside its table (TF Gather's InvalidArgument)."""
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the HIP library (once).  Raises ImportError if it was never built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise ImportError(
+                f"{path} not found: the HIP extension is not built. Run "
+                "`python adversarial-collaborative-filtering_amd/build_native.py` "
+                "(or __graft_entry__.build()). There is no CPU fallback.")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        ver = lib.acf_apr_abi_version()
+        if ver != ABI_VERSION:
+            raise ImportError(f"libacf_apr ABI {ver} != expected {ABI_VERSION}; rebuild it")
+        _lib = lib
+        return lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke a C-ABI function and raise NativeError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != ACF_OK:
+        msg = lib.acf_apr_last_error().decode("utf-8", "replace")
+        cls = NativeIndexError if rc == ACF_E_RANGE else NativeError
+        raise cls(rc, name, msg)
+
+
+def exported_symbols(path: str = LIB_PATH) -> set[str]:
+    """Names from SIGNATURES that the shared object exports (no GPU needed)."""
+    lib = ctypes.CDLL(path)
+    return {n for n in SIGNATURES if hasattr(lib, n)}

@@ -1,0 +1,290 @@
+"""Torch-tensor front end of the C-ABI.
+
+PyTorch provides device memory and the current HIP stream; every computation runs
+in ``libacf_apr.so``.  Arguments are validated here the way TF validated feeds
+(dtype/shape/device errors raise ``TypeError``/``ValueError`` before any launch);
+index ranges are validated on device by the plan / sampler (``NativeIndexError``).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _native
+from ._native import HParams, Tables, call
+
+CLIP_LO = -80.0   # APR.py:148
+CLIP_HI = 1e8
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require(t: torch.Tensor, name: str, dtype: torch.dtype, device: torch.device | None = None,
+             ndim: int | None = None) -> int:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor, got {type(t).__name__}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must live on a HIP device (got {t.device}); there is no CPU path")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if ndim is not None and t.dim() != ndim:
+        raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t.data_ptr()
+
+
+def _idx(t, name, device) -> torch.Tensor:
+    """Accept [N] or [N,1] int tensors/arrays (the placeholders are [None,1])."""
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(t)
+    t = t.reshape(-1)
+    if t.dtype != torch.int32:
+        t = t.to(torch.int32)
+    return t.to(device, non_blocking=True).contiguous()
+
+
+@dataclass
+class StepHParams:
+    """Hyper-parameters of one MF graph (APR.py:86-97)."""
+    lr: float = 0.05
+    eps: float = 0.5
+    reg: float = 0.0
+    reg_adv: float = 1.0
+    adver: int = 0
+    adv: str = "grad"        # "grad" | "random" (APR.py:170-191)
+    seed: int = 0
+    zero_delta: int = 0
+    clip_lo: float = CLIP_LO
+    clip_hi: float = CLIP_HI
+
+    def to_c(self) -> HParams:
+        if self.adv not in ("grad", "random"):
+            raise ValueError(f"adv must be 'grad' or 'random', got {self.adv!r}")
+        return HParams(self.lr, self.eps, self.reg, self.reg_adv, self.clip_lo, self.clip_hi,
+                       int(bool(self.adver)), 0 if self.adv == "grad" else 1,
+                       int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(bool(self.zero_delta)), 0)
+
+
+class APRContext:
+    """Owns an ``acf_apr_ctx``: plan workspace, per-batch scratch, graph cache."""
+
+    def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, max_batch_size: int,
+                 max_batches: int, device: torch.device):
+        self.device = torch.device(device)
+        self.U1, self.I1, self.d = int(num_user_rows), int(num_item_rows), int(dim)
+        self.max_batch_size, self.max_batches = int(max_batch_size), int(max_batches)
+        self._ptr = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            call("acf_apr_create", ctypes.byref(self._ptr), self.U1, self.I1, self.d,
+                 self.max_batch_size, self.max_batches)
+        self.batch_size = 0
+        self.n_batches = 0
+        self._staged = None
+
+    def __del__(self):
+        try:
+            if self._ptr:
+                _native.load().acf_apr_destroy(self._ptr)
+                self._ptr = ctypes.c_void_p()
+        except Exception:
+            pass
+
+    def fits(self, batch_size: int, n_batches: int) -> bool:
+        return batch_size <= self.max_batch_size and n_batches <= self.max_batches
+
+    def plan(self, user, item_pos, item_neg, batch_size: int, check: bool = True) -> int:
+        """Stage triplets and build the dedup plan; returns the number of batches."""
+        u = _idx(user, "user", self.device)
+        i = _idx(item_pos, "item_pos", self.device)
+        j = _idx(item_neg, "item_neg", self.device)
+        if not (u.numel() == i.numel() == j.numel()):
+            raise ValueError(f"triplet lengths differ: {u.numel()}, {i.numel()}, {j.numel()}")
+        if batch_size <= 0 or u.numel() % batch_size:
+            raise ValueError(f"{u.numel()} triplets is not a multiple of batch_size {batch_size}")
+        nb = u.numel() // batch_size
+        if not self.fits(batch_size, nb):
+            raise ValueError(f"plan of {nb} x {batch_size} exceeds context capacity "
+                             f"{self.max_batches} x {self.max_batch_size}")
+        with torch.cuda.device(self.device):
+            call("acf_apr_plan", self._ptr, u.data_ptr(), i.data_ptr(), j.data_ptr(), batch_size, nb,
+                 int(check), _stream_ptr(self.device))
+        self._staged = (u, i, j)  # keep alive until the stream has consumed them
+        self.batch_size, self.n_batches = batch_size, nb
+        return nb
+
+    def _tables(self, P, Q, accP, accQ) -> Tables:
+        for t, n, rows in ((P, "embedding_P", self.U1), (Q, "embedding_Q", self.I1),
+                           (accP, "accumulator_P", self.U1), (accQ, "accumulator_Q", self.I1)):
+            _require(t, n, torch.float32, self.device, 2)
+            if tuple(t.shape) != (rows, self.d):
+                raise ValueError(f"{n} has shape {tuple(t.shape)}, expected {(rows, self.d)}")
+        return Tables(P.data_ptr(), Q.data_ptr(), accP.data_ptr(), accQ.data_ptr())
+
+    def delta_update(self, tables, hp: StepHParams, batch: int) -> None:
+        tb, h = self._tables(*tables), hp.to_c()
+        with torch.cuda.device(self.device):
+            call("acf_apr_delta_update", self._ptr, ctypes.byref(tb), ctypes.byref(h), batch,
+                 _stream_ptr(self.device))
+
+    def optimizer_step(self, tables, hp: StepHParams, batch: int) -> None:
+        tb, h = self._tables(*tables), hp.to_c()
+        with torch.cuda.device(self.device):
+            call("acf_apr_optimizer_step", self._ptr, ctypes.byref(tb), ctypes.byref(h), batch,
+                 _stream_ptr(self.device))
+
+    def train_planned(self, tables, hp: StepHParams, first: int = 0, n: int | None = None,
+                      graph: bool = True) -> None:
+        n = self.n_batches - first if n is None else n
+        tb, h = self._tables(*tables), hp.to_c()
+        with torch.cuda.device(self.device):
+            call("acf_apr_train_planned", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n,
+                 int(bool(graph)), _stream_ptr(self.device))
+
+    def time_kernels(self, tables, hp: StepHParams, first: int = 0, n: int | None = None):
+        """Per-kernel-kind device time (ms) and launch counts over planned batches,
+        measured with start/stop events attached to each launch (tables are
+        trained exactly as by train_planned).  Kinds: clean, adv, apply."""
+        n = self.n_batches - first if n is None else n
+        tb, h = self._tables(*tables), hp.to_c()
+        ms = (ctypes.c_double * 3)()
+        cnt = (ctypes.c_int32 * 3)()
+        with torch.cuda.device(self.device):
+            call("acf_apr_time_kernels", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
+                 _stream_ptr(self.device))
+        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "apply"))}
+
+    def losses(self):
+        """Per-triplet (clean, adversarial) softplus terms of the last steps."""
+        n = self.batch_size * self.n_batches
+        lc = torch.empty(n, dtype=torch.float32, device=self.device)
+        la = torch.empty(n, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            call("acf_apr_copy_losses", self._ptr, lc.data_ptr(), la.data_ptr(),
+                 _stream_ptr(self.device))
+        return lc, la
+
+    def delta_tables(self):
+        """Dense delta_P / delta_Q of the last delta_update (zeros elsewhere)."""
+        dP = torch.zeros(self.U1, self.d, dtype=torch.float32, device=self.device)
+        dQ = torch.zeros(self.I1, self.d, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            call("acf_apr_delta_scatter", self._ptr, dP.data_ptr(), dQ.data_ptr(),
+                 _stream_ptr(self.device))
+        return dP, dQ
+
+
+def bpr_forward(P, Q, user, item_pos, item_neg, batch_size: int, clip_lo=CLIP_LO, clip_hi=CLIP_HI,
+                want_scores: bool = False):
+    """training_loss_acc's forward (utils.py:159-175): per-batch loss sum and #correct."""
+    dev = P.device
+    _require(P, "embedding_P", torch.float32, None, 2)
+    _require(Q, "embedding_Q", torch.float32, dev, 2)
+    if P.shape[1] != Q.shape[1]:
+        raise ValueError("embedding_P and embedding_Q dims differ")
+    u, i, j = (_idx(x, n, dev) for x, n in ((user, "user"), (item_pos, "item_pos"), (item_neg, "item_neg")))
+    n = u.numel()
+    if batch_size <= 0 or n % batch_size or i.numel() != n or j.numel() != n:
+        raise ValueError("triplets must be equal-length multiples of batch_size")
+    nb = n // batch_size
+    _check_range(u, P.shape[0], "user")
+    _check_range(torch.cat([i, j]), Q.shape[0], "item")
+    bl = torch.empty(nb, dtype=torch.float32, device=dev)
+    bc = torch.empty(nb, dtype=torch.int32, device=dev)
+    op = torch.empty(n, dtype=torch.float32, device=dev) if want_scores else None
+    on = torch.empty(n, dtype=torch.float32, device=dev) if want_scores else None
+    with torch.cuda.device(dev):
+        call("acf_bpr_forward", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
+             u.data_ptr(), i.data_ptr(), j.data_ptr(), batch_size, nb, clip_lo, clip_hi,
+             bl.data_ptr(), bc.data_ptr(), op.data_ptr() if op is not None else None,
+             on.data_ptr() if on is not None else None, _stream_ptr(dev))
+    return bl, bc, op, on
+
+
+def _check_range(idx: torch.Tensor, rows: int, name: str) -> None:
+    if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= rows):
+        raise _native.NativeIndexError(_native.ACF_E_RANGE, "range check",
+                                       f"{name} index outside [0, {rows})")
+
+
+def eval_positions_all(P, Q, users, test_items, num_candidates: int, excl_off, excl_items):
+    """_eval_by_user positions over all items minus the exclusion lists."""
+    dev = P.device
+    _require(P, "embedding_P", torch.float32, None, 2)
+    _require(Q, "embedding_Q", torch.float32, dev, 2)
+    u, t = _idx(users, "users", dev), _idx(test_items, "test_items", dev)
+    off = torch.as_tensor(excl_off).to(device=dev, dtype=torch.int64).contiguous()
+    ex = _idx(excl_items, "excl_items", dev) if len(excl_items) else torch.zeros(1, dtype=torch.int32, device=dev)
+    if off.numel() != u.numel() + 1:
+        raise ValueError("excl_off must have len(users) + 1 entries")
+    _check_range(u, P.shape[0], "user")
+    _check_range(t, Q.shape[0], "test item")
+    if num_candidates > Q.shape[0]:
+        raise ValueError("num_candidates exceeds item rows")
+    pos = torch.empty(u.numel(), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        call("acf_eval_positions_all", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
+             u.data_ptr(), t.data_ptr(), u.numel(), int(num_candidates), off.data_ptr(), ex.data_ptr(),
+             pos.data_ptr(), _stream_ptr(dev))
+    return pos
+
+
+def eval_positions_list(P, Q, users, test_items, cand_off, cand_items):
+    """_eval_by_user positions over explicit candidate lists ("sample" mode)."""
+    dev = P.device
+    _require(P, "embedding_P", torch.float32, None, 2)
+    _require(Q, "embedding_Q", torch.float32, dev, 2)
+    u, t = _idx(users, "users", dev), _idx(test_items, "test_items", dev)
+    off = torch.as_tensor(cand_off).to(device=dev, dtype=torch.int64).contiguous()
+    c = _idx(cand_items, "cand_items", dev) if len(cand_items) else torch.zeros(1, dtype=torch.int32, device=dev)
+    _check_range(u, P.shape[0], "user")
+    _check_range(torch.cat([t, c]), Q.shape[0], "item")
+    pos = torch.empty(u.numel(), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        call("acf_eval_positions_list", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
+             u.data_ptr(), t.data_ptr(), u.numel(), off.data_ptr(), c.data_ptr(), pos.data_ptr(),
+             _stream_ptr(dev))
+    return pos
+
+
+def sample_epoch(pos_user, pos_item, batch_size: int, num_items: int, list_off, list_items,
+                 seed: int, max_tries: int = 1 << 20, check: bool = True):
+    """Device-side shuffle + negative sampling for one epoch (APR.py:39-81)."""
+    dev = pos_user.device
+    pu = _idx(pos_user, "pos_user", dev)
+    pi = _idx(pos_item, "pos_item", dev)
+    off = torch.as_tensor(list_off).to(device=dev, dtype=torch.int64).contiguous()
+    li = _idx(list_items, "list_items", dev) if len(list_items) else torch.zeros(1, dtype=torch.int32, device=dev)
+    n_out = (pu.numel() // batch_size) * batch_size
+    ou = torch.empty(n_out, dtype=torch.int32, device=dev)
+    op = torch.empty(n_out, dtype=torch.int32, device=dev)
+    on = torch.empty(n_out, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        call("acf_sample_epoch", pu.data_ptr(), pi.data_ptr(), pu.numel(), batch_size, int(num_items),
+             off.numel() - 1, off.data_ptr(), li.data_ptr(), int(seed) & 0xFFFFFFFFFFFFFFFF,
+             int(max_tries), int(check), ou.data_ptr(), op.data_ptr(), on.data_ptr(), _stream_ptr(dev))
+    return ou, op, on
+
+
+def dns_select(P, Q, user, cand, dns: int):
+    """utils.py:121-133: argmax-score negative among dns candidates per triplet."""
+    dev = P.device
+    _require(P, "embedding_P", torch.float32, None, 2)
+    _require(Q, "embedding_Q", torch.float32, dev, 2)
+    u = _idx(user, "user", dev)
+    c = _idx(cand, "cand", dev)
+    if c.numel() != u.numel() * dns:
+        raise ValueError("cand must hold dns candidates per triplet")
+    _check_range(u, P.shape[0], "user")
+    _check_range(c, Q.shape[0], "item")
+    out = torch.empty(u.numel(), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        call("acf_dns_select", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
+             u.data_ptr(), c.data_ptr(), u.numel(), int(dns), out.data_ptr(), _stream_ptr(dev))
+    return out

@@ -1,0 +1,255 @@
+#!/usr/bin/env python
+"""Benchmark of the APR (adversarial BPR-MF) training hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): APR on ml-1m-shaped synthetic data
+(6,040 users x 3,706 items, ~994k training pairs, heavy-tailed user degree,
+Zipf items), d = 64, eps = 0.5, reg_adv = 1, lr = 0.05 Adagrad, batch 512 —
+the reference's run_adv_ori.py APR phase.  One "step" = one mini-batch of 512
+(u, i, j) triplets through delta_update + optimizer_step (utils.py:117-119).
+
+Timed region: dedup plan + hipGraph replay of the K steps, inputs (triplets,
+tables) already resident in HBM.  value = triplets/s over all ranks.
+
+--gpus N (torchrun, one rank per GPU): N independent APR jobs (replicas, weak
+scaling) — the reference's experiments are independent single-process runs and a
+B = 512 step has no data-parallel split worth an exchange.
+
+Extra fields: "roofline" (dominant kernel, HIP-event kernel times),
+"cpu_baseline" (oracle/apr_oracle.c in the reference's dense-delta mode, 1 core,
+bounded sample), "roofline_large_batch" (same kernels at batch 65,536 on
+10M x 5M tables, d = 128, when --large).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+PKG = "adversarial-collaborative-filtering_amd"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+REF_CPU_TRIPLETS_PER_S = 993792 / 11.4  # ml-1m APR phase, best epoch 11.4 s
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3882, help="timed mini-batches (3882 = 2 ml-1m epochs)")
+    p.add_argument("--warmup", type=int, default=1941)
+    p.add_argument("--batch", type=int, default=512)
+    p.add_argument("--dim", type=int, default=64)
+    p.add_argument("--chunk", type=int, default=1941, help="batches per plan / graph")
+    p.add_argument("--eager", action="store_true", help="eager launches instead of hipGraph replay")
+    p.add_argument("--cpu-batches", type=int, default=5823, help="oracle sample size (batches, ~10-30 s)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--time-batches", type=int, default=400, help="batches in the kernel-timing pass")
+    p.add_argument("--large", action="store_true", help="also measure batch 65536 on 10M x 5M x d128")
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def bytes_per_unit(kind: int, d: int) -> int:
+    """Algorithmic HBM bytes per unit:
+    clean: per triplet, P[u], Q[i], Q[j] + 3 int32 indices;
+    adv:   per triplet, P[u], Q[i], Q[j], dP[u], dQ[i], dQ[j] + 3 indices;
+    apply: per unique row, read w, acc, g + write w, acc."""
+    return {0: 3 * d * 4 + 12, 1: 6 * d * 4 + 12, 2: 5 * d * 4}[kind]
+
+
+def make_triplets(acf, ds, B, n_batches, dev, seed):
+    sampler = acf.DeviceSampler(ds, B, dev, seed=seed)
+    us, is_, js = [], [], []
+    got, e = 0, 0
+    while got < n_batches:
+        ep = sampler.epoch(e)
+        us.append(ep.user); is_.append(ep.item_pos); js.append(ep.item_neg)
+        got += ep.n_batches
+        e += 1
+    n = n_batches * B
+    return torch.cat(us)[:n].contiguous(), torch.cat(is_)[:n].contiguous(), torch.cat(js)[:n].contiguous()
+
+
+def init_tables(U1, I1, d, dev, seed):
+    g = torch.Generator().manual_seed(seed)
+    P = torch.nn.init.trunc_normal_(torch.empty(U1, d), 0, 0.01, -0.02, 0.02, generator=g).to(dev)
+    Q = torch.nn.init.trunc_normal_(torch.empty(I1, d), 0, 0.01, -0.02, 0.02, generator=g).to(dev)
+    return [P, Q, torch.full((U1, d), 0.1, device=dev), torch.full((I1, d), 0.1, device=dev)]
+
+
+def run_batches(ctx, tabs, hp, u, i, j, B, first, count, chunk, graph):
+    b = first
+    while b < first + count:
+        n = min(chunk, first + count - b)
+        s = slice(b * B, (b + n) * B)
+        ctx.plan(u[s], i[s], j[s], B, check=False)
+        ctx.train_planned(tabs, hp, 0, n, graph=graph)
+        b += n
+
+
+def unique_rows_per_batch(u, i, j, B, nb):
+    uu = u[: nb * B].view(nb, B).cpu().numpy()
+    it = torch.cat([i[: nb * B].view(nb, B), j[: nb * B].view(nb, B)], 1).cpu().numpy()
+    return float(np.mean([len(np.unique(r)) for r in uu]) + np.mean([len(np.unique(r)) for r in it]))
+
+
+def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb):
+    s = slice(0, nb * B)
+    ctx.plan(u[s], i[s], j[s], B, check=False)
+    t = ctx.time_kernels(tabs, hp, 0, nb)
+    kinds = ["clean", "adv", "apply"]
+    tot = {k: t[k][0] for k in kinds}
+    dom = max(kinds, key=lambda k: tot[k])
+    kid = kinds.index(dom)
+    avg_ms = t[dom][0] / max(t[dom][1], 1)
+    units = B if kid < 2 else unique_rows_per_batch(u, i, j, B, nb)
+    alg_bytes = bytes_per_unit(kid, d) * units
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    per_kernel_us = {k: round(1e3 * t[k][0] / max(t[k][1], 1), 3) for k in kinds if t[k][1]}
+    return {"bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "bytes_per_launch": int(alg_bytes), "avg_launch_us": round(avg_ms * 1e3, 3),
+            "per_kernel_avg_us": per_kernel_us}
+
+
+def cpu_baseline(u, i, j, P0, Q0, B, nb):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from apr_oracle import COracle, HParams
+    o = COracle()
+    U, I, J = (x[: nb * B].cpu().numpy() for x in (u, i, j))
+    P, Q = P0.cpu().numpy().copy(), Q0.cpu().numpy().copy()
+    aP, aQ = np.full_like(P, 0.1), np.full_like(Q, 0.1)
+    t0 = time.perf_counter()
+    o.apr_train(P, Q, aP, aQ, U, I, J, B, HParams(adver=1), dense=True)
+    dt = time.perf_counter() - t0
+    return {"value": round(nb * B / dt, 1), "unit": "triplets/s", "cores": 1, "kind": "port",
+            "sample": f"{nb} batches x {B} of the same triplet stream, oracle/apr_oracle.c with the "
+                      f"reference's dense full-table delta work (APR.py:183-191), 1 thread, {dt:.1f} s",
+            "reference_published": {"value": round(REF_CPU_TRIPLETS_PER_S, 1),
+                                    "source": "out/janEval/ml-1m-sort_apr_..._11_56_42.out:54-55 (UCL CPU, TF1)"}}
+
+
+def large_batch_roofline(acf, ops, dev):
+    """Batch 65,536 on 10M x 5M tables (d = 128, ~15 GB incl. Adagrad slots):
+    tables far beyond the 256 MB Infinity Cache, so rows come from HBM."""
+    U1, I1, d, B, nb = 10_000_001, 5_000_001, 128, 65536, 8
+    g = torch.Generator(device=dev).manual_seed(5)
+    u = torch.randint(0, U1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
+    i = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
+    j = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
+    tabs = [torch.randn(U1, d, device=dev) * 0.01, torch.randn(I1, d, device=dev) * 0.01,
+            torch.full((U1, d), 0.1, device=dev), torch.full((I1, d), 0.1, device=dev)]
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    hp = ops.StepHParams(adver=1)
+    run_batches(ctx, tabs, hp, u, i, j, B, 0, nb, nb, True)  # warm (graph capture)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run_batches(ctx, tabs, hp, u, i, j, B, 0, nb, nb, True)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    rl = kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb)
+    rl["triplets_per_s"] = round(nb * B / dt, 1)
+    rl["config"] = {"users": U1 - 1, "items": I1 - 1, "dim": d, "batch": B}
+    del tabs
+    torch.cuda.empty_cache()
+    return rl
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    acf = importlib.import_module(PKG)
+    ops = importlib.import_module(PKG + ".ops")
+    B, d = a.batch, a.dim
+    ds = acf.ml1m_like(seed=2019 + rank)
+    U1, I1 = ds.num_users + 1, ds.num_items + 1
+    total = a.warmup + a.steps
+    u, i, j = make_triplets(acf, ds, B, max(total, a.time_batches, a.cpu_batches), dev, seed=rank)
+    tabs = init_tables(U1, I1, d, dev, seed=rank)
+    P0, Q0 = tabs[0].clone(), tabs[1].clone()
+    chunk = min(a.chunk, a.steps)
+    ctx = ops.APRContext(U1, I1, d, B, chunk, dev)
+    hp = ops.StepHParams(lr=0.05, eps=0.5, reg=0.0, reg_adv=1.0, adver=1)
+    graph = not a.eager
+    # warmup: W steps plus every chunk size the timed region uses (graph capture happens here)
+    run_batches(ctx, tabs, hp, u, i, j, B, 0, a.warmup, chunk, graph)
+    if a.warmup < chunk:
+        run_batches(ctx, tabs, hp, u, i, j, B, 0, chunk, chunk, graph)
+    if a.steps % chunk:
+        run_batches(ctx, tabs, hp, u, i, j, B, 0, a.steps % chunk, chunk, graph)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run_batches(ctx, tabs, hp, u, i, j, B, a.warmup, a.steps, chunk, graph)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = world * a.steps * B / elapsed
+    finite = bool(torch.isfinite(tabs[0]).all() and torch.isfinite(tabs[1]).all())
+    # roofline of the dominant kernel (separate eager pass with per-launch events)
+    tctx = ops.APRContext(U1, I1, d, B, a.time_batches, dev)
+    roof = kernel_roofline(ops, tctx, tabs, hp, u, i, j, B, d, a.time_batches)
+    step_bytes = bytes_per_unit(1, d) + 3 * d * 4  # gather of 3 rows + 3 acc rows + indices
+    out = {
+        "metric": "BPR triplets/sec (APR ml-1m d=64)",
+        "value": round(value, 1),
+        "unit": "triplets/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1e3 * elapsed / a.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / REF_CPU_TRIPLETS_PER_S, 2),
+        "dtype": "f32",
+        "data": "synthetic ml-1m-shaped (seeded; users>=20 interactions, Zipf items), device sampler",
+        "config": {"workload": "APR phase, ml-1m-shaped, d=64, batch 512, eps 0.5, reg_adv 1, "
+                               "lr 0.05 Adagrad (run_adv_ori.py --model apr)",
+                   "users": ds.num_users, "items": ds.num_items, "dim": d, "global_batch": B * world,
+                   "per_gpu_batch": B, "parallelism": f"replicas x{world}",
+                   "launch": "eager" if a.eager else "hipGraph"},
+        "roofline": roof,
+        "step_bandwidth": {"bytes_per_triplet": step_bytes,
+                           "achieved_GBs": round(value / world * step_bytes / 1e9, 2),
+                           "frac": round(value / world * step_bytes / 1e9 / HBM_PEAK_GBS, 5)},
+        "tables_finite": finite,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(u, i, j, P0, Q0, B, a.cpu_batches)
+    if rank == 0 and a.large:
+        del ctx, tctx
+        torch.cuda.empty_cache()
+        out["roofline_large_batch"] = large_batch_roofline(acf, ops, dev)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,205 @@
+/*
+ * acf_apr.h — C-ABI of the MI355X-native adversarial BPR-MF (APR) hot path.
+ *
+ * The reference (feay1234/Adversarial-Collaborative-Filtering) has no FFI: its hot
+ * path is a TensorFlow-1 graph driven from Python through `sess.run`.  Every entry
+ * point below replaces one such `sess.run` call site (or the op group behind it);
+ * the citation on each names the reference line it stands in for.  Python binds
+ * these with ctypes (adversarial-collaborative-filtering_amd/_native.py); the
+ * binding a maintainer would add to the reference is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (HIP, gfx950) unless noted.
+ *   - Tables are fp32, row-major, contiguous, [rows, dim]; indices are int32.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy null stream).
+ *   - Every call is asynchronous on `stream` unless documented otherwise.
+ *   - Return value: ACF_OK (0) or an ACF_E_* code; acf_last_error() gives a
+ *     thread-local message for the last failing call.
+ *   - dim must be a multiple of 4 and <= 1024 (all configurations the reference
+ *     runs use dim in {8,16,32,64,128}).
+ */
+#ifndef ACF_APR_H
+#define ACF_APR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACF_APR_ABI_VERSION 1
+
+enum {
+  ACF_OK = 0,
+  ACF_E_INVALID = 1,     /* bad argument (shape, null pointer, unsupported dim) */
+  ACF_E_RANGE = 2,       /* index out of range (TF Gather's InvalidArgument)     */
+  ACF_E_HIP = 3,         /* HIP runtime error                                    */
+  ACF_E_NOMEM = 4,       /* device allocation failed                             */
+  ACF_E_STATE = 5        /* call out of order (e.g. step before plan)            */
+};
+
+/* Opaque per-model context: owns the device workspace, the batch plans and the
+ * cached hipGraph executables.  One context per (process, device, model). */
+typedef struct acf_apr_ctx acf_apr_ctx;
+
+/* Trainable state of MF (APR.py:105-119) plus its Adagrad slots
+ * (APR.py:193-195, TF initial_accumulator_value = 0.1). */
+typedef struct acf_apr_tables {
+  float* P;    /* embedding_P  [num_user_rows, dim] */
+  float* Q;    /* embedding_Q  [num_item_rows, dim] */
+  float* accP; /* Adagrad accumulator of P, same shape */
+  float* accQ; /* Adagrad accumulator of Q, same shape */
+} acf_apr_tables;
+
+/* Hyper-parameters read by MF.__init__ (APR.py:86-97) and the graph constants. */
+typedef struct acf_apr_hparams {
+  float lr;        /* args.lr       (run_adv_ori.py:42, default 0.05)  */
+  float eps;       /* args.eps      (run_adv_ori.py:54, default 0.5)   */
+  float reg;       /* args.reg      (run_adv_ori.py:40, default 0)     */
+  float reg_adv;   /* args.reg_adv  (run_adv_ori.py:44, default 1)     */
+  float clip_lo;   /* clip_by_value lower bound, -80  (APR.py:148)     */
+  float clip_hi;   /* clip_by_value upper bound, 1e8  (APR.py:148)     */
+  int32_t adver;   /* 0: BPR graph, 1: APR graph (APR.py:156)          */
+  int32_t adv_mode;/* 0: "grad" (APR.py:180-191); 1: "random" (APR.py:170-177) */
+  uint64_t seed;   /* counter-based RNG seed for adv_mode = 1          */
+  int32_t zero_delta; /* 1: adversarial terms use delta = 0 (the dns>1 branch of
+                         utils.py:121-139 never runs update_P/update_Q)  */
+  int32_t reserved;
+} acf_apr_hparams;
+
+/* ---- library ------------------------------------------------------------ */
+int acf_apr_abi_version(void);
+const char* acf_apr_last_error(void);
+
+/* ---- context ------------------------------------------------------------ */
+/* Allocates the workspace for plans of up to max_batches_per_plan batches of up
+ * to max_batch_size triplets.  Synchronous.  Replaces MF(...).build_graph()
+ * (APR.py:197-202) as the point where per-model device state is created. */
+int acf_apr_create(acf_apr_ctx** out, int64_t num_user_rows, int64_t num_item_rows,
+                   int32_t dim, int32_t max_batch_size, int32_t max_batches_per_plan);
+int acf_apr_destroy(acf_apr_ctx* ctx);
+
+/* ---- batch planning: TF's sparse-gradient de-duplication ------------------
+ * Stages n_batches consecutive mini-batches (batch b = triplets
+ * [b*batch_size, (b+1)*batch_size)) and builds, per batch, the unique user and
+ * item rows with the ordered list of their occurrences — the structure TF builds
+ * with Unique + UnsortedSegmentSum in Optimizer._apply_sparse_duplicate_indices
+ * (behind APR.py:195) and that IndexedSlices->dense conversion sums
+ * (APR.py:183-187).  If `check` != 0 the call synchronises the stream and
+ * returns ACF_E_RANGE when any index is outside its table (TF CPU Gather raises
+ * InvalidArgument there); with check == 0 bad indices are clamped to row 0. */
+int acf_apr_plan(acf_apr_ctx* ctx, const int32_t* user, const int32_t* item_pos,
+                 const int32_t* item_neg, int32_t batch_size, int32_t n_batches,
+                 int32_t check, void* stream);
+
+/* sess.run([model.update_P, model.update_Q], feed_dict)  (utils.py:117-118,
+ * APR.py:167-191): delta rows for every row touched by planned batch `batch`.
+ * Rows not touched have delta = 0 in the reference and are never read, so only
+ * touched rows are materialised (in the context). */
+int acf_apr_delta_update(acf_apr_ctx* ctx, const acf_apr_tables* tables,
+                         const acf_apr_hparams* hp, int32_t batch, void* stream);
+
+/* sess.run(model.optimizer, feed_dict)  (utils.py:119, APR.py:143-165,193-195):
+ * clean + (if hp->adver) adversarial forward/backward, per-row gradient
+ * aggregation, sparse Adagrad on the unique rows — in place on `tables`.
+ * With hp->adver the delta of the last acf_apr_delta_update on the same batch
+ * is used. */
+int acf_apr_optimizer_step(acf_apr_ctx* ctx, const acf_apr_tables* tables,
+                           const acf_apr_hparams* hp, int32_t batch, void* stream);
+
+/* The hot loop of training_batch (utils.py:106-119, dns == 1): for planned
+ * batches [first_batch, first_batch + n_batches): delta_update (if adver) then
+ * optimizer_step.  graph_mode 1 replays a cached hipGraph of the whole loop
+ * (captured on first use for this (tables, hparams, range)); 0 launches
+ * eagerly. */
+int acf_apr_train_planned(acf_apr_ctx* ctx, const acf_apr_tables* tables,
+                          const acf_apr_hparams* hp, int32_t first_batch,
+                          int32_t n_batches, int32_t graph_mode, void* stream);
+
+/* Kernel timing for roofline accounting: runs planned batches
+ * [first_batch, first_batch + n_batches) exactly like acf_apr_train_planned
+ * (eager, same stream, same kernels, tables updated) but brackets every kernel
+ * with hipExtLaunchKernelGGL start/stop events.  Writes, per kernel kind
+ * k = 0 (clean pass), 1 (adversarial pass), 2 (Adagrad apply), the summed
+ * kernel time in ms to ms_out[k] and the launch count to launches_out[k].
+ * Synchronous.  Not part of the reference surface. */
+int acf_apr_time_kernels(acf_apr_ctx* ctx, const acf_apr_tables* tables,
+                         const acf_apr_hparams* hp, int32_t first_batch,
+                         int32_t n_batches, double* ms_out, int32_t* launches_out,
+                         void* stream);
+
+/* Per-triplet clean / adversarial losses computed by the last step of each
+ * planned batch (softplus(-clip(x)) terms of APR.py:150,162), for the staged
+ * triplets [0, n_batches*batch_size).  Either pointer may be NULL. */
+int acf_apr_copy_losses(acf_apr_ctx* ctx, float* loss_clean, float* loss_adv,
+                        void* stream);
+
+/* Writes the delta rows of the last acf_apr_delta_update into dense tables
+ * delta_P [num_user_rows, dim] / delta_Q [num_item_rows, dim]; untouched rows
+ * are left as the caller initialised them (zero in the reference). */
+int acf_apr_delta_scatter(acf_apr_ctx* ctx, float* delta_P, float* delta_Q,
+                          void* stream);
+
+/* ---- forward only: training_loss_acc (utils.py:159-175) ------------------
+ * Per batch b of n_batches: batch_loss[b] = sum softplus(-clip(x+ - x-)) and
+ * batch_correct[b] = #(x+ - x- > 0); optional per-triplet scores out_pos /
+ * out_neg (model.output / model.output_neg).  Any output may be NULL. */
+int acf_bpr_forward(const float* P, const float* Q, int64_t num_user_rows,
+                    int64_t num_item_rows, int32_t dim, const int32_t* user,
+                    const int32_t* item_pos, const int32_t* item_neg,
+                    int32_t batch_size, int32_t n_batches, float clip_lo,
+                    float clip_hi, float* batch_loss, int32_t* batch_correct,
+                    float* out_pos, float* out_neg, void* stream);
+
+/* ---- evaluation: _eval_by_user (utils.py:244-254) ------------------------
+ * position[u] = #{candidate c : score(u,c) >= score(u,test_item[u])} with
+ * score = P[u] . Q[c].
+ * _all:  candidates = [0, num_candidates) minus the sorted, unique exclusion
+ *        list excl_items[excl_off[k] .. excl_off[k+1]) of user k (the caller
+ *        passes trainList[u] union {test item}, restricted to the range:
+ *        utils.py:211-215).
+ * _list: candidates = cand_items[cand_off[k] .. cand_off[k+1]) verbatim, with
+ *        repeats ("sample" mode, utils.py:201-209). */
+int acf_eval_positions_all(const float* P, const float* Q, int64_t num_user_rows,
+                           int64_t num_item_rows, int32_t dim, const int32_t* users,
+                           const int32_t* test_items, int32_t n_users,
+                           int32_t num_candidates, const int64_t* excl_off,
+                           const int32_t* excl_items, int32_t* positions,
+                           void* stream);
+int acf_eval_positions_list(const float* P, const float* Q, int64_t num_user_rows,
+                            int64_t num_item_rows, int32_t dim, const int32_t* users,
+                            const int32_t* test_items, int32_t n_users,
+                            const int64_t* cand_off, const int32_t* cand_items,
+                            int32_t* positions, void* stream);
+
+/* ---- sampler: shuffle/_get_train_batch (APR.py:39-81) --------------------
+ * Shuffles the n_pos positive pairs with a counter-based permutation of
+ * `seed`, keeps floor(n_pos / batch_size) * batch_size of them (drop-last,
+ * APR.py:52), and draws one negative per triplet uniformly from
+ * [0, num_items), redrawn while it is in the user's list
+ * list_items[list_off[u] .. list_off[u+1]) (sorted ascending; the
+ * OriginalDataset.trainList of APR.py:77).  Writes out_user/out_pos/out_neg of
+ * length n_out = floor(n_pos/batch_size)*batch_size.  Users with a full list
+ * (no admissible negative) get -1 after max_tries draws; with check != 0 the
+ * call synchronises and returns ACF_E_RANGE in that case. */
+int acf_sample_epoch(const int32_t* pos_user, const int32_t* pos_item, int64_t n_pos,
+                     int32_t batch_size, int32_t num_items, int32_t num_lists,
+                     const int64_t* list_off, const int32_t* list_items,
+                     uint64_t seed, int32_t max_tries, int32_t check,
+                     int32_t* out_user, int32_t* out_pos, int32_t* out_neg,
+                     void* stream);
+
+/* dns > 1 negative selection (utils.py:121-133): per triplet, the candidate of
+ * cand[e*dns .. e*dns+dns) with the largest clean score P[user[e]].Q[c] (first
+ * maximum wins, np.argmax). */
+int acf_dns_select(const float* P, const float* Q, int64_t num_user_rows,
+                   int64_t num_item_rows, int32_t dim, const int32_t* user,
+                   const int32_t* cand, int64_t n, int32_t dns, int32_t* out_neg,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ACF_APR_H */

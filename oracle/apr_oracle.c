@@ -1,0 +1,356 @@
+/*
+ * apr_oracle.c — CPU restatement of the reference APR / BPR-MF training step.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed CPU
+ * baseline.  The product path (adversarial-collaborative-filtering_amd) never
+ * calls it.
+ *
+ * What it restates (reference = feay1234/Adversarial-Collaborative-Filtering):
+ *   MF graph           APR.py:121-195  (clean/adv inference, loss, delta, Adagrad)
+ *   training_batch     utils.py:106-119 (update_P/update_Q run, then optimizer run)
+ *   training_loss_acc  utils.py:159-175
+ *   _eval_by_user      utils.py:244-254 (position = #neg >= pos)
+ * with these TensorFlow-1 op semantics (TF is not installed here; the reference
+ * pins no version — the API surface implies TF ~1.13-1.15):
+ *   matmul(p*q, h)        product rounded, then summed                (APR.py:127)
+ *   clip_by_value         gradient passes where lo <= x <= hi          (APR.py:148)
+ *   softplus(f)           f > 13.9424 -> f; f < -13.9424 -> e^f; else log(e^f + 1)
+ *   SoftplusGrad          upstream / (exp(-f) + 1)
+ *   tf.gradients of a gathered table -> IndexedSlices; dense conversion and the
+ *   optimizer's _deduplicate_indexed_slices both sum duplicate rows
+ *   l2_normalize(x, 1)    x * rsqrt(max(sum x^2, 1e-12))               (APR.py:190)
+ *   AdagradOptimizer      acc0 = 0.1; sparse apply: acc += g^2; w -= lr*g*rsqrt(acc)
+ *
+ * Parity status: the training-step arithmetic is PINNED STATISTICALLY only —
+ * TensorFlow is absent, so no op-level output of the reference can be produced
+ * here ("parity unpinned" at op level).  It is cross-checked against an
+ * independent numpy restatement that materialises the TF graph densely
+ * (oracle/apr_oracle.py) and against torch-CPU autograd of the same graph
+ * (tests/test_oracle.py), and against the published Video/ml-1m run logs at
+ * the end-to-end level.  The evaluation and data/sampler restatements are pinned
+ * against fixtures produced by the reference's own Python (tests/golden/).
+ *
+ * `dense` = 1 reproduces the reference's per-batch work literally: the clean
+ * gradient is densified to [rows, d] tables, every row is l2-normalised and
+ * assigned to full delta tables (APR.py:183-191).  `dense` = 0 touches only the
+ * rows in the batch (mathematically identical; rows outside the batch have
+ * delta = 0 and are never read).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+  float lr, eps, reg, reg_adv, clip_lo, clip_hi;
+  int32_t adver;      /* APR graph (1) or BPR graph (0) */
+  int32_t zero_delta; /* dns>1 branch: delta tables never assigned (stay 0) */
+  int32_t dense;      /* 1: reference's dense delta work (see header) */
+  int32_t reserved;
+} oracle_hparams;
+
+#define SOFTPLUS_T 13.942385f
+
+static float dotp(const float* a, const float* b, int d) {
+  /* matmul(p*q, h): elementwise product rounded to fp32, then summed */
+  float s = 0.f;
+  for (int k = 0; k < d; ++k) {
+    float pr = a[k] * b[k];
+    s = s + pr;
+  }
+  return s;
+}
+
+static void bpr_term(float x, float lo, float hi, float* g, float* loss) {
+  float xc = x < lo ? lo : (x > hi ? hi : x);
+  int pass = (x >= lo) && (x <= hi);
+  float f = -xc;
+  *g = pass ? -(1.0f / (expf(-f) + 1.0f)) : 0.0f;
+  *loss = f > SOFTPLUS_T ? f : (f < -SOFTPLUS_T ? expf(f) : logf(expf(f) + 1.0f));
+}
+
+/* row -> slot map for the rows a batch touches */
+typedef struct {
+  int32_t* slot_of; /* [rows], -1 when untouched */
+  int32_t* rows;    /* [cap] unique rows in first-touch order */
+  int32_t* count;   /* [cap] occurrences */
+  float* acc;       /* [cap, d] gradient accumulator */
+  int n, d;
+} rowset;
+
+static int rowset_init(rowset* r, int64_t rows, int cap, int d) {
+  r->slot_of = (int32_t*)malloc(sizeof(int32_t) * (size_t)rows);
+  r->rows = (int32_t*)malloc(sizeof(int32_t) * (size_t)cap);
+  r->count = (int32_t*)malloc(sizeof(int32_t) * (size_t)cap);
+  r->acc = (float*)malloc(sizeof(float) * (size_t)cap * d);
+  if (!r->slot_of || !r->rows || !r->count || !r->acc) return -1;
+  for (int64_t x = 0; x < rows; ++x) r->slot_of[x] = -1;
+  r->n = 0;
+  r->d = d;
+  return 0;
+}
+
+static void rowset_free(rowset* r) {
+  free(r->slot_of); free(r->rows); free(r->count); free(r->acc);
+}
+
+static int rowset_touch(rowset* r, int32_t row) {
+  int s = r->slot_of[row];
+  if (s < 0) {
+    s = r->n++;
+    r->slot_of[row] = s;
+    r->rows[s] = row;
+    r->count[s] = 0;
+    memset(r->acc + (size_t)s * r->d, 0, sizeof(float) * r->d);
+  }
+  return s;
+}
+
+static void rowset_clear(rowset* r) {
+  for (int s = 0; s < r->n; ++s) r->slot_of[r->rows[s]] = -1;
+  r->n = 0;
+}
+
+static void axpy(float* y, float a, const float* x, int d) {
+  for (int k = 0; k < d; ++k) y[k] = y[k] + a * x[k];
+}
+
+/* One mini-batch of training_batch (utils.py:114-119).  Tables are updated in
+ * place.  loss_clean / loss_adv (length B) receive the per-triplet softplus
+ * terms; delta_P / delta_Q (dense, optional) receive the assigned delta tables. */
+int oracle_apr_batch(float* P, float* Q, float* accP, float* accQ, int64_t U1, int64_t I1, int d,
+                     const int32_t* u, const int32_t* ip, const int32_t* in, int B,
+                     const oracle_hparams* hp, float* loss_clean, float* loss_adv,
+                     float* delta_P, float* delta_Q) {
+  for (int b = 0; b < B; ++b)
+    if (u[b] < 0 || u[b] >= U1 || ip[b] < 0 || ip[b] >= I1 || in[b] < 0 || in[b] >= I1) return -2;
+  rowset RU, RI;
+  if (rowset_init(&RU, U1, B, d) || rowset_init(&RI, I1, 2 * B, d)) return -1;
+  float* g = (float*)malloc(sizeof(float) * B);
+  float* ga = (float*)malloc(sizeof(float) * B);
+  float* pp = (float*)malloc(sizeof(float) * d);
+  float* qi = (float*)malloc(sizeof(float) * d);
+  float* qj = (float*)malloc(sizeof(float) * d);
+  /* slot-indexed delta rows (sparse) */
+  float* dU = (float*)calloc((size_t)B * d, sizeof(float));
+  float* dI = (float*)calloc((size_t)2 * B * d, sizeof(float));
+  float* G0U = (float*)calloc((size_t)B * d, sizeof(float));
+  float* G0I = (float*)calloc((size_t)2 * B * d, sizeof(float));
+  float *denseU = NULL, *denseI = NULL;
+  if (!g || !ga || !pp || !qi || !qj || !dU || !dI || !G0U || !G0I) return -1;
+
+  /* 1. clean forward, per-triplet gradient scale (APR.py:146-150) */
+  for (int b = 0; b < B; ++b) {
+    const float* p = P + (int64_t)u[b] * d;
+    float x = dotp(p, Q + (int64_t)ip[b] * d, d) - dotp(p, Q + (int64_t)in[b] * d, d);
+    float l;
+    bpr_term(x, hp->clip_lo, hp->clip_hi, &g[b], &l);
+    if (loss_clean) loss_clean[b] = l;
+  }
+  /* touch rows: users, then items (pos then neg) — the concat order of the
+   * IndexedSlices of the pos branch then the neg branch */
+  for (int b = 0; b < B; ++b) RU.count[rowset_touch(&RU, u[b])]++;
+  for (int b = 0; b < B; ++b) RI.count[rowset_touch(&RI, ip[b])]++;
+  for (int b = 0; b < B; ++b) RI.count[rowset_touch(&RI, in[b])]++;
+
+  if (hp->adver) {
+    /* 2. clean-loss gradient, segment-summed (tf.gradients(loss, [P, Q])) */
+    for (int b = 0; b < B; ++b) { /* pos branch */
+      axpy(G0U + (size_t)RU.slot_of[u[b]] * d, g[b], Q + (int64_t)ip[b] * d, d);
+      axpy(G0I + (size_t)RI.slot_of[ip[b]] * d, g[b], P + (int64_t)u[b] * d, d);
+    }
+    for (int b = 0; b < B; ++b) { /* neg branch */
+      axpy(G0U + (size_t)RU.slot_of[u[b]] * d, -g[b], Q + (int64_t)in[b] * d, d);
+      axpy(G0I + (size_t)RI.slot_of[in[b]] * d, -g[b], P + (int64_t)u[b] * d, d);
+    }
+    /* 3. delta = eps * l2_normalize(grad)   (APR.py:186-191) */
+    if (hp->dense) {
+      /* the reference's dense work: densify, normalise every row, assign */
+      denseU = (float*)calloc((size_t)U1 * d, sizeof(float));
+      denseI = (float*)calloc((size_t)I1 * d, sizeof(float));
+      if (!denseU || !denseI) return -1;
+      for (int s = 0; s < RU.n; ++s)
+        memcpy(denseU + (int64_t)RU.rows[s] * d, G0U + (size_t)s * d, sizeof(float) * d);
+      for (int s = 0; s < RI.n; ++s)
+        memcpy(denseI + (int64_t)RI.rows[s] * d, G0I + (size_t)s * d, sizeof(float) * d);
+      float* tabs[2] = {denseU, denseI};
+      int64_t nrows[2] = {U1, I1};
+      for (int t = 0; t < 2; ++t)
+        for (int64_t r = 0; r < nrows[t]; ++r) {
+          float* x = tabs[t] + r * d;
+          float ss = 0.f;
+          for (int k = 0; k < d; ++k) ss = ss + x[k] * x[k];
+          float inv = 1.0f / sqrtf(ss > 1e-12f ? ss : 1e-12f);
+          for (int k = 0; k < d; ++k) x[k] = hp->zero_delta ? 0.f : (x[k] * inv) * hp->eps;
+        }
+      for (int s = 0; s < RU.n; ++s)
+        memcpy(dU + (size_t)s * d, denseU + (int64_t)RU.rows[s] * d, sizeof(float) * d);
+      for (int s = 0; s < RI.n; ++s)
+        memcpy(dI + (size_t)s * d, denseI + (int64_t)RI.rows[s] * d, sizeof(float) * d);
+    } else {
+      float* src[2] = {G0U, G0I};
+      float* dst[2] = {dU, dI};
+      int ns[2] = {RU.n, RI.n};
+      for (int t = 0; t < 2; ++t)
+        for (int s = 0; s < ns[t]; ++s) {
+          const float* x = src[t] + (size_t)s * d;
+          float ss = 0.f;
+          for (int k = 0; k < d; ++k) ss = ss + x[k] * x[k];
+          float inv = 1.0f / sqrtf(ss > 1e-12f ? ss : 1e-12f);
+          for (int k = 0; k < d; ++k)
+            dst[t][(size_t)s * d + k] = hp->zero_delta ? 0.f : (x[k] * inv) * hp->eps;
+        }
+    }
+    if (delta_P)
+      for (int s = 0; s < RU.n; ++s)
+        memcpy(delta_P + (int64_t)RU.rows[s] * d, dU + (size_t)s * d, sizeof(float) * d);
+    if (delta_Q)
+      for (int s = 0; s < RI.n; ++s)
+        memcpy(delta_Q + (int64_t)RI.rows[s] * d, dI + (size_t)s * d, sizeof(float) * d);
+    /* 4. adversarial forward on p + dP[u], q + dQ[i]   (APR.py:130-141,158-162) */
+    for (int b = 0; b < B; ++b) {
+      const float* du = dU + (size_t)RU.slot_of[u[b]] * d;
+      const float* di = dI + (size_t)RI.slot_of[ip[b]] * d;
+      const float* dj = dI + (size_t)RI.slot_of[in[b]] * d;
+      const float* p = P + (int64_t)u[b] * d;
+      for (int k = 0; k < d; ++k) {
+        pp[k] = p[k] + du[k];
+        qi[k] = Q[(int64_t)ip[b] * d + k] + di[k];
+        qj[k] = Q[(int64_t)in[b] * d + k] + dj[k];
+      }
+      float x = dotp(pp, qi, d) - dotp(pp, qj, d);
+      float l;
+      bpr_term(x, hp->clip_lo, hp->clip_hi, &ga[b], &l);
+      if (loss_adv) loss_adv[b] = l;
+    }
+  }
+
+  /* 5. optimizer gradient of opt_loss, deduplicated (concat order: clean pos,
+   *    clean neg, [adv pos, adv neg]; reg terms add 2*reg*w/(B*d) per
+   *    occurrence, twice in the APR graph) */
+  for (int b = 0; b < B; ++b) {
+    axpy(RU.acc + (size_t)RU.slot_of[u[b]] * d, g[b], Q + (int64_t)ip[b] * d, d);
+    axpy(RI.acc + (size_t)RI.slot_of[ip[b]] * d, g[b], P + (int64_t)u[b] * d, d);
+  }
+  for (int b = 0; b < B; ++b) {
+    axpy(RU.acc + (size_t)RU.slot_of[u[b]] * d, -g[b], Q + (int64_t)in[b] * d, d);
+    axpy(RI.acc + (size_t)RI.slot_of[in[b]] * d, -g[b], P + (int64_t)u[b] * d, d);
+  }
+  if (hp->reg != 0.f) {
+    float coef = (2.0f * hp->reg / ((float)B * (float)d)) * (hp->adver ? 2.0f : 1.0f);
+    for (int s = 0; s < RU.n; ++s)
+      axpy(RU.acc + (size_t)s * d, coef * (float)RU.count[s], P + (int64_t)RU.rows[s] * d, d);
+    for (int s = 0; s < RI.n; ++s)
+      axpy(RI.acc + (size_t)s * d, coef * (float)RI.count[s], Q + (int64_t)RI.rows[s] * d, d);
+  }
+  if (hp->adver) {
+    float lam = hp->reg_adv;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int b = 0; b < B; ++b) {
+        const float* du = dU + (size_t)RU.slot_of[u[b]] * d;
+        const float* p = P + (int64_t)u[b] * d;
+        int item = pass == 0 ? ip[b] : in[b];
+        const float* dq = dI + (size_t)RI.slot_of[item] * d;
+        const float* q = Q + (int64_t)item * d;
+        float sgn = pass == 0 ? 1.f : -1.f;
+        for (int k = 0; k < d; ++k) { pp[k] = p[k] + du[k]; qi[k] = q[k] + dq[k]; }
+        axpy(RU.acc + (size_t)RU.slot_of[u[b]] * d, lam * sgn * ga[b], qi, d);
+        axpy(RI.acc + (size_t)RI.slot_of[item] * d, lam * sgn * ga[b], pp, d);
+      }
+  }
+  /* 6. SparseApplyAdagrad on the unique rows */
+  rowset* sets[2] = {&RU, &RI};
+  float* W[2] = {P, Q};
+  float* A[2] = {accP, accQ};
+  for (int t = 0; t < 2; ++t)
+    for (int s = 0; s < sets[t]->n; ++s) {
+      float* w = W[t] + (int64_t)sets[t]->rows[s] * d;
+      float* a = A[t] + (int64_t)sets[t]->rows[s] * d;
+      const float* gr = sets[t]->acc + (size_t)s * d;
+      for (int k = 0; k < d; ++k) {
+        a[k] = a[k] + gr[k] * gr[k];
+        w[k] = w[k] - (hp->lr * gr[k]) * (1.0f / sqrtf(a[k]));
+      }
+    }
+  rowset_clear(&RU);
+  rowset_clear(&RI);
+  rowset_free(&RU);
+  rowset_free(&RI);
+  free(g); free(ga); free(pp); free(qi); free(qj);
+  free(dU); free(dI); free(G0U); free(G0I); free(denseU); free(denseI);
+  return 0;
+}
+
+/* training_batch over n_batches consecutive batches (utils.py:113-119). */
+int oracle_apr_train(float* P, float* Q, float* accP, float* accQ, int64_t U1, int64_t I1, int d,
+                     const int32_t* u, const int32_t* ip, const int32_t* in, int B, int n_batches,
+                     const oracle_hparams* hp) {
+  for (int t = 0; t < n_batches; ++t) {
+    int64_t o = (int64_t)t * B;
+    int r = oracle_apr_batch(P, Q, accP, accQ, U1, I1, d, u + o, ip + o, in + o, B, hp, NULL, NULL,
+                             NULL, NULL);
+    if (r) return r;
+  }
+  return 0;
+}
+
+/* training_loss_acc (utils.py:159-175) per batch: loss sum and #(x+ > x-). */
+int oracle_bpr_forward(const float* P, const float* Q, int64_t U1, int64_t I1, int d,
+                       const int32_t* u, const int32_t* ip, const int32_t* in, int B,
+                       int n_batches, float lo, float hi, float* batch_loss, int32_t* batch_correct,
+                       float* out_pos, float* out_neg) {
+  for (int t = 0; t < n_batches; ++t) {
+    float ls = 0.f;
+    int32_t c = 0;
+    for (int b = 0; b < B; ++b) {
+      int64_t e = (int64_t)t * B + b;
+      if (u[e] < 0 || u[e] >= U1 || ip[e] < 0 || ip[e] >= I1 || in[e] < 0 || in[e] >= I1) return -2;
+      const float* p = P + (int64_t)u[e] * d;
+      float xp = dotp(p, Q + (int64_t)ip[e] * d, d), xn = dotp(p, Q + (int64_t)in[e] * d, d);
+      float g, l;
+      bpr_term(xp - xn, lo, hi, &g, &l);
+      ls += l;
+      c += (xp - xn) > 0.f;
+      if (out_pos) out_pos[e] = xp;
+      if (out_neg) out_neg[e] = xn;
+    }
+    if (batch_loss) batch_loss[t] = ls;
+    if (batch_correct) batch_correct[t] = c;
+  }
+  return 0;
+}
+
+/* _eval_by_user, "all" candidates (utils.py:211-215, 253-254). */
+int oracle_eval_positions_all(const float* P, const float* Q, int d, const int32_t* users,
+                              const int32_t* tests, int n_users, int num_cand,
+                              const int64_t* excl_off, const int32_t* excl, int32_t* positions) {
+  for (int k = 0; k < n_users; ++k) {
+    const float* p = P + (int64_t)users[k] * d;
+    float st = dotp(p, Q + (int64_t)tests[k] * d, d);
+    int64_t e = excl_off[k], e1 = excl_off[k + 1];
+    int32_t pos = 0;
+    for (int c = 0; c < num_cand; ++c) {
+      while (e < e1 && excl[e] < c) ++e;
+      if (e < e1 && excl[e] == c) continue;
+      pos += dotp(p, Q + (int64_t)c * d, d) >= st;
+    }
+    positions[k] = pos;
+  }
+  return 0;
+}
+
+/* _eval_by_user with an explicit candidate list ("sample" mode). */
+int oracle_eval_positions_list(const float* P, const float* Q, int d, const int32_t* users,
+                               const int32_t* tests, int n_users, const int64_t* cand_off,
+                               const int32_t* cand, int32_t* positions) {
+  for (int k = 0; k < n_users; ++k) {
+    const float* p = P + (int64_t)users[k] * d;
+    float st = dotp(p, Q + (int64_t)tests[k] * d, d);
+    int32_t pos = 0;
+    for (int64_t x = cand_off[k]; x < cand_off[k + 1]; ++x)
+      pos += dotp(p, Q + (int64_t)cand[x] * d, d) >= st;
+    positions[k] = pos;
+  }
+  return 0;
+}

@@ -1,0 +1,287 @@
+"""HIP path vs the CPU oracle (oracle/apr_oracle.c) on identical inputs.
+
+Tolerance: fp32, rtol 1e-5 / atol 1e-6 on tables of magnitude O(0.1-1) — the
+bar north_star sets ("within 1e-5 fp32").  Differences come only from the order
+of the per-row dot-product sums (wavefront butterfly vs sequential).
+"""
+import numpy as np
+import pytest
+import torch
+
+from apr_oracle import HParams
+
+pytestmark = pytest.mark.gpu
+RTOL, ATOL = 1e-5, 1e-6
+
+
+def _problem(seed, U1, I1, d, B, nb, scale=0.3, dup_items=False):
+    rng = np.random.default_rng(seed)
+    P = (rng.standard_normal((U1, d)) * scale).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * scale).astype(np.float32)
+    u = rng.integers(0, U1, nb * B).astype(np.int32)
+    i = rng.integers(0, I1, nb * B).astype(np.int32)
+    j = rng.integers(0, I1, nb * B).astype(np.int32)
+    if dup_items:  # the trainList quirk lets j == i happen; force some
+        j[::7] = i[::7]
+    return P, Q, u, i, j
+
+
+def _gpu_tables(P, Q, dev):
+    return [torch.tensor(P, device=dev), torch.tensor(Q, device=dev),
+            torch.full(P.shape, 0.1, device=dev), torch.full(Q.shape, 0.1, device=dev)]
+
+
+def _oracle_run(oracle, P, Q, u, i, j, B, hp, dense=False):
+    rP, rQ = P.copy(), Q.copy()
+    aP, aQ = np.full(P.shape, 0.1, np.float32), np.full(Q.shape, 0.1, np.float32)
+    lcs, las, deltas = [], [], []
+    for t in range(len(u) // B):
+        s = slice(t * B, (t + 1) * B)
+        lc, la, dP, dQ = oracle.apr_batch(rP, rQ, aP, aQ, u[s], i[s], j[s], hp, dense=dense, want_delta=True)
+        lcs.append(lc)
+        las.append(la)
+        deltas.append((dP, dQ))
+    return (rP, rQ, aP, aQ), np.concatenate(lcs), np.concatenate(las), deltas
+
+
+def _close(got, want, name):
+    got = got.detach().cpu().numpy() if isinstance(got, torch.Tensor) else got
+    np.testing.assert_allclose(got, want, rtol=RTOL, atol=ATOL, err_msg=name)
+
+
+@pytest.mark.parametrize("d", [8, 32, 64, 128])
+@pytest.mark.parametrize("adver", [0, 1])
+@pytest.mark.parametrize("graph", [False, True])
+def test_train_planned_matches_oracle(ops, oracle, dev, d, adver, graph):
+    U1, I1, B, nb = 61, 47, 64, 4
+    P, Q, u, i, j = _problem(d * 10 + adver, U1, I1, d, B, nb, dup_items=True)
+    hp_c = HParams(adver=adver)
+    want, lc_w, la_w, _ = _oracle_run(oracle, P, Q, u, i, j, B, hp_c)
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ctx.train_planned(tabs, ops.StepHParams(adver=adver), graph=graph)
+    lc, la = ctx.losses()
+    torch.cuda.synchronize()
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        _close(g, w, n)
+    _close(lc, lc_w, "loss_clean")
+    if adver:
+        _close(la, la_w, "loss_adv")
+
+
+@pytest.mark.parametrize("reg", [0.0, 0.01])
+@pytest.mark.parametrize("d", [16, 64])
+def test_split_calls_and_delta_match_oracle(ops, oracle, dev, reg, d):
+    """sess.run([update_P, update_Q]) then sess.run(optimizer), batch by batch."""
+    U1, I1, B, nb = 33, 29, 48, 3
+    P, Q, u, i, j = _problem(5 + d, U1, I1, d, B, nb)
+    hp_c = HParams(adver=1, reg=reg)
+    want, _, _, deltas = _oracle_run(oracle, P, Q, u, i, j, B, hp_c)
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    hp = ops.StepHParams(adver=1, reg=reg)
+    for t in range(nb):
+        ctx.delta_update(tabs, hp, t)
+        dP, dQ = ctx.delta_tables()
+        _close(dP, deltas[t][0], f"delta_P batch {t}")
+        _close(dQ, deltas[t][1], f"delta_Q batch {t}")
+        ctx.optimizer_step(tabs, hp, t)
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        _close(g, w, n)
+
+
+def test_dense_oracle_equals_sparse_path(ops, oracle, dev):
+    """The reference's dense full-table delta work vs touched-rows-only: same result."""
+    U1, I1, d, B, nb = 90, 70, 64, 32, 3
+    P, Q, u, i, j = _problem(11, U1, I1, d, B, nb)
+    dense, *_ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=1), dense=True)
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ctx.train_planned(tabs, ops.StepHParams(adver=1))
+    for g, w, n in zip(tabs, dense, ("P", "Q", "accP", "accQ")):
+        _close(g, w, n)
+
+
+def test_zero_delta_dns_branch(ops, oracle, dev):
+    U1, I1, d, B = 20, 25, 32, 16
+    P, Q, u, i, j = _problem(3, U1, I1, d, B, 2)
+    want, *_ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=1, zero_delta=1))
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, 2, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    hp = ops.StepHParams(adver=1, zero_delta=1)
+    ctx.train_planned(tabs, hp, graph=False)
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        _close(g, w, n)
+
+
+def test_random_delta_has_norm_eps(ops, dev):
+    U1, I1, d, B = 30, 30, 64, 32
+    P, Q, u, i, j = _problem(4, U1, I1, d, B, 1)
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, 1, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    hp = ops.StepHParams(adver=1, adv="random", eps=0.5, seed=9)
+    ctx.delta_update(tabs, hp, 0)
+    dP, dQ = ctx.delta_tables()
+    touched_u = np.unique(u)
+    norms = torch.linalg.vector_norm(dP[torch.tensor(touched_u, device=dev)], dim=1).cpu().numpy()
+    np.testing.assert_allclose(norms, 0.5, rtol=1e-5)
+    untouched = np.setdiff1d(np.arange(U1), touched_u)
+    assert float(dP[torch.tensor(untouched, device=dev)].abs().max()) == 0.0 if len(untouched) else True
+
+
+def test_forward_matches_oracle(ops, oracle, dev):
+    U1, I1, d, B, nb = 100, 80, 64, 50, 6
+    P, Q, u, i, j = _problem(21, U1, I1, d, B, nb)
+    bl_w, bc_w, op_w, on_w = oracle.bpr_forward(P, Q, u, i, j, B)
+    Pt, Qt = torch.tensor(P, device=dev), torch.tensor(Q, device=dev)
+    bl, bc, op, on = ops.bpr_forward(Pt, Qt, torch.tensor(u, device=dev), torch.tensor(i, device=dev),
+                                     torch.tensor(j, device=dev), B, want_scores=True)
+    _close(op, op_w, "output")
+    _close(on, on_w, "output_neg")
+    np.testing.assert_allclose(bl.cpu().numpy(), bl_w, rtol=1e-5)
+    # acc counts compare sign(x+ - x-); allow a flip only where |x| is at rounding level
+    x = op_w - on_w
+    unsure = (np.abs(x) < 1e-5).reshape(nb, B).sum(1)
+    assert np.all(np.abs(bc.cpu().numpy() - bc_w) <= unsure)
+
+
+def test_eval_positions_exact(ops, oracle, dev):
+    """Integer-valued tables: every score is exact, so ties (>=) are decided the
+    same way as the reference; positions must match bit for bit."""
+    rng = np.random.default_rng(0)
+    U1, I1, d = 50, 200, 16
+    P = rng.integers(-3, 4, (U1, d)).astype(np.float32)
+    Q = rng.integers(-3, 4, (I1, d)).astype(np.float32)
+    users = np.arange(0, 45, dtype=np.int32)
+    tests = rng.integers(0, I1, len(users)).astype(np.int32)
+    lists = [np.unique(np.append(rng.integers(0, 180, rng.integers(0, 40)), t)).astype(np.int32)
+             for t in tests]
+    lists = [l_[l_ < 180] for l_ in lists]
+    off = np.zeros(len(users) + 1, np.int64)
+    np.cumsum([len(l_) for l_ in lists], out=off[1:])
+    excl = np.concatenate(lists)
+    want = oracle.eval_positions_all(P, Q, users, tests, 180, off, excl)
+    got = ops.eval_positions_all(torch.tensor(P, device=dev), torch.tensor(Q, device=dev),
+                                 torch.tensor(users, device=dev), torch.tensor(tests, device=dev), 180,
+                                 off, excl)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+    cand = rng.integers(0, I1, len(users) * 100).astype(np.int32)
+    coff = np.arange(0, len(users) * 100 + 1, 100, dtype=np.int64)
+    want = oracle.eval_positions_list(P, Q, users, tests, coff, cand)
+    got = ops.eval_positions_list(torch.tensor(P, device=dev), torch.tensor(Q, device=dev),
+                                  torch.tensor(users, device=dev), torch.tensor(tests, device=dev), coff, cand)
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
+def test_eval_positions_random_tables(ops, oracle, dev):
+    rng = np.random.default_rng(1)
+    U1, I1, d = 300, 1000, 64
+    P = rng.standard_normal((U1, d)).astype(np.float32)
+    Q = rng.standard_normal((I1, d)).astype(np.float32)
+    users = np.arange(U1, dtype=np.int32)
+    tests = rng.integers(0, I1, U1).astype(np.int32)
+    lists = [np.unique(np.append(rng.integers(0, I1 - 1, 30), t)).astype(np.int32) for t in tests]
+    lists = [l_[l_ < I1 - 1] for l_ in lists]
+    off = np.zeros(U1 + 1, np.int64)
+    np.cumsum([len(l_) for l_ in lists], out=off[1:])
+    excl = np.concatenate(lists)
+    want = oracle.eval_positions_all(P, Q, users, tests, I1 - 1, off, excl)
+    got = ops.eval_positions_all(torch.tensor(P, device=dev), torch.tensor(Q, device=dev),
+                                 torch.tensor(users, device=dev), torch.tensor(tests, device=dev), I1 - 1,
+                                 off, excl).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+
+
+def test_sampler_properties(ops, acf, dev):
+    ds = acf.synthetic_dataset(500, 300, 20000, seed=3)
+    s = acf.DeviceSampler(ds, 128, dev, seed=1)
+    ep = s.epoch(0)
+    n_out = (len(ds.pair_user) // 128) * 128
+    u, i, j = (t.cpu().numpy() for t in (ep.user, ep.item_pos, ep.item_neg))
+    assert len(u) == n_out
+    off, items = ds.sorted_lists()
+    # every negative in range and not in the user's list; positives are real pairs
+    assert j.min() >= 0 and j.max() < ds.num_items
+    for k in range(0, n_out, 37):
+        lst = items[off[u[k]]:off[u[k] + 1]]
+        assert j[k] not in lst and i[k] in lst
+    # a permutation of the positives (drop-last): no positive used twice
+    key = u.astype(np.int64) * ds.num_items + i
+    assert len(np.unique(key)) == n_out
+    # deterministic per (seed, epoch), different across epochs
+    ep2 = s.epoch(0)
+    assert torch.equal(ep.item_neg, ep2.item_neg)
+    assert not torch.equal(ep.user, s.epoch(1).user)
+    # uniformity of negatives (chi-square-ish): counts per item within 6 sigma
+    counts = np.bincount(j, minlength=ds.num_items)
+    allowed = ds.num_items - np.diff(off).mean()
+    exp = n_out / allowed
+    assert counts.max() < exp + 6 * np.sqrt(exp) + 10
+
+
+def test_dns_select(ops, dev):
+    rng = np.random.default_rng(2)
+    P = rng.standard_normal((10, 32)).astype(np.float32)
+    Q = rng.standard_normal((40, 32)).astype(np.float32)
+    u = rng.integers(0, 10, 64).astype(np.int32)
+    cand = rng.integers(0, 40, 64 * 5).astype(np.int32)
+    got = ops.dns_select(torch.tensor(P, device=dev), torch.tensor(Q, device=dev), torch.tensor(u, device=dev),
+                         torch.tensor(cand, device=dev), 5).cpu().numpy()
+    sc = np.einsum("nd,nkd->nk", P[u], Q[cand.reshape(64, 5)])
+    want = cand.reshape(64, 5)[np.arange(64), sc.argmax(1)]
+    np.testing.assert_array_equal(got, want)
+
+
+def test_out_of_range_index_raises(ops, dev):
+    from importlib import import_module
+    native = import_module("adversarial-collaborative-filtering_amd._native")
+    ctx = ops.APRContext(10, 10, 8, 4, 1, dev)
+    bad = torch.tensor([0, 1, 2, 10], dtype=torch.int32, device=dev)
+    ok = torch.tensor([0, 1, 2, 3], dtype=torch.int32, device=dev)
+    with pytest.raises(native.NativeIndexError):
+        ctx.plan(ok, bad, ok, 4)
+    with pytest.raises(native.NativeIndexError):
+        ctx.plan(bad, ok, ok, 4)
+    # a failed plan leaves the context unplanned
+    with pytest.raises(native.NativeError):
+        ctx.optimizer_step(_gpu_tables(np.zeros((10, 8), np.float32), np.zeros((10, 8), np.float32), dev),
+                           ops.StepHParams(), 0)
+
+
+def test_full_size_ml1m_epoch_deterministic(ops, acf, dev):
+    """ml-1m-shaped epoch (1,941 batches of 512, d=64): graph replay and eager
+    launches give the same bits; two runs give the same bits; everything finite."""
+    ds = acf.ml1m_like(seed=2019)
+    s = acf.DeviceSampler(ds, 512, dev, seed=0)
+    ep = s.epoch(0)
+    assert ep.n_batches == 1941
+    U1, I1, d = ds.num_users + 1, ds.num_items + 1, 64
+    g = torch.Generator().manual_seed(0)
+    P0 = torch.nn.init.trunc_normal_(torch.empty(U1, d), 0, 0.01, -0.02, 0.02, generator=g)
+    Q0 = torch.nn.init.trunc_normal_(torch.empty(I1, d), 0, 0.01, -0.02, 0.02, generator=g)
+    results = []
+    ctx = ops.APRContext(U1, I1, d, 512, 1941, dev)
+    ctx.plan(ep.user, ep.item_pos, ep.item_neg, 512)
+    for graph in (True, False, True):
+        tabs = [P0.to(dev), Q0.to(dev), torch.full((U1, d), 0.1, device=dev),
+                torch.full((I1, d), 0.1, device=dev)]
+        ctx.train_planned(tabs, ops.StepHParams(adver=1), graph=graph)
+        torch.cuda.synchronize()
+        results.append([t.clone() for t in tabs])
+    for a, b in zip(results[0], results[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(results[0], results[2]):
+        assert torch.equal(a, b)
+    P, Q, aP, aQ = results[0]
+    assert torch.isfinite(P).all() and torch.isfinite(Q).all()
+    assert float(aP.min()) >= 0.1 and float(aQ.min()) >= 0.1
+    # every touched row moved, untouched rows did not
+    moved = (P != P0.to(dev)).any(1).cpu().numpy()
+    touched = np.zeros(U1, bool)
+    touched[ep.user.cpu().numpy()] = True
+    assert np.array_equal(moved, touched)
