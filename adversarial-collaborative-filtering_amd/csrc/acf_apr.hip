@@ -10,15 +10,16 @@
 //   IndexedSlices (Optimizer, APR.py:195) and       (batch, row, occurrence) keys for a
 //   IndexedSlices->dense (APR.py:183-187)           whole epoch -> per-batch unique rows
 //                                                   + ordered occurrence records
-//   sess.run([update_P, update_Q]):                 k_clean: one row-group (d/4 lanes,
-//     gather, (p*q)h, clip, softplus, grads,        float4 per lane) per UNIQUE row; it
-//     dense l2_normalize * eps, full-table assign   sums its occurrences' clean-loss
-//                                                   gradient in occurrence order and
-//                                                   writes delta = eps*g/|g| for that row
-//   sess.run(optimizer):                            k_adv: same row-centric pass over
-//     clean + adversarial fwd/bwd, dedup,           p+dP, q+dQ; writes the row's total
-//     SparseApplyAdagrad                            gradient.  k_apply: Adagrad on the
-//                                                   unique rows, in place.
+//   sess.run([update_P, update_Q]):                 k_clean: one wavefront per UNIQUE
+//     gather, (p*q)h, clip, softplus, grads,        row; its lane-groups (d/4 lanes,
+//     dense l2_normalize * eps, full-table assign   float4 each) take the row's
+//                                                   occurrences in parallel, sum their
+//                                                   clean-loss gradients and write
+//                                                   delta = eps*g/|g| for that row
+//   sess.run(optimizer):                            k_adv: same pass over p+dP, q+dQ,
+//     clean + adversarial fwd/bwd, dedup,           total gradient, Adagrad; the new
+//     SparseApplyAdagrad                            row goes to scratch and is flushed
+//                                                   by the next batch's k_clean
 //
 // Row-centric aggregation keeps every sum in a fixed order (bitwise
 // reproducible, no float atomics).  Rows untouched by a batch have delta = 0 in
@@ -214,14 +215,6 @@ __device__ __forceinline__ float trunc_normal(uint64_t key, float stddev) {
 // ---------------------------------------------------------------------------
 // plan kernels
 // ---------------------------------------------------------------------------
-struct PlanBits {
-  uint32_t occ_bits;   // bits of the occurrence index
-  uint64_t occ_mask;
-};
-
-// Stage triplets, validate ranges, build sort keys.
-// user key  = ((t*U1 + u)      << ob_u) | x          (x = triplet index)
-// item key  = ((t*I1 + item)   << ob_i) | (2x + role) (role 0 = pos, 1 = neg)
 __global__ void k_stage(const int32_t* __restrict__ user, const int32_t* __restrict__ ipos,
                         const int32_t* __restrict__ ineg, int64_t E, int32_t B, int64_t U1,
                         int64_t I1, int32_t* __restrict__ tu, int32_t* __restrict__ ti,
@@ -282,112 +275,331 @@ __global__ void k_compact(const uint64_t* __restrict__ key, const int32_t* __res
   }
 }
 
-// Per-occurrence records so that step kernels reach partner rows in one hop.
-// user occurrence x (triplet e):  {i, j, slot(i), slot(j)}
-// item occurrence x (e, role):    {u, other item, slot(u), slot(other)}
+
+// For every unique row of batch t: where its current value lives when batch t
+// starts.  Rows updated by batch t-1 are still in that batch's W scratch (the
+// flush to the table happens inside batch t's first kernel), so the plan encodes
+// src = ~(local slot in batch t-1) for them and src = row otherwise.
+// user local slot = g - ubs[t]; item local slot = nU(t) + g - ibs[t].
+__global__ void k_prev_src(const int32_t* __restrict__ uniq, const int32_t* __restrict__ bofs,
+                           const int32_t* __restrict__ ubs, const int32_t* __restrict__ bstart,
+                           int32_t n_uniq, int32_t nb, int32_t item_side,
+                           int32_t* __restrict__ src) {
+  int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (g >= n_uniq) return;
+  // batch of g: last t with bstart[t] <= g
+  int lo = 0, hi = nb;  // answer in [0, nb)
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (bstart[mid] <= g) lo = mid; else hi = mid;
+  }
+  const int t = lo;
+  const int32_t row = uniq[g];
+  int32_t s = row;
+  if (t > 0) {
+    int a = bstart[t - 1], b = bstart[t];
+    while (a < b) {
+      int mid = (a + b) >> 1;
+      if (uniq[mid] < row) a = mid + 1; else b = mid;
+    }
+    if (a < bstart[t] && uniq[a] == row) {
+      const int nU_prev = ubs[t] - ubs[t - 1];
+      const int local = item_side ? nU_prev + (a - bstart[t - 1]) : (a - bstart[t - 1]);
+      s = ~local;
+    }
+  }
+  src[g] = s;
+  (void)bofs;
+}
+
+// Occurrence record: everything one lane-group needs to process one occurrence
+// of a unique row, so that a step kernel reaches the partner rows after ONE
+// dependent load.  Records are written in CSR order (all occurrences) and the
+// first R of each slot are also inlined at [batch][slot][r] so the kernel finds
+// them by address arithmetic alone.  `gen` tags the plan that wrote a record:
+// inlined records of an older plan read as absent.
+struct __align__(16) OccRec {
+  int32_t own_row;  // the unique row this slot updates
+  int32_t own_src;  // where its value lives at batch start (see k_prev_src)
+  int32_t meta;     // occurrence count | ITEM_BIT for item slots
+  int32_t ovf;      // CSR index of the slot's first occurrence
+  int32_t e_role;   // user slot: triplet e; item slot: 2e + role (0 pos, 1 neg)
+  int32_t pa_row;   // user slot: item i;  item slot: user u
+  int32_t pb_row;   // user slot: item j;  item slot: the other item of the triplet
+  int32_t pa_src;
+  int32_t pb_src;
+  int32_t pa_slot;  // local slot of pa in batch t (for its delta)
+  int32_t pb_slot;
+  int32_t gen;
+};
+#define ACF_ITEM_BIT (1 << 28)
+#define ACF_COUNT_MASK ((1 << 28) - 1)
+
 __global__ void k_records(const int32_t* __restrict__ uocc, const int32_t* __restrict__ iocc,
-                          int64_t E, const int32_t* __restrict__ tu,
-                          const int32_t* __restrict__ ti, const int32_t* __restrict__ tj,
-                          const int32_t* __restrict__ uslot, const int32_t* __restrict__ pslot,
-                          const int32_t* __restrict__ nslot, int4* __restrict__ urec,
-                          int4* __restrict__ irec) {
-  int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+                          int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen,
+                          const int32_t* __restrict__ tu, const int32_t* __restrict__ ti,
+                          const int32_t* __restrict__ tj, const int32_t* __restrict__ uslot,
+                          const int32_t* __restrict__ pslot, const int32_t* __restrict__ nslot,
+                          const int32_t* __restrict__ uuniq, const int32_t* __restrict__ uoff,
+                          const int32_t* __restrict__ ubs, const int32_t* __restrict__ usrc,
+                          const int32_t* __restrict__ iuniq, const int32_t* __restrict__ ioff,
+                          const int32_t* __restrict__ ibs, const int32_t* __restrict__ isrc,
+                          OccRec* __restrict__ urec, OccRec* __restrict__ irec,
+                          OccRec* __restrict__ inl, int32_t* __restrict__ gen_ptr) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x == 0) *gen_ptr = gen;
   if (x < E) {
-    int32_t e = uocc[x];
-    urec[x] = make_int4(ti[e], tj[e], pslot[e], nslot[e]);
+    const int32_t e = uocc[x];
+    const int32_t g = uslot[e];
+    const int32_t t = e / B;
+    const int32_t nU = ubs[t + 1] - ubs[t];
+    OccRec r;
+    r.own_row = uuniq[g];
+    r.own_src = usrc[g];
+    r.meta = uoff[g + 1] - uoff[g];
+    r.ovf = uoff[g];
+    r.e_role = e;
+    r.pa_row = ti[e];
+    r.pb_row = tj[e];
+    r.pa_src = isrc[pslot[e]];
+    r.pb_src = isrc[nslot[e]];
+    r.pa_slot = nU + (pslot[e] - ibs[t]);
+    r.pb_slot = nU + (nslot[e] - ibs[t]);
+    r.gen = gen;
+    urec[x] = r;
+    const int32_t k = g - ubs[t];
+    const int32_t rr = (int32_t)(x - uoff[g]);
+    if (rr < R) inl[((int64_t)t * S + k) * R + rr] = r;
   }
   if (x < 2 * E) {
-    int32_t v = iocc[x];
-    int32_t e = v >> 1;
-    if (v & 1)
-      irec[x] = make_int4(tu[e], ti[e], uslot[e], pslot[e]);
-    else
-      irec[x] = make_int4(tu[e], tj[e], uslot[e], nslot[e]);
+    const int32_t v = iocc[x];
+    const int32_t e = v >> 1, role = v & 1;
+    const int32_t g = role ? nslot[e] : pslot[e];
+    const int32_t og = role ? pslot[e] : nslot[e];
+    const int32_t t = e / B;
+    const int32_t nU = ubs[t + 1] - ubs[t];
+    OccRec r;
+    r.own_row = iuniq[g];
+    r.own_src = isrc[g];
+    r.meta = (ioff[g + 1] - ioff[g]) | ACF_ITEM_BIT;
+    r.ovf = ioff[g];
+    r.e_role = v;
+    r.pa_row = tu[e];
+    r.pb_row = role ? ti[e] : tj[e];
+    r.pa_src = usrc[uslot[e]];
+    r.pb_src = isrc[og];
+    r.pa_slot = uslot[e] - ubs[t];
+    r.pb_slot = nU + (og - ibs[t]);
+    r.gen = gen;
+    irec[x] = r;
+    const int32_t k = nU + (g - ibs[t]);
+    const int32_t rr = (int32_t)(x - ioff[g]);
+    if (rr < R) inl[((int64_t)t * S + k) * R + rr] = r;
   }
 }
 
 // ---------------------------------------------------------------------------
-// step kernels
+// step kernels: one wavefront per unique row ("slot") of the batch.  The 64
+// lanes form OPW = 64/LPR lane-groups; group g takes occurrences g, g+OPW, ...
+// of the slot, so the gathers of a popular row's occurrences are in flight
+// together; the groups' partial sums are then added by a fixed butterfly.
+//
+// Table updates never go to the tables inside the batch that computes them:
+// the Adagrad result of batch t goes to W scratch wnew[t%2][slot], and batch
+// t+1's first kernel (a) reads rows that batch t touched from there (the plan's
+// src encoding) and (b) flushes them to the tables.  So every kernel reads a
+// consistent snapshot without a grid barrier, and a batch costs 2 kernels (APR)
+// or 1 kernel (BPR).
 // ---------------------------------------------------------------------------
 struct StepArgs {
   float* P;
   float* Q;
   float* accP;
   float* accQ;
-  const int32_t* uuniq;
-  const int32_t* uoff;
-  const int32_t* ubs;
-  const int32_t* uocc;
-  const int4* urec;
-  const int32_t* iuniq;
-  const int32_t* ioff;
-  const int32_t* ibs;
-  const int32_t* iocc;
-  const int4* irec;
-  float* g0;      // [3B, d] clean-loss gradient per local slot
-  float* delta;   // [3B, d] delta per local slot
-  float* gsum;    // [3B, d] total gradient per local slot
-  float* loss_clean;  // [E]
-  float* loss_adv;    // [E]
-  int32_t d;
-  int32_t B;
-  int32_t t;
+  const OccRec* inl;   // [nb][S][R]
+  const OccRec* urec;  // CSR, user occurrences
+  const OccRec* irec;  // CSR, item occurrences
+  float* g0;           // [S, d] clean-loss gradient per slot
+  float* delta;        // [S, d] delta per slot
+  float* wnew_cur;     // [S, d] updated rows of batch t
+  float* wnew_prev;    // [S, d] updated rows of batch t-1 (read + flushed)
+  float* loss_clean;   // [E]
+  float* loss_adv;     // [E]
+  const int32_t* gen_ptr;  // plan generation (device: graphs stay valid across plans)
+  int32_t d, B, S, R, t;
+  int32_t prev_valid;  // 1: rows of batch t-1 are still pending in wnew_prev
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
 };
 
-// Phase 1 (= sess.run([update_P, update_Q]) and the clean half of the
-// optimizer): for every unique row of batch t, the clean-loss gradient summed
-// over its occurrences, and (adver) its delta.
+__device__ __forceinline__ OccRec load_rec(const OccRec* __restrict__ p) {
+  const int4* q = reinterpret_cast<const int4*>(p);
+  const int4 a = q[0], b = q[1], c = q[2];
+  OccRec r;
+  r.own_row = a.x; r.own_src = a.y; r.meta = a.z; r.ovf = a.w;
+  r.e_role = b.x; r.pa_row = b.y; r.pb_row = b.z; r.pa_src = b.w;
+  r.pb_src = c.x; r.pa_slot = c.y; r.pb_slot = c.z; r.gen = c.w;
+  return r;
+}
+
+// current value of a row at batch start: pending scratch or the table
+__device__ __forceinline__ const float* row_src(const StepArgs& a, const float* table, int32_t row,
+                                                int32_t src) {
+  return (src < 0 && a.prev_valid) ? a.wnew_prev + (int64_t)(~src) * a.d
+                                   : table + (int64_t)row * a.d;
+}
+
 template <int LPR, int NV>
-__global__ void __launch_bounds__(256) k_clean(StepArgs a) {
-  const int64_t gtid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int grp = (int)(gtid / LPR);
-  const int l = threadIdx.x & (LPR - 1);
-  const int ub0 = a.ubs[a.t], nU = a.ubs[a.t + 1] - ub0;
-  const int ib0 = a.ibs[a.t], nI = a.ibs[a.t + 1] - ib0;
-  if (grp >= nU + nI) return;
-  const int d = a.d;
-  RowV<NV> G = zero_row<NV>();
-  int64_t row;
-  bool is_user = grp < nU;
-  if (is_user) {
-    const int s = ub0 + grp;
-    row = a.uuniq[s];
-    const RowV<NV> p = load_row<LPR, NV>(a.P, row, d, l);
-    const int o1 = a.uoff[s + 1];
-    for (int o = a.uoff[s]; o < o1; ++o) {
-      const int4 r = a.urec[o];
-      const RowV<NV> qi = load_row<LPR, NV>(a.Q, r.x, d, l);
-      const RowV<NV> qj = load_row<LPR, NV>(a.Q, r.y, d, l);
-      const float x = dot_row<LPR, NV>(p, qi) - dot_row<LPR, NV>(p, qj);
-      float g, loss;
-      bpr_term(x, a.clip_lo, a.clip_hi, g, loss);
-      axpy_row(G, g, qi);   // pos branch: dx+/dp = qi
-      axpy_row(G, -g, qj);  // neg branch: dx-/dp = qj
-      if (l == 0) a.loss_clean[a.uocc[o]] = loss;
-    }
-  } else {
-    const int s = ib0 + (grp - nU);
-    row = a.iuniq[s];
-    const RowV<NV> q = load_row<LPR, NV>(a.Q, row, d, l);
-    const int o1 = a.ioff[s + 1];
-    for (int o = a.ioff[s]; o < o1; ++o) {
-      const int4 r = a.irec[o];
-      const int role = a.iocc[o] & 1;
-      const RowV<NV> p = load_row<LPR, NV>(a.P, r.x, d, l);
-      const RowV<NV> qo = load_row<LPR, NV>(a.Q, r.y, d, l);
-      const float dq = dot_row<LPR, NV>(p, q), dqo = dot_row<LPR, NV>(p, qo);
-      const float x = role ? (dqo - dq) : (dq - dqo);
-      float g, loss;
-      bpr_term(x, a.clip_lo, a.clip_hi, g, loss);
-      axpy_row(G, role ? -g : g, p);
+__device__ __forceinline__ RowV<NV> load_at(const float* __restrict__ p, int d, int l) {
+  return load_row<LPR, NV>(p, 0, d, l);
+}
+
+// butterfly over the lane-groups of a wave (fixed order -> deterministic)
+template <int LPR, int NV>
+__device__ __forceinline__ void group_allreduce(RowV<NV>& G) {
+#pragma unroll
+  for (int m = LPR; m < 64; m <<= 1) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      G.v[v].x += __shfl_xor(G.v[v].x, m, 64);
+      G.v[v].y += __shfl_xor(G.v[v].y, m, 64);
+      G.v[v].z += __shfl_xor(G.v[v].z, m, 64);
+      G.v[v].w += __shfl_xor(G.v[v].w, m, 64);
     }
   }
-  const int64_t slot = grp;
-  store_row<LPR, NV>(a.g0, slot, d, l, G);
-  if (!a.adver) return;
+}
+
+// Slot header from the group-0 inline record, broadcast to the wave.
+struct SlotHdr {
+  int32_t count, is_item, own_row, own_src, ovf;
+};
+
+template <int LPR>
+__device__ __forceinline__ SlotHdr slot_header(const StepArgs& a, int k, int g, OccRec& r0) {
+  const int OPW = 64 / LPR;
+  const int32_t gen = *a.gen_ptr;
+  r0.gen = -1;
+  if (g < a.R && g < OPW) r0 = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R + g);
+  if (r0.gen != gen) r0.gen = -1;
+  const int lane0 = 0;
+  const int32_t meta = __shfl(r0.gen != -1 ? r0.meta : 0, lane0, 64);
+  SlotHdr h;
+  h.count = meta & ACF_COUNT_MASK;
+  h.is_item = (meta & ACF_ITEM_BIT) != 0;
+  h.own_row = __shfl(r0.own_row, lane0, 64);
+  h.own_src = __shfl(r0.own_src, lane0, 64);
+  h.ovf = __shfl(r0.ovf, lane0, 64);
+  return h;
+}
+
+// record of occurrence idx of the slot (idx < count)
+__device__ __forceinline__ OccRec occ_rec(const StepArgs& a, const SlotHdr& h, int idx, int g,
+                                          const OccRec& r0) {
+  if (idx == g && g < a.R && r0.gen != -1) return r0;
+  return load_rec((h.is_item ? a.irec : a.urec) + h.ovf + idx);
+}
+
+// copy the pending rows of batch t-1 (wnew_prev) to the tables
+template <int LPR, int NV>
+__device__ void flush_slot(const StepArgs& a, int tb, const float* __restrict__ wsrc, int k) {
+  const int lane = threadIdx.x & 63;
+  const OccRec r = load_rec(a.inl + ((int64_t)tb * a.S + k) * a.R);
+  if (r.gen != *a.gen_ptr || (r.meta & ACF_COUNT_MASK) == 0) return;
+  float* dst = ((r.meta & ACF_ITEM_BIT) ? a.Q : a.P) + (int64_t)r.own_row * a.d;
+  const float* src = wsrc + (int64_t)k * a.d;
+  for (int c = lane; c * 4 < a.d; c += 64)
+    *reinterpret_cast<float4*>(dst + c * 4) = *reinterpret_cast<const float4*>(src + c * 4);
+}
+
+// Adagrad (TF SparseApplyAdagrad after the dedup) for one row held by a
+// lane-group, plus the reg*mean(w^2) terms of APR.py:153-154,164-165.
+template <int NV>
+__device__ __forceinline__ void adagrad_row(const StepArgs& a, RowV<NV>& G, const RowV<NV>& w,
+                                            RowV<NV>& acc, int m, RowV<NV>& wout) {
+  if (a.reg != 0.f) {
+    const float coef = (2.0f * a.reg / ((float)a.B * (float)a.d)) * (float)(a.adver ? 2 * m : m);
+    axpy_row(G, coef, w);
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    float4& c = acc.v[v];
+    const float4 g = G.v[v];
+    const float4 x = w.v[v];
+    c.x = c.x + g.x * g.x;
+    c.y = c.y + g.y * g.y;
+    c.z = c.z + g.z * g.z;
+    c.w = c.w + g.w * g.w;
+    wout.v[v].x = x.x - (a.lr * g.x) * (1.0f / sqrtf(c.x));
+    wout.v[v].y = x.y - (a.lr * g.y) * (1.0f / sqrtf(c.y));
+    wout.v[v].z = x.z - (a.lr * g.z) * (1.0f / sqrtf(c.z));
+    wout.v[v].w = x.w - (a.lr * g.w) * (1.0f / sqrtf(c.w));
+  }
+}
+
+// Phase 1 = sess.run([update_P, update_Q]) (APR.py:180-191) and the clean half
+// of the optimizer: clean-loss gradient of every unique row of batch t summed
+// over its occurrences, its delta (APR graph), or — BPR graph, FUSE_APPLY — the
+// Adagrad update straight away.  Waves [S, 2S) flush batch t-1's rows.
+template <int LPR, int NV, bool FUSE_APPLY>
+__global__ void __launch_bounds__(256) k_clean(StepArgs a) {
+  constexpr int OPW = 64 / LPR;
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR, l = lane & (LPR - 1);
+  if (wave >= a.S) {
+    if (a.prev_valid && wave < 2 * a.S) flush_slot<LPR, NV>(a, a.t - 1, a.wnew_prev, wave - a.S);
+    return;
+  }
+  const int k = wave;
+  OccRec r0;
+  const SlotHdr h = slot_header<LPR>(a, k, g, r0);
+  if (h.count == 0) return;
+  const int d = a.d;
+  const float* own_tab = h.is_item ? a.Q : a.P;
+  const RowV<NV> own = load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l);
+  RowV<NV> acc;
+  if (FUSE_APPLY && g == 0)
+    acc = load_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l);
+  RowV<NV> G = zero_row<NV>();
+  for (int base = 0; base < h.count; base += OPW) {
+    const int idx = base + g;
+    const bool active = idx < h.count;
+    RowV<NV> ra = zero_row<NV>(), rb = zero_row<NV>();
+    OccRec r;
+    if (active) {
+      r = occ_rec(a, h, idx, g, r0);
+      // user slot: ra = Q[i], rb = Q[j];  item slot: ra = P[u], rb = Q[other]
+      ra = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r.pa_row, r.pa_src), d, l);
+      rb = load_at<LPR, NV>(row_src(a, a.Q, r.pb_row, r.pb_src), d, l);
+    }
+    float gb, loss;
+    if (!h.is_item) {
+      const float x = dot_row<LPR, NV>(own, ra) - dot_row<LPR, NV>(own, rb);
+      bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
+      if (active) {
+        axpy_row(G, gb, ra);   // pos branch: dx+/dp = q_i
+        axpy_row(G, -gb, rb);  // neg branch: dx-/dp = q_j
+        if (l == 0) a.loss_clean[r.e_role] = loss;
+      }
+    } else {
+      const float dq = dot_row<LPR, NV>(ra, own), dqo = dot_row<LPR, NV>(ra, rb);
+      const int role = active ? (r.e_role & 1) : 0;
+      const float x = role ? (dqo - dq) : (dq - dqo);
+      bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
+      if (active) axpy_row(G, role ? -gb : gb, ra);
+    }
+  }
+  group_allreduce<LPR, NV>(G);
+  if (FUSE_APPLY) {
+    if (g == 0) {
+      RowV<NV> wout;
+      adagrad_row(a, G, own, acc, h.count, wout);
+      store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
+      store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+    }
+    return;
+  }
   RowV<NV> dl;
   if (a.zero_delta) {
     dl = zero_row<NV>();
@@ -399,148 +611,107 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
   } else {
     // "random": l2_normalize(truncated_normal(0, 0.01)) * eps, redrawn every run
     RowV<NV> z;
-    const uint64_t rk = mix64(a.seed ^ mix64(((uint64_t)a.t << 1) | (is_user ? 0 : 1))) ^
-                        mix64((uint64_t)row * 0x100000001B3ull);
+    const uint64_t rk = mix64(a.seed ^ mix64(((uint64_t)a.t << 1) | (h.is_item ? 1 : 0))) ^
+                        mix64((uint64_t)h.own_row * 0x100000001B3ull);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int c = l + LPR * v;
       float e4[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        e4[k] = (c * 4 + k < d) ? trunc_normal(rk ^ mix64((uint64_t)(c * 4 + k)), 0.01f) : 0.f;
+      for (int q = 0; q < 4; ++q)
+        e4[q] = (c * 4 + q < d) ? trunc_normal(rk ^ mix64((uint64_t)(c * 4 + q)), 0.01f) : 0.f;
       z.v[v] = make_float4(e4[0], e4[1], e4[2], e4[3]);
     }
     const float ss = dot_row<LPR, NV>(z, z);
     const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
     dl = scale_row(scale_row(z, inv), a.eps);
   }
-  store_row<LPR, NV>(a.delta, slot, d, l, dl);
+  if (g == 0) {
+    store_row<LPR, NV>(a.g0, k, d, l, G);
+    store_row<LPR, NV>(a.delta, k, d, l, dl);
+  }
 }
 
-// Phase 2 (adversarial half of sess.run(optimizer), APR.py:130-141,156-165):
-// loss on p+dP[u], q+dQ[i] with the deltas of phase 1; the row's total
-// gradient G = G_clean + reg_adv * G_adv.
+// Phase 2 = adversarial half of sess.run(optimizer) (APR.py:130-141,156-165)
+// and SparseApplyAdagrad: loss on p+dP[u], q+dQ[i]; G = G_clean + reg_adv*G_adv;
+// Adagrad into wnew_cur.  The tables are current (flushed by phase 1).
 template <int LPR, int NV>
 __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
-  const int64_t gtid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int grp = (int)(gtid / LPR);
-  const int l = threadIdx.x & (LPR - 1);
-  const int ub0 = a.ubs[a.t], nU = a.ubs[a.t + 1] - ub0;
-  const int ib0 = a.ibs[a.t], nI = a.ibs[a.t + 1] - ib0;
-  if (grp >= nU + nI) return;
+  constexpr int OPW = 64 / LPR;
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  const int g = lane / LPR, l = lane & (LPR - 1);
+  if (wave >= a.S) return;
+  const int k = wave;
+  OccRec r0;
+  const SlotHdr h = slot_header<LPR>(a, k, g, r0);
+  if (h.count == 0) return;
   const int d = a.d;
+  const RowV<NV> own = load_row<LPR, NV>(h.is_item ? a.Q : a.P, h.own_row, d, l);
+  const RowV<NV> ownp = add_row(own, load_row<LPR, NV>(a.delta, k, d, l));
+  RowV<NV> acc, G0;
+  if (g == 0) {
+    acc = load_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l);
+    G0 = load_row<LPR, NV>(a.g0, k, d, l);
+  }
   RowV<NV> G = zero_row<NV>();
-  if (grp < nU) {
-    const int s = ub0 + grp;
-    const int64_t row = a.uuniq[s];
-    const RowV<NV> pp = add_row(load_row<LPR, NV>(a.P, row, d, l),
-                                load_row<LPR, NV>(a.delta, grp, d, l));
-    const int o1 = a.uoff[s + 1];
-    for (int o = a.uoff[s]; o < o1; ++o) {
-      const int4 r = a.urec[o];
-      const RowV<NV> qi = add_row(load_row<LPR, NV>(a.Q, r.x, d, l),
-                                  load_row<LPR, NV>(a.delta, nU + (r.z - ib0), d, l));
-      const RowV<NV> qj = add_row(load_row<LPR, NV>(a.Q, r.y, d, l),
-                                  load_row<LPR, NV>(a.delta, nU + (r.w - ib0), d, l));
-      const float x = dot_row<LPR, NV>(pp, qi) - dot_row<LPR, NV>(pp, qj);
-      float g, loss;
-      bpr_term(x, a.clip_lo, a.clip_hi, g, loss);
-      axpy_row(G, g, qi);
-      axpy_row(G, -g, qj);
-      if (l == 0) a.loss_adv[a.uocc[o]] = loss;
+  for (int base = 0; base < h.count; base += OPW) {
+    const int idx = base + g;
+    const bool active = idx < h.count;
+    RowV<NV> ra = zero_row<NV>(), rb = zero_row<NV>();
+    OccRec r;
+    if (active) {
+      r = occ_rec(a, h, idx, g, r0);
+      ra = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r.pa_row, d, l),
+                   load_row<LPR, NV>(a.delta, r.pa_slot, d, l));
+      rb = add_row(load_row<LPR, NV>(a.Q, r.pb_row, d, l),
+                   load_row<LPR, NV>(a.delta, r.pb_slot, d, l));
     }
-  } else {
-    const int k = grp - nU;
-    const int s = ib0 + k;
-    const int64_t row = a.iuniq[s];
-    const RowV<NV> qq = add_row(load_row<LPR, NV>(a.Q, row, d, l),
-                                load_row<LPR, NV>(a.delta, grp, d, l));
-    const int o1 = a.ioff[s + 1];
-    for (int o = a.ioff[s]; o < o1; ++o) {
-      const int4 r = a.irec[o];
-      const int role = a.iocc[o] & 1;
-      const RowV<NV> pp = add_row(load_row<LPR, NV>(a.P, r.x, d, l),
-                                  load_row<LPR, NV>(a.delta, r.z - ub0, d, l));
-      const RowV<NV> qo = add_row(load_row<LPR, NV>(a.Q, r.y, d, l),
-                                  load_row<LPR, NV>(a.delta, nU + (r.w - ib0), d, l));
-      const float dq = dot_row<LPR, NV>(pp, qq), dqo = dot_row<LPR, NV>(pp, qo);
+    float gb, loss;
+    if (!h.is_item) {
+      const float x = dot_row<LPR, NV>(ownp, ra) - dot_row<LPR, NV>(ownp, rb);
+      bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
+      if (active) {
+        axpy_row(G, gb, ra);
+        axpy_row(G, -gb, rb);
+        if (l == 0) a.loss_adv[r.e_role] = loss;
+      }
+    } else {
+      const float dq = dot_row<LPR, NV>(ra, ownp), dqo = dot_row<LPR, NV>(ra, rb);
+      const int role = active ? (r.e_role & 1) : 0;
       const float x = role ? (dqo - dq) : (dq - dqo);
-      float g, loss;
-      bpr_term(x, a.clip_lo, a.clip_hi, g, loss);
-      axpy_row(G, role ? -g : g, pp);
+      bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
+      if (active) axpy_row(G, role ? -gb : gb, ra);
     }
   }
-  RowV<NV> G0 = load_row<LPR, NV>(a.g0, grp, d, l);
-  axpy_row(G0, a.reg_adv, G);
-  store_row<LPR, NV>(a.gsum, grp, d, l, G0);
+  group_allreduce<LPR, NV>(G);
+  if (g == 0) {
+    axpy_row(G0, a.reg_adv, G);
+    RowV<NV> wout;
+    adagrad_row(a, G0, own, acc, h.count, wout);
+    store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
+    store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+  }
 }
 
-// Sparse Adagrad on the unique rows (TF SparseApplyAdagrad after the dedup):
-//   acc += g*g;  w -= lr * g * rsqrt(acc)
-// plus the reg * mean(w^2) terms of APR.py:153-154,164-165 (2*reg*w/(B*d) per
-// occurrence, counted twice in the APR graph).
-__global__ void __launch_bounds__(256) k_apply(StepArgs a) {
-  const int64_t gtid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int d4 = a.d >> 2;
-  const int slot = (int)(gtid / d4);
-  const int c = (int)(gtid - (int64_t)slot * d4);
-  const int ub0 = a.ubs[a.t], nU = a.ubs[a.t + 1] - ub0;
-  const int ib0 = a.ibs[a.t], nI = a.ibs[a.t + 1] - ib0;
-  if (slot >= nU + nI) return;
-  float* W;
-  float* A;
-  int64_t row;
-  int m;
-  if (slot < nU) {
-    const int s = ub0 + slot;
-    row = a.uuniq[s];
-    m = a.uoff[s + 1] - a.uoff[s];
-    W = a.P;
-    A = a.accP;
-  } else {
-    const int s = ib0 + (slot - nU);
-    row = a.iuniq[s];
-    m = a.ioff[s + 1] - a.ioff[s];
-    W = a.Q;
-    A = a.accQ;
-  }
-  const float* Gsrc = a.adver ? a.gsum : a.g0;
-  float4 g = *reinterpret_cast<const float4*>(Gsrc + (int64_t)slot * a.d + c * 4);
-  float4* wp = reinterpret_cast<float4*>(W + row * a.d + c * 4);
-  float4* ap = reinterpret_cast<float4*>(A + row * a.d + c * 4);
-  float4 w = *wp, acc = *ap;
-  if (a.reg != 0.f) {
-    const float coef = (2.0f * a.reg / ((float)a.B * (float)a.d)) * (float)(a.adver ? 2 * m : m);
-    g.x = g.x + coef * w.x;
-    g.y = g.y + coef * w.y;
-    g.z = g.z + coef * w.z;
-    g.w = g.w + coef * w.w;
-  }
-  acc.x = acc.x + g.x * g.x;
-  acc.y = acc.y + g.y * g.y;
-  acc.z = acc.z + g.z * g.z;
-  acc.w = acc.w + g.w * g.w;
-  w.x -= (a.lr * g.x) * (1.0f / sqrtf(acc.x));
-  w.y -= (a.lr * g.y) * (1.0f / sqrtf(acc.y));
-  w.z -= (a.lr * g.z) * (1.0f / sqrtf(acc.z));
-  w.w -= (a.lr * g.w) * (1.0f / sqrtf(acc.w));
-  *ap = acc;
-  *wp = w;
+// Flush the pending rows of batch t (wnew_cur) to the tables (end of a call).
+template <int LPR, int NV>
+__global__ void __launch_bounds__(256) k_flush(StepArgs a) {
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  if (wave >= a.S) return;
+  flush_slot<LPR, NV>(a, a.t, a.wnew_cur, wave);
 }
 
 __global__ void k_delta_scatter(StepArgs a, float* __restrict__ dP, float* __restrict__ dQ) {
-  const int64_t gtid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int d4 = a.d >> 2;
-  const int slot = (int)(gtid / d4);
-  const int c = (int)(gtid - (int64_t)slot * d4);
-  const int ub0 = a.ubs[a.t], nU = a.ubs[a.t + 1] - ub0;
-  const int ib0 = a.ibs[a.t], nI = a.ibs[a.t + 1] - ib0;
-  if (slot >= nU + nI) return;
-  const float4 v = *reinterpret_cast<const float4*>(a.delta + (int64_t)slot * a.d + c * 4);
-  if (slot < nU)
-    *reinterpret_cast<float4*>(dP + (int64_t)a.uuniq[ub0 + slot] * a.d + c * 4) = v;
-  else
-    *reinterpret_cast<float4*>(dQ + (int64_t)a.iuniq[ib0 + slot - nU] * a.d + c * 4) = v;
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wave >= a.S) return;
+  const OccRec r = load_rec(a.inl + ((int64_t)a.t * a.S + wave) * a.R);
+  if (r.gen != *a.gen_ptr || (r.meta & ACF_COUNT_MASK) == 0) return;
+  float* dst = ((r.meta & ACF_ITEM_BIT) ? dQ : dP) + (int64_t)r.own_row * a.d;
+  const float* src = a.delta + (int64_t)wave * a.d;
+  for (int c = lane; c * 4 < a.d; c += 64)
+    *reinterpret_cast<float4*>(dst + c * 4) = *reinterpret_cast<const float4*>(src + c * 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -798,7 +969,7 @@ struct GraphKey {
 
 struct acf_apr_ctx {
   int64_t U1 = 0, I1 = 0;
-  int32_t d = 0, maxB = 0, maxNB = 0;
+  int32_t d = 0, maxB = 0, maxNB = 0, lpr = 0, nv = 0, R = 0;
   int64_t maxE = 0;
   // staged triplets
   int32_t *tu = nullptr, *ti = nullptr, *tj = nullptr;
@@ -807,16 +978,16 @@ struct acf_apr_ctx {
   int32_t *flag = nullptr, *inc = nullptr;
   int32_t *uuniq = nullptr, *uoff = nullptr, *ubs = nullptr, *uocc = nullptr, *uslot = nullptr;
   int32_t *iuniq = nullptr, *ioff = nullptr, *ibs = nullptr, *iocc = nullptr;
-  int32_t *pslot = nullptr, *nslot = nullptr;
-  int4 *urec = nullptr, *irec = nullptr;
-  int32_t* err = nullptr;
+  int32_t *pslot = nullptr, *nslot = nullptr, *usrc = nullptr, *isrc = nullptr;
+  OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr;
+  int32_t *err = nullptr, *gen_dev = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   // per-batch scratch
-  float *g0 = nullptr, *delta = nullptr, *gsum = nullptr;
+  float *g0 = nullptr, *delta = nullptr, *wnew[2] = {nullptr, nullptr};
   float *loss_clean = nullptr, *loss_adv = nullptr;
   // state
-  int32_t B = 0, nb = 0;
+  int32_t B = 0, nb = 0, gen = 0;
   int32_t last_delta_batch = -1;
   hipStream_t cap_stream = nullptr;
   std::map<GraphKey, hipGraphExec_t> graphs;
@@ -909,7 +1080,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
             "table rows must be in [1, 2^31): got %lld, %lld", (long long)U1, (long long)I1);
   ACF_CHECK(maxB > 0 && maxNB > 0, ACF_E_INVALID, "max_batch_size and max_batches must be > 0");
   int64_t maxE = (int64_t)maxB * maxNB;
-  ACF_CHECK(2 * maxE < (1ll << 31), ACF_E_INVALID, "plan too large: %lld triplets", (long long)maxE);
+  ACF_CHECK(2 * maxE < (1ll << 30), ACF_E_INVALID, "plan too large: %lld triplets", (long long)maxE);
   uint32_t ob_i = bits_for((uint64_t)(2 * maxE));
   uint32_t sb_i = bits_for((uint64_t)maxNB * (uint64_t)I1);
   uint32_t sb_u = bits_for((uint64_t)maxNB * (uint64_t)U1);
@@ -917,6 +1088,9 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
             "plan key does not fit 64 bits (rows x batches x batch too large)");
   acf_apr_ctx* c = new acf_apr_ctx();
   c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB; c->maxNB = maxNB; c->maxE = maxE;
+  geometry(d, &c->lpr, &c->nv);
+  c->R = std::min(64 / c->lpr, 4);
+  const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
   auto A = [&](auto** p, size_t n) { if (r == ACF_OK) r = dalloc(c, p, n); };
   A(&c->tu, maxE); A(&c->ti, maxE); A(&c->tj, maxE);
@@ -924,13 +1098,14 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->ikey_in, 2 * maxE); A(&c->ikey_out, 2 * maxE);
   A(&c->flag, 2 * maxE); A(&c->inc, 2 * maxE);
   A(&c->uuniq, maxE); A(&c->uoff, maxE + 1); A(&c->ubs, maxNB + 1); A(&c->uocc, maxE);
-  A(&c->uslot, maxE);
+  A(&c->uslot, maxE); A(&c->usrc, maxE);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1); A(&c->iocc, 2 * maxE);
-  A(&c->pslot, maxE); A(&c->nslot, maxE);
+  A(&c->pslot, maxE); A(&c->nslot, maxE); A(&c->isrc, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE);
-  A(&c->err, 4);
-  A(&c->g0, (size_t)3 * maxB * d); A(&c->delta, (size_t)3 * maxB * d);
-  A(&c->gsum, (size_t)3 * maxB * d);
+  A(&c->inl, (size_t)maxNB * S * c->R);
+  A(&c->err, 4); A(&c->gen_dev, 4);
+  A(&c->g0, S * d); A(&c->delta, S * d);
+  A(&c->wnew[0], S * d); A(&c->wnew[1], S * d);
   A(&c->loss_clean, maxE); A(&c->loss_adv, maxE);
   if (r != ACF_OK) { acf_apr_destroy(c); return r; }
   size_t b1 = 0, b2 = 0, b3 = 0;
@@ -950,7 +1125,10 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipStreamCreate failed");
   }
-  if (hipMemset(c->err, 0, 16) != hipSuccess) {
+  // generation 0 never matches a plan: zeroed inline records read as absent
+  if (hipMemset(c->inl, 0, (size_t)maxNB * S * c->R * sizeof(OccRec)) != hipSuccess ||
+      hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->gen_dev, 0, 16) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipMemset failed");
   }
@@ -974,6 +1152,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->B = 0;
   c->nb = 0;
   c->last_delta_batch = -1;
+  const int32_t gen = ++c->gen;
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
   k_stage<<<grid_for(E), 256, 0, s>>>(user, ipos, ineg, E, B, c->U1, c->I1, c->tu, c->ti, c->tj,
                                       c->ukey_in, c->ikey_in, ob_u, ob_i, c->err);
@@ -994,8 +1173,14 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   HIP_TRY(rocprim::inclusive_scan(c->tmp, tb, c->flag, c->inc, (size_t)(2 * E), rocprim::plus<int32_t>(), s));
   k_compact<<<grid_for(2 * E), 256, 0, s>>>(c->ikey_out, c->inc, 2 * E, ob_i, (1ull << ob_i) - 1, c->I1,
                                             nb, c->iuniq, c->ioff, c->ibs, c->iocc, c->pslot, c->nslot, 1);
-  k_records<<<grid_for(2 * E), 256, 0, s>>>(c->uocc, c->iocc, E, c->tu, c->ti, c->tj, c->uslot,
-                                            c->pslot, c->nslot, c->urec, c->irec);
+  // where each unique row's value lives at batch start, then the records
+  k_prev_src<<<grid_for(E), 256, 0, s>>>(c->uuniq, nullptr, c->ubs, c->ubs, (int32_t)E, nb, 0, c->usrc);
+  k_prev_src<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, nullptr, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
+                                              c->isrc);
+  k_records<<<grid_for(2 * E), 256, 0, s>>>(c->uocc, c->iocc, E, B, 3 * B, c->R, gen, c->tu, c->ti, c->tj,
+                                            c->uslot, c->pslot, c->nslot, c->uuniq, c->uoff, c->ubs,
+                                            c->usrc, c->iuniq, c->ioff, c->ibs, c->isrc, c->urec,
+                                            c->irec, c->inl, c->gen_dev);
   HIP_TRY(hipGetLastError());
   if (check) {
     int32_t herr = 0;
@@ -1011,33 +1196,52 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
 }
 
 static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
-                          int32_t t) {
+                          int32_t t, int32_t prev_valid) {
   StepArgs a;
   a.P = tb->P; a.Q = tb->Q; a.accP = tb->accP; a.accQ = tb->accQ;
-  a.uuniq = c->uuniq; a.uoff = c->uoff; a.ubs = c->ubs; a.uocc = c->uocc; a.urec = c->urec;
-  a.iuniq = c->iuniq; a.ioff = c->ioff; a.ibs = c->ibs; a.iocc = c->iocc; a.irec = c->irec;
-  a.g0 = c->g0; a.delta = c->delta; a.gsum = c->gsum;
+  a.inl = c->inl; a.urec = c->urec; a.irec = c->irec;
+  a.g0 = c->g0; a.delta = c->delta;
+  a.wnew_cur = c->wnew[t & 1];
+  a.wnew_prev = c->wnew[(t + 1) & 1];
   a.loss_clean = c->loss_clean; a.loss_adv = c->loss_adv;
-  a.d = c->d; a.B = c->B; a.t = t;
+  a.gen_ptr = c->gen_dev;
+  a.d = c->d; a.B = c->B; a.S = 3 * c->B; a.R = c->R; a.t = t;
+  a.prev_valid = prev_valid;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
   return a;
 }
 
+// kernel kinds for timing: 0 = phase-1 (clean, or fused BPR), 1 = adversarial, 2 = flush
 template <int LPR, int NV>
-static void launch_clean(const StepArgs& a, hipStream_t s) {
-  const int64_t threads = (int64_t)3 * a.B * LPR;
-  k_clean<LPR, NV><<<grid_for(threads), 256, 0, s>>>(a);
+static void kernel_ptrs(void** k0_apr, void** k0_bpr, void** k1, void** k2) {
+  *k0_apr = reinterpret_cast<void*>(&k_clean<LPR, NV, false>);
+  *k0_bpr = reinterpret_cast<void*>(&k_clean<LPR, NV, true>);
+  *k1 = reinterpret_cast<void*>(&k_adv<LPR, NV>);
+  *k2 = reinterpret_cast<void*>(&k_flush<LPR, NV>);
 }
-template <int LPR, int NV>
-static void launch_adv(const StepArgs& a, hipStream_t s) {
-  const int64_t threads = (int64_t)3 * a.B * LPR;
-  k_adv<LPR, NV><<<grid_for(threads), 256, 0, s>>>(a);
+
+struct Kernels {
+  void *clean_apr = nullptr, *clean_bpr = nullptr, *adv = nullptr, *flush = nullptr;
+};
+
+static int get_kernels(int d, Kernels* k) {
+  return DISPATCH_GEOM(d, kernel_ptrs, &k->clean_apr, &k->clean_bpr, &k->adv, &k->flush);
 }
-static void launch_apply(const StepArgs& a, hipStream_t s) {
-  const int64_t threads = (int64_t)3 * a.B * (a.d / 4);
-  k_apply<<<grid_for(threads), 256, 0, s>>>(a);
+
+typedef void (*StepKernel)(StepArgs);
+
+// Launch one step kernel; with events (timing mode) via hipExtLaunchKernelGGL.
+static int launch(void* fn, const StepArgs& a, int waves, hipStream_t s, hipEvent_t e0 = nullptr,
+                  hipEvent_t e1 = nullptr) {
+  const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+  if (e0)
+    hipExtLaunchKernelGGL(reinterpret_cast<StepKernel>(fn), grid, block, 0, s, e0, e1, 0, a);
+  else
+    hipLaunchKernelGGL(reinterpret_cast<StepKernel>(fn), grid, block, 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return ACF_OK;
 }
 
 static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
@@ -1049,12 +1253,32 @@ static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hp
   return ACF_OK;
 }
 
-// one batch: [clean] [adv] apply, eagerly on stream s
-static int run_batch(acf_apr_ctx* c, const StepArgs& a, bool need_clean, hipStream_t s) {
-  if (need_clean) ACF_RET(DISPATCH_GEOM(c->d, launch_clean, a, s));
-  if (a.adver) ACF_RET(DISPATCH_GEOM(c->d, launch_adv, a, s));
-  launch_apply(a, s);
-  HIP_TRY(hipGetLastError());
+// training_batch over planned batches [first, first+n): per batch phase 1
+// (+ flush of the previous batch) and, for APR, phase 2; a final flush.
+// events != nullptr: timing mode, 2 events per launch, kinds[] per launch.
+static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
+                    int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds) {
+  Kernels K;
+  ACF_RET(get_kernels(c->d, &K));
+  const int S = 3 * c->B;
+  int li = 0;
+  auto L = [&](void* fn, const StepArgs& a, int waves, int kind) -> int {
+    hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
+    if (kinds) kinds[li] = kind;
+    ++li;
+    return launch(fn, a, waves, s, e0, e1);
+  };
+  for (int32_t t = first; t < first + n; ++t) {
+    const int pv = t > first ? 1 : 0;
+    const StepArgs a = make_args(c, tb, hp, t, pv);
+    if (hp->adver) {
+      ACF_RET(L(K.clean_apr, a, pv ? 2 * S : S, 0));
+      ACF_RET(L(K.adv, a, S, 1));
+    } else {
+      ACF_RET(L(K.clean_bpr, a, pv ? 2 * S : S, 0));
+    }
+  }
+  ACF_RET(L(K.flush, make_args(c, tb, hp, first + n - 1, 0), S, 2));
   return ACF_OK;
 }
 
@@ -1063,9 +1287,9 @@ extern "C" int acf_apr_delta_update(acf_apr_ctx* c, const acf_apr_tables* tb,
   ACF_RET(check_step(c, tb, hp, t));
   ACF_CHECK(hp->adver, ACF_E_INVALID, "delta_update needs hparams.adver = 1 (APR graph)");
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  StepArgs a = make_args(c, tb, hp, t);
-  ACF_RET(DISPATCH_GEOM(c->d, launch_clean, a, s));
-  HIP_TRY(hipGetLastError());
+  Kernels K;
+  ACF_RET(get_kernels(c->d, &K));
+  ACF_RET(launch(K.clean_apr, make_args(c, tb, hp, t, 0), 3 * c->B, s));
   c->last_delta_batch = t;
   return ACF_OK;
 }
@@ -1074,15 +1298,17 @@ extern "C" int acf_apr_optimizer_step(acf_apr_ctx* c, const acf_apr_tables* tb,
                                       const acf_apr_hparams* hp, int32_t t, void* stream_) {
   ACF_RET(check_step(c, tb, hp, t));
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  StepArgs a = make_args(c, tb, hp, t);
-  bool need_clean = true;
+  Kernels K;
+  ACF_RET(get_kernels(c->d, &K));
+  const StepArgs a = make_args(c, tb, hp, t, 0);
   if (hp->adver) {
     ACF_CHECK(c->last_delta_batch == t, ACF_E_STATE,
               "APR optimizer step on batch %d needs acf_apr_delta_update on the same batch first", t);
-    need_clean = false;
+    ACF_RET(launch(K.adv, a, 3 * c->B, s));
+  } else {
+    ACF_RET(launch(K.clean_bpr, a, 3 * c->B, s));
   }
-  ACF_RET(run_batch(c, a, need_clean, s));
-  c->last_delta_batch = -1;
+  ACF_RET(launch(K.flush, a, 3 * c->B, s));
   return ACF_OK;
 }
 
@@ -1094,11 +1320,8 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
             "batch range [%d, %d) outside planned range [0, %d)", first, first + n, c->nb);
   ACF_RET(check_step(c, tb, hp, first));
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  if (!graph_mode) {
-    for (int32_t t = first; t < first + n; ++t) ACF_RET(run_batch(c, make_args(c, tb, hp, t), true, s));
-    c->last_delta_batch = -1;
-    return ACF_OK;
-  }
+  c->last_delta_batch = -1;
+  if (!graph_mode) return run_loop(c, tb, hp, first, n, s, nullptr, nullptr);
   GraphKey key;
   memset(&key, 0, sizeof(key));
   key.ptrs[0] = tb->P; key.ptrs[1] = tb->Q; key.ptrs[2] = tb->accP; key.ptrs[3] = tb->accQ;
@@ -1108,9 +1331,7 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
     HIP_TRY(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
-    int r = ACF_OK;
-    for (int32_t t = first; t < first + n && r == ACF_OK; ++t)
-      r = run_batch(c, make_args(c, tb, hp, t), true, c->cap_stream);
+    int r = run_loop(c, tb, hp, first, n, c->cap_stream, nullptr, nullptr);
     hipError_t ec = hipStreamEndCapture(c->cap_stream, &g);
     if (r != ACF_OK) { if (g) (void)hipGraphDestroy(g); return r; }
     if (ec != hipSuccess) return set_error(ACF_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
@@ -1125,15 +1346,7 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
     it = c->graphs.emplace(key, ex).first;
   }
   HIP_TRY(hipGraphLaunch(it->second, s));
-  c->last_delta_batch = -1;
   return ACF_OK;
-}
-
-// kernel pointer per geometry, so hipExtLaunchKernelGGL can bracket it with events
-template <int LPR, int NV>
-static void pick_kernels(void** clean, void** adv) {
-  *clean = reinterpret_cast<void*>(&k_clean<LPR, NV>);
-  *adv = reinterpret_cast<void*>(&k_adv<LPR, NV>);
 }
 
 extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
@@ -1144,40 +1357,26 @@ extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
             "batch range [%d, %d) outside planned range [0, %d)", first, first + n, c->nb);
   ACF_RET(check_step(c, tb, hp, first));
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  void *kc = nullptr, *ka = nullptr;
-  int lpr = 0, nv = 0;
-  geometry(c->d, &lpr, &nv);
-  ACF_RET(DISPATCH_GEOM(c->d, pick_kernels, &kc, &ka));
-  const int kinds = 3;
-  std::vector<hipEvent_t> ev((size_t)2 * kinds * n, nullptr);
+  const int nl = 2 * n + 1;
+  std::vector<hipEvent_t> ev((size_t)2 * nl, nullptr);
+  std::vector<int> kinds(nl, -1);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
-  for (int k = 0; k < kinds; ++k) { ms_out[k] = 0.0; launches_out[k] = 0; }
-  for (int32_t t = first; t < first + n; ++t) {
-    StepArgs a = make_args(c, tb, hp, t);
-    const size_t base = (size_t)2 * kinds * (t - first);
-    const dim3 gr((unsigned)grid_for((int64_t)3 * a.B * lpr)), bl(256);
-    hipExtLaunchKernelGGL(reinterpret_cast<void (*)(StepArgs)>(kc), gr, bl, 0, s, ev[base + 0],
-                          ev[base + 1], 0, a);
-    if (a.adver)
-      hipExtLaunchKernelGGL(reinterpret_cast<void (*)(StepArgs)>(ka), gr, bl, 0, s, ev[base + 2],
-                            ev[base + 3], 0, a);
-    hipExtLaunchKernelGGL(k_apply, dim3(grid_for((int64_t)3 * a.B * (a.d / 4))), bl, 0, s,
-                          ev[base + 4], ev[base + 5], 0, a);
-    HIP_TRY(hipGetLastError());
-  }
-  HIP_TRY(hipStreamSynchronize(s));
-  for (int32_t t = 0; t < n; ++t)
-    for (int k = 0; k < kinds; ++k) {
-      if (k == 1 && !hp->adver) continue;
-      float ms = 0.f;
-      const size_t base = (size_t)2 * kinds * t + 2 * k;
-      HIP_TRY(hipEventElapsedTime(&ms, ev[base], ev[base + 1]));
-      ms_out[k] += ms;
-      launches_out[k] += 1;
+  int r = run_loop(c, tb, hp, first, n, s, ev.data(), kinds.data());
+  if (r == ACF_OK && hipStreamSynchronize(s) != hipSuccess) r = set_error(ACF_E_HIP, "sync failed");
+  for (int k = 0; k < 3; ++k) { ms_out[k] = 0.0; launches_out[k] = 0; }
+  for (int x = 0; r == ACF_OK && x < nl; ++x) {
+    if (kinds[x] < 0) continue;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev[2 * x], ev[2 * x + 1]) != hipSuccess) {
+      r = set_error(ACF_E_HIP, "hipEventElapsedTime failed");
+      break;
     }
+    ms_out[kinds[x]] += ms;
+    launches_out[kinds[x]] += 1;
+  }
   for (auto& e : ev) (void)hipEventDestroy(e);
   c->last_delta_batch = -1;
-  return ACF_OK;
+  return r;
 }
 
 extern "C" int acf_apr_copy_losses(acf_apr_ctx* c, float* lc, float* la, void* stream_) {
@@ -1197,8 +1396,8 @@ extern "C" int acf_apr_delta_scatter(acf_apr_ctx* c, float* dP, float* dQ, void*
   acf_apr_tables tb{nullptr, nullptr, nullptr, nullptr};
   acf_apr_hparams hp;
   memset(&hp, 0, sizeof(hp));
-  StepArgs a = make_args(c, &tb, &hp, c->last_delta_batch);
-  k_delta_scatter<<<grid_for((int64_t)3 * c->B * (c->d / 4)), 256, 0, s>>>(a, dP, dQ);
+  StepArgs a = make_args(c, &tb, &hp, c->last_delta_batch, 0);
+  k_delta_scatter<<<(3 * c->B + 3) / 4, 256, 0, s>>>(a, dP, dQ);
   HIP_TRY(hipGetLastError());
   return ACF_OK;
 }

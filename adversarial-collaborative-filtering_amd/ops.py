@@ -150,7 +150,8 @@ class APRContext:
     def time_kernels(self, tables, hp: StepHParams, first: int = 0, n: int | None = None):
         """Per-kernel-kind device time (ms) and launch counts over planned batches,
         measured with start/stop events attached to each launch (tables are
-        trained exactly as by train_planned).  Kinds: clean, adv, apply."""
+        trained exactly as by train_planned).  Kinds: clean (phase 1, or the fused
+        BPR step), adv (phase 2 + Adagrad), flush (end-of-call write-back)."""
         n = self.n_batches - first if n is None else n
         tb, h = self._tables(*tables), hp.to_c()
         ms = (ctypes.c_double * 3)()
@@ -158,7 +159,7 @@ class APRContext:
         with torch.cuda.device(self.device):
             call("acf_apr_time_kernels", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
                  _stream_ptr(self.device))
-        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "apply"))}
+        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush"))}
 
     def losses(self):
         """Per-triplet (clean, adversarial) softplus terms of the last steps."""

@@ -62,8 +62,8 @@ def bytes_per_unit(kind: int, d: int) -> int:
     """Algorithmic HBM bytes per unit:
     clean: per triplet, P[u], Q[i], Q[j] + 3 int32 indices;
     adv:   per triplet, P[u], Q[i], Q[j], dP[u], dQ[i], dQ[j] + 3 indices (SURVEY §8(d));
-    apply: per unique row, read w, acc, g + write w, acc."""
-    return {0: 3 * d * 4 + 12, 1: 6 * d * 4 + 12, 2: 5 * d * 4}[kind]
+    flush: per unique row, read the scratch row + write the table row."""
+    return {0: 3 * d * 4 + 12, 1: 6 * d * 4 + 12, 2: 2 * d * 4}[kind]
 
 
 def make_triplets(acf, ds, B, n_batches, dev, seed):
@@ -106,7 +106,7 @@ def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb):
     s = slice(0, nb * B)
     ctx.plan(u[s], i[s], j[s], B, check=False)
     t = ctx.time_kernels(tabs, hp, 0, nb)
-    kinds = ["clean", "adv", "apply"]
+    kinds = ["clean", "adv", "flush"]
     tot = {k: t[k][0] for k in kinds}
     dom = max(kinds, key=lambda k: tot[k])
     kid = kinds.index(dom)
