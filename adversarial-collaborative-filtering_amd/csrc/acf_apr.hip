@@ -157,8 +157,29 @@ __device__ __forceinline__ RowV<NV> scale_row(const RowV<NV>& a, float s) {
   return r;
 }
 
-// Row dot product (p*q)·h of APR.py:127: per-lane partial sums, then a butterfly
-// over the row-group.  Every lane of the group ends with the same bits.
+// DPP lane exchange inside a 16-lane row (v_add_f32_dpp, no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the LPR lanes of a row-group.  xor1 / xor2 (quad_perm), then the
+// half-row and row mirrors (lane i <-> 7-i, 15-i): after each step the lanes of
+// the merged block hold identical bits, so pairing by mirror equals pairing by
+// xor.  Beyond 16 lanes, __shfl_xor.  Every lane ends with the same bits.
+template <int LPR>
+__device__ __forceinline__ float group_sum(float s) {
+  if (LPR >= 2) s += dpp<0xB1>(s);   // quad_perm [1,0,3,2]
+  if (LPR >= 4) s += dpp<0x4E>(s);   // quad_perm [2,3,0,1]
+  if (LPR >= 8) s += dpp<0x141>(s);  // row_half_mirror
+  if (LPR >= 16) s += dpp<0x140>(s); // row_mirror
+  if (LPR >= 32) s += __shfl_xor(s, 16, 64);
+  if (LPR >= 64) s += __shfl_xor(s, 32, 64);
+  return s;
+}
+
+// Row dot product (p*q)·h of APR.py:127: per-lane partial sums of rounded
+// products, then the row-group sum.
 template <int LPR, int NV>
 __device__ __forceinline__ float dot_row(const RowV<NV>& a, const RowV<NV>& b) {
   float s = 0.f;
@@ -169,9 +190,7 @@ __device__ __forceinline__ float dot_row(const RowV<NV>& a, const RowV<NV>& b) {
     s = s + a.v[v].z * b.v[v].z;
     s = s + a.v[v].w * b.v[v].w;
   }
-#pragma unroll
-  for (int m = LPR / 2; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
-  return s;
+  return group_sum<LPR>(s);
 }
 
 // softplus threshold of TF's SoftplusOp: log(FLT_EPSILON) + 2.
@@ -184,7 +203,7 @@ __device__ __forceinline__ void bpr_term(float x, float lo, float hi, float& g, 
   float xc = fminf(fmaxf(x, lo), hi);
   bool pass = (x >= lo) && (x <= hi);
   float ex = expf(xc);
-  g = pass ? -1.0f / (ex + 1.0f) : 0.0f;
+  g = pass ? -__builtin_amdgcn_rcpf(ex + 1.0f) : 0.0f;  // v_rcp_f32 (1 ulp)
   float f = -xc;
   loss = f > ACF_SOFTPLUS_T ? f : (f < -ACF_SOFTPLUS_T ? expf(f) : logf(expf(f) + 1.0f));
 }
@@ -399,6 +418,28 @@ __global__ void k_records(const int32_t* __restrict__ uocc, const int32_t* __res
 }
 
 // ---------------------------------------------------------------------------
+// Diagnostic build only (-DACF_DIAG, libacf_apr_diag.so): per-wave
+// s_memrealtime stamps (100 MHz) to locate latency inside the step kernels.
+// The product library compiles every STAMP() to nothing.
+// ---------------------------------------------------------------------------
+#ifdef ACF_DIAG
+__device__ uint64_t* g_stamps = nullptr;
+__device__ int g_stamp_launch = 0;
+__device__ int g_stamp_cap = 0;
+#define STAMP(launch, wave, i)                                                       \
+  do {                                                                               \
+    uint64_t t_;                                                                     \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    if (g_stamps && (threadIdx.x & 63) == 0 && (wave) < g_stamp_cap)                 \
+      g_stamps[((int64_t)(launch) * g_stamp_cap + (wave)) * 8 + (i)] = t_;          \
+  } while (0)
+#else
+#define STAMP(launch, wave, i) \
+  do {                         \
+  } while (0)
+#endif
+
+// ---------------------------------------------------------------------------
 // step kernels: one wavefront per unique row ("slot") of the batch.  The 64
 // lanes form OPW = 64/LPR lane-groups; group g takes occurrences g, g+OPW, ...
 // of the slot, so the gathers of a popular row's occurrences are in flight
@@ -417,6 +458,8 @@ struct StepArgs {
   float* accP;
   float* accQ;
   const OccRec* inl;   // [nb][S][R]
+  const OccRec* hot_cur;  // [S][R] batch t's inline records, copied warm by batch t-1
+  OccRec* hot_next;       // [S][R] where this batch's last kernel copies batch t+1's
   const OccRec* urec;  // CSR, user occurrences
   const OccRec* irec;  // CSR, item occurrences
   float* g0;           // [S, d] clean-loss gradient per slot
@@ -428,6 +471,9 @@ struct StepArgs {
   const int32_t* gen_ptr;  // plan generation (device: graphs stay valid across plans)
   int32_t d, B, S, R, t;
   int32_t prev_valid;  // 1: rows of batch t-1 are still pending in wnew_prev
+  int32_t diag_launch; // diagnostic build: stamp slot of this launch
+  int32_t use_hot;     // phase 1 reads its slot records from hot_cur
+  int32_t write_hot;   // the batch's last kernel copies batch t+1's records to hot_next
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -480,7 +526,9 @@ __device__ __forceinline__ SlotHdr slot_header(const StepArgs& a, int k, int g, 
   const int OPW = 64 / LPR;
   const int32_t gen = *a.gen_ptr;
   r0.gen = -1;
-  if (g < a.R && g < OPW) r0 = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R + g);
+  if (g < a.R && g < OPW)
+    r0 = load_rec(a.use_hot ? a.hot_cur + (int64_t)k * a.R + g
+                            : a.inl + ((int64_t)a.t * a.S + k) * a.R + g);
   if (r0.gen != gen) r0.gen = -1;
   const int lane0 = 0;
   const int32_t meta = __shfl(r0.gen != -1 ? r0.meta : 0, lane0, 64);
@@ -498,6 +546,29 @@ __device__ __forceinline__ OccRec occ_rec(const StepArgs& a, const SlotHdr& h, i
                                           const OccRec& r0) {
   if (idx == g && g < a.R && r0.gen != -1) return r0;
   return load_rec((h.is_item ? a.irec : a.urec) + h.ovf + idx);
+}
+
+// Warm copy of batch t+1's inline records of slot k (issued early by the
+// batch's last kernel, stored at its end): the next batch's first kernel then
+// finds them in the Infinity Cache instead of HBM.
+struct HotCopy {
+  int4 a, b, c;
+};
+
+__device__ __forceinline__ HotCopy hot_load(const StepArgs& a, int k, int g) {
+  HotCopy h;
+  if (a.write_hot && g < a.R) {
+    const int4* q = reinterpret_cast<const int4*>(a.inl + ((int64_t)(a.t + 1) * a.S + k) * a.R + g);
+    h.a = q[0]; h.b = q[1]; h.c = q[2];
+  }
+  return h;
+}
+
+__device__ __forceinline__ void hot_store(const StepArgs& a, int k, int g, int l, const HotCopy& h) {
+  if (a.write_hot && g < a.R && l == 0) {
+    int4* q = reinterpret_cast<int4*>(a.hot_next + (int64_t)k * a.R + g);
+    q[0] = h.a; q[1] = h.b; q[2] = h.c;
+  }
 }
 
 // copy the pending rows of batch t-1 (wnew_prev) to the tables
@@ -530,10 +601,11 @@ __device__ __forceinline__ void adagrad_row(const StepArgs& a, RowV<NV>& G, cons
     c.y = c.y + g.y * g.y;
     c.z = c.z + g.z * g.z;
     c.w = c.w + g.w * g.w;
-    wout.v[v].x = x.x - (a.lr * g.x) * (1.0f / sqrtf(c.x));
-    wout.v[v].y = x.y - (a.lr * g.y) * (1.0f / sqrtf(c.y));
-    wout.v[v].z = x.z - (a.lr * g.z) * (1.0f / sqrtf(c.z));
-    wout.v[v].w = x.w - (a.lr * g.w) * (1.0f / sqrtf(c.w));
+    // Eigen's a.rsqrt(); v_rsq_f32 (1 ulp)
+    wout.v[v].x = x.x - (a.lr * g.x) * __builtin_amdgcn_rsqf(c.x);
+    wout.v[v].y = x.y - (a.lr * g.y) * __builtin_amdgcn_rsqf(c.y);
+    wout.v[v].z = x.z - (a.lr * g.z) * __builtin_amdgcn_rsqf(c.z);
+    wout.v[v].w = x.w - (a.lr * g.w) * __builtin_amdgcn_rsqf(c.w);
   }
 }
 
@@ -547,14 +619,20 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   const int g = lane / LPR, l = lane & (LPR - 1);
-  if (wave >= a.S) {
-    if (a.prev_valid && wave < 2 * a.S) flush_slot<LPR, NV>(a, a.t - 1, a.wnew_prev, wave - a.S);
-    return;
-  }
+  STAMP(a.diag_launch, wave, 0);
+  if (wave >= a.S) return;
   const int k = wave;
+  // the same wave also writes back slot k of batch t-1 (independent loads)
+  if (a.prev_valid) flush_slot<LPR, NV>(a, a.t - 1, a.wnew_prev, k);
+  HotCopy hc;
+  if (FUSE_APPLY) hc = hot_load(a, k, g);
   OccRec r0;
   const SlotHdr h = slot_header<LPR>(a, k, g, r0);
-  if (h.count == 0) return;
+  STAMP(a.diag_launch, wave, 1);
+  if (h.count == 0) {
+    if (FUSE_APPLY) hot_store(a, k, g, l, hc);
+    return;
+  }
   const int d = a.d;
   const float* own_tab = h.is_item ? a.Q : a.P;
   const RowV<NV> own = load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l);
@@ -590,6 +668,7 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
       if (active) axpy_row(G, role ? -gb : gb, ra);
     }
   }
+  STAMP(a.diag_launch, wave, 2);
   group_allreduce<LPR, NV>(G);
   if (FUSE_APPLY) {
     if (g == 0) {
@@ -598,6 +677,7 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
       store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
       store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
     }
+    hot_store(a, k, g, l, hc);
     return;
   }
   RowV<NV> dl;
@@ -606,7 +686,7 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
   } else if (a.adv_mode == 0) {
     // tf.nn.l2_normalize(g, 1) * eps  (epsilon 1e-12 on the squared norm)
     const float ss = dot_row<LPR, NV>(G, G);
-    const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+    const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
     dl = scale_row(scale_row(G, inv), a.eps);
   } else {
     // "random": l2_normalize(truncated_normal(0, 0.01)) * eps, redrawn every run
@@ -623,13 +703,15 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
       z.v[v] = make_float4(e4[0], e4[1], e4[2], e4[3]);
     }
     const float ss = dot_row<LPR, NV>(z, z);
-    const float inv = 1.0f / sqrtf(fmaxf(ss, 1e-12f));
+    const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
     dl = scale_row(scale_row(z, inv), a.eps);
   }
+  STAMP(a.diag_launch, wave, 3);
   if (g == 0) {
     store_row<LPR, NV>(a.g0, k, d, l, G);
     store_row<LPR, NV>(a.delta, k, d, l, dl);
   }
+  STAMP(a.diag_launch, wave, 4);
 }
 
 // Phase 2 = adversarial half of sess.run(optimizer) (APR.py:130-141,156-165)
@@ -641,11 +723,17 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   const int g = lane / LPR, l = lane & (LPR - 1);
+  STAMP(a.diag_launch, wave, 0);
   if (wave >= a.S) return;
   const int k = wave;
+  const HotCopy hc = hot_load(a, k, g);
   OccRec r0;
   const SlotHdr h = slot_header<LPR>(a, k, g, r0);
-  if (h.count == 0) return;
+  STAMP(a.diag_launch, wave, 1);
+  if (h.count == 0) {
+    hot_store(a, k, g, l, hc);
+    return;
+  }
   const int d = a.d;
   const RowV<NV> own = load_row<LPR, NV>(h.is_item ? a.Q : a.P, h.own_row, d, l);
   const RowV<NV> ownp = add_row(own, load_row<LPR, NV>(a.delta, k, d, l));
@@ -684,6 +772,7 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
       if (active) axpy_row(G, role ? -gb : gb, ra);
     }
   }
+  STAMP(a.diag_launch, wave, 2);
   group_allreduce<LPR, NV>(G);
   if (g == 0) {
     axpy_row(G0, a.reg_adv, G);
@@ -692,6 +781,8 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
     store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
     store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
   }
+  hot_store(a, k, g, l, hc);
+  STAMP(a.diag_launch, wave, 4);
 }
 
 // Flush the pending rows of batch t (wnew_cur) to the tables (end of a call).
@@ -979,7 +1070,7 @@ struct acf_apr_ctx {
   int32_t *uuniq = nullptr, *uoff = nullptr, *ubs = nullptr, *uocc = nullptr, *uslot = nullptr;
   int32_t *iuniq = nullptr, *ioff = nullptr, *ibs = nullptr, *iocc = nullptr;
   int32_t *pslot = nullptr, *nslot = nullptr, *usrc = nullptr, *isrc = nullptr;
-  OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr;
+  OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr, *hot[2] = {nullptr, nullptr};
   int32_t *err = nullptr, *gen_dev = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -1103,6 +1194,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->pslot, maxE); A(&c->nslot, maxE); A(&c->isrc, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
+  A(&c->hot[0], S * c->R); A(&c->hot[1], S * c->R);
   A(&c->err, 4); A(&c->gen_dev, 4);
   A(&c->g0, S * d); A(&c->delta, S * d);
   A(&c->wnew[0], S * d); A(&c->wnew[1], S * d);
@@ -1200,6 +1292,10 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   StepArgs a;
   a.P = tb->P; a.Q = tb->Q; a.accP = tb->accP; a.accQ = tb->accQ;
   a.inl = c->inl; a.urec = c->urec; a.irec = c->irec;
+  a.hot_cur = c->hot[t & 1];
+  a.hot_next = c->hot[(t + 1) & 1];
+  a.use_hot = 0;
+  a.write_hot = 0;
   a.g0 = c->g0; a.delta = c->delta;
   a.wnew_cur = c->wnew[t & 1];
   a.wnew_prev = c->wnew[(t + 1) & 1];
@@ -1207,6 +1303,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.gen_ptr = c->gen_dev;
   a.d = c->d; a.B = c->B; a.S = 3 * c->B; a.R = c->R; a.t = t;
   a.prev_valid = prev_valid;
+  a.diag_launch = 0;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -1265,17 +1362,23 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   auto L = [&](void* fn, const StepArgs& a, int waves, int kind) -> int {
     hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
     if (kinds) kinds[li] = kind;
+    StepArgs b = a;
+    b.diag_launch = li;
     ++li;
-    return launch(fn, a, waves, s, e0, e1);
+    return launch(fn, b, waves, s, e0, e1);
   };
   for (int32_t t = first; t < first + n; ++t) {
     const int pv = t > first ? 1 : 0;
-    const StepArgs a = make_args(c, tb, hp, t, pv);
+    StepArgs a = make_args(c, tb, hp, t, pv);
+    a.use_hot = pv;                       // batch t-1's last kernel copied our records
+    a.write_hot = t + 1 < first + n ? 1 : 0;
     if (hp->adver) {
-      ACF_RET(L(K.clean_apr, a, pv ? 2 * S : S, 0));
+      StepArgs a1 = a;
+      a1.write_hot = 0;
+      ACF_RET(L(K.clean_apr, a1, S, 0));
       ACF_RET(L(K.adv, a, S, 1));
     } else {
-      ACF_RET(L(K.clean_bpr, a, pv ? 2 * S : S, 0));
+      ACF_RET(L(K.clean_bpr, a, S, 0));
     }
   }
   ACF_RET(L(K.flush, make_args(c, tb, hp, first + n - 1, 0), S, 2));
@@ -1512,3 +1615,13 @@ extern "C" int acf_dns_select(const float* P, const float* Q, int64_t U1, int64_
   HIP_TRY(hipGetLastError());
   return ACF_OK;
 }
+
+#ifdef ACF_DIAG
+// diagnostic build only: stamp buffer [launches][cap waves][8] of uint64
+extern "C" int acf_diag_set_stamps(void* buf, int32_t cap) {
+  uint64_t* p = static_cast<uint64_t*>(buf);
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)));
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_cap), &cap, sizeof(cap)));
+  return ACF_OK;
+}
+#endif

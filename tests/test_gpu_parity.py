@@ -285,3 +285,58 @@ def test_full_size_ml1m_epoch_deterministic(ops, acf, dev):
     touched = np.zeros(U1, bool)
     touched[ep.user.cpu().numpy()] = True
     assert np.array_equal(moved, touched)
+
+
+@pytest.mark.parametrize("adver", [0, 1])
+def test_piecewise_calls_equal_one_call(ops, oracle, dev, adver):
+    """train_planned over [0,2)+[2,5) and per-batch optimizer_step == one call,
+    and all match the oracle (exercises the deferred flush across calls)."""
+    U1, I1, d, B, nb = 40, 35, 64, 32, 5
+    P, Q, u, i, j = _problem(17 + adver, U1, I1, d, B, nb, dup_items=True)
+    want, *_ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=adver))
+    hp = ops.StepHParams(adver=adver)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    a = _gpu_tables(P, Q, dev)
+    ctx.train_planned(a, hp, 0, 2, graph=True)
+    ctx.train_planned(a, hp, 2, 3, graph=False)
+    b = _gpu_tables(P, Q, dev)
+    for t in range(nb):
+        if adver:
+            ctx.delta_update(b, hp, t)
+        ctx.optimizer_step(b, hp, t)
+    torch.cuda.synchronize()
+    for x, y, w, n in zip(a, b, want, ("P", "Q", "accP", "accQ")):
+        assert torch.equal(x, y), n
+        _close(x, w, n)
+
+
+def test_hot_rows_many_occurrences(ops, oracle, dev):
+    """A few rows with hundreds of occurrences per batch (overflow records,
+    many rounds per wave) still match the oracle."""
+    U1, I1, d, B, nb = 12, 9, 64, 1024, 2
+    P, Q, u, i, j = _problem(23, U1, I1, d, B, nb)
+    want, *_ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=1))
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ctx.train_planned(tabs, ops.StepHParams(adver=1))
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        np.testing.assert_allclose(g.cpu().numpy(), w, rtol=1e-4, atol=1e-5, err_msg=n)
+
+
+def test_replan_reuses_graph(ops, oracle, dev):
+    """A cached graph stays valid after a new plan (plan generation is read on device)."""
+    U1, I1, d, B, nb = 50, 40, 32, 64, 3
+    P, Q, u, i, j = _problem(31, U1, I1, d, B, 2 * nb)
+    want, *_ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=1))
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    hp = ops.StepHParams(adver=1)
+    for c in range(2):
+        s = slice(c * nb * B, (c + 1) * nb * B)
+        ctx.plan(torch.tensor(u[s], device=dev), torch.tensor(i[s], device=dev),
+                 torch.tensor(j[s], device=dev), B)
+        ctx.train_planned(tabs, hp, 0, nb, graph=True)
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        _close(g, w, n)
