@@ -1,11 +1,6 @@
-"""Build the in-tree native libraries.
-
-- ``lib/libacf_apr.so``: the HIP kernels + C-ABI (``include/acf_apr.h``), built
-  with ``hipcc --offload-arch=gfx950``.  This is the product.
-- ``oracle/_build/liboracle_apr.so``: the CPU restatement used only by tests and
-  by ``bench.py``'s ``cpu_baseline`` leg (built with gcc).
-
-Both land inside the repository so that ``gpurun`` ships them to the GPU box.
+"""Build the in-tree HIP library ``lib/libacf_apr.so`` (kernels + C-ABI of
+``include/acf_apr.h``) with ``hipcc --offload-arch=gfx950``.  It lands inside the
+repository so that ``gpurun`` ships it to the GPU box.
 """
 from __future__ import annotations
 
@@ -17,8 +12,6 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 HIP_SRC = os.path.join(PKG_DIR, "csrc", "acf_apr.hip")
 HIP_LIB = os.path.join(PKG_DIR, "lib", "libacf_apr.so")
-ORACLE_SRC = os.path.join(REPO, "oracle", "apr_oracle.c")
-ORACLE_LIB = os.path.join(REPO, "oracle", "_build", "liboracle_apr.so")
 HEADER = os.path.join(REPO, "include", "acf_apr.h")
 
 HIPCC_FLAGS = [
@@ -53,24 +46,9 @@ def build_hip(force: bool = False, verbose: bool = True) -> str:
     return HIP_LIB
 
 
-def build_oracle(force: bool = False, verbose: bool = True) -> str:
-    if force or _stale(ORACLE_LIB, [ORACLE_SRC, __file__]):
-        os.makedirs(os.path.dirname(ORACLE_LIB), exist_ok=True)
-        tmp = ORACLE_LIB + ".tmp"
-        cmd = ["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-fPIC", "-shared",
-               "-Wall", ORACLE_SRC, "-o", tmp, "-lm"]
-        if verbose:
-            print("[build]", " ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-        os.replace(tmp, ORACLE_LIB)
-    return ORACLE_LIB
-
-
 def main(argv: list[str]) -> int:
     force = "--force" in argv
     build_hip(force)
-    if os.path.exists(ORACLE_SRC):
-        build_oracle(force)
     return 0
 
 

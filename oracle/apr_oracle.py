@@ -74,12 +74,10 @@ class COracle:
     def __init__(self, path: str = LIB_PATH):
         if not os.path.exists(path):
             import importlib.util
-            spec = importlib.util.spec_from_file_location(
-                "_acf_build", os.path.join(os.path.dirname(HERE),
-                                           "adversarial-collaborative-filtering_amd", "build_native.py"))
+            spec = importlib.util.spec_from_file_location("_acf_oracle_build", os.path.join(HERE, "build.py"))
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
-            mod.build_oracle(verbose=False)
+            mod.build(verbose=False)
         self.lib = ctypes.CDLL(path)
         L = self.lib
         P = ctypes.c_void_p
