@@ -187,11 +187,14 @@ class Session:
         m = self.model
         single = not isinstance(fetches, (list, tuple))
         fl = [fetches] if single else list(fetches)
-        names = [f.name if isinstance(f, _Handle) else f for f in fl]
+        # variables are fetched by value, like TF returns their numpy arrays (utils.py:92)
+        names = [f.name if isinstance(f, _Handle) else
+                 ("embedding_P" if f is m.embedding_P else "embedding_Q" if f is m.embedding_Q else f)
+                 if isinstance(f, torch.Tensor) else f for f in fl]
         fd = {k.name if isinstance(k, _Handle) else k: v for k, v in (feed_dict or {}).items()}
         u, i, j = fd.get("user_input"), fd.get("item_input_pos"), fd.get("item_input_neg")
         out = {}
-        if any(n in ("update_P", "update_Q") for n in names):
+        if any(isinstance(n, str) and n in ("update_P", "update_Q") for n in names):
             if not m.adver and m.adv == "grad":
                 # the BPR graph has no update ops in the reference; keep TF's error class
                 raise ValueError("update_P/update_Q exist only in the APR graph (adver=1)")
@@ -200,7 +203,8 @@ class Session:
         if "optimizer" in names:
             m.optimizer_step(u, i, j)
             out["optimizer"] = None
-        if any(n in ("loss", "output_neg") for n in names) or ("output" in names and j is not None):
+        if any(isinstance(n, str) and n in ("loss", "output_neg") for n in names) or (
+                "output" in names and j is not None):
             uu = ops._idx(u, "user_input", m.device)
             n = uu.numel()
             bl, bc, op, on = ops.bpr_forward(m.embedding_P, m.embedding_Q, uu, i, j, n, want_scores=True)
@@ -213,6 +217,10 @@ class Session:
             out["embedding_P"] = m.embedding_P.cpu().numpy()
         if "embedding_Q" in names:
             out["embedding_Q"] = m.embedding_Q.cpu().numpy()
+        for k, n in enumerate(names):
+            if isinstance(n, torch.Tensor):  # any other tensor: its value
+                names[k] = "_t%d" % k
+                out[names[k]] = n.detach().cpu().numpy()
         missing = [n for n in names if n not in out]
         if missing:
             raise NotImplementedError(f"fetch(es) {missing} not supported by the APR session")
