@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "e2e"))
     a = ap.parse_args()
+    a.out = os.path.abspath(a.out)
     cli = importlib.import_module("adversarial-collaborative-filtering_amd.cli")
     work = tempfile.mkdtemp(prefix="acf_e2e_")
     os.makedirs(os.path.join(work, "data"))
