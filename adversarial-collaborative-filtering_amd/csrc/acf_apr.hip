@@ -479,13 +479,30 @@ struct StepArgs {
   uint64_t seed;
 };
 
-__device__ __forceinline__ OccRec load_rec(const OccRec* __restrict__ p) {
+// An OccRec as three int4 registers (kept in VGPRs; a struct of scalars passed
+// by reference got demoted to scratch).  Field order as in OccRec.
+struct RecV {
+  int4 a, b, c;
+  __device__ int own_row() const { return a.x; }
+  __device__ int own_src() const { return a.y; }
+  __device__ int meta() const { return a.z; }
+  __device__ int ovf() const { return a.w; }
+  __device__ int e_role() const { return b.x; }
+  __device__ int pa_row() const { return b.y; }
+  __device__ int pb_row() const { return b.z; }
+  __device__ int pa_src() const { return b.w; }
+  __device__ int pb_src() const { return c.x; }
+  __device__ int pa_slot() const { return c.y; }
+  __device__ int pb_slot() const { return c.z; }
+  __device__ int gen() const { return c.w; }
+};
+
+__device__ __forceinline__ RecV load_rec(const OccRec* __restrict__ p) {
   const int4* q = reinterpret_cast<const int4*>(p);
-  const int4 a = q[0], b = q[1], c = q[2];
-  OccRec r;
-  r.own_row = a.x; r.own_src = a.y; r.meta = a.z; r.ovf = a.w;
-  r.e_role = b.x; r.pa_row = b.y; r.pb_row = b.z; r.pa_src = b.w;
-  r.pb_src = c.x; r.pa_slot = c.y; r.pb_slot = c.z; r.gen = c.w;
+  RecV r;
+  r.a = q[0];
+  r.b = q[1];
+  r.c = q[2];
   return r;
 }
 
@@ -521,31 +538,38 @@ struct SlotHdr {
   int32_t count, is_item, own_row, own_src, ovf;
 };
 
+// Inline record of lane-group g for slot k (valid iff its gen matches the plan)
+// and the slot header broadcast from lane 0.
+struct SlotRec {
+  SlotHdr h;
+  RecV r0;
+  bool r0_valid;
+};
+
 template <int LPR>
-__device__ __forceinline__ SlotHdr slot_header(const StepArgs& a, int k, int g, OccRec& r0) {
+__device__ __forceinline__ SlotRec slot_header(const StepArgs& a, int k, int g) {
   const int OPW = 64 / LPR;
   const int32_t gen = *a.gen_ptr;
-  r0.gen = -1;
+  SlotRec s;
+  s.r0.a = s.r0.b = s.r0.c = make_int4(0, 0, 0, -1);
   if (g < a.R && g < OPW)
-    r0 = load_rec(a.use_hot ? a.hot_cur + (int64_t)k * a.R + g
-                            : a.inl + ((int64_t)a.t * a.S + k) * a.R + g);
-  if (r0.gen != gen) r0.gen = -1;
+    s.r0 = load_rec(a.use_hot ? a.hot_cur + (int64_t)k * a.R + g
+                              : a.inl + ((int64_t)a.t * a.S + k) * a.R + g);
+  s.r0_valid = s.r0.gen() == gen;
   const int lane0 = 0;
-  const int32_t meta = __shfl(r0.gen != -1 ? r0.meta : 0, lane0, 64);
-  SlotHdr h;
-  h.count = meta & ACF_COUNT_MASK;
-  h.is_item = (meta & ACF_ITEM_BIT) != 0;
-  h.own_row = __shfl(r0.own_row, lane0, 64);
-  h.own_src = __shfl(r0.own_src, lane0, 64);
-  h.ovf = __shfl(r0.ovf, lane0, 64);
-  return h;
+  const int32_t meta = __shfl(s.r0_valid ? s.r0.meta() : 0, lane0, 64);
+  s.h.count = meta & ACF_COUNT_MASK;
+  s.h.is_item = (meta & ACF_ITEM_BIT) != 0;
+  s.h.own_row = __shfl(s.r0.own_row(), lane0, 64);
+  s.h.own_src = __shfl(s.r0.own_src(), lane0, 64);
+  s.h.ovf = __shfl(s.r0.ovf(), lane0, 64);
+  return s;
 }
 
 // record of occurrence idx of the slot (idx < count)
-__device__ __forceinline__ OccRec occ_rec(const StepArgs& a, const SlotHdr& h, int idx, int g,
-                                          const OccRec& r0) {
-  if (idx == g && g < a.R && r0.gen != -1) return r0;
-  return load_rec((h.is_item ? a.irec : a.urec) + h.ovf + idx);
+__device__ __forceinline__ RecV occ_rec(const StepArgs& a, const SlotRec& s, int idx, int g) {
+  if (idx == g && g < a.R && s.r0_valid) return s.r0;
+  return load_rec((s.h.is_item ? a.irec : a.urec) + s.h.ovf + idx);
 }
 
 // Warm copy of batch t+1's inline records of slot k (issued early by the
@@ -575,9 +599,9 @@ __device__ __forceinline__ void hot_store(const StepArgs& a, int k, int g, int l
 template <int LPR, int NV>
 __device__ void flush_slot(const StepArgs& a, int tb, const float* __restrict__ wsrc, int k) {
   const int lane = threadIdx.x & 63;
-  const OccRec r = load_rec(a.inl + ((int64_t)tb * a.S + k) * a.R);
-  if (r.gen != *a.gen_ptr || (r.meta & ACF_COUNT_MASK) == 0) return;
-  float* dst = ((r.meta & ACF_ITEM_BIT) ? a.Q : a.P) + (int64_t)r.own_row * a.d;
+  const RecV r = load_rec(a.inl + ((int64_t)tb * a.S + k) * a.R);
+  if (r.gen() != *a.gen_ptr || (r.meta() & ACF_COUNT_MASK) == 0) return;
+  float* dst = ((r.meta() & ACF_ITEM_BIT) ? a.Q : a.P) + (int64_t)r.own_row() * a.d;
   const float* src = wsrc + (int64_t)k * a.d;
   for (int c = lane; c * 4 < a.d; c += 64)
     *reinterpret_cast<float4*>(dst + c * 4) = *reinterpret_cast<const float4*>(src + c * 4);
@@ -626,8 +650,8 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
   if (a.prev_valid) flush_slot<LPR, NV>(a, a.t - 1, a.wnew_prev, k);
   HotCopy hc;
   if (FUSE_APPLY) hc = hot_load(a, k, g);
-  OccRec r0;
-  const SlotHdr h = slot_header<LPR>(a, k, g, r0);
+  const SlotRec sr = slot_header<LPR>(a, k, g);
+  const SlotHdr& h = sr.h;
   STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
     if (FUSE_APPLY) hot_store(a, k, g, l, hc);
@@ -644,12 +668,12 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
     const int idx = base + g;
     const bool active = idx < h.count;
     RowV<NV> ra = zero_row<NV>(), rb = zero_row<NV>();
-    OccRec r;
+    RecV r;
     if (active) {
-      r = occ_rec(a, h, idx, g, r0);
+      r = occ_rec(a, sr, idx, g);
       // user slot: ra = Q[i], rb = Q[j];  item slot: ra = P[u], rb = Q[other]
-      ra = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r.pa_row, r.pa_src), d, l);
-      rb = load_at<LPR, NV>(row_src(a, a.Q, r.pb_row, r.pb_src), d, l);
+      ra = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r.pa_row(), r.pa_src()), d, l);
+      rb = load_at<LPR, NV>(row_src(a, a.Q, r.pb_row(), r.pb_src()), d, l);
     }
     float gb, loss;
     if (!h.is_item) {
@@ -658,11 +682,11 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
       if (active) {
         axpy_row(G, gb, ra);   // pos branch: dx+/dp = q_i
         axpy_row(G, -gb, rb);  // neg branch: dx-/dp = q_j
-        if (l == 0) a.loss_clean[r.e_role] = loss;
+        if (l == 0) a.loss_clean[r.e_role()] = loss;
       }
     } else {
       const float dq = dot_row<LPR, NV>(ra, own), dqo = dot_row<LPR, NV>(ra, rb);
-      const int role = active ? (r.e_role & 1) : 0;
+      const int role = active ? (r.e_role() & 1) : 0;
       const float x = role ? (dqo - dq) : (dq - dqo);
       bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
       if (active) axpy_row(G, role ? -gb : gb, ra);
@@ -727,8 +751,8 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
   if (wave >= a.S) return;
   const int k = wave;
   const HotCopy hc = hot_load(a, k, g);
-  OccRec r0;
-  const SlotHdr h = slot_header<LPR>(a, k, g, r0);
+  const SlotRec sr = slot_header<LPR>(a, k, g);
+  const SlotHdr& h = sr.h;
   STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
     hot_store(a, k, g, l, hc);
@@ -747,13 +771,13 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
     const int idx = base + g;
     const bool active = idx < h.count;
     RowV<NV> ra = zero_row<NV>(), rb = zero_row<NV>();
-    OccRec r;
+    RecV r;
     if (active) {
-      r = occ_rec(a, h, idx, g, r0);
-      ra = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r.pa_row, d, l),
-                   load_row<LPR, NV>(a.delta, r.pa_slot, d, l));
-      rb = add_row(load_row<LPR, NV>(a.Q, r.pb_row, d, l),
-                   load_row<LPR, NV>(a.delta, r.pb_slot, d, l));
+      r = occ_rec(a, sr, idx, g);
+      ra = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r.pa_row(), d, l),
+                   load_row<LPR, NV>(a.delta, r.pa_slot(), d, l));
+      rb = add_row(load_row<LPR, NV>(a.Q, r.pb_row(), d, l),
+                   load_row<LPR, NV>(a.delta, r.pb_slot(), d, l));
     }
     float gb, loss;
     if (!h.is_item) {
@@ -762,11 +786,11 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
       if (active) {
         axpy_row(G, gb, ra);
         axpy_row(G, -gb, rb);
-        if (l == 0) a.loss_adv[r.e_role] = loss;
+        if (l == 0) a.loss_adv[r.e_role()] = loss;
       }
     } else {
       const float dq = dot_row<LPR, NV>(ra, ownp), dqo = dot_row<LPR, NV>(ra, rb);
-      const int role = active ? (r.e_role & 1) : 0;
+      const int role = active ? (r.e_role() & 1) : 0;
       const float x = role ? (dqo - dq) : (dq - dqo);
       bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
       if (active) axpy_row(G, role ? -gb : gb, ra);
@@ -797,9 +821,9 @@ __global__ void k_delta_scatter(StepArgs a, float* __restrict__ dP, float* __res
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   if (wave >= a.S) return;
-  const OccRec r = load_rec(a.inl + ((int64_t)a.t * a.S + wave) * a.R);
-  if (r.gen != *a.gen_ptr || (r.meta & ACF_COUNT_MASK) == 0) return;
-  float* dst = ((r.meta & ACF_ITEM_BIT) ? dQ : dP) + (int64_t)r.own_row * a.d;
+  const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + wave) * a.R);
+  if (r.gen() != *a.gen_ptr || (r.meta() & ACF_COUNT_MASK) == 0) return;
+  float* dst = ((r.meta() & ACF_ITEM_BIT) ? dQ : dP) + (int64_t)r.own_row() * a.d;
   const float* src = a.delta + (int64_t)wave * a.d;
   for (int c = lane; c * 4 < a.d; c += 64)
     *reinterpret_cast<float4*>(dst + c * 4) = *reinterpret_cast<const float4*>(src + c * 4);
