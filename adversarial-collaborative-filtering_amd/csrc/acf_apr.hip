@@ -433,7 +433,17 @@ __device__ int g_stamp_cap = 0;
     if (g_stamps && (threadIdx.x & 63) == 0 && (wave) < g_stamp_cap)                 \
       g_stamps[((int64_t)(launch) * g_stamp_cap + (wave)) * 8 + (i)] = t_;          \
   } while (0)
+#define CLOCKSTAMP(launch, wave, i)                                                  \
+  do {                                                                               \
+    uint64_t t_;                                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+    if (g_stamps && (threadIdx.x & 63) == 0 && (wave) < g_stamp_cap)                 \
+      g_stamps[((int64_t)(launch) * g_stamp_cap + (wave)) * 8 + (i)] = t_;          \
+  } while (0)
 #else
+#define CLOCKSTAMP(launch, wave, i) \
+  do {                              \
+  } while (0)
 #define STAMP(launch, wave, i) \
   do {                         \
   } while (0)
@@ -538,72 +548,79 @@ struct SlotHdr {
   int32_t count, is_item, own_row, own_src, ovf;
 };
 
-// Inline record of lane-group g for slot k (valid iff its gen matches the plan)
-// and the slot header broadcast from lane 0.
+// Lane-groups are organised in teams of TEAM groups; a team owns one slot and
+// member m of the team takes occurrences m, m+TEAM, ...  TEAM = 64/LPR is one
+// wave per slot (hot rows of small batches); TEAM = 1 packs 64/LPR slots per
+// wave (large batches, where almost every slot has one occurrence).
 struct SlotRec {
   SlotHdr h;
   RecV r0;
   bool r0_valid;
 };
 
-template <int LPR>
-__device__ __forceinline__ SlotRec slot_header(const StepArgs& a, int k, int g) {
-  const int OPW = 64 / LPR;
+// Record m of slot k (members m < R) and the slot header broadcast from the
+// team leader's lane.
+template <int LPR, int TEAM>
+__device__ __forceinline__ SlotRec slot_header(const StepArgs& a, int k, int m, int leader_lane) {
   const int32_t gen = *a.gen_ptr;
   SlotRec s;
   s.r0.a = s.r0.b = s.r0.c = make_int4(0, 0, 0, -1);
-  if (g < a.R && g < OPW)
-    s.r0 = load_rec(a.use_hot ? a.hot_cur + (int64_t)k * a.R + g
-                              : a.inl + ((int64_t)a.t * a.S + k) * a.R + g);
+  if (m < a.R && k < a.S)
+    s.r0 = load_rec(a.use_hot ? a.hot_cur + (int64_t)k * a.R + m
+                              : a.inl + ((int64_t)a.t * a.S + k) * a.R + m);
   s.r0_valid = s.r0.gen() == gen;
-  const int lane0 = 0;
-  const int32_t meta = __shfl(s.r0_valid ? s.r0.meta() : 0, lane0, 64);
+  const int32_t meta = __shfl(s.r0_valid ? s.r0.meta() : 0, leader_lane, 64);
   s.h.count = meta & ACF_COUNT_MASK;
   s.h.is_item = (meta & ACF_ITEM_BIT) != 0;
-  s.h.own_row = __shfl(s.r0.own_row(), lane0, 64);
-  s.h.own_src = __shfl(s.r0.own_src(), lane0, 64);
-  s.h.ovf = __shfl(s.r0.ovf(), lane0, 64);
+  s.h.own_row = __shfl(s.r0.own_row(), leader_lane, 64);
+  s.h.own_src = __shfl(s.r0.own_src(), leader_lane, 64);
+  s.h.ovf = __shfl(s.r0.ovf(), leader_lane, 64);
   return s;
 }
 
-// record of occurrence idx of the slot (idx < count)
-__device__ __forceinline__ RecV occ_rec(const StepArgs& a, const SlotRec& s, int idx, int g) {
-  if (idx == g && g < a.R && s.r0_valid) return s.r0;
+// record of occurrence idx of the slot (idx < count): the member's inline
+// record for its first occurrence, the CSR records otherwise
+__device__ __forceinline__ RecV occ_rec(const StepArgs& a, const SlotRec& s, int idx, int m) {
+  if (idx == m && m < a.R && s.r0_valid) return s.r0;
   return load_rec((s.h.is_item ? a.irec : a.urec) + s.h.ovf + idx);
 }
 
 // Warm copy of batch t+1's inline records of slot k (issued early by the
 // batch's last kernel, stored at its end): the next batch's first kernel then
-// finds them in the Infinity Cache instead of HBM.
+// finds them in the Infinity Cache instead of HBM.  Member m copies record m
+// (m < R); in packed mode that is the slot's first record only.
 struct HotCopy {
   int4 a, b, c;
 };
 
-__device__ __forceinline__ HotCopy hot_load(const StepArgs& a, int k, int g) {
+template <int TEAM>
+__device__ __forceinline__ HotCopy hot_load(const StepArgs& a, int k, int m) {
   HotCopy h;
-  if (a.write_hot && g < a.R) {
-    const int4* q = reinterpret_cast<const int4*>(a.inl + ((int64_t)(a.t + 1) * a.S + k) * a.R + g);
-    h.a = q[0]; h.b = q[1]; h.c = q[2];
+  if (a.write_hot && k < a.S && m < a.R) {
+    const int4* p = reinterpret_cast<const int4*>(a.inl + ((int64_t)(a.t + 1) * a.S + k) * a.R + m);
+    h.a = p[0]; h.b = p[1]; h.c = p[2];
   }
   return h;
 }
 
-__device__ __forceinline__ void hot_store(const StepArgs& a, int k, int g, int l, const HotCopy& h) {
-  if (a.write_hot && g < a.R && l == 0) {
-    int4* q = reinterpret_cast<int4*>(a.hot_next + (int64_t)k * a.R + g);
-    q[0] = h.a; q[1] = h.b; q[2] = h.c;
+template <int TEAM>
+__device__ __forceinline__ void hot_store(const StepArgs& a, int k, int m, int l, const HotCopy& h) {
+  if (a.write_hot && k < a.S && m < a.R && l == 0) {
+    int4* p = reinterpret_cast<int4*>(a.hot_next + (int64_t)k * a.R + m);
+    p[0] = h.a; p[1] = h.b; p[2] = h.c;
   }
 }
 
-// copy the pending rows of batch t-1 (wnew_prev) to the tables
-template <int LPR, int NV>
-__device__ void flush_slot(const StepArgs& a, int tb, const float* __restrict__ wsrc, int k) {
-  const int lane = threadIdx.x & 63;
+// copy the pending row of slot k of batch tb (in wsrc) to its table; the
+// team's tl-th lane of tn copies float4 chunks tl, tl+tn, ...
+__device__ __forceinline__ void flush_slot(const StepArgs& a, int tb, const float* __restrict__ wsrc,
+                                           int k, int tl, int tn) {
+  if (k >= a.S) return;
   const RecV r = load_rec(a.inl + ((int64_t)tb * a.S + k) * a.R);
   if (r.gen() != *a.gen_ptr || (r.meta() & ACF_COUNT_MASK) == 0) return;
   float* dst = ((r.meta() & ACF_ITEM_BIT) ? a.Q : a.P) + (int64_t)r.own_row() * a.d;
   const float* src = wsrc + (int64_t)k * a.d;
-  for (int c = lane; c * 4 < a.d; c += 64)
+  for (int c = tl; c * 4 < a.d; c += tn)
     *reinterpret_cast<float4*>(dst + c * 4) = *reinterpret_cast<const float4*>(src + c * 4);
 }
 
@@ -633,44 +650,73 @@ __device__ __forceinline__ void adagrad_row(const StepArgs& a, RowV<NV>& G, cons
   }
 }
 
+// butterfly over the TEAM lane-groups of a team (fixed order -> deterministic)
+template <int LPR, int TEAM, int NV>
+__device__ __forceinline__ void team_allreduce(RowV<NV>& G) {
+#pragma unroll
+  for (int m = LPR; m < LPR * TEAM; m <<= 1) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      G.v[v].x += __shfl_xor(G.v[v].x, m, 64);
+      G.v[v].y += __shfl_xor(G.v[v].y, m, 64);
+      G.v[v].z += __shfl_xor(G.v[v].z, m, 64);
+      G.v[v].w += __shfl_xor(G.v[v].w, m, 64);
+    }
+  }
+}
+
+// Lane geometry of a step kernel: slot k of this team, member m, lane l in the
+// row-group, the team leader's lane, the lane index inside the team.
+template <int LPR, int TEAM>
+struct Geo {
+  int wave, k, m, l, leader, tl;
+  __device__ Geo() {
+    constexpr int OPW = 64 / LPR;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPR;
+    wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+    k = wave * (OPW / TEAM) + g / TEAM;
+    m = g % TEAM;
+    l = lane & (LPR - 1);
+    leader = (g / TEAM) * TEAM * LPR;
+    tl = lane - leader;
+  }
+};
+
 // Phase 1 = sess.run([update_P, update_Q]) (APR.py:180-191) and the clean half
 // of the optimizer: clean-loss gradient of every unique row of batch t summed
 // over its occurrences, its delta (APR graph), or — BPR graph, FUSE_APPLY — the
-// Adagrad update straight away.  Waves [S, 2S) flush batch t-1's rows.
-template <int LPR, int NV, bool FUSE_APPLY>
+// Adagrad update straight away.  The team also writes back slot k of batch t-1.
+template <int LPR, int NV, bool FUSE_APPLY, int TEAM>
 __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
-  constexpr int OPW = 64 / LPR;
-  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
-  const int lane = threadIdx.x & 63;
-  const int g = lane / LPR, l = lane & (LPR - 1);
-  STAMP(a.diag_launch, wave, 0);
-  if (wave >= a.S) return;
-  const int k = wave;
-  // the same wave also writes back slot k of batch t-1 (independent loads)
-  if (a.prev_valid) flush_slot<LPR, NV>(a, a.t - 1, a.wnew_prev, k);
+  const Geo<LPR, TEAM> q;
+  const int k = q.k, m = q.m, l = q.l;
+  STAMP(a.diag_launch, q.wave, 0);
+  CLOCKSTAMP(a.diag_launch, q.wave, 6);
+  if (a.prev_valid) flush_slot(a, a.t - 1, a.wnew_prev, k, q.tl, TEAM * LPR);
   HotCopy hc;
-  if (FUSE_APPLY) hc = hot_load(a, k, g);
-  const SlotRec sr = slot_header<LPR>(a, k, g);
+  if (FUSE_APPLY) hc = hot_load<TEAM>(a, k, m);
+  const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, q.leader);
   const SlotHdr& h = sr.h;
-  STAMP(a.diag_launch, wave, 1);
+  STAMP(a.diag_launch, q.wave, 1);
   if (h.count == 0) {
-    if (FUSE_APPLY) hot_store(a, k, g, l, hc);
+    if (FUSE_APPLY) hot_store<TEAM>(a, k, m, l, hc);
     return;
   }
   const int d = a.d;
   const float* own_tab = h.is_item ? a.Q : a.P;
   const RowV<NV> own = load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l);
   RowV<NV> acc;
-  if (FUSE_APPLY && g == 0)
+  if (FUSE_APPLY && m == 0)
     acc = load_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l);
   RowV<NV> G = zero_row<NV>();
-  for (int base = 0; base < h.count; base += OPW) {
-    const int idx = base + g;
+  for (int base = 0; base < h.count; base += TEAM) {
+    const int idx = base + m;
     const bool active = idx < h.count;
     RowV<NV> ra = zero_row<NV>(), rb = zero_row<NV>();
     RecV r;
     if (active) {
-      r = occ_rec(a, sr, idx, g);
+      r = occ_rec(a, sr, idx, m);
       // user slot: ra = Q[i], rb = Q[j];  item slot: ra = P[u], rb = Q[other]
       ra = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r.pa_row(), r.pa_src()), d, l);
       rb = load_at<LPR, NV>(row_src(a, a.Q, r.pb_row(), r.pb_src()), d, l);
@@ -692,16 +738,16 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
       if (active) axpy_row(G, role ? -gb : gb, ra);
     }
   }
-  STAMP(a.diag_launch, wave, 2);
-  group_allreduce<LPR, NV>(G);
+  STAMP(a.diag_launch, q.wave, 2);
+  team_allreduce<LPR, TEAM, NV>(G);
   if (FUSE_APPLY) {
-    if (g == 0) {
+    if (m == 0) {
       RowV<NV> wout;
       adagrad_row(a, G, own, acc, h.count, wout);
       store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
       store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
     }
-    hot_store(a, k, g, l, hc);
+    hot_store<TEAM>(a, k, m, l, hc);
     return;
   }
   RowV<NV> dl;
@@ -722,58 +768,55 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
       const int c = l + LPR * v;
       float e4[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        e4[q] = (c * 4 + q < d) ? trunc_normal(rk ^ mix64((uint64_t)(c * 4 + q)), 0.01f) : 0.f;
+      for (int e = 0; e < 4; ++e)
+        e4[e] = (c * 4 + e < d) ? trunc_normal(rk ^ mix64((uint64_t)(c * 4 + e)), 0.01f) : 0.f;
       z.v[v] = make_float4(e4[0], e4[1], e4[2], e4[3]);
     }
     const float ss = dot_row<LPR, NV>(z, z);
     const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
     dl = scale_row(scale_row(z, inv), a.eps);
   }
-  STAMP(a.diag_launch, wave, 3);
-  if (g == 0) {
+  STAMP(a.diag_launch, q.wave, 3);
+  if (m == 0) {
     store_row<LPR, NV>(a.g0, k, d, l, G);
     store_row<LPR, NV>(a.delta, k, d, l, dl);
   }
-  STAMP(a.diag_launch, wave, 4);
+  STAMP(a.diag_launch, q.wave, 4);
+  CLOCKSTAMP(a.diag_launch, q.wave, 7);
 }
 
 // Phase 2 = adversarial half of sess.run(optimizer) (APR.py:130-141,156-165)
 // and SparseApplyAdagrad: loss on p+dP[u], q+dQ[i]; G = G_clean + reg_adv*G_adv;
 // Adagrad into wnew_cur.  The tables are current (flushed by phase 1).
-template <int LPR, int NV>
+template <int LPR, int NV, int TEAM>
 __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
-  constexpr int OPW = 64 / LPR;
-  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
-  const int lane = threadIdx.x & 63;
-  const int g = lane / LPR, l = lane & (LPR - 1);
-  STAMP(a.diag_launch, wave, 0);
-  if (wave >= a.S) return;
-  const int k = wave;
-  const HotCopy hc = hot_load(a, k, g);
-  const SlotRec sr = slot_header<LPR>(a, k, g);
+  const Geo<LPR, TEAM> q;
+  const int k = q.k, m = q.m, l = q.l;
+  STAMP(a.diag_launch, q.wave, 0);
+  const HotCopy hc = hot_load<TEAM>(a, k, m);
+  const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, q.leader);
   const SlotHdr& h = sr.h;
-  STAMP(a.diag_launch, wave, 1);
+  STAMP(a.diag_launch, q.wave, 1);
   if (h.count == 0) {
-    hot_store(a, k, g, l, hc);
+    hot_store<TEAM>(a, k, m, l, hc);
     return;
   }
   const int d = a.d;
   const RowV<NV> own = load_row<LPR, NV>(h.is_item ? a.Q : a.P, h.own_row, d, l);
   const RowV<NV> ownp = add_row(own, load_row<LPR, NV>(a.delta, k, d, l));
   RowV<NV> acc, G0;
-  if (g == 0) {
+  if (m == 0) {
     acc = load_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l);
     G0 = load_row<LPR, NV>(a.g0, k, d, l);
   }
   RowV<NV> G = zero_row<NV>();
-  for (int base = 0; base < h.count; base += OPW) {
-    const int idx = base + g;
+  for (int base = 0; base < h.count; base += TEAM) {
+    const int idx = base + m;
     const bool active = idx < h.count;
     RowV<NV> ra = zero_row<NV>(), rb = zero_row<NV>();
     RecV r;
     if (active) {
-      r = occ_rec(a, sr, idx, g);
+      r = occ_rec(a, sr, idx, m);
       ra = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r.pa_row(), d, l),
                    load_row<LPR, NV>(a.delta, r.pa_slot(), d, l));
       rb = add_row(load_row<LPR, NV>(a.Q, r.pb_row(), d, l),
@@ -796,25 +839,24 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
       if (active) axpy_row(G, role ? -gb : gb, ra);
     }
   }
-  STAMP(a.diag_launch, wave, 2);
-  group_allreduce<LPR, NV>(G);
-  if (g == 0) {
+  STAMP(a.diag_launch, q.wave, 2);
+  team_allreduce<LPR, TEAM, NV>(G);
+  if (m == 0) {
     axpy_row(G0, a.reg_adv, G);
     RowV<NV> wout;
     adagrad_row(a, G0, own, acc, h.count, wout);
     store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
     store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
   }
-  hot_store(a, k, g, l, hc);
-  STAMP(a.diag_launch, wave, 4);
+  hot_store<TEAM>(a, k, m, l, hc);
+  STAMP(a.diag_launch, q.wave, 4);
 }
 
-// Flush the pending rows of batch t (wnew_cur) to the tables (end of a call).
-template <int LPR, int NV>
+// Flush the pending rows of batch t (wnew_cur) to the tables (end of a call):
+// one wave per slot.
 __global__ void __launch_bounds__(256) k_flush(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
-  if (wave >= a.S) return;
-  flush_slot<LPR, NV>(a, a.t, a.wnew_cur, wave);
+  flush_slot(a, a.t, a.wnew_cur, wave, threadIdx.x & 63, 64);
 }
 
 __global__ void k_delta_scatter(StepArgs a, float* __restrict__ dP, float* __restrict__ dQ) {
@@ -1078,7 +1120,7 @@ __global__ void __launch_bounds__(256) k_dns_select(const float* __restrict__ P,
 struct GraphKey {
   const void* ptrs[4];
   acf_apr_hparams hp;
-  int32_t first, n, B, d;
+  int32_t first, n, B, d, mapping, pad;
   bool operator<(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
 
@@ -1104,6 +1146,7 @@ struct acf_apr_ctx {
   // state
   int32_t B = 0, nb = 0, gen = 0;
   int32_t last_delta_batch = -1;
+  int32_t mapping = 0;  // slot mapping, see get_kernels
   hipStream_t cap_stream = nullptr;
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<void*> allocs;
@@ -1335,20 +1378,35 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
 }
 
 // kernel kinds for timing: 0 = phase-1 (clean, or fused BPR), 1 = adversarial, 2 = flush
-template <int LPR, int NV>
-static void kernel_ptrs(void** k0_apr, void** k0_bpr, void** k1, void** k2) {
-  *k0_apr = reinterpret_cast<void*>(&k_clean<LPR, NV, false>);
-  *k0_bpr = reinterpret_cast<void*>(&k_clean<LPR, NV, true>);
-  *k1 = reinterpret_cast<void*>(&k_adv<LPR, NV>);
-  *k2 = reinterpret_cast<void*>(&k_flush<LPR, NV>);
-}
-
 struct Kernels {
   void *clean_apr = nullptr, *clean_bpr = nullptr, *adv = nullptr, *flush = nullptr;
+  int slots_per_wave = 1;
 };
 
-static int get_kernels(int d, Kernels* k) {
-  return DISPATCH_GEOM(d, kernel_ptrs, &k->clean_apr, &k->clean_bpr, &k->adv, &k->flush);
+template <int LPR, int NV>
+static void kernel_ptrs(Kernels* k, int packed) {
+  constexpr int OPW = 64 / LPR;
+  if (packed && OPW > 1) {
+    k->clean_apr = reinterpret_cast<void*>(&k_clean<LPR, NV, false, 1>);
+    k->clean_bpr = reinterpret_cast<void*>(&k_clean<LPR, NV, true, 1>);
+    k->adv = reinterpret_cast<void*>(&k_adv<LPR, NV, 1>);
+    k->slots_per_wave = OPW;
+  } else {
+    k->clean_apr = reinterpret_cast<void*>(&k_clean<LPR, NV, false, OPW>);
+    k->clean_bpr = reinterpret_cast<void*>(&k_clean<LPR, NV, true, OPW>);
+    k->adv = reinterpret_cast<void*>(&k_adv<LPR, NV, OPW>);
+    k->slots_per_wave = 1;
+  }
+  k->flush = reinterpret_cast<void*>(&k_flush);
+}
+
+// slot mapping: 0 auto (packed for batches >= ACF_PACKED_MIN_BATCH), 1 one wave
+// per slot, 2 one lane-group per slot
+#define ACF_PACKED_MIN_BATCH 4096
+
+static int get_kernels(const acf_apr_ctx* c, Kernels* k) {
+  const int packed = c->mapping == 2 || (c->mapping == 0 && c->B >= ACF_PACKED_MIN_BATCH);
+  return DISPATCH_GEOM(c->d, kernel_ptrs, k, packed);
 }
 
 typedef void (*StepKernel)(StepArgs);
@@ -1380,8 +1438,9 @@ static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hp
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                     int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds) {
   Kernels K;
-  ACF_RET(get_kernels(c->d, &K));
+  ACF_RET(get_kernels(c, &K));
   const int S = 3 * c->B;
+  const int SW = (S + K.slots_per_wave - 1) / K.slots_per_wave;  // waves of a step kernel
   int li = 0;
   auto L = [&](void* fn, const StepArgs& a, int waves, int kind) -> int {
     hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
@@ -1399,10 +1458,10 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     if (hp->adver) {
       StepArgs a1 = a;
       a1.write_hot = 0;
-      ACF_RET(L(K.clean_apr, a1, S, 0));
-      ACF_RET(L(K.adv, a, S, 1));
+      ACF_RET(L(K.clean_apr, a1, SW, 0));
+      ACF_RET(L(K.adv, a, SW, 1));
     } else {
-      ACF_RET(L(K.clean_bpr, a, S, 0));
+      ACF_RET(L(K.clean_bpr, a, SW, 0));
     }
   }
   ACF_RET(L(K.flush, make_args(c, tb, hp, first + n - 1, 0), S, 2));
@@ -1415,8 +1474,9 @@ extern "C" int acf_apr_delta_update(acf_apr_ctx* c, const acf_apr_tables* tb,
   ACF_CHECK(hp->adver, ACF_E_INVALID, "delta_update needs hparams.adver = 1 (APR graph)");
   hipStream_t s = static_cast<hipStream_t>(stream_);
   Kernels K;
-  ACF_RET(get_kernels(c->d, &K));
-  ACF_RET(launch(K.clean_apr, make_args(c, tb, hp, t, 0), 3 * c->B, s));
+  ACF_RET(get_kernels(c, &K));
+  const int SW = (3 * c->B + K.slots_per_wave - 1) / K.slots_per_wave;
+  ACF_RET(launch(K.clean_apr, make_args(c, tb, hp, t, 0), SW, s));
   c->last_delta_batch = t;
   return ACF_OK;
 }
@@ -1426,14 +1486,15 @@ extern "C" int acf_apr_optimizer_step(acf_apr_ctx* c, const acf_apr_tables* tb,
   ACF_RET(check_step(c, tb, hp, t));
   hipStream_t s = static_cast<hipStream_t>(stream_);
   Kernels K;
-  ACF_RET(get_kernels(c->d, &K));
+  ACF_RET(get_kernels(c, &K));
+  const int SW = (3 * c->B + K.slots_per_wave - 1) / K.slots_per_wave;
   const StepArgs a = make_args(c, tb, hp, t, 0);
   if (hp->adver) {
     ACF_CHECK(c->last_delta_batch == t, ACF_E_STATE,
               "APR optimizer step on batch %d needs acf_apr_delta_update on the same batch first", t);
-    ACF_RET(launch(K.adv, a, 3 * c->B, s));
+    ACF_RET(launch(K.adv, a, SW, s));
   } else {
-    ACF_RET(launch(K.clean_bpr, a, 3 * c->B, s));
+    ACF_RET(launch(K.clean_bpr, a, SW, s));
   }
   ACF_RET(launch(K.flush, a, 3 * c->B, s));
   return ACF_OK;
@@ -1453,7 +1514,7 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   memset(&key, 0, sizeof(key));
   key.ptrs[0] = tb->P; key.ptrs[1] = tb->Q; key.ptrs[2] = tb->accP; key.ptrs[3] = tb->accQ;
   key.hp = *hp;
-  key.first = first; key.n = n; key.B = c->B; key.d = c->d;
+  key.first = first; key.n = n; key.B = c->B; key.d = c->d; key.mapping = c->mapping;
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -1504,6 +1565,13 @@ extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
   for (auto& e : ev) (void)hipEventDestroy(e);
   c->last_delta_batch = -1;
   return r;
+}
+
+extern "C" int acf_apr_set_slot_mapping(acf_apr_ctx* c, int32_t mode) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(mode >= 0 && mode <= 2, ACF_E_INVALID, "slot mapping must be 0 (auto), 1 or 2, got %d", mode);
+  c->mapping = mode;
+  return ACF_OK;
 }
 
 extern "C" int acf_apr_copy_losses(acf_apr_ctx* c, float* lc, float* la, void* stream_) {

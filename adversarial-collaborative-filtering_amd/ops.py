@@ -147,6 +147,11 @@ class APRContext:
             call("acf_apr_train_planned", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n,
                  int(bool(graph)), _stream_ptr(self.device))
 
+    def set_slot_mapping(self, mode: str | int) -> None:
+        """'auto' | 'wave' (one wavefront per unique row) | 'group' (one lane-group per row)."""
+        m = {"auto": 0, "wave": 1, "group": 2}.get(mode, mode)
+        call("acf_apr_set_slot_mapping", self._ptr, int(m))
+
     def time_kernels(self, tables, hp: StepHParams, first: int = 0, n: int | None = None):
         """Per-kernel-kind device time (ms) and launch counts over planned batches,
         measured with start/stop events attached to each launch (tables are

@@ -138,10 +138,10 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
                                     "source": "out/janEval/ml-1m-sort_apr_..._11_56_42.out:54-55 (UCL CPU, TF1)"}}
 
 
-def large_batch_roofline(acf, ops, dev):
-    """Batch 65,536 on 10M x 5M tables (d = 128, ~15 GB incl. Adagrad slots):
+def large_batch_roofline(acf, ops, dev, d=128):
+    """Batch 65,536 on 10M x 5M tables (d = 128: ~15 GB incl. Adagrad slots):
     tables far beyond the 256 MB Infinity Cache, so rows come from HBM."""
-    U1, I1, d, B, nb = 10_000_001, 5_000_001, 128, 65536, 8
+    U1, I1, B, nb = 10_000_001, 5_000_001, 65536, 8
     g = torch.Generator(device=dev).manual_seed(5)
     u = torch.randint(0, U1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
     i = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
@@ -244,7 +244,9 @@ def main():
     if rank == 0 and a.large:
         del ctx, tctx
         torch.cuda.empty_cache()
-        out["roofline_large_batch"] = large_batch_roofline(acf, ops, dev)
+        out["roofline_large_batch"] = large_batch_roofline(acf, ops, dev, 128)
+        torch.cuda.empty_cache()
+        out["roofline_large_batch_d64"] = large_batch_roofline(acf, ops, dev, 64)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

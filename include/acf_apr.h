@@ -129,6 +129,14 @@ int acf_apr_time_kernels(acf_apr_ctx* ctx, const acf_apr_tables* tables,
                          int32_t n_batches, double* ms_out, int32_t* launches_out,
                          void* stream);
 
+/* How step kernels map unique rows ("slots") to lanes: 0 = auto (default: one
+ * wavefront per slot below 4,096 triplets per batch, where hot rows have many
+ * occurrences; one lane-group of dim/4 lanes per slot at and above it, where
+ * almost every row occurs once), 1 = one wavefront per slot, 2 = one lane-group
+ * per slot.  Results are deterministic for a given mapping and agree across
+ * mappings to fp32 summation order.  Not part of the reference surface. */
+int acf_apr_set_slot_mapping(acf_apr_ctx* ctx, int32_t mode);
+
 /* Per-triplet clean / adversarial losses computed by the last step of each
  * planned batch (softplus(-clip(x)) terms of APR.py:150,162), for the staged
  * triplets [0, n_batches*batch_size).  Either pointer may be NULL. */

@@ -49,16 +49,18 @@ def _close(got, want, name):
     np.testing.assert_allclose(got, want, rtol=RTOL, atol=ATOL, err_msg=name)
 
 
-@pytest.mark.parametrize("d", [8, 32, 64, 128])
+@pytest.mark.parametrize("d", [8, 32, 64, 128, 256, 512])
 @pytest.mark.parametrize("adver", [0, 1])
 @pytest.mark.parametrize("graph", [False, True])
-def test_train_planned_matches_oracle(ops, oracle, dev, d, adver, graph):
+@pytest.mark.parametrize("mapping", ["wave", "group"])
+def test_train_planned_matches_oracle(ops, oracle, dev, d, adver, graph, mapping):
     U1, I1, B, nb = 61, 47, 64, 4
     P, Q, u, i, j = _problem(d * 10 + adver, U1, I1, d, B, nb, dup_items=True)
     hp_c = HParams(adver=adver)
     want, lc_w, la_w, _ = _oracle_run(oracle, P, Q, u, i, j, B, hp_c)
     tabs = _gpu_tables(P, Q, dev)
     ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_slot_mapping(mapping)
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ctx.train_planned(tabs, ops.StepHParams(adver=adver), graph=graph)
     lc, la = ctx.losses()
@@ -288,7 +290,8 @@ def test_full_size_ml1m_epoch_deterministic(ops, acf, dev):
 
 
 @pytest.mark.parametrize("adver", [0, 1])
-def test_piecewise_calls_equal_one_call(ops, oracle, dev, adver):
+@pytest.mark.parametrize("mapping", ["wave", "group"])
+def test_piecewise_calls_equal_one_call(ops, oracle, dev, adver, mapping):
     """train_planned over [0,2)+[2,5) and per-batch optimizer_step == one call,
     and all match the oracle (exercises the deferred flush across calls)."""
     U1, I1, d, B, nb = 40, 35, 64, 32, 5
@@ -296,6 +299,7 @@ def test_piecewise_calls_equal_one_call(ops, oracle, dev, adver):
     want, *_ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=adver))
     hp = ops.StepHParams(adver=adver)
     ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_slot_mapping(mapping)
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     a = _gpu_tables(P, Q, dev)
     ctx.train_planned(a, hp, 0, 2, graph=True)
@@ -311,14 +315,16 @@ def test_piecewise_calls_equal_one_call(ops, oracle, dev, adver):
         _close(x, w, n)
 
 
-def test_hot_rows_many_occurrences(ops, oracle, dev):
+@pytest.mark.parametrize("mapping", ["wave", "group"])
+def test_hot_rows_many_occurrences(ops, oracle, dev, mapping):
     """A few rows with hundreds of occurrences per batch (overflow records,
-    many rounds per wave) still match the oracle."""
+    many rounds per wave / group) still match the oracle."""
     U1, I1, d, B, nb = 12, 9, 64, 1024, 2
     P, Q, u, i, j = _problem(23, U1, I1, d, B, nb)
     want, *_ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=1))
     tabs = _gpu_tables(P, Q, dev)
     ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_slot_mapping(mapping)
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ctx.train_planned(tabs, ops.StepHParams(adver=1))
     for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
@@ -340,3 +346,22 @@ def test_replan_reuses_graph(ops, oracle, dev):
         ctx.train_planned(tabs, hp, 0, nb, graph=True)
     for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
         _close(g, w, n)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_large_batch_auto_mapping_matches_oracle(ops, oracle, dev, d):
+    """B = 8,192 (auto -> one lane-group per slot) on 200k x 100k tables."""
+    U1, I1, B, nb = 200_000, 100_000, 8192, 2
+    rng = np.random.default_rng(d)
+    P = (rng.standard_normal((U1, d)) * 0.1).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.1).astype(np.float32)
+    u = rng.integers(0, U1, nb * B).astype(np.int32)
+    i = (rng.zipf(1.3, nb * B) % I1).astype(np.int32)
+    j = rng.integers(0, I1, nb * B).astype(np.int32)
+    want, *_ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=1))
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ctx.train_planned(tabs, ops.StepHParams(adver=1))
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        np.testing.assert_allclose(g.cpu().numpy(), w, rtol=1e-4, atol=1e-6, err_msg=n)

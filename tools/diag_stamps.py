@@ -90,6 +90,15 @@ def main():
             v = [r["seg_median_ns"].get(key) for r in out["launches"][par:-1:2] if r["seg_median_ns"]]
             if v:
                 summary[f"{key}_{name}_ns"] = float(np.median(v))
+    # shader clock during phase-1 waves: d(s_memtime) / d(s_memrealtime) * 100 MHz
+    clk = []
+    for li in range(0, n_launch - 1, 2):
+        w = st[li]
+        ok = (w[:, 4] > 0) & (w[:, 7] > w[:, 6])
+        if ok.any():
+            clk.append(np.median((w[ok, 7] - w[ok, 6]) / np.maximum(w[ok, 4] - w[ok, 0], 1)) * 100.0)
+    if clk:
+        summary["shader_clock_MHz_median"] = float(np.median(clk))
     print(json.dumps(summary, indent=1))
     with open(os.path.join(REPO, "gpurun_out", f"diag_g{int(graph)}_a{hp.adver}.json"), "w") as f:
         json.dump(out, f, indent=1)
