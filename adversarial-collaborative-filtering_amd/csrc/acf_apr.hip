@@ -300,7 +300,8 @@ __global__ void k_compact(const uint64_t* __restrict__ key, const int32_t* __res
 // flush to the table happens inside batch t's first kernel), so the plan encodes
 // src = ~(local slot in batch t-1) for them and src = row otherwise.
 // user local slot = g - ubs[t]; item local slot = nU(t) + g - ibs[t].
-__global__ void k_prev_src(const int32_t* __restrict__ uniq, const int32_t* __restrict__ bofs,
+// nxt[g] = 1 when batch t+1 touches the row too.
+__global__ void k_prev_src(const int32_t* __restrict__ uniq, int32_t* __restrict__ nxt,
                            const int32_t* __restrict__ ubs, const int32_t* __restrict__ bstart,
                            int32_t n_uniq, int32_t nb, int32_t item_side,
                            int32_t* __restrict__ src) {
@@ -328,7 +329,16 @@ __global__ void k_prev_src(const int32_t* __restrict__ uniq, const int32_t* __re
     }
   }
   src[g] = s;
-  (void)bofs;
+  int32_t in_next = 0;
+  if (t + 1 < nb) {
+    int a = bstart[t + 1], b = bstart[t + 2];
+    while (a < b) {
+      int mid = (a + b) >> 1;
+      if (uniq[mid] < row) a = mid + 1; else b = mid;
+    }
+    in_next = (a < bstart[t + 2] && uniq[a] == row) ? 1 : 0;
+  }
+  nxt[g] = in_next;
 }
 
 // Occurrence record: everything one lane-group needs to process one occurrence
@@ -352,7 +362,42 @@ struct __align__(16) OccRec {
   int32_t gen;
 };
 #define ACF_ITEM_BIT (1 << 28)
+#define ACF_SINGLE_BIT (1 << 29)   // the slot's only occurrence is a fused triplet
+#define ACF_INPLACE_BIT (1 << 30)  // the fused triplet writes this row to the table itself
 #define ACF_COUNT_MASK ((1 << 28) - 1)
+
+// A triplet is FUSED when its user, positive and negative item each occur once
+// in the batch (so i != j): its rows' batch-aggregated gradients are its own
+// contributions, and the whole APR step for it runs in one lane-group with no
+// batch-wide reduction (k_single).  A fused row is written straight to its table
+// ("in place") unless the next batch touches it or it is pending from the
+// previous batch; otherwise it goes through the W scratch like any other row.
+struct FuseInfo {
+  int fused, in_u, in_i, in_j;
+};
+
+__device__ __forceinline__ FuseInfo fuse_info(int32_t e, const int32_t* __restrict__ uslot,
+                                              const int32_t* __restrict__ pslot,
+                                              const int32_t* __restrict__ nslot,
+                                              const int32_t* __restrict__ uoff,
+                                              const int32_t* __restrict__ ioff,
+                                              const int32_t* __restrict__ usrc,
+                                              const int32_t* __restrict__ isrc,
+                                              const int32_t* __restrict__ unxt,
+                                              const int32_t* __restrict__ inxt) {
+  const int32_t gu = uslot[e], gi = pslot[e], gj = nslot[e];
+  FuseInfo f;
+  f.fused = (uoff[gu + 1] - uoff[gu]) == 1 && (ioff[gi + 1] - ioff[gi]) == 1 &&
+            (ioff[gj + 1] - ioff[gj]) == 1;
+  f.in_u = f.fused && usrc[gu] >= 0 && !unxt[gu];
+  f.in_i = f.fused && isrc[gi] >= 0 && !inxt[gi];
+  f.in_j = f.fused && isrc[gj] >= 0 && !inxt[gj];
+  return f;
+}
+
+// Fused-triplet record (same 48-B shape as OccRec; fields by position):
+//  a = {u, i, j, local slot of u}, b = {slot i, slot j, src u, src i},
+//  c = {src j, flags (1 fused | 2 in-place u | 4 in-place i | 8 in-place j), e, gen}
 
 __global__ void k_records(const int32_t* __restrict__ uocc, const int32_t* __restrict__ iocc,
                           int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen,
@@ -363,8 +408,10 @@ __global__ void k_records(const int32_t* __restrict__ uocc, const int32_t* __res
                           const int32_t* __restrict__ ubs, const int32_t* __restrict__ usrc,
                           const int32_t* __restrict__ iuniq, const int32_t* __restrict__ ioff,
                           const int32_t* __restrict__ ibs, const int32_t* __restrict__ isrc,
+                          const int32_t* __restrict__ unxt, const int32_t* __restrict__ inxt,
                           OccRec* __restrict__ urec, OccRec* __restrict__ irec,
-                          OccRec* __restrict__ inl, int32_t* __restrict__ gen_ptr) {
+                          OccRec* __restrict__ inl, OccRec* __restrict__ trec,
+                          int32_t* __restrict__ gen_ptr) {
   const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x == 0) *gen_ptr = gen;
   if (x < E) {
@@ -372,10 +419,11 @@ __global__ void k_records(const int32_t* __restrict__ uocc, const int32_t* __res
     const int32_t g = uslot[e];
     const int32_t t = e / B;
     const int32_t nU = ubs[t + 1] - ubs[t];
+    const FuseInfo f = fuse_info(e, uslot, pslot, nslot, uoff, ioff, usrc, isrc, unxt, inxt);
     OccRec r;
     r.own_row = uuniq[g];
     r.own_src = usrc[g];
-    r.meta = uoff[g + 1] - uoff[g];
+    r.meta = (uoff[g + 1] - uoff[g]) | (f.fused ? ACF_SINGLE_BIT : 0) | (f.in_u ? ACF_INPLACE_BIT : 0);
     r.ovf = uoff[g];
     r.e_role = e;
     r.pa_row = ti[e];
@@ -389,6 +437,15 @@ __global__ void k_records(const int32_t* __restrict__ uocc, const int32_t* __res
     const int32_t k = g - ubs[t];
     const int32_t rr = (int32_t)(x - uoff[g]);
     if (rr < R) inl[((int64_t)t * S + k) * R + rr] = r;
+    // the triplet's fused record (one per triplet: written by its user occurrence)
+    OccRec q;
+    q.own_row = tu[e]; q.own_src = ti[e]; q.meta = tj[e]; q.ovf = k;
+    q.e_role = nU + (pslot[e] - ibs[t]); q.pa_row = nU + (nslot[e] - ibs[t]);
+    q.pb_row = usrc[g]; q.pa_src = isrc[pslot[e]];
+    q.pb_src = isrc[nslot[e]];
+    q.pa_slot = (f.fused ? 1 : 0) | (f.in_u ? 2 : 0) | (f.in_i ? 4 : 0) | (f.in_j ? 8 : 0);
+    q.pb_slot = e; q.gen = gen;
+    trec[e] = q;
   }
   if (x < 2 * E) {
     const int32_t v = iocc[x];
@@ -397,10 +454,13 @@ __global__ void k_records(const int32_t* __restrict__ uocc, const int32_t* __res
     const int32_t og = role ? pslot[e] : nslot[e];
     const int32_t t = e / B;
     const int32_t nU = ubs[t + 1] - ubs[t];
+    const FuseInfo f = fuse_info(e, uslot, pslot, nslot, uoff, ioff, usrc, isrc, unxt, inxt);
+    const int in_place = role ? f.in_j : f.in_i;
     OccRec r;
     r.own_row = iuniq[g];
     r.own_src = isrc[g];
-    r.meta = (ioff[g + 1] - ioff[g]) | ACF_ITEM_BIT;
+    r.meta = (ioff[g + 1] - ioff[g]) | ACF_ITEM_BIT | (f.fused ? ACF_SINGLE_BIT : 0) |
+             (in_place ? ACF_INPLACE_BIT : 0);
     r.ovf = ioff[g];
     r.e_role = v;
     r.pa_row = tu[e];
@@ -472,6 +532,7 @@ struct StepArgs {
   OccRec* hot_next;       // [S][R] where this batch's last kernel copies batch t+1's
   const OccRec* urec;  // CSR, user occurrences
   const OccRec* irec;  // CSR, item occurrences
+  const OccRec* trec;  // [E] fused-triplet records (see fuse_info)
   float* g0;           // [S, d] clean-loss gradient per slot
   float* delta;        // [S, d] delta per slot
   float* wnew_cur;     // [S, d] updated rows of batch t
@@ -484,6 +545,8 @@ struct StepArgs {
   int32_t diag_launch; // diagnostic build: stamp slot of this launch
   int32_t use_hot;     // phase 1 reads its slot records from hot_cur
   int32_t write_hot;   // the batch's last kernel copies batch t+1's records to hot_next
+  int32_t use_single;  // fused triplets run in k_single waves; their slots are skipped
+  int32_t slot_waves;  // waves [0, slot_waves) are slot waves, the rest fused-triplet waves
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -570,7 +633,8 @@ __device__ __forceinline__ SlotRec slot_header(const StepArgs& a, int k, int m, 
                               : a.inl + ((int64_t)a.t * a.S + k) * a.R + m);
   s.r0_valid = s.r0.gen() == gen;
   const int32_t meta = __shfl(s.r0_valid ? s.r0.meta() : 0, leader_lane, 64);
-  s.h.count = meta & ACF_COUNT_MASK;
+  // a fused triplet's slots are handled by its k_single lane-group
+  s.h.count = (a.use_single && (meta & ACF_SINGLE_BIT)) ? 0 : (meta & ACF_COUNT_MASK);
   s.h.is_item = (meta & ACF_ITEM_BIT) != 0;
   s.h.own_row = __shfl(s.r0.own_row(), leader_lane, 64);
   s.h.own_src = __shfl(s.r0.own_src(), leader_lane, 64);
@@ -618,6 +682,7 @@ __device__ __forceinline__ void flush_slot(const StepArgs& a, int tb, const floa
   if (k >= a.S) return;
   const RecV r = load_rec(a.inl + ((int64_t)tb * a.S + k) * a.R);
   if (r.gen() != *a.gen_ptr || (r.meta() & ACF_COUNT_MASK) == 0) return;
+  if (a.use_single && (r.meta() & ACF_INPLACE_BIT)) return;  // written by its fused triplet
   float* dst = ((r.meta() & ACF_ITEM_BIT) ? a.Q : a.P) + (int64_t)r.own_row() * a.d;
   const float* src = wsrc + (int64_t)k * a.d;
   for (int c = tl; c * 4 < a.d; c += tn)
@@ -683,13 +748,112 @@ struct Geo {
   }
 };
 
+// delta of one row from its batch-summed clean gradient G (APR.py:180-191)
+template <int LPR, int NV>
+__device__ __forceinline__ RowV<NV> make_delta(const StepArgs& a, const RowV<NV>& G, int is_item,
+                                               int32_t row, int l) {
+  if (a.zero_delta) return zero_row<NV>();
+  if (a.adv_mode == 0) {
+    // tf.nn.l2_normalize(g, 1) * eps  (epsilon 1e-12 on the squared norm)
+    const float ss = dot_row<LPR, NV>(G, G);
+    const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
+    return scale_row(scale_row(G, inv), a.eps);
+  }
+  // "random": l2_normalize(truncated_normal(0, 0.01)) * eps, redrawn every run
+  RowV<NV> z;
+  const uint64_t rk = mix64(a.seed ^ mix64(((uint64_t)a.t << 1) | (is_item ? 1 : 0))) ^
+                      mix64((uint64_t)row * 0x100000001B3ull);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = l + LPR * v;
+    float e4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      e4[e] = (c * 4 + e < a.d) ? trunc_normal(rk ^ mix64((uint64_t)(c * 4 + e)), 0.01f) : 0.f;
+    z.v[v] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+  }
+  const float ss = dot_row<LPR, NV>(z, z);
+  const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
+  return scale_row(scale_row(z, inv), a.eps);
+}
+
+// A fused triplet (fuse_info): its whole step in one lane-group.  The operation
+// sequence per row is the one the slot kernels execute for a row with a single
+// occurrence (same products, same rounding order), so fused and slot paths give
+// identical bits.  ADV (APR graph, inside k_adv): the tables are current and
+// the row goes clean -> delta -> adversarial -> Adagrad; otherwise (BPR graph,
+// inside k_clean<FUSE_APPLY>) rows are read through their batch-start source and
+// the clean gradient is applied.
+template <int LPR, int NV, bool ADV>
+__device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
+  if (b >= a.B) return;
+  const int64_t e = (int64_t)a.t * a.B + b;
+  const RecV r = load_rec(a.trec + e);
+  if (r.c.w != *a.gen_ptr || !(r.c.y & 1)) return;
+  const int d = a.d;
+  const int32_t u = r.a.x, i = r.a.y, j = r.a.z, flags = r.c.y;
+  RowV<NV> p, qi, qj;
+  if (ADV) {
+    p = load_row<LPR, NV>(a.P, u, d, l);
+    qi = load_row<LPR, NV>(a.Q, i, d, l);
+    qj = load_row<LPR, NV>(a.Q, j, d, l);
+  } else {
+    p = load_at<LPR, NV>(row_src(a, a.P, u, r.b.z), d, l);
+    qi = load_at<LPR, NV>(row_src(a, a.Q, i, r.b.w), d, l);
+    qj = load_at<LPR, NV>(row_src(a, a.Q, j, r.c.x), d, l);
+  }
+  RowV<NV> cu = load_row<LPR, NV>(a.accP, u, d, l);
+  RowV<NV> ci = load_row<LPR, NV>(a.accQ, i, d, l);
+  RowV<NV> cj = load_row<LPR, NV>(a.accQ, j, d, l);
+  float g, loss;
+  bpr_term(dot_row<LPR, NV>(p, qi) - dot_row<LPR, NV>(p, qj), a.clip_lo, a.clip_hi, g, loss);
+  if (l == 0) a.loss_clean[e] = loss;
+  RowV<NV> Gu = zero_row<NV>(), Gi = zero_row<NV>(), Gj = zero_row<NV>();
+  axpy_row(Gu, g, qi);
+  axpy_row(Gu, -g, qj);
+  axpy_row(Gi, g, p);
+  axpy_row(Gj, -g, p);
+  if (ADV) {
+    const RowV<NV> pp = add_row(p, make_delta<LPR, NV>(a, Gu, 0, u, l));
+    const RowV<NV> qip = add_row(qi, make_delta<LPR, NV>(a, Gi, 1, i, l));
+    const RowV<NV> qjp = add_row(qj, make_delta<LPR, NV>(a, Gj, 1, j, l));
+    float ga, la;
+    bpr_term(dot_row<LPR, NV>(pp, qip) - dot_row<LPR, NV>(pp, qjp), a.clip_lo, a.clip_hi, ga, la);
+    if (l == 0) a.loss_adv[e] = la;
+    RowV<NV> Au = zero_row<NV>(), Ai = zero_row<NV>(), Aj = zero_row<NV>();
+    axpy_row(Au, ga, qip);
+    axpy_row(Au, -ga, qjp);
+    axpy_row(Ai, ga, pp);
+    axpy_row(Aj, -ga, pp);
+    axpy_row(Gu, a.reg_adv, Au);
+    axpy_row(Gi, a.reg_adv, Ai);
+    axpy_row(Gj, a.reg_adv, Aj);
+  }
+  RowV<NV> wu, wi, wj;
+  adagrad_row(a, Gu, p, cu, 1, wu);
+  adagrad_row(a, Gi, qi, ci, 1, wi);
+  adagrad_row(a, Gj, qj, cj, 1, wj);
+  store_row<LPR, NV>(a.accP, u, d, l, cu);
+  store_row<LPR, NV>(a.accQ, i, d, l, ci);
+  store_row<LPR, NV>(a.accQ, j, d, l, cj);
+  // in place unless the row is pending from batch t-1 or read by batch t+1
+  store_row<LPR, NV>((flags & 2) ? a.P : a.wnew_cur, (flags & 2) ? u : r.a.w, d, l, wu);
+  store_row<LPR, NV>((flags & 4) ? a.Q : a.wnew_cur, (flags & 4) ? i : r.b.x, d, l, wi);
+  store_row<LPR, NV>((flags & 8) ? a.Q : a.wnew_cur, (flags & 8) ? j : r.b.y, d, l, wj);
+}
+
 // Phase 1 = sess.run([update_P, update_Q]) (APR.py:180-191) and the clean half
 // of the optimizer: clean-loss gradient of every unique row of batch t summed
 // over its occurrences, its delta (APR graph), or — BPR graph, FUSE_APPLY — the
 // Adagrad update straight away.  The team also writes back slot k of batch t-1.
-template <int LPR, int NV, bool FUSE_APPLY, int TEAM>
+template <int LPR, int NV, bool FUSE_APPLY, int TEAM, bool SINGLE = false>
 __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
   const Geo<LPR, TEAM> q;
+  if (SINGLE && FUSE_APPLY && q.wave >= a.slot_waves) {
+    k_single<LPR, NV, false>(a, (q.wave - a.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR,
+                             q.l);
+    return;
+  }
   const int k = q.k, m = q.m, l = q.l;
   STAMP(a.diag_launch, q.wave, 0);
   CLOCKSTAMP(a.diag_launch, q.wave, 6);
@@ -750,32 +914,7 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
     hot_store<TEAM>(a, k, m, l, hc);
     return;
   }
-  RowV<NV> dl;
-  if (a.zero_delta) {
-    dl = zero_row<NV>();
-  } else if (a.adv_mode == 0) {
-    // tf.nn.l2_normalize(g, 1) * eps  (epsilon 1e-12 on the squared norm)
-    const float ss = dot_row<LPR, NV>(G, G);
-    const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
-    dl = scale_row(scale_row(G, inv), a.eps);
-  } else {
-    // "random": l2_normalize(truncated_normal(0, 0.01)) * eps, redrawn every run
-    RowV<NV> z;
-    const uint64_t rk = mix64(a.seed ^ mix64(((uint64_t)a.t << 1) | (h.is_item ? 1 : 0))) ^
-                        mix64((uint64_t)h.own_row * 0x100000001B3ull);
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = l + LPR * v;
-      float e4[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        e4[e] = (c * 4 + e < d) ? trunc_normal(rk ^ mix64((uint64_t)(c * 4 + e)), 0.01f) : 0.f;
-      z.v[v] = make_float4(e4[0], e4[1], e4[2], e4[3]);
-    }
-    const float ss = dot_row<LPR, NV>(z, z);
-    const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
-    dl = scale_row(scale_row(z, inv), a.eps);
-  }
+  const RowV<NV> dl = make_delta<LPR, NV>(a, G, h.is_item, h.own_row, l);
   STAMP(a.diag_launch, q.wave, 3);
   if (m == 0) {
     store_row<LPR, NV>(a.g0, k, d, l, G);
@@ -788,9 +927,14 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
 // Phase 2 = adversarial half of sess.run(optimizer) (APR.py:130-141,156-165)
 // and SparseApplyAdagrad: loss on p+dP[u], q+dQ[i]; G = G_clean + reg_adv*G_adv;
 // Adagrad into wnew_cur.  The tables are current (flushed by phase 1).
-template <int LPR, int NV, int TEAM>
+template <int LPR, int NV, int TEAM, bool SINGLE = false>
 __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
   const Geo<LPR, TEAM> q;
+  if (SINGLE && q.wave >= a.slot_waves) {
+    k_single<LPR, NV, true>(a, (q.wave - a.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR,
+                            q.l);
+    return;
+  }
   const int k = q.k, m = q.m, l = q.l;
   STAMP(a.diag_launch, q.wave, 0);
   const HotCopy hc = hot_load<TEAM>(a, k, m);
@@ -1120,7 +1264,7 @@ __global__ void __launch_bounds__(256) k_dns_select(const float* __restrict__ P,
 struct GraphKey {
   const void* ptrs[4];
   acf_apr_hparams hp;
-  int32_t first, n, B, d, mapping, pad;
+  int32_t first, n, B, d, mapping, fusion;
   bool operator<(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
 
@@ -1136,6 +1280,8 @@ struct acf_apr_ctx {
   int32_t *uuniq = nullptr, *uoff = nullptr, *ubs = nullptr, *uocc = nullptr, *uslot = nullptr;
   int32_t *iuniq = nullptr, *ioff = nullptr, *ibs = nullptr, *iocc = nullptr;
   int32_t *pslot = nullptr, *nslot = nullptr, *usrc = nullptr, *isrc = nullptr;
+  int32_t *unxt = nullptr, *inxt = nullptr;
+  OccRec* trec = nullptr;
   OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr, *hot[2] = {nullptr, nullptr};
   int32_t *err = nullptr, *gen_dev = nullptr;
   void* tmp = nullptr;
@@ -1147,6 +1293,7 @@ struct acf_apr_ctx {
   int32_t B = 0, nb = 0, gen = 0;
   int32_t last_delta_batch = -1;
   int32_t mapping = 0;  // slot mapping, see get_kernels
+  int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
   hipStream_t cap_stream = nullptr;
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<void*> allocs;
@@ -1259,7 +1406,8 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->uslot, maxE); A(&c->usrc, maxE);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1); A(&c->iocc, 2 * maxE);
   A(&c->pslot, maxE); A(&c->nslot, maxE); A(&c->isrc, 2 * maxE);
-  A(&c->urec, maxE); A(&c->irec, 2 * maxE);
+  A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
+  A(&c->unxt, maxE); A(&c->inxt, 2 * maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
   A(&c->hot[0], S * c->R); A(&c->hot[1], S * c->R);
   A(&c->err, 4); A(&c->gen_dev, 4);
@@ -1333,13 +1481,13 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   k_compact<<<grid_for(2 * E), 256, 0, s>>>(c->ikey_out, c->inc, 2 * E, ob_i, (1ull << ob_i) - 1, c->I1,
                                             nb, c->iuniq, c->ioff, c->ibs, c->iocc, c->pslot, c->nslot, 1);
   // where each unique row's value lives at batch start, then the records
-  k_prev_src<<<grid_for(E), 256, 0, s>>>(c->uuniq, nullptr, c->ubs, c->ubs, (int32_t)E, nb, 0, c->usrc);
-  k_prev_src<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, nullptr, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
+  k_prev_src<<<grid_for(E), 256, 0, s>>>(c->uuniq, c->unxt, c->ubs, c->ubs, (int32_t)E, nb, 0, c->usrc);
+  k_prev_src<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, c->inxt, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
                                               c->isrc);
   k_records<<<grid_for(2 * E), 256, 0, s>>>(c->uocc, c->iocc, E, B, 3 * B, c->R, gen, c->tu, c->ti, c->tj,
                                             c->uslot, c->pslot, c->nslot, c->uuniq, c->uoff, c->ubs,
-                                            c->usrc, c->iuniq, c->ioff, c->ibs, c->isrc, c->urec,
-                                            c->irec, c->inl, c->gen_dev);
+                                            c->usrc, c->iuniq, c->ioff, c->ibs, c->isrc, c->unxt,
+                                            c->inxt, c->urec, c->irec, c->inl, c->trec, c->gen_dev);
   HIP_TRY(hipGetLastError());
   if (check) {
     int32_t herr = 0;
@@ -1358,7 +1506,9 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
                           int32_t t, int32_t prev_valid) {
   StepArgs a;
   a.P = tb->P; a.Q = tb->Q; a.accP = tb->accP; a.accQ = tb->accQ;
-  a.inl = c->inl; a.urec = c->urec; a.irec = c->irec;
+  a.inl = c->inl; a.urec = c->urec; a.irec = c->irec; a.trec = c->trec;
+  a.use_single = 0;
+  a.slot_waves = 1 << 30;  // set by the launcher
   a.hot_cur = c->hot[t & 1];
   a.hot_next = c->hot[(t + 1) & 1];
   a.use_hot = 0;
@@ -1383,18 +1533,27 @@ struct Kernels {
   int slots_per_wave = 1;
 };
 
+template <int LPR, int NV, int TEAM>
+static void kernel_ptrs_team(Kernels* k, int fused) {
+  k->clean_apr = reinterpret_cast<void*>(&k_clean<LPR, NV, false, TEAM>);
+  if (fused) {
+    k->clean_bpr = reinterpret_cast<void*>(&k_clean<LPR, NV, true, TEAM, true>);
+    k->adv = reinterpret_cast<void*>(&k_adv<LPR, NV, TEAM, true>);
+  } else {
+    k->clean_bpr = reinterpret_cast<void*>(&k_clean<LPR, NV, true, TEAM>);
+    k->adv = reinterpret_cast<void*>(&k_adv<LPR, NV, TEAM>);
+  }
+}
+
+// fused: the phase-2 (APR) / fused-BPR kernels also run the fused-triplet waves
 template <int LPR, int NV>
-static void kernel_ptrs(Kernels* k, int packed) {
+static void kernel_ptrs(Kernels* k, int packed, int fused) {
   constexpr int OPW = 64 / LPR;
   if (packed && OPW > 1) {
-    k->clean_apr = reinterpret_cast<void*>(&k_clean<LPR, NV, false, 1>);
-    k->clean_bpr = reinterpret_cast<void*>(&k_clean<LPR, NV, true, 1>);
-    k->adv = reinterpret_cast<void*>(&k_adv<LPR, NV, 1>);
+    kernel_ptrs_team<LPR, NV, 1>(k, fused);
     k->slots_per_wave = OPW;
   } else {
-    k->clean_apr = reinterpret_cast<void*>(&k_clean<LPR, NV, false, OPW>);
-    k->clean_bpr = reinterpret_cast<void*>(&k_clean<LPR, NV, true, OPW>);
-    k->adv = reinterpret_cast<void*>(&k_adv<LPR, NV, OPW>);
+    kernel_ptrs_team<LPR, NV, OPW>(k, fused);
     k->slots_per_wave = 1;
   }
   k->flush = reinterpret_cast<void*>(&k_flush);
@@ -1404,9 +1563,9 @@ static void kernel_ptrs(Kernels* k, int packed) {
 // per slot, 2 one lane-group per slot
 #define ACF_PACKED_MIN_BATCH 4096
 
-static int get_kernels(const acf_apr_ctx* c, Kernels* k) {
+static int get_kernels(const acf_apr_ctx* c, Kernels* k, int fused = 0) {
   const int packed = c->mapping == 2 || (c->mapping == 0 && c->B >= ACF_PACKED_MIN_BATCH);
-  return DISPATCH_GEOM(c->d, kernel_ptrs, k, packed);
+  return DISPATCH_GEOM(c->d, kernel_ptrs, k, packed, fused);
 }
 
 typedef void (*StepKernel)(StepArgs);
@@ -1415,6 +1574,8 @@ typedef void (*StepKernel)(StepArgs);
 static int launch(void* fn, const StepArgs& a, int waves, hipStream_t s, hipEvent_t e0 = nullptr,
                   hipEvent_t e1 = nullptr) {
   const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+  // waves past slot_waves run fused triplets: only when fusion is on
+  if (!a.use_single && a.slot_waves < waves) return set_error(ACF_E_STATE, "bad step geometry");
   if (e0)
     hipExtLaunchKernelGGL(reinterpret_cast<StepKernel>(fn), grid, block, 0, s, e0, e1, 0, a);
   else
@@ -1438,9 +1599,11 @@ static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hp
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                     int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds) {
   Kernels K;
-  ACF_RET(get_kernels(c, &K));
+  ACF_RET(get_kernels(c, &K, c->fusion));
   const int S = 3 * c->B;
-  const int SW = (S + K.slots_per_wave - 1) / K.slots_per_wave;  // waves of a step kernel
+  const int SW = (S + K.slots_per_wave - 1) / K.slots_per_wave;  // slot waves of a step kernel
+  const int fuse = c->fusion;
+  const int TW = fuse ? (c->B + 64 / c->lpr - 1) / (64 / c->lpr) : 0;  // fused-triplet waves
   int li = 0;
   auto L = [&](void* fn, const StepArgs& a, int waves, int kind) -> int {
     hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
@@ -1455,16 +1618,21 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     StepArgs a = make_args(c, tb, hp, t, pv);
     a.use_hot = pv;                       // batch t-1's last kernel copied our records
     a.write_hot = t + 1 < first + n ? 1 : 0;
+    a.use_single = fuse;
+    a.slot_waves = SW;
     if (hp->adver) {
       StepArgs a1 = a;
       a1.write_hot = 0;
       ACF_RET(L(K.clean_apr, a1, SW, 0));
-      ACF_RET(L(K.adv, a, SW, 1));
+      ACF_RET(L(K.adv, a, SW + TW, 1));
     } else {
-      ACF_RET(L(K.clean_bpr, a, SW, 0));
+      ACF_RET(L(K.clean_bpr, a, SW + TW, 0));
     }
   }
-  ACF_RET(L(K.flush, make_args(c, tb, hp, first + n - 1, 0), S, 2));
+  StepArgs af = make_args(c, tb, hp, first + n - 1, 0);
+  af.use_single = fuse;
+  af.slot_waves = S;
+  ACF_RET(L(K.flush, af, S, 2));
   return ACF_OK;
 }
 
@@ -1476,7 +1644,9 @@ extern "C" int acf_apr_delta_update(acf_apr_ctx* c, const acf_apr_tables* tb,
   Kernels K;
   ACF_RET(get_kernels(c, &K));
   const int SW = (3 * c->B + K.slots_per_wave - 1) / K.slots_per_wave;
-  ACF_RET(launch(K.clean_apr, make_args(c, tb, hp, t, 0), SW, s));
+  StepArgs a = make_args(c, tb, hp, t, 0);
+  a.slot_waves = SW;
+  ACF_RET(launch(K.clean_apr, a, SW, s));
   c->last_delta_batch = t;
   return ACF_OK;
 }
@@ -1488,7 +1658,8 @@ extern "C" int acf_apr_optimizer_step(acf_apr_ctx* c, const acf_apr_tables* tb,
   Kernels K;
   ACF_RET(get_kernels(c, &K));
   const int SW = (3 * c->B + K.slots_per_wave - 1) / K.slots_per_wave;
-  const StepArgs a = make_args(c, tb, hp, t, 0);
+  StepArgs a = make_args(c, tb, hp, t, 0);
+  a.slot_waves = SW;
   if (hp->adver) {
     ACF_CHECK(c->last_delta_batch == t, ACF_E_STATE,
               "APR optimizer step on batch %d needs acf_apr_delta_update on the same batch first", t);
@@ -1496,6 +1667,7 @@ extern "C" int acf_apr_optimizer_step(acf_apr_ctx* c, const acf_apr_tables* tb,
   } else {
     ACF_RET(launch(K.clean_bpr, a, SW, s));
   }
+  a.slot_waves = 3 * c->B;
   ACF_RET(launch(K.flush, a, 3 * c->B, s));
   return ACF_OK;
 }
@@ -1515,6 +1687,7 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   key.ptrs[0] = tb->P; key.ptrs[1] = tb->Q; key.ptrs[2] = tb->accP; key.ptrs[3] = tb->accQ;
   key.hp = *hp;
   key.first = first; key.n = n; key.B = c->B; key.d = c->d; key.mapping = c->mapping;
+  key.fusion = c->fusion;
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -1571,6 +1744,13 @@ extern "C" int acf_apr_set_slot_mapping(acf_apr_ctx* c, int32_t mode) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_CHECK(mode >= 0 && mode <= 2, ACF_E_INVALID, "slot mapping must be 0 (auto), 1 or 2, got %d", mode);
   c->mapping = mode;
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_set_fusion(acf_apr_ctx* c, int32_t on) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "fusion must be 0 or 1, got %d", on);
+  c->fusion = on;
   return ACF_OK;
 }
 

@@ -152,6 +152,11 @@ class APRContext:
         m = {"auto": 0, "wave": 1, "group": 2}.get(mode, mode)
         call("acf_apr_set_slot_mapping", self._ptr, int(m))
 
+    def set_fusion(self, on: bool) -> None:
+        """Fuse triplets whose three rows occur once in their batch (default on;
+        identical results either way).  Applies to train_planned / time_kernels."""
+        call("acf_apr_set_fusion", self._ptr, int(bool(on)))
+
     def time_kernels(self, tables, hp: StepHParams, first: int = 0, n: int | None = None):
         """Per-kernel-kind device time (ms) and launch counts over planned batches,
         measured with start/stop events attached to each launch (tables are

@@ -137,6 +137,14 @@ int acf_apr_time_kernels(acf_apr_ctx* ctx, const acf_apr_tables* tables,
  * mappings to fp32 summation order.  Not part of the reference surface. */
 int acf_apr_set_slot_mapping(acf_apr_ctx* ctx, int32_t mode);
 
+/* Triplet fusion in acf_apr_train_planned / acf_apr_time_kernels (1 = on, the
+ * default; 0 = off).  A triplet whose user, positive and negative item each
+ * occur once in its batch is stepped start to finish by one lane-group (no
+ * batch-wide aggregation is needed for it); the arithmetic per row is the slot
+ * kernels' own, so on and off give identical bits.  The split per-batch calls
+ * (delta_update / optimizer_step) never fuse.  Not part of the reference surface. */
+int acf_apr_set_fusion(acf_apr_ctx* ctx, int32_t on);
+
 /* Per-triplet clean / adversarial losses computed by the last step of each
  * planned batch (softplus(-clip(x)) terms of APR.py:150,162), for the staged
  * triplets [0, n_batches*batch_size).  Either pointer may be NULL. */

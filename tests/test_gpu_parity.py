@@ -365,3 +365,86 @@ def test_large_batch_auto_mapping_matches_oracle(ops, oracle, dev, d):
     ctx.train_planned(tabs, ops.StepHParams(adver=1))
     for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
         np.testing.assert_allclose(g.cpu().numpy(), w, rtol=1e-4, atol=1e-6, err_msg=n)
+
+
+def _sparse_stream(seed, U1, I1, B, nb, hot=64, p_hot=0.05):
+    """Mostly rows that occur once per batch (fused triplets), plus a small hot
+    set that recurs across consecutive batches (pending / next-batch rows)."""
+    rng = np.random.default_rng(seed)
+    n = nb * B
+
+    def draw(N):
+        x = rng.integers(0, N, n)
+        h = rng.random(n) < p_hot
+        x[h] = rng.integers(0, hot, int(h.sum()))
+        return x.astype(np.int32)
+    return draw(U1), draw(I1), draw(I1)
+
+
+def _fused_fraction(u, i, j, B):
+    frac = []
+    for t in range(len(u) // B):
+        s = slice(t * B, (t + 1) * B)
+        cu = np.unique(u[s], return_counts=True)
+        ci = np.unique(np.concatenate([i[s], j[s]]), return_counts=True)
+        once_u = set(cu[0][cu[1] == 1].tolist())
+        once_i = set(ci[0][ci[1] == 1].tolist())
+        frac.append(np.mean([a in once_u and b in once_i and c in once_i
+                             for a, b, c in zip(u[s], i[s], j[s])]))
+    return float(np.mean(frac))
+
+
+@pytest.mark.parametrize("d", [16, 64, 128, 512])
+@pytest.mark.parametrize("adver,adv", [(0, "grad"), (1, "grad"), (1, "random")])
+@pytest.mark.parametrize("mapping", ["wave", "group"])
+def test_fused_triplets_bit_identical_to_slot_path(ops, dev, d, adver, adv, mapping):
+    """Triplet fusion on vs off: identical bits for tables, accumulators and
+    losses, over one call and over piecewise calls (in-place rows, rows pending
+    from the previous batch, rows read by the next one)."""
+    U1, I1, B, nb = 6000, 5000, 256, 6
+    u, i, j = _sparse_stream(d + adver, U1, I1, B, nb)
+    assert _fused_fraction(u, i, j, B) > 0.5
+    rng = np.random.default_rng(d)
+    P = (rng.standard_normal((U1, d)) * 0.2).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
+    hp = ops.StepHParams(adver=adver, adv=adv, reg=0.01, seed=5)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_slot_mapping(mapping)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    runs = []
+    for fuse, pieces in ((False, [(0, nb)]), (True, [(0, nb)]), (True, [(0, 1), (1, 3), (4, 2)])):
+        ctx.set_fusion(fuse)
+        tabs = _gpu_tables(P, Q, dev)
+        for first, n in pieces:
+            ctx.train_planned(tabs, hp, first, n, graph=first == 0)
+        lc, la = ctx.losses()
+        runs.append(tabs + [lc.clone(), la.clone()])
+    torch.cuda.synchronize()
+    names = ("P", "Q", "accP", "accQ", "loss_clean", "loss_adv")
+    for other in runs[1:]:
+        for x, y, n in zip(runs[0], other, names):
+            if n == "loss_adv" and not adver:
+                continue
+            assert torch.equal(x, y), n
+
+
+@pytest.mark.parametrize("adver", [0, 1])
+def test_fused_large_batch_matches_oracle(ops, oracle, dev, adver):
+    """B = 8,192 on 400k x 300k tables (~85% fused triplets) vs the oracle."""
+    U1, I1, d, B, nb = 400_000, 300_000, 64, 8192, 3
+    u, i, j = _sparse_stream(40 + adver, U1, I1, B, nb, hot=256, p_hot=0.02)
+    assert _fused_fraction(u, i, j, B) > 0.8
+    rng = np.random.default_rng(adver)
+    P = (rng.standard_normal((U1, d)) * 0.1).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.1).astype(np.float32)
+    want, lc_w, la_w, _ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=adver))
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ctx.train_planned(tabs, ops.StepHParams(adver=adver))
+    lc, la = ctx.losses()
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        np.testing.assert_allclose(g.cpu().numpy(), w, rtol=1e-4, atol=1e-6, err_msg=n)
+    _close(lc, lc_w, "loss_clean")
+    if adver:
+        _close(la, la_w, "loss_adv")

@@ -58,7 +58,7 @@ def main():
         if not started.any():
             continue
         t0 = w[started, 0].min()
-        tend = w[started].max()
+        tend = w[started][:, :6].max()
         last = np.where(w[:, 4] > 0, w[:, 4], np.where(w[:, 5] > 0, w[:, 5], w[:, 1]))
         full = (w[:, 4] > 0)
         seg = {}
