@@ -234,12 +234,32 @@ __device__ __forceinline__ float trunc_normal(uint64_t key, float stddev) {
 // ---------------------------------------------------------------------------
 // plan kernels
 // ---------------------------------------------------------------------------
+// The plan sorts every occurrence by its segment (t, row) — users and items in
+// one sort, items after users — with the occurrence index as tie-break so the
+// order inside a segment is the occurrence order.  Two key layouts:
+//   Key64: (segment << ob | occurrence) in one 64-bit key;
+//   Key32: 32-bit segment key, occurrence as the sort value (fewer radix passes;
+//          used when batches x rows fits 31 bits).
+struct Key64 {
+  const uint64_t* k;
+  uint32_t ob;
+  uint64_t kmask;  // clears the item bit
+  __device__ uint64_t seg(int64_t x) const { return (k[x] & kmask) >> ob; }
+  __device__ int32_t occ(int64_t x) const { return (int32_t)(k[x] & ((1ull << ob) - 1)); }
+};
+struct Key32 {
+  const uint32_t* k;
+  const int32_t* v;
+  uint32_t kmask;
+  __device__ uint64_t seg(int64_t x) const { return k[x] & kmask; }
+  __device__ int32_t occ(int64_t x) const { return v[x]; }
+};
+
+template <bool PAIRS>
 __global__ void k_stage(const int32_t* __restrict__ user, const int32_t* __restrict__ ipos,
                         const int32_t* __restrict__ ineg, int64_t E, int32_t B, int64_t U1,
-                        int64_t I1, int32_t* __restrict__ tu, int32_t* __restrict__ ti,
-                        int32_t* __restrict__ tj, uint64_t* __restrict__ ukey,
-                        uint64_t* __restrict__ ikey, uint32_t ob_u, uint32_t ob_i,
-                        int32_t* __restrict__ err) {
+                        int64_t I1, void* __restrict__ keys, int32_t* __restrict__ vals,
+                        uint32_t ob_u, uint32_t ob_i, uint64_t item_bit, int32_t* __restrict__ err) {
   int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x >= E) return;
   int64_t t = x / B;
@@ -247,45 +267,59 @@ __global__ void k_stage(const int32_t* __restrict__ user, const int32_t* __restr
   if (u < 0 || u >= U1) { atomicOr(err, 1); u = 0; }
   if (i < 0 || i >= I1) { atomicOr(err, 2); i = 0; }
   if (j < 0 || j >= I1) { atomicOr(err, 2); j = 0; }
-  tu[x] = u; ti[x] = i; tj[x] = j;
-  ukey[x] = ((uint64_t)(t * U1 + u) << ob_u) | (uint64_t)x;
-  ikey[2 * x] = ((uint64_t)(t * I1 + i) << ob_i) | (uint64_t)(2 * x);
-  ikey[2 * x + 1] = ((uint64_t)(t * I1 + j) << ob_i) | (uint64_t)(2 * x + 1);
+  // [E user keys | 2E item keys]; item_bit (above both key ranges) puts every
+  // item key after every user key
+  if (PAIRS) {
+    uint32_t* k = static_cast<uint32_t*>(keys);
+    k[x] = (uint32_t)(t * U1 + u);
+    k[E + 2 * x] = (uint32_t)item_bit | (uint32_t)(t * I1 + i);
+    k[E + 2 * x + 1] = (uint32_t)item_bit | (uint32_t)(t * I1 + j);
+    vals[x] = (int32_t)x;
+    vals[E + 2 * x] = (int32_t)(2 * x);
+    vals[E + 2 * x + 1] = (int32_t)(2 * x + 1);
+  } else {
+    uint64_t* k = static_cast<uint64_t*>(keys);
+    k[x] = ((uint64_t)(t * U1 + u) << ob_u) | (uint64_t)x;
+    k[E + 2 * x] = item_bit | ((uint64_t)(t * I1 + i) << ob_i) | (uint64_t)(2 * x);
+    k[E + 2 * x + 1] = item_bit | ((uint64_t)(t * I1 + j) << ob_i) | (uint64_t)(2 * x + 1);
+  }
 }
 
-__global__ void k_heads(const uint64_t* __restrict__ key, int64_t n, uint32_t ob,
-                        int32_t* __restrict__ flag) {
+// head flags over the sorted [E user keys | 2E item keys]
+template <class KT>
+__global__ void k_heads(KT ku, KT ki, int64_t E, int32_t* __restrict__ flag) {
   int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= n) return;
-  flag[x] = (x == 0 || (key[x] >> ob) != (key[x - 1] >> ob)) ? 1 : 0;
+  if (x >= 3 * E) return;
+  bool h;
+  if (x < E) h = x == 0 || ku.seg(x) != ku.seg(x - 1);
+  else h = x == E || ki.seg(x - E) != ki.seg(x - E - 1);
+  flag[x] = h ? 1 : 0;
 }
 
 // After an inclusive scan of the head flags: unique rows, occurrence offsets,
-// per-batch unique ranges, the slot of every occurrence, occurrence values.
-__global__ void k_compact(const uint64_t* __restrict__ key, const int32_t* __restrict__ inc,
-                          int64_t n, uint32_t ob, uint64_t omask, int64_t R, int32_t nb,
-                          int32_t* __restrict__ uniq, int32_t* __restrict__ off,
-                          int32_t* __restrict__ bstart, int32_t* __restrict__ occ,
-                          int32_t* __restrict__ slot_a, int32_t* __restrict__ slot_b,
-                          int32_t item_side) {
+// per-batch unique ranges, and for every triplet the slots and CSR positions of
+// its occurrences.  Item side: the scan ran over users and items together,
+// *sbase = user uniques.
+template <class KT>
+__global__ void k_compact(KT key, const int32_t* __restrict__ inc, const int32_t* __restrict__ sbase,
+                          int64_t n, int64_t R, int32_t nb, int32_t* __restrict__ uniq,
+                          int32_t* __restrict__ off, int32_t* __restrict__ bstart,
+                          int32_t* __restrict__ tsl, int32_t* __restrict__ tpos, int32_t item_side) {
   int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x >= n) return;
-  uint64_t k = key[x];
-  uint64_t seg = k >> ob;
-  int32_t v = (int32_t)(k & omask);
-  int32_t s = inc[x] - 1;
-  occ[x] = v;
-  if (item_side) {
-    if (v & 1) slot_b[v >> 1] = s; else slot_a[v >> 1] = s;
-  } else {
-    slot_a[v] = s;
-  }
-  bool head = (x == 0) || ((key[x - 1] >> ob) != seg);
+  const uint64_t seg = key.seg(x);
+  const int32_t v = key.occ(x);
+  const int32_t s = inc[x] - 1 - (sbase ? *sbase : 0);
+  // tsl[e] = {user slot, positive-item slot, negative-item slot, -}; tpos alike
+  const int64_t at = item_side ? (int64_t)(v >> 1) * 4 + 1 + (v & 1) : (int64_t)v * 4;
+  tsl[at] = s;
+  tpos[at] = (int32_t)x;
+  const bool head = (x == 0) || key.seg(x - 1) != seg;
   if (head) {
     uniq[s] = (int32_t)(seg % (uint64_t)R);
     off[s] = (int32_t)x;
     int64_t t = (int64_t)(seg / (uint64_t)R);
-    bool bhead = (x == 0) || (((key[x - 1] >> ob) / (uint64_t)R) != (uint64_t)t);
+    bool bhead = (x == 0) || (key.seg(x - 1) / (uint64_t)R) != (uint64_t)t;
     if (bhead) bstart[t] = s;
   }
   if (x == n - 1) {
@@ -294,19 +328,19 @@ __global__ void k_compact(const uint64_t* __restrict__ key, const int32_t* __res
   }
 }
 
-
 // For every unique row of batch t: where its current value lives when batch t
 // starts.  Rows updated by batch t-1 are still in that batch's W scratch (the
 // flush to the table happens inside batch t's first kernel), so the plan encodes
 // src = ~(local slot in batch t-1) for them and src = row otherwise.
 // user local slot = g - ubs[t]; item local slot = nU(t) + g - ibs[t].
-// nxt[g] = 1 when batch t+1 touches the row too.
-__global__ void k_prev_src(const int32_t* __restrict__ uniq, int32_t* __restrict__ nxt,
-                           const int32_t* __restrict__ ubs, const int32_t* __restrict__ bstart,
-                           int32_t n_uniq, int32_t nb, int32_t item_side,
-                           int32_t* __restrict__ src) {
+// info[g] = {row, src, occurrence count | NEXT (batch t+1 touches the row too),
+//            CSR offset of the first occurrence}.
+#define ACF_INFO_NEXT (1 << 30)
+__global__ void k_slot_info(const int32_t* __restrict__ uniq, const int32_t* __restrict__ off,
+                            const int32_t* __restrict__ ubs, const int32_t* __restrict__ bstart,
+                            int32_t n_uniq, int32_t nb, int32_t item_side, int4* __restrict__ info) {
   int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (g >= n_uniq) return;
+  if (g >= n_uniq || g >= bstart[nb]) return;  // bstart[nb] = unique rows of the plan
   // batch of g: last t with bstart[t] <= g
   int lo = 0, hi = nb;  // answer in [0, nb)
   while (hi - lo > 1) {
@@ -328,7 +362,6 @@ __global__ void k_prev_src(const int32_t* __restrict__ uniq, int32_t* __restrict
       s = ~local;
     }
   }
-  src[g] = s;
   int32_t in_next = 0;
   if (t + 1 < nb) {
     int a = bstart[t + 1], b = bstart[t + 2];
@@ -338,7 +371,8 @@ __global__ void k_prev_src(const int32_t* __restrict__ uniq, int32_t* __restrict
     }
     in_next = (a < bstart[t + 2] && uniq[a] == row) ? 1 : 0;
   }
-  nxt[g] = in_next;
+  const int32_t o = off[g];
+  info[g] = make_int4(row, s, (off[g + 1] - o) | (in_next ? ACF_INFO_NEXT : 0), o);
 }
 
 // Occurrence record: everything one lane-group needs to process one occurrence
@@ -376,22 +410,14 @@ struct FuseInfo {
   int fused, in_u, in_i, in_j;
 };
 
-__device__ __forceinline__ FuseInfo fuse_info(int32_t e, const int32_t* __restrict__ uslot,
-                                              const int32_t* __restrict__ pslot,
-                                              const int32_t* __restrict__ nslot,
-                                              const int32_t* __restrict__ uoff,
-                                              const int32_t* __restrict__ ioff,
-                                              const int32_t* __restrict__ usrc,
-                                              const int32_t* __restrict__ isrc,
-                                              const int32_t* __restrict__ unxt,
-                                              const int32_t* __restrict__ inxt) {
-  const int32_t gu = uslot[e], gi = pslot[e], gj = nslot[e];
+__device__ __forceinline__ int info_count(const int4& f) { return f.z & (ACF_INFO_NEXT - 1); }
+
+__device__ __forceinline__ FuseInfo fuse_info(const int4& U, const int4& I, const int4& J) {
   FuseInfo f;
-  f.fused = (uoff[gu + 1] - uoff[gu]) == 1 && (ioff[gi + 1] - ioff[gi]) == 1 &&
-            (ioff[gj + 1] - ioff[gj]) == 1;
-  f.in_u = f.fused && usrc[gu] >= 0 && !unxt[gu];
-  f.in_i = f.fused && isrc[gi] >= 0 && !inxt[gi];
-  f.in_j = f.fused && isrc[gj] >= 0 && !inxt[gj];
+  f.fused = info_count(U) == 1 && info_count(I) == 1 && info_count(J) == 1;
+  f.in_u = f.fused && U.y >= 0 && !(U.z & ACF_INFO_NEXT);
+  f.in_i = f.fused && I.y >= 0 && !(I.z & ACF_INFO_NEXT);
+  f.in_j = f.fused && J.y >= 0 && !(J.z & ACF_INFO_NEXT);
   return f;
 }
 
@@ -399,81 +425,79 @@ __device__ __forceinline__ FuseInfo fuse_info(int32_t e, const int32_t* __restri
 //  a = {u, i, j, local slot of u}, b = {slot i, slot j, src u, src i},
 //  c = {src j, flags (1 fused | 2 in-place u | 4 in-place i | 8 in-place j), e, gen}
 
-__global__ void k_records(const int32_t* __restrict__ uocc, const int32_t* __restrict__ iocc,
-                          int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen,
-                          const int32_t* __restrict__ tu, const int32_t* __restrict__ ti,
-                          const int32_t* __restrict__ tj, const int32_t* __restrict__ uslot,
-                          const int32_t* __restrict__ pslot, const int32_t* __restrict__ nslot,
-                          const int32_t* __restrict__ uuniq, const int32_t* __restrict__ uoff,
-                          const int32_t* __restrict__ ubs, const int32_t* __restrict__ usrc,
-                          const int32_t* __restrict__ iuniq, const int32_t* __restrict__ ioff,
-                          const int32_t* __restrict__ ibs, const int32_t* __restrict__ isrc,
-                          const int32_t* __restrict__ unxt, const int32_t* __restrict__ inxt,
+// item occurrence record: own = the item's slot info, oth = the triplet's other item
+__device__ __forceinline__ OccRec item_rec(const int4& own, const int4& oth, const int4& U, int32_t v,
+                                           int32_t ku, int32_t k_oth, int fused, int in_place,
+                                           int32_t gen) {
+  OccRec r;
+  r.own_row = own.x;
+  r.own_src = own.y;
+  r.meta = info_count(own) | ACF_ITEM_BIT | (fused ? ACF_SINGLE_BIT : 0) |
+           (in_place ? ACF_INPLACE_BIT : 0);
+  r.ovf = own.w;
+  r.e_role = v;
+  r.pa_row = U.x;
+  r.pb_row = oth.x;
+  r.pa_src = U.y;
+  r.pb_src = oth.y;
+  r.pa_slot = ku;
+  r.pb_slot = k_oth;
+  r.gen = gen;
+  return r;
+}
+
+// One thread per triplet: its user and two item occurrence records and, when
+// fused, its fused-triplet record.  The first R records of a slot go inline
+// only (that is the only place they are read from), later ones to the CSR.
+__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen,
+                          const int4* __restrict__ tsl, const int4* __restrict__ tpos,
+                          const int4* __restrict__ uinfo, const int4* __restrict__ iinfo,
+                          const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
                           OccRec* __restrict__ urec, OccRec* __restrict__ irec,
                           OccRec* __restrict__ inl, OccRec* __restrict__ trec,
                           int32_t* __restrict__ gen_ptr) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x == 0) *gen_ptr = gen;
-  if (x < E) {
-    const int32_t e = uocc[x];
-    const int32_t g = uslot[e];
-    const int32_t t = e / B;
-    const int32_t nU = ubs[t + 1] - ubs[t];
-    const FuseInfo f = fuse_info(e, uslot, pslot, nslot, uoff, ioff, usrc, isrc, unxt, inxt);
-    OccRec r;
-    r.own_row = uuniq[g];
-    r.own_src = usrc[g];
-    r.meta = (uoff[g + 1] - uoff[g]) | (f.fused ? ACF_SINGLE_BIT : 0) | (f.in_u ? ACF_INPLACE_BIT : 0);
-    r.ovf = uoff[g];
-    r.e_role = e;
-    r.pa_row = ti[e];
-    r.pb_row = tj[e];
-    r.pa_src = isrc[pslot[e]];
-    r.pb_src = isrc[nslot[e]];
-    r.pa_slot = nU + (pslot[e] - ibs[t]);
-    r.pb_slot = nU + (nslot[e] - ibs[t]);
-    r.gen = gen;
-    urec[x] = r;
-    const int32_t k = g - ubs[t];
-    const int32_t rr = (int32_t)(x - uoff[g]);
-    if (rr < R) inl[((int64_t)t * S + k) * R + rr] = r;
-    // the triplet's fused record (one per triplet: written by its user occurrence)
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e == 0) *gen_ptr = gen;
+  if (e >= E) return;
+  const int4 sl = tsl[e], ps = tpos[e];
+  const int4 U = uinfo[sl.x], I = iinfo[sl.y], J = iinfo[sl.z];
+  const int32_t t = (int32_t)(e / B);
+  const int32_t nU = ubs[t + 1] - ubs[t];
+  const int32_t k = sl.x - ubs[t], ki = nU + (sl.y - ibs[t]), kj = nU + (sl.z - ibs[t]);
+  const FuseInfo f = fuse_info(U, I, J);
+  OccRec r;
+  r.own_row = U.x;
+  r.own_src = U.y;
+  r.meta = info_count(U) | (f.fused ? ACF_SINGLE_BIT : 0) | (f.in_u ? ACF_INPLACE_BIT : 0);
+  r.ovf = U.w;
+  r.e_role = (int32_t)e;
+  r.pa_row = I.x;
+  r.pb_row = J.x;
+  r.pa_src = I.y;
+  r.pb_src = J.y;
+  r.pa_slot = ki;
+  r.pb_slot = kj;
+  r.gen = gen;
+  const int64_t base = (int64_t)t * S;
+  int32_t rr = ps.x - U.w;
+  if (rr < R) inl[(base + k) * R + rr] = r;
+  else urec[ps.x] = r;
+  const OccRec ri = item_rec(I, J, U, (int32_t)(2 * e), k, kj, f.fused, f.in_i, gen);
+  rr = ps.y - I.w;
+  if (rr < R) inl[(base + ki) * R + rr] = ri;
+  else irec[ps.y] = ri;
+  const OccRec rj = item_rec(J, I, U, (int32_t)(2 * e + 1), k, ki, f.fused, f.in_j, gen);
+  rr = ps.z - J.w;
+  if (rr < R) inl[(base + kj) * R + rr] = rj;
+  else irec[ps.z] = rj;
+  if (f.fused) {  // other triplets' records read as absent (older generation)
     OccRec q;
-    q.own_row = tu[e]; q.own_src = ti[e]; q.meta = tj[e]; q.ovf = k;
-    q.e_role = nU + (pslot[e] - ibs[t]); q.pa_row = nU + (nslot[e] - ibs[t]);
-    q.pb_row = usrc[g]; q.pa_src = isrc[pslot[e]];
-    q.pb_src = isrc[nslot[e]];
-    q.pa_slot = (f.fused ? 1 : 0) | (f.in_u ? 2 : 0) | (f.in_i ? 4 : 0) | (f.in_j ? 8 : 0);
-    q.pb_slot = e; q.gen = gen;
+    q.own_row = U.x; q.own_src = I.x; q.meta = J.x; q.ovf = k;
+    q.e_role = ki; q.pa_row = kj; q.pb_row = U.y; q.pa_src = I.y;
+    q.pb_src = J.y;
+    q.pa_slot = 1 | (f.in_u ? 2 : 0) | (f.in_i ? 4 : 0) | (f.in_j ? 8 : 0);
+    q.pb_slot = (int32_t)e; q.gen = gen;
     trec[e] = q;
-  }
-  if (x < 2 * E) {
-    const int32_t v = iocc[x];
-    const int32_t e = v >> 1, role = v & 1;
-    const int32_t g = role ? nslot[e] : pslot[e];
-    const int32_t og = role ? pslot[e] : nslot[e];
-    const int32_t t = e / B;
-    const int32_t nU = ubs[t + 1] - ubs[t];
-    const FuseInfo f = fuse_info(e, uslot, pslot, nslot, uoff, ioff, usrc, isrc, unxt, inxt);
-    const int in_place = role ? f.in_j : f.in_i;
-    OccRec r;
-    r.own_row = iuniq[g];
-    r.own_src = isrc[g];
-    r.meta = (ioff[g + 1] - ioff[g]) | ACF_ITEM_BIT | (f.fused ? ACF_SINGLE_BIT : 0) |
-             (in_place ? ACF_INPLACE_BIT : 0);
-    r.ovf = ioff[g];
-    r.e_role = v;
-    r.pa_row = tu[e];
-    r.pb_row = role ? ti[e] : tj[e];
-    r.pa_src = usrc[uslot[e]];
-    r.pb_src = isrc[og];
-    r.pa_slot = uslot[e] - ubs[t];
-    r.pb_slot = nU + (og - ibs[t]);
-    r.gen = gen;
-    irec[x] = r;
-    const int32_t k = nU + (g - ibs[t]);
-    const int32_t rr = (int32_t)(x - ioff[g]);
-    if (rr < R) inl[((int64_t)t * S + k) * R + rr] = r;
   }
 }
 
@@ -1261,6 +1285,8 @@ __global__ void __launch_bounds__(256) k_dns_select(const float* __restrict__ P,
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+#define ACF_PACKED_MIN_BATCH 4096  // auto slot mapping: packed from this batch size
+
 struct GraphKey {
   const void* ptrs[4];
   acf_apr_hparams hp;
@@ -1272,15 +1298,14 @@ struct acf_apr_ctx {
   int64_t U1 = 0, I1 = 0;
   int32_t d = 0, maxB = 0, maxNB = 0, lpr = 0, nv = 0, R = 0;
   int64_t maxE = 0;
-  // staged triplets
-  int32_t *tu = nullptr, *ti = nullptr, *tj = nullptr;
   // plan
-  uint64_t *ukey_in = nullptr, *ukey_out = nullptr, *ikey_in = nullptr, *ikey_out = nullptr;
+  uint64_t *key_in = nullptr, *key_out = nullptr;  // [E user keys | 2E item keys]
   int32_t *flag = nullptr, *inc = nullptr;
-  int32_t *uuniq = nullptr, *uoff = nullptr, *ubs = nullptr, *uocc = nullptr, *uslot = nullptr;
-  int32_t *iuniq = nullptr, *ioff = nullptr, *ibs = nullptr, *iocc = nullptr;
-  int32_t *pslot = nullptr, *nslot = nullptr, *usrc = nullptr, *isrc = nullptr;
-  int32_t *unxt = nullptr, *inxt = nullptr;
+  int32_t *uuniq = nullptr, *uoff = nullptr, *ubs = nullptr;
+  int32_t* tsl = nullptr;                    // [E][4] slots of each triplet's rows
+  int32_t* tpos = nullptr;                   // [E][4] CSR positions of its occurrences
+  int4 *uinfo = nullptr, *iinfo = nullptr;   // per unique row, see k_slot_info
+  int32_t *iuniq = nullptr, *ioff = nullptr, *ibs = nullptr;
   OccRec* trec = nullptr;
   OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr, *hot[2] = {nullptr, nullptr};
   int32_t *err = nullptr, *gen_dev = nullptr;
@@ -1293,6 +1318,7 @@ struct acf_apr_ctx {
   int32_t B = 0, nb = 0, gen = 0;
   int32_t last_delta_batch = -1;
   int32_t mapping = 0;  // slot mapping, see get_kernels
+  int32_t plan_R = 1;   // inline records per slot in the current plan (<= R)
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
   hipStream_t cap_stream = nullptr;
   std::map<GraphKey, hipGraphExec_t> graphs;
@@ -1389,7 +1415,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   uint32_t ob_i = bits_for((uint64_t)(2 * maxE));
   uint32_t sb_i = bits_for((uint64_t)maxNB * (uint64_t)I1);
   uint32_t sb_u = bits_for((uint64_t)maxNB * (uint64_t)U1);
-  ACF_CHECK(ob_i + sb_i <= 64 && ob_i + sb_u <= 64, ACF_E_INVALID,
+  ACF_CHECK(ob_i + sb_i < 64 && ob_i + sb_u < 64, ACF_E_INVALID,
             "plan key does not fit 64 bits (rows x batches x batch too large)");
   acf_apr_ctx* c = new acf_apr_ctx();
   c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB; c->maxNB = maxNB; c->maxE = maxE;
@@ -1398,16 +1424,13 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
   auto A = [&](auto** p, size_t n) { if (r == ACF_OK) r = dalloc(c, p, n); };
-  A(&c->tu, maxE); A(&c->ti, maxE); A(&c->tj, maxE);
-  A(&c->ukey_in, maxE); A(&c->ukey_out, maxE);
-  A(&c->ikey_in, 2 * maxE); A(&c->ikey_out, 2 * maxE);
-  A(&c->flag, 2 * maxE); A(&c->inc, 2 * maxE);
-  A(&c->uuniq, maxE); A(&c->uoff, maxE + 1); A(&c->ubs, maxNB + 1); A(&c->uocc, maxE);
-  A(&c->uslot, maxE); A(&c->usrc, maxE);
-  A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1); A(&c->iocc, 2 * maxE);
-  A(&c->pslot, maxE); A(&c->nslot, maxE); A(&c->isrc, 2 * maxE);
+  A(&c->key_in, 3 * maxE); A(&c->key_out, 3 * maxE);
+  A(&c->flag, 3 * maxE); A(&c->inc, 3 * maxE);
+  A(&c->uuniq, maxE); A(&c->uoff, maxE + 1); A(&c->ubs, maxNB + 1);
+  A(&c->tsl, 4 * maxE); A(&c->tpos, 4 * maxE); A(&c->uinfo, maxE);
+  A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
+  A(&c->iinfo, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
-  A(&c->unxt, maxE); A(&c->inxt, 2 * maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
   A(&c->hot[0], S * c->R); A(&c->hot[1], S * c->R);
   A(&c->err, 4); A(&c->gen_dev, 4);
@@ -1416,12 +1439,14 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->loss_clean, maxE); A(&c->loss_adv, maxE);
   if (r != ACF_OK) { acf_apr_destroy(c); return r; }
   size_t b1 = 0, b2 = 0, b3 = 0;
-  if (rocprim::radix_sort_keys(nullptr, b1, c->ikey_in, c->ikey_out, (size_t)(2 * maxE), 0, 64) !=
+  uint32_t* k32 = reinterpret_cast<uint32_t*>(c->key_in);
+  int32_t* v32 = reinterpret_cast<int32_t*>(k32 + 3 * maxE);
+  if (rocprim::radix_sort_keys(nullptr, b1, c->key_in, c->key_out, (size_t)(3 * maxE), 0, 64) !=
           hipSuccess ||
-      rocprim::inclusive_scan(nullptr, b2, c->flag, c->inc, (size_t)(2 * maxE),
-                              rocprim::plus<int32_t>()) != hipSuccess ||
-      rocprim::radix_sort_keys(nullptr, b3, c->ukey_in, c->ukey_out, (size_t)maxE, 0, 64) !=
-          hipSuccess) {
+      rocprim::radix_sort_pairs(nullptr, b3, k32, k32, v32, v32, (size_t)(3 * maxE), 0, 32) !=
+          hipSuccess ||
+      rocprim::inclusive_scan(nullptr, b2, c->flag, c->inc, (size_t)(3 * maxE),
+                              rocprim::plus<int32_t>()) != hipSuccess) {
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "rocprim temporary-storage query failed");
   }
@@ -1432,14 +1457,30 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipStreamCreate failed");
   }
-  // generation 0 never matches a plan: zeroed inline records read as absent
+  // generation 0 never matches a plan: zeroed inline / fused-triplet records read as absent
   if (hipMemset(c->inl, 0, (size_t)maxNB * S * c->R * sizeof(OccRec)) != hipSuccess ||
+      hipMemset(c->trec, 0, (size_t)maxE * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->gen_dev, 0, 16) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipMemset failed");
   }
   *out = c;
+  return ACF_OK;
+}
+
+// sorted keys -> head flags -> one scan -> per-side compaction
+template <class KT>
+static int plan_groups(acf_apr_ctx* c, const KT& ku, const KT& ki, int64_t E, int32_t nb,
+                       hipStream_t s) {
+  k_heads<KT><<<grid_for(3 * E), 256, 0, s>>>(ku, ki, E, c->flag);
+  size_t tb = c->tmp_bytes;
+  HIP_TRY(rocprim::inclusive_scan(c->tmp, tb, c->flag, c->inc, (size_t)(3 * E), rocprim::plus<int32_t>(), s));
+  k_compact<KT><<<grid_for(E), 256, 0, s>>>(ku, c->inc, nullptr, E, c->U1, nb, c->uuniq, c->uoff, c->ubs,
+                                            c->tsl, c->tpos, 0);
+  k_compact<KT><<<grid_for(2 * E), 256, 0, s>>>(ki, c->inc + E, c->inc + E - 1, 2 * E, c->I1, nb, c->iuniq,
+                                                c->ioff, c->ibs, c->tsl, c->tpos, 1);
+  HIP_TRY(hipGetLastError());
   return ACF_OK;
 }
 
@@ -1455,39 +1496,51 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   const uint32_t ob_u = bits_for((uint64_t)E), ob_i = bits_for((uint64_t)(2 * E));
   const uint32_t eb_u = ob_u + bits_for((uint64_t)nb * (uint64_t)c->U1);
   const uint32_t eb_i = ob_i + bits_for((uint64_t)nb * (uint64_t)c->I1);
-  ACF_CHECK(eb_u <= 64 && eb_i <= 64, ACF_E_INVALID, "plan key does not fit 64 bits");
+  const uint32_t eb = std::max(eb_u, eb_i);  // item keys carry bit eb
+  ACF_CHECK(eb < 64, ACF_E_INVALID, "plan key does not fit 64 bits");
   c->B = 0;
   c->nb = 0;
   c->last_delta_batch = -1;
   const int32_t gen = ++c->gen;
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
-  k_stage<<<grid_for(E), 256, 0, s>>>(user, ipos, ineg, E, B, c->U1, c->I1, c->tu, c->ti, c->tj,
-                                      c->ukey_in, c->ikey_in, ob_u, ob_i, c->err);
-  HIP_TRY(hipGetLastError());
+  // 32-bit keys (segment only, occurrence as the sort value) when they fit
+  const uint32_t sb = std::max(bits_for((uint64_t)nb * (uint64_t)c->U1),
+                               bits_for((uint64_t)nb * (uint64_t)c->I1));
+  const bool pairs = sb < 32;
+  const uint64_t item_bit = 1ull << (pairs ? sb : eb);
+  const int64_t n3 = 3 * E;
   size_t tb = c->tmp_bytes;
-  HIP_TRY(rocprim::radix_sort_keys(c->tmp, tb, c->ukey_in, c->ukey_out, (size_t)E, 0, eb_u, s));
-  tb = c->tmp_bytes;
-  HIP_TRY(rocprim::radix_sort_keys(c->tmp, tb, c->ikey_in, c->ikey_out, (size_t)(2 * E), 0, eb_i, s));
-  // users
-  k_heads<<<grid_for(E), 256, 0, s>>>(c->ukey_out, E, ob_u, c->flag);
-  tb = c->tmp_bytes;
-  HIP_TRY(rocprim::inclusive_scan(c->tmp, tb, c->flag, c->inc, (size_t)E, rocprim::plus<int32_t>(), s));
-  k_compact<<<grid_for(E), 256, 0, s>>>(c->ukey_out, c->inc, E, ob_u, (1ull << ob_u) - 1, c->U1, nb,
-                                        c->uuniq, c->uoff, c->ubs, c->uocc, c->uslot, nullptr, 0);
-  // items
-  k_heads<<<grid_for(2 * E), 256, 0, s>>>(c->ikey_out, 2 * E, ob_i, c->flag);
-  tb = c->tmp_bytes;
-  HIP_TRY(rocprim::inclusive_scan(c->tmp, tb, c->flag, c->inc, (size_t)(2 * E), rocprim::plus<int32_t>(), s));
-  k_compact<<<grid_for(2 * E), 256, 0, s>>>(c->ikey_out, c->inc, 2 * E, ob_i, (1ull << ob_i) - 1, c->I1,
-                                            nb, c->iuniq, c->ioff, c->ibs, c->iocc, c->pslot, c->nslot, 1);
+  if (pairs) {
+    uint32_t* kin = reinterpret_cast<uint32_t*>(c->key_in);
+    int32_t* vin = reinterpret_cast<int32_t*>(kin + n3);
+    uint32_t* kout = reinterpret_cast<uint32_t*>(c->key_out);
+    int32_t* vout = reinterpret_cast<int32_t*>(kout + n3);
+    k_stage<true><<<grid_for(E), 256, 0, s>>>(user, ipos, ineg, E, B, c->U1, c->I1, kin, vin, 0, 0,
+                                              item_bit, c->err);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(rocprim::radix_sort_pairs(c->tmp, tb, kin, kout, vin, vout, (size_t)n3, 0, sb + 1, s));
+    const Key32 ku{kout, vout, ~0u}, ki{kout + E, vout + E, ~(uint32_t)item_bit};
+    ACF_RET(plan_groups(c, ku, ki, E, nb, s));
+  } else {
+    k_stage<false><<<grid_for(E), 256, 0, s>>>(user, ipos, ineg, E, B, c->U1, c->I1, c->key_in,
+                                               nullptr, ob_u, ob_i, item_bit, c->err);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(rocprim::radix_sort_keys(c->tmp, tb, c->key_in, c->key_out, (size_t)n3, 0, eb + 1, s));
+    const Key64 ku{c->key_out, ob_u, ~0ull}, ki{c->key_out + E, ob_i, ~item_bit};
+    ACF_RET(plan_groups(c, ku, ki, E, nb, s));
+  }
   // where each unique row's value lives at batch start, then the records
-  k_prev_src<<<grid_for(E), 256, 0, s>>>(c->uuniq, c->unxt, c->ubs, c->ubs, (int32_t)E, nb, 0, c->usrc);
-  k_prev_src<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, c->inxt, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
-                                              c->isrc);
-  k_records<<<grid_for(2 * E), 256, 0, s>>>(c->uocc, c->iocc, E, B, 3 * B, c->R, gen, c->tu, c->ti, c->tj,
-                                            c->uslot, c->pslot, c->nslot, c->uuniq, c->uoff, c->ubs,
-                                            c->usrc, c->iuniq, c->ioff, c->ibs, c->isrc, c->unxt,
-                                            c->inxt, c->urec, c->irec, c->inl, c->trec, c->gen_dev);
+  k_slot_info<<<grid_for(E), 256, 0, s>>>(c->uuniq, c->uoff, c->ubs, c->ubs, (int32_t)E, nb, 0,
+                                          c->uinfo);
+  k_slot_info<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, c->ioff, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
+                                              c->iinfo);
+  // one lane-group per slot (large batches) reads only a slot's first record inline
+  const int packed = c->mapping == 2 || (c->mapping == 0 && B >= ACF_PACKED_MIN_BATCH);
+  c->plan_R = packed ? 1 : c->R;
+  k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen,
+                                        reinterpret_cast<const int4*>(c->tsl),
+                                        reinterpret_cast<const int4*>(c->tpos), c->uinfo, c->iinfo,
+                                        c->ubs, c->ibs, c->urec, c->irec, c->inl, c->trec, c->gen_dev);
   HIP_TRY(hipGetLastError());
   if (check) {
     int32_t herr = 0;
@@ -1518,7 +1571,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.wnew_prev = c->wnew[(t + 1) & 1];
   a.loss_clean = c->loss_clean; a.loss_adv = c->loss_adv;
   a.gen_ptr = c->gen_dev;
-  a.d = c->d; a.B = c->B; a.S = 3 * c->B; a.R = c->R; a.t = t;
+  a.d = c->d; a.B = c->B; a.S = 3 * c->B; a.R = c->plan_R; a.t = t;
   a.prev_valid = prev_valid;
   a.diag_launch = 0;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
@@ -1561,7 +1614,6 @@ static void kernel_ptrs(Kernels* k, int packed, int fused) {
 
 // slot mapping: 0 auto (packed for batches >= ACF_PACKED_MIN_BATCH), 1 one wave
 // per slot, 2 one lane-group per slot
-#define ACF_PACKED_MIN_BATCH 4096
 
 static int get_kernels(const acf_apr_ctx* c, Kernels* k, int fused = 0) {
   const int packed = c->mapping == 2 || (c->mapping == 0 && c->B >= ACF_PACKED_MIN_BATCH);

@@ -101,6 +101,7 @@ class MF:
         self._create_variables(device, generator)
         self._create_fetches()
         self._ctx = None
+        self._pipe = None
         self._delta_feed = None
         self.built = True
         return self
@@ -123,6 +124,14 @@ class MF:
             self._ctx = ctx = ops.APRContext(self.num_user_rows, self.num_item_rows,
                                              self.embedding_size, cap_b, cap_n, self.device)
         return ctx
+
+    def pipeline(self, batch_size: int, chunk: int = 512) -> ops.PlanPipeline:
+        """Epoch trainer: chunks of `chunk` batches, next chunk planned while one trains."""
+        p = self._pipe
+        if p is None or p.batch_size != batch_size or p.chunk != chunk:
+            self._pipe = p = ops.PlanPipeline(self.num_user_rows, self.num_item_rows,
+                                              self.embedding_size, batch_size, chunk, self.device)
+        return p
 
     def reset_optimizer(self):
         """A fresh MF in the reference means fresh Adagrad slots (run_adv_ori.py:108)."""

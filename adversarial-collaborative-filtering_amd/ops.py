@@ -191,6 +191,84 @@ class APRContext:
         return dP, dQ
 
 
+class PlanPipeline:
+    """training_batch's epoch loop with the dedup plan off the critical path.
+
+    A long triplet stream is trained in chunks of ``chunk`` batches.  The plan of
+    chunk c+1 (sort / dedup / records — it reads triplets only, never the tables)
+    runs on a side stream while chunk c trains on the caller's stream; two
+    contexts alternate so a plan never overwrites records still in use.  Chunks
+    are independent calls of train_planned (each ends with its flush), so the
+    result is the one of planning and training the chunks in sequence.
+
+    overlap=False plans on the caller's stream instead: at small batches the step
+    kernels are latency-bound and a concurrent plan slows them more than it saves.
+    """
+
+    def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, batch_size: int,
+                 chunk: int, device: torch.device, overlap: bool = True):
+        self.device = torch.device(device)
+        self.overlap = bool(overlap)
+        self.batch_size, self.chunk = int(batch_size), int(chunk)
+        self.ctx = [APRContext(num_user_rows, num_item_rows, dim, batch_size, chunk, self.device)
+                    for _ in range(2)]
+        self.side = torch.cuda.Stream(self.device)
+        self._free = [None, None]  # event: the last training on ctx[k] has been issued before it
+
+    def set_fusion(self, on: bool) -> None:
+        for c in self.ctx:
+            c.set_fusion(on)
+
+    def set_slot_mapping(self, mode) -> None:
+        for c in self.ctx:
+            c.set_slot_mapping(mode)
+
+    def _plan(self, k, u, i, j, b, n, check):
+        B, c = self.batch_size, self.ctx[k % 2]
+        s = slice(b * B, (b + n) * B)
+        if not self.overlap:
+            c.plan(u[s], i[s], j[s], B, check=check)
+            return None
+        with torch.cuda.stream(self.side):
+            if self._free[k % 2] is not None:
+                self.side.wait_event(self._free[k % 2])
+            c.plan(u[s], i[s], j[s], B, check=check)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        return ev
+
+    def run(self, tables, hp: StepHParams, user, item_pos, item_neg, first_batch: int = 0,
+            n_batches: int | None = None, graph: bool = True, check: bool = False) -> None:
+        """Train batches [first_batch, first_batch + n_batches) of the stream."""
+        B = self.batch_size
+        u, i, j = (_idx(x, n, self.device) for x, n in ((user, "user"), (item_pos, "item_pos"),
+                                                       (item_neg, "item_neg")))
+        total = u.numel() // B
+        n_batches = total - first_batch if n_batches is None else int(n_batches)
+        if first_batch < 0 or n_batches <= 0 or first_batch + n_batches > total:
+            raise ValueError(f"batches [{first_batch}, {first_batch + n_batches}) outside the "
+                             f"{total} batches of the stream")
+        main = torch.cuda.current_stream(self.device)
+        if self.overlap:
+            ready = torch.cuda.Event()
+            ready.record(main)  # triplets produced on the caller's stream
+            self.side.wait_event(ready)
+        chunks = [(b, min(self.chunk, first_batch + n_batches - b))
+                  for b in range(first_batch, first_batch + n_batches, self.chunk)]
+        planned = self._plan(0, u, i, j, *chunks[0], check)
+        for k, (b, n) in enumerate(chunks):
+            if planned is not None:
+                main.wait_event(planned)
+            self.ctx[k % 2].train_planned(tables, hp, 0, n, graph=graph)
+            if self.overlap:
+                done = torch.cuda.Event()
+                done.record(main)
+                self._free[k % 2] = done
+            if k + 1 < len(chunks):
+                planned = self._plan(k + 1, u, i, j, *chunks[k + 1], check)
+        self._staged = (u, i, j)
+
+
 def bpr_forward(P, Q, user, item_pos, item_neg, batch_size: int, clip_lo=CLIP_LO, clip_hi=CLIP_HI,
                 want_scores: bool = False):
     """training_loss_acc's forward (utils.py:159-175): per-batch loss sum and #correct."""

@@ -59,8 +59,9 @@ def _as_epoch(model, batches) -> EpochTriplets:
 
 
 def training_batch(model, sess, batches, adver=False, graph=True):
-    """utils.py:106-140.  dns == 1: the whole epoch is planned once and replayed as
-    one hipGraph (delta_update + optimizer_step per batch, in batch order).
+    """utils.py:106-140.  dns == 1: the epoch is planned in chunks of 512 batches,
+    each replayed as one hipGraph (delta_update + optimizer_step per batch, in
+    batch order) while the next chunk is planned on a side stream.
     dns > 1: per batch, the highest-scoring of dns negatives under the current
     weights, then the optimizer step (the reference never runs update_P/update_Q
     on this branch, so the adversarial terms see delta = 0)."""
@@ -68,12 +69,8 @@ def training_batch(model, sess, batches, adver=False, graph=True):
         ep = _as_epoch(model, batches)
         B, nb = ep.batch_size, ep.n_batches
         hp = model.hparams(adver=int(bool(adver)))
-        ctx = model.context(B, min(nb, _MAX_PLAN_BATCHES))
-        for first in range(0, nb, ctx.max_batches):
-            n = min(ctx.max_batches, nb - first)
-            sl = slice(first * B, (first + n) * B)
-            ctx.plan(ep.user[sl], ep.item_pos[sl], ep.item_neg[sl], B)
-            ctx.train_planned(model.tables, hp, 0, n, graph=graph)
+        pipe = model.pipeline(B, min(nb, _PLAN_CHUNK))
+        pipe.run(model.tables, hp, ep.user, ep.item_pos, ep.item_neg, graph=graph, check=True)
         return ep
     user_input, item_input_pos, user_dns_list, item_dns_list = batches
     hp = model.hparams(adver=int(bool(adver)))
@@ -94,7 +91,7 @@ def training_batch(model, sess, batches, adver=False, graph=True):
     return user_input, item_input_pos, negs
 
 
-_MAX_PLAN_BATCHES = 4096
+_PLAN_CHUNK = 512  # batches per plan / graph; the next chunk is planned during this one
 
 
 def training_loss_acc(model, sess, train_batches, output_adv=0):

@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=1941)
     p.add_argument("--batch", type=int, default=512)
     p.add_argument("--dim", type=int, default=64)
-    p.add_argument("--chunk", type=int, default=1941, help="batches per plan / graph")
+    p.add_argument("--chunk", type=int, default=647,
+                   help="batches per plan / graph (the next chunk's plan overlaps this chunk's training)")
     p.add_argument("--eager", action="store_true", help="eager launches instead of hipGraph replay")
     p.add_argument("--cpu-batches", type=int, default=5823, help="oracle sample size (batches, ~10-30 s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,12 +59,30 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def bytes_per_unit(kind: int, d: int) -> int:
-    """Algorithmic HBM bytes per unit:
-    clean: per triplet, P[u], Q[i], Q[j] + 3 int32 indices;
-    adv:   per triplet, P[u], Q[i], Q[j], dP[u], dQ[i], dQ[j] + 3 indices (SURVEY §8(d));
-    flush: per unique row, read the scratch row + write the table row."""
-    return {0: 3 * d * 4 + 12, 1: 6 * d * 4 + 12, 2: 2 * d * 4}[kind]
+def batch_stats(u, i, j, B, nb, U1, I1):
+    """Per-batch averages of the plan's shapes: unique user rows, unique item
+    rows, fused triplets (user, positive and negative each occurring once)."""
+    n = nb * B
+    t = torch.arange(n, device=u.device, dtype=torch.int64) // B
+    _, inv_u, cnt_u = torch.unique(t * U1 + u[:n].long(), return_inverse=True, return_counts=True)
+    it = torch.cat([t * I1 + i[:n].long(), t * I1 + j[:n].long()])
+    _, inv_i, cnt_i = torch.unique(it, return_inverse=True, return_counts=True)
+    fused = (cnt_u[inv_u] == 1) & (cnt_i[inv_i[:n]] == 1) & (cnt_i[inv_i[n:]] == 1)
+    return {"unique_user_rows": cnt_u.numel() / nb, "unique_item_rows": cnt_i.numel() / nb,
+            "fused_triplets": float(fused.sum()) / nb}
+
+
+def bytes_per_launch(kind: int, d: int, B: int, st: dict) -> float:
+    """Algorithmic HBM bytes of one launch, fp32 rows of 4d bytes:
+    clean (phase 1): P[u], Q[i], Q[j] + 3 int32 indices per triplet that is not fused;
+    adv (phase 2 + fused triplets + Adagrad): every unique row of the batch is read and
+      written with its Adagrad slot (4 row transfers) + 3 indices per triplet;
+    flush: read the scratch row + write the table row, per unique row (upper bound:
+      rows a fused triplet wrote in place are not flushed)."""
+    rows = st["unique_user_rows"] + st["unique_item_rows"]
+    return {0: (3 * d * 4 + 12) * (B - st["fused_triplets"]),
+            1: 4 * d * 4 * rows + 12 * B,
+            2: 2 * d * 4 * rows}[kind]
 
 
 def make_triplets(acf, ds, B, n_batches, dev, seed):
@@ -86,23 +105,7 @@ def init_tables(U1, I1, d, dev, seed):
     return [P, Q, torch.full((U1, d), 0.1, device=dev), torch.full((I1, d), 0.1, device=dev)]
 
 
-def run_batches(ctx, tabs, hp, u, i, j, B, first, count, chunk, graph):
-    b = first
-    while b < first + count:
-        n = min(chunk, first + count - b)
-        s = slice(b * B, (b + n) * B)
-        ctx.plan(u[s], i[s], j[s], B, check=False)
-        ctx.train_planned(tabs, hp, 0, n, graph=graph)
-        b += n
-
-
-def unique_rows_per_batch(u, i, j, B, nb):
-    uu = u[: nb * B].view(nb, B).cpu().numpy()
-    it = torch.cat([i[: nb * B].view(nb, B), j[: nb * B].view(nb, B)], 1).cpu().numpy()
-    return float(np.mean([len(np.unique(r)) for r in uu]) + np.mean([len(np.unique(r)) for r in it]))
-
-
-def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb):
+def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb, st):
     s = slice(0, nb * B)
     ctx.plan(u[s], i[s], j[s], B, check=False)
     t = ctx.time_kernels(tabs, hp, 0, nb)
@@ -111,8 +114,7 @@ def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb):
     dom = max(kinds, key=lambda k: tot[k])
     kid = kinds.index(dom)
     avg_ms = t[dom][0] / max(t[dom][1], 1)
-    units = B if kid < 2 else unique_rows_per_batch(u, i, j, B, nb)
-    alg_bytes = bytes_per_unit(kid, d) * units
+    alg_bytes = bytes_per_launch(kid, d, B, st)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     per_kernel_us = {k: round(1e3 * t[k][0] / max(t[k][1], 1), 3) for k in kinds if t[k][1]}
     return {"bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -141,24 +143,31 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
 def large_batch_roofline(acf, ops, dev, d=128):
     """Batch 65,536 on 10M x 5M tables (d = 128: ~15 GB incl. Adagrad slots):
     tables far beyond the 256 MB Infinity Cache, so rows come from HBM."""
-    U1, I1, B, nb = 10_000_001, 5_000_001, 65536, 8
+    U1, I1, B, nb, chunk = 10_000_001, 5_000_001, 65536, 16, 2
     g = torch.Generator(device=dev).manual_seed(5)
     u = torch.randint(0, U1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
     i = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
     j = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
     tabs = [torch.randn(U1, d, device=dev) * 0.01, torch.randn(I1, d, device=dev) * 0.01,
             torch.full((U1, d), 0.1, device=dev), torch.full((I1, d), 0.1, device=dev)]
-    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev)
     hp = ops.StepHParams(adver=1)
-    run_batches(ctx, tabs, hp, u, i, j, B, 0, nb, nb, True)  # warm (graph capture)
+    pipe.run(tabs, hp, u, i, j, 0, nb)  # warm (graph capture)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    run_batches(ctx, tabs, hp, u, i, j, B, 0, nb, nb, True)
+    pipe.run(tabs, hp, u, i, j, 0, nb)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    rl = kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb)
+    st = batch_stats(u, i, j, B, nb, U1, I1)
+    rl = kernel_roofline(ops, pipe.ctx[0], tabs, hp, u, i, j, B, d, chunk, st)
     rl["triplets_per_s"] = round(nb * B / dt, 1)
-    rl["config"] = {"users": U1 - 1, "items": I1 - 1, "dim": d, "batch": B}
+    step_bytes = bytes_per_launch(1, d, B, st)
+    rl["step_bandwidth"] = {"bytes_per_batch": int(step_bytes),
+                            "achieved_GBs": round(step_bytes * nb / dt / 1e9, 2),
+                            "frac": round(step_bytes * nb / dt / 1e9 / HBM_PEAK_GBS, 5)}
+    rl["batch_stats"] = {k: round(v, 1) for k, v in st.items()}
+    rl["config"] = {"users": U1 - 1, "items": I1 - 1, "dim": d, "batch": B, "batches": nb,
+                    "chunk": chunk}
     del tabs
     torch.cuda.empty_cache()
     return rl
@@ -186,21 +195,21 @@ def main():
     tabs = init_tables(U1, I1, d, dev, seed=rank)
     P0, Q0 = tabs[0].clone(), tabs[1].clone()
     chunk = min(a.chunk, a.steps)
-    ctx = ops.APRContext(U1, I1, d, B, chunk, dev)
+    # B = 512 steps are latency-bound: planning concurrently slows them
+    pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False)
     hp = ops.StepHParams(lr=0.05, eps=0.5, reg=0.0, reg_adv=1.0, adver=1)
     graph = not a.eager
-    # warmup: W steps plus every chunk size the timed region uses (graph capture happens here)
-    run_batches(ctx, tabs, hp, u, i, j, B, 0, a.warmup, chunk, graph)
-    if a.warmup < chunk:
-        run_batches(ctx, tabs, hp, u, i, j, B, 0, chunk, chunk, graph)
+    # warmup: W steps plus every chunk size the timed region uses on both contexts
+    # (graph capture happens here)
+    pipe.run(tabs, hp, u, i, j, 0, max(a.warmup, 2 * chunk), graph=graph)
     if a.steps % chunk:
-        run_batches(ctx, tabs, hp, u, i, j, B, 0, a.steps % chunk, chunk, graph)
+        pipe.run(tabs, hp, u, i, j, 0, 2 * chunk + a.steps % chunk, graph=graph)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    run_batches(ctx, tabs, hp, u, i, j, B, a.warmup, a.steps, chunk, graph)
+    pipe.run(tabs, hp, u, i, j, a.warmup, a.steps, graph=graph)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -213,8 +222,9 @@ def main():
     finite = bool(torch.isfinite(tabs[0]).all() and torch.isfinite(tabs[1]).all())
     # roofline of the dominant kernel (separate eager pass with per-launch events)
     tctx = ops.APRContext(U1, I1, d, B, a.time_batches, dev)
-    roof = kernel_roofline(ops, tctx, tabs, hp, u, i, j, B, d, a.time_batches)
-    step_bytes = bytes_per_unit(1, d) + 3 * d * 4  # gather of 3 rows + 3 acc rows + indices
+    st = batch_stats(u, i, j, B, a.time_batches, U1, I1)
+    roof = kernel_roofline(ops, tctx, tabs, hp, u, i, j, B, d, a.time_batches, st)
+    step_bytes = bytes_per_launch(1, d, B, st)  # every unique row: w, acc read + written
     out = {
         "metric": "BPR triplets/sec (APR ml-1m d=64)",
         "value": round(value, 1),
@@ -234,15 +244,16 @@ def main():
                    "per_gpu_batch": B, "parallelism": f"replicas x{world}",
                    "launch": "eager" if a.eager else "hipGraph"},
         "roofline": roof,
-        "step_bandwidth": {"bytes_per_triplet": step_bytes,
-                           "achieved_GBs": round(value / world * step_bytes / 1e9, 2),
-                           "frac": round(value / world * step_bytes / 1e9 / HBM_PEAK_GBS, 5)},
+        "step_bandwidth": {"bytes_per_batch": int(step_bytes),
+                           "achieved_GBs": round(value / world / B * step_bytes / 1e9, 2),
+                           "frac": round(value / world / B * step_bytes / 1e9 / HBM_PEAK_GBS, 5)},
+        "batch_stats": {k: round(v, 1) for k, v in st.items()},
         "tables_finite": finite,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(u, i, j, P0, Q0, B, a.cpu_batches)
     if rank == 0 and a.large:
-        del ctx, tctx
+        del pipe, tctx
         torch.cuda.empty_cache()
         out["roofline_large_batch"] = large_batch_roofline(acf, ops, dev, 128)
         torch.cuda.empty_cache()
