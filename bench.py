@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--chunk", type=int, default=647,
                    help="batches per plan / graph (the next chunk's plan overlaps this chunk's training)")
     p.add_argument("--eager", action="store_true", help="eager launches instead of hipGraph replay")
-    p.add_argument("--cpu-batches", type=int, default=5823, help="oracle sample size (batches, ~10-30 s)")
+    p.add_argument("--cpu-batches", type=int, default=17469, help="oracle sample size (batches, ~10-30 s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--time-batches", type=int, default=400, help="batches in the kernel-timing pass")
     p.add_argument("--large", action="store_true", help="also measure batch 65536 on 10M x 5M x d128")
@@ -73,16 +73,22 @@ def batch_stats(u, i, j, B, nb, U1, I1):
 
 
 def bytes_per_launch(kind: int, d: int, B: int, st: dict) -> float:
-    """Algorithmic HBM bytes of one launch, fp32 rows of 4d bytes:
-    clean (phase 1): P[u], Q[i], Q[j] + 3 int32 indices per triplet that is not fused;
-    adv (phase 2 + fused triplets + Adagrad): every unique row of the batch is read and
-      written with its Adagrad slot (4 row transfers) + 3 indices per triplet;
+    """Algorithmic HBM bytes of one launch, fp32 rows of 4d bytes.
+    adv (phase 2 + fused triplets + Adagrad) uses SURVEY.md §8(d)'s official figure:
+      per triplet, reads of P[u], Q[i], Q[j] and their 3 Adagrad rows + 12 B of indices;
+    clean (phase 1): P[u], Q[i], Q[j] + indices per triplet that is not fused;
     flush: read the scratch row + write the table row, per unique row (upper bound:
       rows a fused triplet wrote in place are not flushed)."""
     rows = st["unique_user_rows"] + st["unique_item_rows"]
     return {0: (3 * d * 4 + 12) * (B - st["fused_triplets"]),
-            1: 4 * d * 4 * rows + 12 * B,
+            1: (6 * d * 4 + 12) * B,
             2: 2 * d * 4 * rows}[kind]
+
+
+def unique_rw_bytes(d: int, B: int, st: dict) -> float:
+    """Compulsory traffic of a whole step with duplicates deflated: every unique
+    row's weights and Adagrad slot read once and written once + the indices."""
+    return 4 * d * 4 * (st["unique_user_rows"] + st["unique_item_rows"]) + 12 * B
 
 
 def make_triplets(acf, ds, B, n_batches, dev, seed):
@@ -105,6 +111,36 @@ def init_tables(U1, I1, d, dev, seed):
     return [P, Q, torch.full((U1, d), 0.1, device=dev), torch.full((I1, d), 0.1, device=dev)]
 
 
+def step_kernel_name(kind: str, d: int, B: int) -> str:
+    """Template instance of the step kernel the library launches for (d, B) with
+    fusion on (csrc/acf_apr.hip: geometry(), get_kernels())."""
+    d4 = d // 4
+    lpr = 1
+    while lpr < d4 and lpr < 64:
+        lpr <<= 1
+    nv = (d4 + lpr - 1) // lpr
+    team = 1 if B >= 4096 or lpr == 64 else 64 // lpr
+    if kind == "adv":
+        return f"k_adv<{lpr}, {nv}, {team}, true>"
+    if kind == "clean":
+        return f"k_clean<{lpr}, {nv}, false, {team}, false>"
+    return "k_flush"
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch from the newest profiles/rNN/pmc_traffic.json (rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes of this bench, tools/profile_bench.sh), or None."""
+    root = os.path.join(REPO, "profiles")
+    for r in sorted(os.listdir(root) if os.path.isdir(root) else [], reverse=True):
+        f = os.path.join(root, r, "pmc_traffic.json")
+        if os.path.isfile(f):
+            with open(f) as fh:
+                rec = json.load(fh).get(kernel)
+            if rec:
+                return rec["traffic_bytes_per_launch"], f"{r}/pmc_traffic.json"
+    return None
+
+
 def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb, st):
     s = slice(0, nb * B)
     ctx.plan(u[s], i[s], j[s], B, check=False)
@@ -116,11 +152,28 @@ def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb, st):
     avg_ms = t[dom][0] / max(t[dom][1], 1)
     alg_bytes = bytes_per_launch(kid, d, B, st)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    rw = unique_rw_bytes(d, B, st) / (avg_ms * 1e-3) / 1e9 if kid == 1 else None
     per_kernel_us = {k: round(1e3 * t[k][0] / max(t[k][1], 1), 3) for k in kinds if t[k][1]}
-    return {"bound": "hbm", "kernel": f"k_{dom}", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+    name = step_kernel_name(dom, d, B)
+    tr = pmc_traffic(name)
+    return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None if tr is None else tr[0],
+            "traffic_source": None if tr is None else tr[1],
             "bytes_per_launch": int(alg_bytes), "avg_launch_us": round(avg_ms * 1e3, 3),
-            "per_kernel_avg_us": per_kernel_us}
+            "per_kernel_avg_us": per_kernel_us,
+            "achieved_unique_rw_GBs": None if rw is None else round(rw, 2)}
+
+
+def step_bandwidth(d, B, st, triplets_per_s):
+    """Whole-step rates per GPU: SURVEY §8(d)'s HBM-read roofline (official) and the
+    duplicate-deflated unique-row read+write traffic."""
+    official = (6 * d * 4 + 12) * triplets_per_s / 1e9
+    rw = unique_rw_bytes(d, B, st) * triplets_per_s / B / 1e9
+    return {"bytes_per_triplet": 6 * d * 4 + 12, "achieved_GBs": round(official, 2),
+            "frac": round(official / HBM_PEAK_GBS, 5),
+            "unique_rw_bytes_per_batch": int(unique_rw_bytes(d, B, st)),
+            "unique_rw_GBs": round(rw, 2)}
 
 
 def cpu_baseline(u, i, j, P0, Q0, B, nb):
@@ -143,7 +196,7 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
 def large_batch_roofline(acf, ops, dev, d=128):
     """Batch 65,536 on 10M x 5M tables (d = 128: ~15 GB incl. Adagrad slots):
     tables far beyond the 256 MB Infinity Cache, so rows come from HBM."""
-    U1, I1, B, nb, chunk = 10_000_001, 5_000_001, 65536, 16, 2
+    U1, I1, B, nb, chunk = 10_000_001, 5_000_001, 65536, 32, 8
     g = torch.Generator(device=dev).manual_seed(5)
     u = torch.randint(0, U1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
     i = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
@@ -161,10 +214,7 @@ def large_batch_roofline(acf, ops, dev, d=128):
     st = batch_stats(u, i, j, B, nb, U1, I1)
     rl = kernel_roofline(ops, pipe.ctx[0], tabs, hp, u, i, j, B, d, chunk, st)
     rl["triplets_per_s"] = round(nb * B / dt, 1)
-    step_bytes = bytes_per_launch(1, d, B, st)
-    rl["step_bandwidth"] = {"bytes_per_batch": int(step_bytes),
-                            "achieved_GBs": round(step_bytes * nb / dt / 1e9, 2),
-                            "frac": round(step_bytes * nb / dt / 1e9 / HBM_PEAK_GBS, 5)}
+    rl["step_bandwidth"] = step_bandwidth(d, B, st, nb * B / dt)
     rl["batch_stats"] = {k: round(v, 1) for k, v in st.items()}
     rl["config"] = {"users": U1 - 1, "items": I1 - 1, "dim": d, "batch": B, "batches": nb,
                     "chunk": chunk}
@@ -224,7 +274,7 @@ def main():
     tctx = ops.APRContext(U1, I1, d, B, a.time_batches, dev)
     st = batch_stats(u, i, j, B, a.time_batches, U1, I1)
     roof = kernel_roofline(ops, tctx, tabs, hp, u, i, j, B, d, a.time_batches, st)
-    step_bytes = bytes_per_launch(1, d, B, st)  # every unique row: w, acc read + written
+
     out = {
         "metric": "BPR triplets/sec (APR ml-1m d=64)",
         "value": round(value, 1),
@@ -244,9 +294,7 @@ def main():
                    "per_gpu_batch": B, "parallelism": f"replicas x{world}",
                    "launch": "eager" if a.eager else "hipGraph"},
         "roofline": roof,
-        "step_bandwidth": {"bytes_per_batch": int(step_bytes),
-                           "achieved_GBs": round(value / world / B * step_bytes / 1e9, 2),
-                           "frac": round(value / world / B * step_bytes / 1e9 / HBM_PEAK_GBS, 5)},
+        "step_bandwidth": step_bandwidth(d, B, st, value / world),
         "batch_stats": {k: round(v, 1) for k, v in st.items()},
         "tables_finite": finite,
     }
