@@ -14,9 +14,11 @@ module also registers itself as ``acf_amd``).
 import sys as _sys
 
 from . import _native  # noqa: F401
-from .data import OriginalDataset, SyntheticDataset, get_dataset, ml1m_like, pinterest_like, synthetic_dataset
+from .data import (OriginalDataset, SyntheticDataset, get_dataset, ml1m_like, pinterest_like,
+                   synthetic_dataset, yelp_like)
 from .evaluate import evaluate, init_eval_model
 from .model import MF, Session
+from .neumf import AdversarialNeuMF, NeuMF
 from .recommender import APR, Recommender
 from .sampler import DeviceSampler, EpochTriplets, sampling, shuffle
 from .train import (output_evaluate, prediction2file, training, training_batch, training_loss_acc,
@@ -25,8 +27,8 @@ from .train import (output_evaluate, prediction2file, training, training_batch, 
 _sys.modules.setdefault("acf_amd", _sys.modules[__name__])
 
 __all__ = [
-    "APR", "DeviceSampler", "EpochTriplets", "MF", "OriginalDataset", "Recommender", "Session",
+    "APR", "AdversarialNeuMF", "DeviceSampler", "EpochTriplets", "MF", "NeuMF", "OriginalDataset", "Recommender", "Session",
     "SyntheticDataset", "evaluate", "get_dataset", "init_eval_model", "ml1m_like", "output_evaluate",
     "pinterest_like", "prediction2file", "sampling", "shuffle", "synthetic_dataset", "training",
-    "training_batch", "training_loss_acc", "write2file",
+    "training_batch", "training_loss_acc", "write2file", "yelp_like",
 ]

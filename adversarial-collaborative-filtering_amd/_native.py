@@ -117,3 +117,63 @@ def exported_symbols(path: str = LIB_PATH) -> set[str]:
     """Names from SIGNATURES that the shared object exports (no GPU needed)."""
     lib = ctypes.CDLL(path)
     return {n for n in SIGNATURES if hasattr(lib, n)}
+
+
+# --- libacf_neumf.so (include/acf_neumf.h) ------------------------------------
+NEUMF_LIB_PATH = os.path.join(PKG_DIR, "lib", "libacf_neumf.so")
+
+
+class NeuMFHParams(ctypes.Structure):
+    """acf_neumf_hparams."""
+    _fields_ = [("lr", _F), ("beta1", _F), ("beta2", _F), ("adam_eps", _F), ("eps", _F),
+                ("reg_adv", _F), ("adver", _I32), ("reserved", _I32)]
+
+
+NEUMF_SIGNATURES = {
+    "acf_neumf_last_error": (ctypes.c_char_p, []),
+    "acf_neumf_param_count": (_I64, [_I64, _I64, _I32]),
+    "acf_neumf_param_offsets": (ctypes.c_int, [_I64, _I64, _I32, ctypes.POINTER(_I64)]),
+    "acf_neumf_create": (ctypes.c_int, [ctypes.POINTER(_P), _I64, _I64, _I32, _I32]),
+    "acf_neumf_destroy": (ctypes.c_int, [_P]),
+    "acf_neumf_grad": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, ctypes.POINTER(NeuMFHParams), _P,
+                                      _I32, _P]),
+    "acf_neumf_adam": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, ctypes.POINTER(NeuMFHParams), _P]),
+    "acf_neumf_predict": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P]),
+    "acf_neumf_train": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I64,
+                                       ctypes.POINTER(NeuMFHParams), _P, _P]),
+}
+
+_neumf = None
+
+
+def load_neumf(path: str = NEUMF_LIB_PATH) -> ctypes.CDLL:
+    """Load libacf_neumf.so (once).  Raises ImportError if it was never built."""
+    global _neumf
+    with _lock:
+        if _neumf is not None:
+            return _neumf
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not found: the HIP extension is not built. Run "
+                              "`python adversarial-collaborative-filtering_amd/build_native.py`. "
+                              "There is no CPU fallback.")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in NEUMF_SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _neumf = lib
+        return lib
+
+
+def call_neumf(name: str, *args) -> None:
+    lib = load_neumf()
+    rc = getattr(lib, name)(*args)
+    if rc != ACF_OK:
+        msg = lib.acf_neumf_last_error().decode("utf-8", "replace")
+        cls = NativeIndexError if rc == ACF_E_RANGE else NativeError
+        raise cls(rc, name, msg)
+
+
+def neumf_exported_symbols(path: str = NEUMF_LIB_PATH) -> set[str]:
+    lib = ctypes.CDLL(path)
+    return {n for n in NEUMF_SIGNATURES if hasattr(lib, n)}

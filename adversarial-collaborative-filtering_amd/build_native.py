@@ -1,6 +1,7 @@
-"""Build the in-tree HIP library ``lib/libacf_apr.so`` (kernels + C-ABI of
-``include/acf_apr.h``) with ``hipcc --offload-arch=gfx950``.  It lands inside the
-repository so that ``gpurun`` ships it to the GPU box.
+"""Build the in-tree HIP libraries with ``hipcc --offload-arch=gfx950``:
+``lib/libacf_apr.so`` (APR path, C-ABI of ``include/acf_apr.h``) and
+``lib/libacf_neumf.so`` (NeuMF path, ``include/acf_neumf.h``).  They land inside
+the repository so that ``gpurun`` ships them to the GPU box.
 """
 from __future__ import annotations
 
@@ -13,6 +14,10 @@ REPO = os.path.dirname(PKG_DIR)
 HIP_SRC = os.path.join(PKG_DIR, "csrc", "acf_apr.hip")
 HIP_LIB = os.path.join(PKG_DIR, "lib", "libacf_apr.so")
 HEADER = os.path.join(REPO, "include", "acf_apr.h")
+NEUMF_SRC = os.path.join(PKG_DIR, "csrc", "acf_neumf.hip")
+NEUMF_LIB = os.path.join(PKG_DIR, "lib", "libacf_neumf.so")
+NEUMF_HEADER = os.path.join(REPO, "include", "acf_neumf.h")
+TARGETS = [(HIP_SRC, HIP_LIB, [HEADER]), (NEUMF_SRC, NEUMF_LIB, [HEADER, NEUMF_HEADER])]
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -34,15 +39,16 @@ def _stale(target: str, sources: list[str]) -> bool:
 
 
 def build_hip(force: bool = False, verbose: bool = True) -> str:
-    if force or _stale(HIP_LIB, [HIP_SRC, HEADER, __file__]):
-        os.makedirs(os.path.dirname(HIP_LIB), exist_ok=True)
-        hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-        tmp = HIP_LIB + ".tmp"
-        cmd = [hipcc, *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), HIP_SRC, "-o", tmp]
-        if verbose:
-            print("[build]", " ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
-        os.replace(tmp, HIP_LIB)
+    for src, lib, headers in TARGETS:
+        if force or _stale(lib, [src, *headers, __file__]):
+            os.makedirs(os.path.dirname(lib), exist_ok=True)
+            hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+            tmp = lib + ".tmp"
+            cmd = [hipcc, *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), src, "-o", tmp]
+            if verbose:
+                print("[build]", " ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+            os.replace(tmp, lib)
     return HIP_LIB
 
 

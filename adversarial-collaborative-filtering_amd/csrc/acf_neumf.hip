@@ -1,0 +1,843 @@
+// acf_neumf.hip — MI355X (gfx950) kernels + C-ABI for NeuMF and adversarial
+// NeuMF training (include/acf_neumf.h; SURVEY.md §8(f)3, BASELINE configs[3]).
+//
+// Reference graph: NeuMF.py:10-52 (Keras), trained by MF.py:30-33 (fit: mean
+// binary cross-entropy + Adam) and scored by MF.py:38-40.  One training step
+// (Keras train_on_batch) here:
+//
+//   k_nmf_inst<CLEAN>   one workgroup per 16 instances: gather MF_U[u], MF_I[i],
+//                       MLP_U[u], MLP_I[i]; MLP [2d -> 2d -> d] relu on f32 MFMA
+//                       (16x16x4, exact f32 products); head; BCE
+//                       (prediction clipped to [1e-7, 1-1e-7]); backward through
+//                       head and MLP; per-instance row contributions + the
+//                       activations the weight gradients need (scratch)
+//   k_nmf_wpart/wsum    weight gradients as split-K outer-product sums: LDS
+//                       tiles of 32x32 outputs x 64 instances, then the chunks
+//                       summed in a fixed order (deterministic, no atomics)
+//   k_nmf_rows          one wave per (instance, side): the row's first
+//                       occurrence owns it and sums every occurrence's
+//                       contribution in instance order into the gradient row;
+//                       with adver also delta = eps * g / |g| of that row
+//   (adver) k_nmf_inst<ADV>, k_nmf_wgrad, k_nmf_rows on the perturbed rows,
+//                       scaled by reg_adv
+//   k_nmf_adam          Keras 2.2 Adam over the WHOLE flat parameter buffer
+//                       (Keras densifies the embedding IndexedSlices, so every
+//                       row's moments decay and every row moves): one HBM
+//                       stream of p, g, m, v, zeroing g behind it.
+//
+// The MLP is tiny per instance (2d x 2d and 2d x d at d = 64) and the step is
+// bound by the dense Adam stream over the tables, not by the GEMMs.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "acf_apr.h"
+#include "acf_neumf.h"
+
+static thread_local std::string g_neumf_error;
+
+static int set_error(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_neumf_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                             \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess)                                                         \
+      return set_error(ACF_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define ACF_CHECK(cond, code, ...)                      \
+  do {                                                  \
+    if (!(cond)) return set_error((code), __VA_ARGS__); \
+  } while (0)
+
+// parameter segments, in Keras order
+enum { S_MF_U = 0, S_MF_I, S_MLP_U, S_MLP_I, S_W1, S_B1, S_W2, S_B2, S_WO, S_BO, S_COUNT };
+
+struct Layout {
+  int64_t off[S_COUNT];
+  int64_t total;
+};
+
+static Layout make_layout(int64_t U1, int64_t I1, int64_t d) {
+  Layout L;
+  L.off[S_MF_U] = 0;
+  L.off[S_MF_I] = U1 * d;
+  L.off[S_MLP_U] = (U1 + I1) * d;
+  L.off[S_MLP_I] = (2 * U1 + I1) * d;
+  L.off[S_W1] = 2 * (U1 + I1) * d;
+  L.off[S_B1] = L.off[S_W1] + 4 * d * d;
+  L.off[S_W2] = L.off[S_B1] + 2 * d;
+  L.off[S_B2] = L.off[S_W2] + 2 * d * d;
+  L.off[S_WO] = L.off[S_B2] + d;
+  L.off[S_BO] = L.off[S_WO] + 2 * d;
+  L.total = L.off[S_BO] + 4;  // bo + pad: every segment starts 16-B aligned
+  return L;
+}
+
+
+struct NArgs {
+  const float* P;
+  float* G;
+  int64_t off[S_COUNT];
+  const int32_t* u;
+  const int32_t* i;
+  const float* y;
+  int64_t U1, I1;
+  int32_t B, d;
+  float scale_over_B;  // 1/B (clean) or reg_adv/B (adversarial)
+  // scratch [B, ...]
+  float *h0, *a1, *f, *dz1, *dz2, *dlogit, *loss, *contrib;  // contrib [B][4][d]
+  const float* delta;    // [B][4][d], rows written at their owner instance
+  const int32_t* owner;  // [B][2] first occurrence of the instance's user / item
+  float* pred;
+  int32_t* err;
+};
+
+__device__ __forceinline__ int32_t clamp_idx(int32_t r, int64_t n) { return (r < 0 || r >= n) ? 0 : r; }
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int MR = 16;  // instances per workgroup = the MFMA tile height
+
+// W1 and W2 are staged in LDS (row stride +1 float: the transposed reads of the
+// backward products are then conflict-free) when they fit beside the activations
+__host__ __device__ __forceinline__ bool weights_in_lds(int d) { return d <= 64; }
+
+// C[MR x N] = A[MR x K] . w(k, n) on v_mfma_f32_16x16x4_f32 (exact f32 products,
+// k-ordered fma chain).  A: LDS, row-major with leading dimension lda (padded so
+// the 16 lanes reading one k hit different banks); w(k, n) = W[k*ldw + n], or
+// W[n*ldw + k] with TRANS (the backward products with W^T).  The 4 waves take
+// 32-column panels (two 16x16 tiles, two independent accumulators) round-robin;
+// epi(row, col, value) consumes every output element.
+// Lane maps (cdna_hip_programming.md §3): A[l&15][k0 + (l>>4)], B[k0 + (l>>4)][l&15],
+// C/D: col = l&15, row = 4*(l>>4) + reg.
+template <bool TRANS>
+__device__ __forceinline__ float w_at(const float* __restrict__ W, int ldw, int k, int col) {
+  return TRANS ? W[(int64_t)col * ldw + k] : W[(int64_t)k * ldw + col];
+}
+
+template <bool TRANS, class Epi>
+__device__ __forceinline__ void mfma_panel(const float* sA, int lda, const float* __restrict__ W, int ldw,
+                                           int K, int N, Epi epi) {
+  constexpr int KB = 8;  // k-steps whose operands are read before their MFMAs issue
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, h = lane >> 4;
+  if (N > 64) {
+    // two 16-column tiles per wave (independent accumulators), 32-column panels
+    for (int n0 = wave * 32; n0 < N; n0 += 4 * 32) {
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+      const int ca = n0 + r, cb = n0 + 16 + r;
+      for (int kb = 0; kb < K; kb += 4 * KB) {
+        float av[KB], ba[KB], bb[KB];
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+          const int k = kb + 4 * j + h;
+          const bool ok = k < K;
+          av[j] = ok ? sA[r * lda + k] : 0.f;
+          ba[j] = (ok && ca < N) ? w_at<TRANS>(W, ldw, k, ca) : 0.f;
+          bb[j] = (ok && cb < N) ? w_at<TRANS>(W, ldw, k, cb) : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+          c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], ba[j], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bb[j], c1, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (ca < N) epi(4 * h + q, ca, c0[q]);
+        if (cb < N) epi(4 * h + q, cb, c1[q]);
+      }
+    }
+  } else {
+    // N <= 64: one 16-column tile per wave, K split over two accumulators
+    const int c = wave * 16 + r;
+    if (wave * 16 >= N) return;
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < K; kb += 8 * KB) {
+      float a0[KB], a1[KB], w0[KB], w1[KB];
+#pragma unroll
+      for (int j = 0; j < KB; ++j) {
+        const int k = kb + 8 * j + h, k1 = k + 4;
+        a0[j] = k < K ? sA[r * lda + k] : 0.f;
+        a1[j] = k1 < K ? sA[r * lda + k1] : 0.f;
+        w0[j] = (k < K && c < N) ? w_at<TRANS>(W, ldw, k, c) : 0.f;
+        w1[j] = (k1 < K && c < N) ? w_at<TRANS>(W, ldw, k1, c) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < KB; ++j) {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], w0[j], c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], w1[j], c1, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (c < N) epi(4 * h + q, c, c0[q] + c1[q]);
+  }
+}
+
+#ifdef NMF_DIAG  // diagnostic build only: phase stamps (100 MHz) of workgroup 0, clean pass
+__device__ uint64_t g_nmf_stamps[16];
+#define NSTAMP(i)                                                                          \
+  do {                                                                                     \
+    uint64_t t_;                                                                           \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    if (MODE == 0 && blockIdx.x == 0 && threadIdx.x == 0) g_nmf_stamps[i] = t_;           \
+  } while (0)
+#else
+#define NSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
+template <int MODE>
+__global__ void __launch_bounds__(256) k_nmf_inst(NArgs a) {
+  extern __shared__ float sm[];
+  NSTAMP(0);
+  const int d = a.d, d2 = 2 * d, tid = threadIdx.x;
+  const int L2 = d2 + 1, L1 = d + 1;  // padded leading dimensions
+  const int64_t b0 = (int64_t)blockIdx.x * MR;
+  const int nt = (int)min((int64_t)MR, (int64_t)a.B - b0);
+  float* s_x = sm;                 // [MR][L2]  h0 = MLP_U[u] | MLP_I[i]; later dz1
+  float* s_a1 = s_x + MR * L2;     // [MR][L2]
+  float* s_f = s_a1 + MR * L2;     // [MR][L2]  MF_U*MF_I | a2
+  float* s_mu = s_f + MR * L2;     // [MR][L1]
+  float* s_mi = s_mu + MR * L1;    // [MR][L1]
+  float* s_dz2 = s_mi + MR * L1;   // [MR][L1]
+  float* s_dl = s_dz2 + MR * L1;   // [MR]
+  float* s_vec = s_dl + MR;        // b1 [2d] | b2 [d] | Wo [2d] | bo (+3)
+  float* s_b1 = s_vec, *s_b2 = s_vec + d2, *s_wo = s_b2 + d, *s_bo = s_wo + d2;
+  float* s_w1 = s_bo + 4;          // [2d][2d+1] (weights_in_lds)
+  float* s_w2 = s_w1 + d2 * L2;    // [2d][d+1]
+  const bool wl = weights_in_lds(d);
+  // One round trip for everything the workgroup needs: each thread issues its
+  // index -> row gathers, its share of W1 / W2 and of the bias / head vectors,
+  // and only then stores them to LDS.
+  constexpr int QG = MR * 128 / 256;  // gather elements per thread (d <= 128)
+  float g[QG][4];
+#pragma unroll
+  for (int q = 0; q < QG; ++q) {
+    const int x = tid + 256 * q;
+    const int t = x / d, k = x - t * d;
+    g[q][0] = g[q][1] = g[q][2] = g[q][3] = 0.f;
+    if (x < MR * d && t < nt) {
+      int32_t uu = a.u[b0 + t], ii = a.i[b0 + t];
+      if (uu < 0 || uu >= a.U1) { if (k == 0) atomicOr(a.err, 1); uu = 0; }
+      if (ii < 0 || ii >= a.I1) { if (k == 0) atomicOr(a.err, 2); ii = 0; }
+      const int64_t ru = (int64_t)uu * d + k, ri = (int64_t)ii * d + k;
+      g[q][0] = a.P[a.off[S_MF_U] + ru];
+      g[q][1] = a.P[a.off[S_MF_I] + ri];
+      g[q][2] = a.P[a.off[S_MLP_U] + ru];
+      g[q][3] = a.P[a.off[S_MLP_I] + ri];
+      if (MODE == 1) {
+        const int64_t b = b0 + t;
+        const float* du = a.delta + (int64_t)a.owner[2 * b] * 4 * d;
+        const float* di = a.delta + (int64_t)a.owner[2 * b + 1] * 4 * d;
+        g[q][0] = g[q][0] + du[0 * d + k];
+        g[q][1] = g[q][1] + di[1 * d + k];
+        g[q][2] = g[q][2] + du[2 * d + k];
+        g[q][3] = g[q][3] + di[3 * d + k];
+      }
+    }
+  }
+  constexpr int Q1 = 64 * 64 * 4 / 4 / 256, Q2 = 64 * 64 * 2 / 4 / 256;  // weights_in_lds: d <= 64
+  const int n1 = wl ? d2 * d2 / 4 : 0, n2 = wl ? d2 * d / 4 : 0;
+  float4 v1[Q1], v2[Q2];
+  {
+    const float4* g1 = reinterpret_cast<const float4*>(a.P + a.off[S_W1]);
+    const float4* g2 = reinterpret_cast<const float4*>(a.P + a.off[S_W2]);
+#pragma unroll
+    for (int q = 0; q < Q1; ++q) if (tid + 256 * q < n1) v1[q] = g1[tid + 256 * q];
+#pragma unroll
+    for (int q = 0; q < Q2; ++q) if (tid + 256 * q < n2) v2[q] = g2[tid + 256 * q];
+  }
+  const int nvec = 5 * d + 1;  // b1, b2, Wo, bo
+  constexpr int QV = (5 * 128 + 1 + 255) / 256;  // d <= 128
+  float vv[QV];
+#pragma unroll
+  for (int q = 0; q < QV; ++q) {
+    const int x = tid + 256 * q;
+    vv[q] = 0.f;
+    if (x < nvec) {
+      const int64_t src = x < d2 ? a.off[S_B1] + x
+                                 : x < 3 * d ? a.off[S_B2] + (x - d2)
+                                             : x < 5 * d ? a.off[S_WO] + (x - 3 * d) : a.off[S_BO];
+      vv[q] = a.P[src];
+    }
+  }
+  // stores
+#pragma unroll
+  for (int q = 0; q < QV; ++q)
+    if (tid + 256 * q < nvec) s_vec[tid + 256 * q] = vv[q];
+#pragma unroll
+  for (int q = 0; q < Q1; ++q) {
+    const int x = tid + 256 * q;
+    if (x < n1) {
+      const int e = 4 * x, rr = e / d2, cc = e - rr * d2;
+      float* dst = s_w1 + rr * L2 + cc;
+      dst[0] = v1[q].x; dst[1] = v1[q].y; dst[2] = v1[q].z; dst[3] = v1[q].w;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < Q2; ++q) {
+    const int x = tid + 256 * q;
+    if (x < n2) {
+      const int e = 4 * x, rr = e / d, cc = e - rr * d;
+      float* dst = s_w2 + rr * L1 + cc;
+      dst[0] = v2[q].x; dst[1] = v2[q].y; dst[2] = v2[q].z; dst[3] = v2[q].w;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < QG; ++q) {
+    const int x = tid + 256 * q;
+    if (x < MR * d) {
+      const int t = x / d, k = x - t * d;
+      const float mu = g[q][0], mi = g[q][1], lu = g[q][2], li = g[q][3];
+      if (MODE != 2 && t < nt) {
+        a.h0[(b0 + t) * d2 + k] = lu;
+        a.h0[(b0 + t) * d2 + d + k] = li;
+      }
+      s_mu[t * L1 + k] = mu;
+      s_mi[t * L1 + k] = mi;
+      s_x[t * L2 + k] = lu;
+      s_x[t * L2 + d + k] = li;
+      s_f[t * L2 + k] = mu * mi;  // GMF tower
+    }
+  }
+  __syncthreads();
+  NSTAMP(1);
+  NSTAMP(2);
+  const float* W1 = wl ? s_w1 : a.P + a.off[S_W1];
+  const float* W2 = wl ? s_w2 : a.P + a.off[S_W2];
+  const int ld1 = wl ? L2 : d2, ld2 = wl ? L1 : d;
+  const float* Wo = s_wo;
+  const float* b1 = s_b1;
+  const float* b2 = s_b2;
+  // layer 1: a1 = relu(h0 W1 + b1)
+  mfma_panel<false>(s_x, L2, W1, ld1, d2, d2, [&](int row, int col, float v) {
+    const float z = v + b1[col];
+    s_a1[row * L2 + col] = z > 0.f ? z : 0.f;
+  });
+  __syncthreads();
+  NSTAMP(3);
+  // layer 2: a2 = relu(a1 W2 + b2) -> f[d:2d]
+  mfma_panel<false>(s_a1, L2, W2, ld2, d2, d, [&](int row, int col, float v) {
+    const float z = v + b2[col];
+    s_f[row * L2 + d + col] = z > 0.f ? z : 0.f;
+  });
+  __syncthreads();
+  NSTAMP(4);
+  // head: 16 lanes per instance, p = sigmoid(f Wo + bo); Keras BCE on clip(p)
+  {
+    const int row = tid >> 4, part = tid & 15;
+    float sacc = 0.f;
+    for (int k = part; k < d2; k += 16) sacc = sacc + s_f[row * L2 + k] * Wo[k];
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) sacc += __shfl_xor(sacc, m, 64);
+    if (part == 0) {
+      const float logit = sacc + s_bo[0];
+      const float p = 1.0f / (1.0f + expf(-logit));
+      if (MODE == 2) {
+        if (row < nt) a.pred[b0 + row] = p;
+      } else {
+        const float y = row < nt ? a.y[b0 + row] : 0.f;
+        const bool inside = p >= 1e-7f && p <= 1.0f - 1e-7f;  // clip_by_value's gradient
+        const float dl = (row < nt && inside) ? (p - y) * a.scale_over_B : 0.f;
+        const float pc = fminf(fmaxf(p, 1e-7f), 1.0f - 1e-7f);
+        s_dl[row] = dl;
+        if (row < nt) {
+          a.dlogit[b0 + row] = dl;
+          a.loss[b0 + row] = -(y * logf(pc) + (1.0f - y) * logf(1.0f - pc));
+        }
+      }
+    }
+  }
+  if (MODE == 2) return;
+  __syncthreads();
+  NSTAMP(5);
+  // dz2 = (dl * Wo[d:2d]) * (a2 > 0); GMF row contributions dmf * MF_I / dmf * MF_U
+  for (int x = tid; x < MR * d; x += 256) {
+    const int t = x / d, k = x - t * d;
+    const float dl = s_dl[t];
+    const float dz = s_f[t * L2 + d + k] > 0.f ? dl * Wo[d + k] : 0.f;
+    s_dz2[t * L1 + k] = dz;
+    if (t < nt) {
+      const float dmf = dl * Wo[k];
+      a.contrib[((b0 + t) * 4 + S_MF_U) * d + k] = dmf * s_mi[t * L1 + k];
+      a.contrib[((b0 + t) * 4 + S_MF_I) * d + k] = dmf * s_mu[t * L1 + k];
+      a.dz2[(b0 + t) * d + k] = dz;
+    }
+  }
+  __syncthreads();
+  NSTAMP(6);
+  // dz1 = (dz2 W2^T) * (a1 > 0) -> s_x (h0 is already in the scratch)
+  mfma_panel<true>(s_dz2, L1, W2, ld2, d, d2, [&](int row, int col, float v) {
+    s_x[row * L2 + col] = s_a1[row * L2 + col] > 0.f ? v : 0.f;
+  });
+  __syncthreads();
+  NSTAMP(7);
+  // dh0 = dz1 W1^T -> MLP_U / MLP_I row contributions
+  mfma_panel<true>(s_x, L2, W1, ld1, d2, d2, [&](int row, int col, float v) {
+    if (row < nt) {
+      const int tab = col < d ? S_MLP_U : S_MLP_I, kk = col < d ? col : col - d;
+      a.contrib[((b0 + row) * 4 + tab) * d + kk] = v;
+    }
+  });
+  // activations for the weight gradients
+  for (int x = tid; x < MR * d2; x += 256) {
+    const int t = x / d2, k = x - t * d2;
+    if (t < nt) {
+      const int64_t g = (b0 + t) * d2 + k;
+      a.a1[g] = s_a1[t * L2 + k];
+      a.f[g] = s_f[t * L2 + k];
+      a.dz1[g] = s_x[t * L2 + k];
+    }
+  }
+  NSTAMP(8);
+}
+
+// Weight gradients: every one is a sum over the batch of an outer product,
+// out[k][n] = sum_b A[b][k] * Bm[b][n] (A = 1 for biases and the loss):
+//   0 W1 = h0^T dz1 [2d,2d]   1 W2 = a1^T dz2 [2d,d]   2 Wo = f^T dlogit [2d,1]
+//   3 b1 = 1^T dz1 [1,2d]     4 b2 = 1^T dz2 [1,d]     5 bo = 1^T dlogit   6 loss sum
+// k_nmf_wpart: one workgroup per (32x32 output tile, chunk of 64 instances),
+// operands staged in LDS, 4 outputs per thread, summed in instance order;
+// k_nmf_wsum: one thread per output, the chunks summed in order (deterministic).
+constexpr int WT = 32, WCH = 64, NMAT = 7;
+
+struct WMat {
+  const float* A;  // [B][lda] or nullptr (ones)
+  const float* Bm; // [B][ldb]
+  int K, N, lda, ldb;
+  int64_t out_off;  // offset in the partial / output vector
+  int tiles_n, tile0;
+};
+
+struct WJobs {
+  WMat m[NMAT];
+  int ntiles;
+  int64_t nout;
+};
+
+static WJobs make_jobs(const NArgs& a) {
+  const int d = a.d, d2 = 2 * d;
+  WJobs J;
+  const float* ones = nullptr;
+  const WMat base[NMAT] = {{a.h0, a.dz1, d2, d2, d2, d2, 0, 0, 0},  {a.a1, a.dz2, d2, d, d2, d, 0, 0, 0},
+                           {a.f, a.dlogit, d2, 1, d2, 1, 0, 0, 0},  {ones, a.dz1, 1, d2, 0, d2, 0, 0, 0},
+                           {ones, a.dz2, 1, d, 0, d, 0, 0, 0},      {ones, a.dlogit, 1, 1, 0, 1, 0, 0, 0},
+                           {ones, a.loss, 1, 1, 0, 1, 0, 0, 0}};
+  int64_t off = 0;
+  int tiles = 0;
+  for (int q = 0; q < NMAT; ++q) {
+    J.m[q] = base[q];
+    J.m[q].out_off = off;
+    J.m[q].tiles_n = (base[q].N + WT - 1) / WT;
+    J.m[q].tile0 = tiles;
+    off += (int64_t)base[q].K * base[q].N;
+    tiles += ((base[q].K + WT - 1) / WT) * J.m[q].tiles_n;
+  }
+  J.ntiles = tiles;
+  J.nout = off;
+  return J;
+}
+
+__global__ void __launch_bounds__(256) k_nmf_wpart(WJobs J, int B, float* __restrict__ part) {
+  __shared__ float sA[WCH][WT + 1], sB[WCH][WT + 1];
+  const int tile = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x;
+  int q = 0;
+  while (q + 1 < NMAT && tile >= J.m[q + 1].tile0) ++q;
+  const WMat& M = J.m[q];
+  const int lt = tile - M.tile0, kt = lt / M.tiles_n, ntl = lt - kt * M.tiles_n;
+  const int k0 = kt * WT, n0 = ntl * WT, b0 = chunk * WCH;
+  for (int x = tid; x < WCH * WT; x += 256) {
+    const int r = x / WT, c = x - r * WT, b = b0 + r;
+    const bool inb = b < B;
+    sA[r][c] = (inb && k0 + c < M.K) ? (M.A ? M.A[(int64_t)b * M.lda + k0 + c] : 1.0f) : 0.f;
+    sB[r][c] = (inb && n0 + c < M.N) ? M.Bm[(int64_t)b * M.ldb + n0 + c] : 0.f;
+  }
+  __syncthreads();
+  const int kl = tid >> 3, nl = (tid & 7) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int nb = min(WCH, B - b0);
+  for (int r = 0; r < nb; ++r) {
+    const float av = sA[r][kl];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = acc[j] + av * sB[r][nl + j];
+  }
+  const int k = k0 + kl;
+  if (k < M.K) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (n0 + nl + j < M.N) part[(int64_t)chunk * J.nout + M.out_off + (int64_t)k * M.N + n0 + nl + j] = acc[j];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_nmf_wsum(NArgs a, WJobs J, int nchunks, const float* __restrict__ part,
+                                                  float* loss_out, int which) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= J.nout) return;
+  float acc = 0.f;
+  for (int c = 0; c < nchunks; ++c) acc = acc + part[(int64_t)c * J.nout + x];
+  const int64_t loss_at = J.m[6].out_off;
+  if (x == loss_at) {
+    if (loss_out) loss_out[which] = acc / (float)a.B;
+    return;
+  }
+  // output segment -> parameter segment
+  static constexpr int seg_of[NMAT - 1] = {S_W1, S_W2, S_WO, S_B1, S_B2, S_BO};
+  int q = 0;
+  while (q + 1 < NMAT - 1 && x >= J.m[q + 1].out_off) ++q;
+  float* dst = a.G + a.off[seg_of[q]] + (x - J.m[q].out_off);
+  *dst = *dst + acc;
+}
+
+constexpr int MAX_Q = 2;  // d <= 128: each lane holds up to 2 of a row's elements
+
+// One wave per (instance b, side s): s = 0 the user's MF_U / MLP_U rows, s = 1
+// the item's MF_I / MLP_I rows.  The first occurrence of the row in the batch
+// owns it: sums all its occurrences' contributions in instance order, adds the
+// sum to the gradient rows and (with_delta) writes delta = eps*g/|g| per table.
+__global__ void __launch_bounds__(256) k_nmf_rows(NArgs a, int32_t* __restrict__ owner,
+                                                  float* __restrict__ delta, int with_delta,
+                                                  float eps) {
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int B = a.B, d = a.d;
+  if (wave >= 2 * (int64_t)B) return;
+  const int b = (int)(wave >> 1), s = (int)(wave & 1);
+  const int32_t* idx = s ? a.i : a.u;
+  const int64_t nrows = s ? a.I1 : a.U1;
+  const int32_t r = clamp_idx(idx[b], nrows);
+  int first = b;
+  for (int base = 0; base < b; base += 64) {
+    const int j = base + lane;
+    const bool m = j < b && clamp_idx(idx[j], nrows) == r;
+    const uint64_t mask = __ballot(m);
+    if (mask) {
+      first = base + __ffsll((unsigned long long)mask) - 1;
+      break;
+    }
+  }
+  if (lane == 0) owner[2 * b + s] = first;
+  if (first != b) return;
+  const int tA = s ? S_MF_I : S_MF_U, tB = s ? S_MLP_I : S_MLP_U;
+  float gA[MAX_Q], gB[MAX_Q];
+#pragma unroll
+  for (int q = 0; q < MAX_Q; ++q) gA[q] = gB[q] = 0.f;
+  for (int base = b; base < B; base += 64) {
+    const int j = base + lane;
+    uint64_t mask = __ballot(j < B && clamp_idx(idx[j], nrows) == r);
+    while (mask) {
+      const int jj = base + __ffsll((unsigned long long)mask) - 1;
+      mask &= mask - 1;
+#pragma unroll
+      for (int q = 0; q < MAX_Q; ++q) {
+        const int k = lane + 64 * q;
+        if (k < d) {
+          gA[q] = gA[q] + a.contrib[((int64_t)jj * 4 + tA) * d + k];
+          gB[q] = gB[q] + a.contrib[((int64_t)jj * 4 + tB) * d + k];
+        }
+      }
+    }
+  }
+  float ssA = 0.f, ssB = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAX_Q; ++q) {
+    const int k = lane + 64 * q;
+    if (k < d) {
+      float* ga = a.G + a.off[tA] + (int64_t)r * d + k;
+      float* gb = a.G + a.off[tB] + (int64_t)r * d + k;
+      *ga = *ga + gA[q];
+      *gb = *gb + gB[q];
+      ssA = ssA + gA[q] * gA[q];
+      ssB = ssB + gB[q] * gB[q];
+    }
+  }
+  if (!with_delta) return;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    ssA += __shfl_xor(ssA, m, 64);
+    ssB += __shfl_xor(ssB, m, 64);
+  }
+  const float invA = 1.0f / sqrtf(fmaxf(ssA, 1e-12f)), invB = 1.0f / sqrtf(fmaxf(ssB, 1e-12f));
+#pragma unroll
+  for (int q = 0; q < MAX_Q; ++q) {
+    const int k = lane + 64 * q;
+    if (k < d) {
+      delta[((int64_t)b * 4 + tA) * d + k] = gA[q] * invA * eps;
+      delta[((int64_t)b * 4 + tB) * d + k] = gB[q] * invB * eps;
+    }
+  }
+}
+
+// Keras 2.2 Adam (keras/optimizers.py Adam.get_updates), dense, float4 stream:
+// m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g^2; p -= lr_t*m / (sqrt(v) + eps); g = 0.
+__global__ void __launch_bounds__(256) k_nmf_adam(float4* __restrict__ p, float4* __restrict__ g,
+                                                  float4* __restrict__ m, float4* __restrict__ v,
+                                                  int64_t n4, float b1, float b2, float lr_t,
+                                                  float eps) {
+  const float c1 = 1.0f - b1, c2 = 1.0f - b2;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const float4 gg = g[x];
+    float4 mm = m[x], vv = v[x], pp = p[x];
+#define ACF_ADAM(c)                                        \
+  mm.c = b1 * mm.c + c1 * gg.c;                            \
+  vv.c = b2 * vv.c + c2 * (gg.c * gg.c);                   \
+  pp.c = pp.c - (lr_t * mm.c) / (sqrtf(vv.c) + eps);
+    ACF_ADAM(x) ACF_ADAM(y) ACF_ADAM(z) ACF_ADAM(w)
+#undef ACF_ADAM
+    m[x] = mm;
+    v[x] = vv;
+    p[x] = pp;
+    g[x] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct acf_neumf_ctx {
+  int64_t U1 = 0, I1 = 0;
+  int32_t d = 0, maxB = 0;
+  Layout L;
+  float *h0 = nullptr, *a1 = nullptr, *f = nullptr, *dz1 = nullptr, *dz2 = nullptr;
+  float *dlogit = nullptr, *loss = nullptr, *contrib = nullptr, *delta = nullptr;
+  float* wpart = nullptr;  // [B/64 chunks][weight-gradient outputs]
+  int32_t *owner = nullptr, *err = nullptr;
+  std::vector<void*> allocs;
+};
+
+extern "C" const char* acf_neumf_last_error(void) { return g_neumf_error.c_str(); }
+
+static int check_dims(int64_t U1, int64_t I1, int32_t d) {
+  ACF_CHECK(U1 > 0 && I1 > 0 && U1 < (1ll << 31) && I1 < (1ll << 31), ACF_E_INVALID,
+            "table rows must be in [1, 2^31): got %lld, %lld", (long long)U1, (long long)I1);
+  ACF_CHECK(d >= 4 && d <= 64 * MAX_Q && d % 4 == 0, ACF_E_INVALID,
+            "dim must be a multiple of 4 in [4, %d], got %d", 64 * MAX_Q, d);
+  return ACF_OK;
+}
+
+extern "C" int64_t acf_neumf_param_count(int64_t U1, int64_t I1, int32_t d) {
+  if (check_dims(U1, I1, d) != ACF_OK) return -1;
+  return make_layout(U1, I1, d).total;
+}
+
+extern "C" int acf_neumf_param_offsets(int64_t U1, int64_t I1, int32_t d, int64_t* off) {
+  int r = check_dims(U1, I1, d);
+  if (r != ACF_OK) return r;
+  ACF_CHECK(off != nullptr, ACF_E_INVALID, "offsets pointer is NULL");
+  const Layout L = make_layout(U1, I1, d);
+  for (int k = 0; k < S_COUNT; ++k) off[k] = L.off[k];
+  return ACF_OK;
+}
+
+extern "C" int acf_neumf_destroy(acf_neumf_ctx* c) {
+  if (!c) return ACF_OK;
+  for (void* p : c->allocs) (void)hipFree(p);
+  delete c;
+  return ACF_OK;
+}
+
+static int set_inst_smem_limit();
+
+extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int32_t d,
+                                int32_t maxB) {
+  ACF_CHECK(out != nullptr, ACF_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int r = check_dims(U1, I1, d);
+  if (r != ACF_OK) return r;
+  ACF_CHECK(maxB > 0 && maxB <= (1 << 24), ACF_E_INVALID, "max_batch must be in (0, 2^24], got %d", maxB);
+  acf_neumf_ctx* c = new acf_neumf_ctx();
+  c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB;
+  c->L = make_layout(U1, I1, d);
+  const size_t B = (size_t)maxB, dd = (size_t)d;
+  auto A = [&](auto** p, size_t n) {
+    if (r != ACF_OK) return;
+    void* q = nullptr;
+    if (hipMalloc(&q, n * sizeof(**p) + 16) != hipSuccess) {
+      (void)hipGetLastError();
+      r = set_error(ACF_E_NOMEM, "hipMalloc of %zu bytes failed", n * sizeof(**p));
+      return;
+    }
+    c->allocs.push_back(q);
+    *p = static_cast<std::remove_reference_t<decltype(*p)>>(q);
+  };
+  A(&c->h0, B * 2 * dd); A(&c->a1, B * 2 * dd); A(&c->f, B * 2 * dd); A(&c->dz1, B * 2 * dd);
+  A(&c->dz2, B * dd); A(&c->dlogit, B); A(&c->loss, B); A(&c->contrib, B * 4 * dd);
+  A(&c->delta, B * 4 * dd); A(&c->owner, 2 * B); A(&c->err, 4);
+  const size_t nout = 4 * dd * dd + 2 * dd + 2 * dd * dd + dd + 2 * dd + 2 + 4;
+  A(&c->wpart, ((B + WCH - 1) / WCH) * nout);
+  if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+    r = set_error(ACF_E_HIP, "hipMemset failed");
+  if (r == ACF_OK) r = set_inst_smem_limit();
+  if (r != ACF_OK) { acf_neumf_destroy(c); return r; }
+  *out = c;
+  return ACF_OK;
+}
+
+static NArgs make_args(acf_neumf_ctx* c, const float* P, float* G, const int32_t* u, const int32_t* i,
+                       const float* y, int32_t B, float scale) {
+  NArgs a;
+  a.P = P; a.G = G;
+  for (int k = 0; k < S_COUNT; ++k) a.off[k] = c->L.off[k];
+  a.u = u; a.i = i; a.y = y;
+  a.U1 = c->U1; a.I1 = c->I1; a.B = B; a.d = c->d;
+  a.scale_over_B = (float)((double)scale / (double)B);
+  a.h0 = c->h0; a.a1 = c->a1; a.f = c->f; a.dz1 = c->dz1; a.dz2 = c->dz2;
+  a.dlogit = c->dlogit; a.loss = c->loss; a.contrib = c->contrib;
+  a.delta = c->delta; a.owner = c->owner; a.pred = nullptr; a.err = c->err;
+  return a;
+}
+
+static size_t inst_smem(int d) {
+  size_t f = (size_t)3 * MR * (2 * d + 1) + 3 * MR * (d + 1) + MR + 5 * d + 4;
+  if (weights_in_lds(d)) f += (size_t)2 * d * (2 * d + 1) + (size_t)2 * d * (d + 1);
+  return f * sizeof(float);
+}
+
+// allow the large dynamic LDS of k_nmf_inst (gfx950: 160 KB per CU)
+static int set_inst_smem_limit() {
+  static int done = 0;
+  if (done) return ACF_OK;
+  const int bytes = 150 * 1024;
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_inst<0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_inst<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_inst<2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done = 1;
+  return ACF_OK;
+}
+
+static int read_err(acf_neumf_ctx* c, hipStream_t s) {
+  int32_t herr = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ACF_CHECK(herr == 0, ACF_E_RANGE, "index out of range (%s%s)", (herr & 1) ? "user >= num_user_rows " : "",
+            (herr & 2) ? "item >= num_item_rows" : "");
+  return ACF_OK;
+}
+
+static int launch_grad(acf_neumf_ctx* c, const float* P, float* G, const int32_t* u, const int32_t* i,
+                       const float* y, int32_t B, const acf_neumf_hparams* hp, float* loss_out,
+                       hipStream_t s) {
+  const int d = c->d;
+  const unsigned gi = (unsigned)((B + MR - 1) / MR);
+  const unsigned gr = (unsigned)((2 * (int64_t)B * 64 + 255) / 256);
+  NArgs a = make_args(c, P, G, u, i, y, B, 1.0f);
+  const WJobs J = make_jobs(a);
+  const int nch = (B + WCH - 1) / WCH;
+  const dim3 gp((unsigned)J.ntiles, (unsigned)nch);
+  const unsigned gs = (unsigned)((J.nout + 255) / 256);
+  k_nmf_inst<0><<<gi, 256, inst_smem(d), s>>>(a);
+  k_nmf_wpart<<<gp, 256, 0, s>>>(J, B, c->wpart);
+  k_nmf_wsum<<<gs, 256, 0, s>>>(a, J, nch, c->wpart, loss_out, 0);
+  k_nmf_rows<<<gr, 256, 0, s>>>(a, c->owner, c->delta, hp->adver ? 1 : 0, hp->eps);
+  HIP_TRY(hipGetLastError());
+  if (hp->adver) {
+    NArgs b = make_args(c, P, G, u, i, y, B, hp->reg_adv);
+    k_nmf_inst<1><<<gi, 256, inst_smem(d), s>>>(b);
+    k_nmf_wpart<<<gp, 256, 0, s>>>(J, B, c->wpart);
+    k_nmf_wsum<<<gs, 256, 0, s>>>(b, J, nch, c->wpart, loss_out, 1);
+    k_nmf_rows<<<gr, 256, 0, s>>>(b, c->owner, c->delta, 0, 0.f);
+    HIP_TRY(hipGetLastError());
+  } else if (loss_out) {
+    HIP_TRY(hipMemsetAsync(loss_out + 1, 0, sizeof(float), s));
+  }
+  return ACF_OK;
+}
+
+extern "C" int acf_neumf_grad(acf_neumf_ctx* c, const float* P, float* G, const int32_t* u,
+                              const int32_t* i, const float* y, int32_t B, const acf_neumf_hparams* hp,
+                              float* loss_out, int32_t check, void* stream_) {
+  ACF_CHECK(c && P && G && u && i && y && hp, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(B > 0 && B <= c->maxB, ACF_E_INVALID, "batch %d outside (0, %d]", B, c->maxB);
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  if (check) HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  int r = launch_grad(c, P, G, u, i, y, B, hp, loss_out, s);
+  if (r != ACF_OK) return r;
+  if (check) return read_err(c, s);
+  return ACF_OK;
+}
+
+static int launch_adam(acf_neumf_ctx* c, float* P, float* G, float* m, float* v, int64_t t,
+                       const acf_neumf_hparams* hp, hipStream_t s) {
+  // lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t), evaluated in float32 as Keras does
+  const float tt = (float)t;
+  const float lr_t = hp->lr * (sqrtf(1.0f - powf(hp->beta2, tt)) / (1.0f - powf(hp->beta1, tt)));
+  const int64_t n4 = c->L.total / 4;
+  const unsigned grid = (unsigned)std::min<int64_t>((n4 + 255) / 256, 256 * 32);
+  k_nmf_adam<<<grid, 256, 0, s>>>(reinterpret_cast<float4*>(P), reinterpret_cast<float4*>(G),
+                                  reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v), n4,
+                                  hp->beta1, hp->beta2, lr_t, hp->adam_eps);
+  HIP_TRY(hipGetLastError());
+  return ACF_OK;
+}
+
+extern "C" int acf_neumf_adam(acf_neumf_ctx* c, float* P, float* G, float* m, float* v, int64_t t,
+                              const acf_neumf_hparams* hp, void* stream_) {
+  ACF_CHECK(c && P && G && m && v && hp, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(t >= 1, ACF_E_INVALID, "Adam iteration must be >= 1, got %lld", (long long)t);
+  return launch_adam(c, P, G, m, v, t, hp, static_cast<hipStream_t>(stream_));
+}
+
+extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, float* v,
+                               const int32_t* u, const int32_t* i, const float* y, int64_t n,
+                               int32_t batch, int64_t t_first, const acf_neumf_hparams* hp,
+                               float* losses, void* stream_) {
+  ACF_CHECK(c && P && G && m && v && u && i && y && hp, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(batch > 0 && batch <= c->maxB, ACF_E_INVALID, "batch %d outside (0, %d]", batch, c->maxB);
+  ACF_CHECK(n >= 0 && t_first >= 1, ACF_E_INVALID, "bad instance count or Adam iteration");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  int64_t k = 0;
+  for (int64_t o = 0; o < n; o += batch, ++k) {
+    const int32_t B = (int32_t)std::min<int64_t>(batch, n - o);
+    int r = launch_grad(c, P, G, u + o, i + o, y + o, B, hp, losses ? losses + 2 * k : nullptr, s);
+    if (r == ACF_OK) r = launch_adam(c, P, G, m, v, t_first + k, hp, s);
+    if (r != ACF_OK) return r;
+  }
+  return read_err(c, s);
+}
+
+#ifdef NMF_DIAG
+extern "C" int acf_neumf_diag_stamps(uint64_t* out) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nmf_stamps), 16 * sizeof(uint64_t)));
+  return ACF_OK;
+}
+#endif
+
+extern "C" int acf_neumf_predict(acf_neumf_ctx* c, const float* P, const int32_t* u, const int32_t* i,
+                                 int64_t n, float* out, void* stream_) {
+  ACF_CHECK(c && P && u && i && out, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(n >= 0, ACF_E_INVALID, "negative count");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  const int64_t chunk = 1 << 28;
+  for (int64_t o = 0; o < n; o += chunk) {
+    const int32_t m = (int32_t)std::min(chunk, n - o);
+    NArgs a = make_args(c, P, nullptr, u + o, i + o, nullptr, m, 1.0f);
+    a.pred = out + o;
+    k_nmf_inst<2><<<(unsigned)((m + MR - 1) / MR), 256, inst_smem(c->d), s>>>(a);
+    HIP_TRY(hipGetLastError());
+  }
+  return read_err(c, s);
+}

@@ -21,6 +21,9 @@ import numpy as np
 
 ML1M_SHAPE = dict(num_users=6040, num_items=3706, n_train=994169)
 PINTEREST_SHAPE = dict(num_users=55187, num_items=9916, n_train=1445622)
+# yelp-sort: 25,677 users (the test file), 25,815 items and 730,791 ratings in the
+# public release, one held out per user (train file absent here)
+YELP_SHAPE = dict(num_users=25677, num_items=25815, n_train=705114, min_degree=10)
 
 
 class _DatasetBase:
@@ -231,14 +234,20 @@ def pinterest_like(seed: int = 2019) -> SyntheticDataset:
     return synthetic_dataset(**PINTEREST_SHAPE, seed=seed, name="pinterest-20-synthetic")
 
 
+def yelp_like(seed: int = 2019) -> SyntheticDataset:
+    return synthetic_dataset(**YELP_SHAPE, seed=seed, name="yelp-sort-synthetic")
+
+
 def get_dataset(name: str, path: str = "", seed: int = 2019):
     """Resolve --dataset: a file prefix under <path>data/, or a synthetic shape
-    ("ml-1m-synthetic", "pinterest-20-synthetic", "synthetic:U:I:N")."""
+    ("ml-1m-synthetic", "pinterest-20-synthetic", "yelp-sort-synthetic", "synthetic:U:I:N")."""
     import os
     if name == "ml-1m-synthetic":
         return ml1m_like(seed)
     if name == "pinterest-20-synthetic":
         return pinterest_like(seed)
+    if name == "yelp-sort-synthetic":
+        return yelp_like(seed)
     if name.startswith("synthetic:"):
         _, U, I, N = name.split(":")
         return synthetic_dataset(int(U), int(I), int(N), seed=seed)

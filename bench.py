@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--time-batches", type=int, default=400, help="batches in the kernel-timing pass")
     p.add_argument("--large", action="store_true", help="also measure batch 65536 on 10M x 5M x d128")
+    p.add_argument("--no-neumf", action="store_true", help="skip the adversarial-NeuMF line (configs[3])")
     return p.parse_args()
 
 
@@ -223,6 +224,59 @@ def large_batch_roofline(acf, ops, dev, d=128):
     return rl
 
 
+def neumf_bench(acf, dev):
+    """BASELINE configs[3]: adversarial NeuMF (GMF + MLP towers perturbed) on
+    yelp-sort-shaped synthetic data, d = 64, batch 512 (run.py --bs default), one
+    epoch of Keras-style training (libacf_neumf.so).  Dominant kernel: the dense
+    Adam stream over the flat parameter buffer (8 x 4 B per parameter per step)."""
+    import scipy.sparse as sp
+    nm = importlib.import_module(PKG + ".neumf")
+    ds = acf.yelp_like()
+    train = sp.coo_matrix((np.ones(len(ds.pair_user), np.float32), (ds.pair_user, ds.pair_item)),
+                          shape=(ds.num_users, ds.num_items))
+    B, d = 512, 64
+    r = nm.AdversarialNeuMF(ds.num_users, ds.num_items, d, weight=1.0, pop_percent=0.2, seed=0,
+                            device=dev)
+    x, y = r.get_train_instances(train)
+    n = len(y)
+    perm = np.random.default_rng(0).permutation(n)
+    U = torch.as_tensor(x[0][perm], dtype=torch.int32, device=dev)
+    I = torch.as_tensor(x[1][perm], dtype=torch.int32, device=dev)
+    Y = torch.as_tensor(y[perm], dtype=torch.float32, device=dev)
+    ctx = r._context(B)
+    hp = r.hparams()
+    ctx.train(U[: 64 * B], I[: 64 * B], Y[: 64 * B], B, hp)  # warm
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    losses = ctx.train(U, I, Y, B, hp)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    nb = losses.shape[0]
+    st = r.state
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 50
+    e0.record()
+    for _ in range(reps):
+        ctx.adam(hp)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    adam_us = e0.elapsed_time(e1) * 1e3 / reps
+    nparam = st.params.numel()
+    achieved = 8 * 4 * nparam / (adam_us * 1e-6) / 1e9
+    return {"metric": "adversarial NeuMF training instances/sec (yelp-sort-shaped, d=64)",
+            "value": round(n / dt, 1), "unit": "instances/s", "ms_per_step": round(1e3 * dt / nb, 4),
+            "dtype": "f32", "data": "synthetic yelp-sort-shaped (25,677 users x 25,815 items, 705k "
+                                    "pairs) + 1 rejected negative each (MF.py:42-56)",
+            "config": {"workload": "AdversarialNeuMF, FGSM on the 4 embedding tables, eps 0.5, "
+                                   "weight 1, Keras Adam lr 0.001, batch 512", "dim": d, "batch": B,
+                       "instances": n, "params": nparam},
+            "final_loss": round(float(losses[-1, 0]), 5),
+            "roofline": {"bound": "hbm", "kernel": "k_nmf_adam", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "bytes_per_launch": 8 * 4 * nparam, "avg_launch_us": round(adam_us, 3),
+                         "traffic": None}}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -300,6 +354,8 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(u, i, j, P0, Q0, B, a.cpu_batches)
+    if rank == 0 and not a.no_neumf:
+        out["neumf"] = neumf_bench(acf, dev)
     if rank == 0 and a.large:
         del pipe, tctx
         torch.cuda.empty_cache()

@@ -1,0 +1,84 @@
+/* acf_neumf.h — C-ABI of the MI355X NeuMF / adversarial-NeuMF training path
+ * (libacf_neumf.so).  §8(f)3 of SURVEY.md, BASELINE.json configs[3].
+ *
+ * The reference model is the Keras `NeuMF` (NeuMF.py:10-52) trained by run.py
+ * (`ranker.train(x_train, y_train, batch_size)`, MF.py:30-33 = Keras fit with
+ * binary cross-entropy and Adam) on MF.py:42-56 `get_train_instances`, and scored
+ * by `ranker.rank(users, items)` (MF.py:38-40) in evaluation.py:54-80.  The
+ * reference's `AdversarialNeuMF` (NeuMF.py:58-185) does not run (NeuMF.py:131);
+ * the adversarial step here is APR's FGSM applied to the four embedding tables
+ * (oracle/neumf_oracle.py states it).
+ *
+ * Parameters live in ONE flat fp32 buffer in Keras order (offsets from
+ * acf_neumf_param_offsets): MF_U [U1,d], MF_I [I1,d], MLP_U [U1,d], MLP_I [I1,d],
+ * W1 [2d,2d], b1 [2d], W2 [2d,d], b2 [d], Wo [2d,1], bo [1] (+3 pad).  Gradient
+ * and Adam moments use the same layout, so the dense Keras Adam is one stream.
+ * All pointers are device pointers; `stream` is a hipStream_t.  Return 0 or an
+ * ACF_E_* code (acf_apr.h); acf_neumf_last_error() holds the message.
+ */
+#ifndef ACF_NEUMF_H
+#define ACF_NEUMF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct acf_neumf_ctx acf_neumf_ctx;
+
+typedef struct {
+  float lr;       /* Adam learning rate (Keras default 0.001) */
+  float beta1;    /* 0.9 */
+  float beta2;    /* 0.999 */
+  float adam_eps; /* 1e-7 (Keras 2.2 K.epsilon()) */
+  float eps;      /* adversarial perturbation norm */
+  float reg_adv;  /* weight of the adversarial loss */
+  int32_t adver;  /* 0: NeuMF (NeuMF.py:10-52); 1: + FGSM adversarial loss */
+  int32_t reserved;
+} acf_neumf_hparams;
+
+const char* acf_neumf_last_error(void);
+
+/* Number of floats of the flat parameter buffer, and the 10 segment offsets. */
+int64_t acf_neumf_param_count(int64_t num_user_rows, int64_t num_item_rows, int32_t dim);
+int acf_neumf_param_offsets(int64_t num_user_rows, int64_t num_item_rows, int32_t dim,
+                            int64_t* offsets10);
+
+/* Workspace for batches of up to max_batch instances; dim % 4 == 0, dim <= 256. */
+int acf_neumf_create(acf_neumf_ctx** ctx, int64_t num_user_rows, int64_t num_item_rows,
+                     int32_t dim, int32_t max_batch);
+int acf_neumf_destroy(acf_neumf_ctx* ctx);
+
+/* Gradient of the batch's mean binary cross-entropy (Keras train_on_batch loss,
+ * MF.py:30-33) w.r.t. every parameter, ADDED to `grad` (zero it before the first
+ * call; acf_neumf_adam re-zeroes it).  adver = 1 adds reg_adv x the loss on the
+ * embedding rows perturbed by eps * g/|g| (g: the clean gradient of the row).
+ * loss_out (device, 2 floats, may be NULL): clean and adversarial mean loss.
+ * check = 1: indices are validated (synchronises; ACF_E_RANGE when outside). */
+int acf_neumf_grad(acf_neumf_ctx* ctx, const float* params, float* grad, const int32_t* user,
+                   const int32_t* item, const float* label, int32_t batch,
+                   const acf_neumf_hparams* hp, float* loss_out, int32_t check, void* stream);
+
+/* Keras 2.2 Adam over the whole buffer, iteration t (1-based); zeroes grad. */
+int acf_neumf_adam(acf_neumf_ctx* ctx, float* params, float* grad, float* m, float* v,
+                   int64_t t, const acf_neumf_hparams* hp, void* stream);
+
+/* One Keras fit epoch over n already-shuffled instances (MF.py:30-33): batches
+ * of `batch` (the last one partial), each acf_neumf_grad + acf_neumf_adam with
+ * Adam iterations t_first, t_first+1, ...  losses (device, [ceil(n/batch)][2],
+ * may be NULL): per-batch clean / adversarial mean loss.  Indices are validated
+ * once at the end (ACF_E_RANGE; out-of-range rows were read as row 0). */
+int acf_neumf_train(acf_neumf_ctx* ctx, float* params, float* grad, float* m, float* v,
+                    const int32_t* user, const int32_t* item, const float* label, int64_t n,
+                    int32_t batch, int64_t t_first, const acf_neumf_hparams* hp, float* losses,
+                    void* stream);
+
+/* ranker.rank(users, items) (MF.py:38-40): sigmoid scores of n (user, item) pairs. */
+int acf_neumf_predict(acf_neumf_ctx* ctx, const float* params, const int32_t* user,
+                      const int32_t* item, int64_t n, float* scores, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,162 @@
+"""NeuMF / adversarial NeuMF HIP path (libacf_neumf.so) vs the CPU oracle
+(oracle/neumf_oracle.py, itself checked against torch autograd in
+test_neumf_oracle.py).  Tolerance: fp32, rtol 1e-4 / atol 1e-6 on gradients —
+the MLP sums run in a different order than numpy's BLAS.  Parity with the
+reference's own adversarial NeuMF is unpinned (it does not run, NeuMF.py:131)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import neumf_oracle as N
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def nm(acf):
+    import importlib
+    from conftest import PKG
+    return importlib.import_module(PKG + ".neumf")
+
+
+def _problem(seed, U1=41, I1=37, d=16, B=96):
+    P = N.init_params(U1, I1, d, seed)
+    rng = np.random.default_rng(seed + 7)
+    u = rng.integers(0, U1, B).astype(np.int32)
+    i = rng.integers(0, I1, B).astype(np.int32)
+    u[:6] = 5
+    i[10:20] = 3
+    y = (rng.random(B) < 0.5).astype(np.float32)
+    return P, u, i, y
+
+
+def _state(nm, P, dev):
+    U1, d = P["MF_U"].shape
+    st = nm.NeuMFState(U1, P["MF_I"].shape[0], d, dev)
+    st.load(P)
+    return st
+
+
+@pytest.mark.parametrize("d", [8, 16, 64, 128])
+@pytest.mark.parametrize("adver", [0, 1])
+def test_grad_matches_oracle(nm, dev, d, adver):
+    P, u, i, y = _problem(d + adver, d=d)
+    hp_o = N.NeuMFHParams(adver=adver, eps=0.5, reg_adv=0.7)
+    want, lc, la = N.grad_step(P, u, i, y, hp_o)
+    st = _state(nm, P, dev)
+    ctx = nm.NeuMFContext(st, 256)
+    loss = torch.zeros(2, device=dev)
+    ctx.grad(u, i, y, ctx.hparams(adver=adver, eps=0.5, reg_adv=0.7), loss)
+    torch.cuda.synchronize()
+    for n in N.NAMES:
+        np.testing.assert_allclose(st.view(n, st.grad).cpu().numpy(), want[n], rtol=1e-4, atol=1e-6,
+                                   err_msg=n)
+    np.testing.assert_allclose(loss.cpu().numpy(), [lc, la], rtol=1e-5)
+
+
+def test_predict_matches_oracle(nm, dev):
+    P, u, i, _ = _problem(3, d=64, B=1000)
+    st = _state(nm, P, dev)
+    ctx = nm.NeuMFContext(st, 64)
+    got = ctx.predict(u, i).cpu().numpy()
+    np.testing.assert_allclose(got, N.predict(P, u, i), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("adver", [0, 1])
+def test_training_steps_match_oracle(nm, dev, adver):
+    """Several grad + dense-Adam steps (Keras train_on_batch) track the oracle."""
+    P, _, _, _ = _problem(11, d=32)
+    st = _state(nm, P, dev)
+    ctx = nm.NeuMFContext(st, 128)
+    hp = ctx.hparams(adver=adver, reg_adv=1.0)
+    hp_o = N.NeuMFHParams(adver=adver, reg_adv=1.0)
+    m = {n: np.zeros_like(P[n]) for n in N.NAMES}
+    v = {n: np.zeros_like(P[n]) for n in N.NAMES}
+    rng = np.random.default_rng(5)
+    for t in range(1, 6):
+        u = rng.integers(0, 41, 128).astype(np.int32)
+        i = rng.integers(0, 37, 128).astype(np.int32)
+        y = (rng.random(128) < 0.5).astype(np.float32)
+        g, *_ = N.grad_step(P, u, i, y, hp_o)
+        N.adam(P, g, m, v, t, hp_o)
+        ctx.grad(u, i, y, hp)
+        ctx.adam(hp)
+    torch.cuda.synchronize()
+    assert float(st.grad.abs().max()) == 0.0  # Adam re-zeroes the gradient
+    for n in N.NAMES:
+        np.testing.assert_allclose(st.view(n).cpu().numpy(), P[n], rtol=1e-4, atol=2e-6, err_msg=n)
+
+
+def test_dense_adam_moves_untouched_rows(nm, dev):
+    """Keras densifies the embedding gradient: rows outside the batch still move
+    once their first moment is non-zero."""
+    P, u, i, y = _problem(2, d=16)
+    st = _state(nm, P, dev)
+    ctx = nm.NeuMFContext(st, 128)
+    hp = ctx.hparams()
+    ctx.grad(u[:10], i[:10], y[:10], hp)
+    ctx.adam(hp)
+    before = st.view("MF_U").clone()
+    ctx.grad(u[10:12], i[10:12], y[10:12], hp)
+    ctx.adam(hp)
+    moved = (st.view("MF_U") != before).any(1).cpu().numpy()
+    assert moved[np.setdiff1d(np.unique(u[:10]), u[10:12])].all()
+
+
+def test_out_of_range_raises(nm, dev):
+    from conftest import PKG
+    import importlib
+    native = importlib.import_module(PKG + "._native")
+    P, u, i, y = _problem(4)
+    st = _state(nm, P, dev)
+    ctx = nm.NeuMFContext(st, 128)
+    u = u.copy()
+    u[3] = 41
+    with pytest.raises(native.NativeIndexError):
+        ctx.grad(u, i, y, ctx.hparams())
+
+
+def test_recommender_surface(nm, dev):
+    """get_train_instances / train / rank as run.py drives them (run.py:242-248)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(0)
+    U, I = 60, 80
+    train = sp.dok_matrix((U + 1, I + 1), dtype=np.float32)
+    for uu in range(1, U + 1):
+        for ii in rng.choice(np.arange(1, I + 1), 6, replace=False):
+            train[uu, ii] = 1
+    for cls, kw in ((nm.NeuMF, {}), (nm.AdversarialNeuMF, {"weight": 1.0, "pop_percent": 0.2})):
+        r = cls(U, I, 16, seed=1, device=dev, **kw)
+        x, y = r.get_train_instances(train)
+        assert len(x[0]) == 2 * train.nnz and y.sum() == train.nnz
+        neg = x[1][1::2]
+        assert not any((int(a), int(b)) in train for a, b in zip(x[0][1::2], neg))
+        losses = [r.train(x, y, 64) for _ in range(30)]
+        assert losses[-1] < losses[0]
+        s = r.rank(np.full(5, 3), np.arange(1, 6))
+        assert s.shape == (5, 1) and np.all((s > 0) & (s < 1))
+
+
+def test_train_epoch_equals_stepwise(nm, dev):
+    """acf_neumf_train (native batch loop) == grad + adam per batch, bit for bit,
+    including the trailing partial batch."""
+    P, _, _, _ = _problem(21, d=64)
+    rng = np.random.default_rng(9)
+    n, B = 1000, 96
+    u = rng.integers(0, 41, n).astype(np.int32)
+    i = rng.integers(0, 37, n).astype(np.int32)
+    y = (rng.random(n) < 0.5).astype(np.float32)
+    for adver in (0, 1):
+        a, b = _state(nm, P, dev), _state(nm, P, dev)
+        ca, cb = nm.NeuMFContext(a, B), nm.NeuMFContext(b, B)
+        hp = ca.hparams(adver=adver)
+        la = ca.train(u, i, y, B, hp)
+        lb = torch.zeros_like(la)
+        for k, o in enumerate(range(0, n, B)):
+            cb.grad(u[o:o + B], i[o:o + B], y[o:o + B], hp, lb[k])
+            cb.adam(hp)
+        torch.cuda.synchronize()
+        assert a.t == b.t == (n + B - 1) // B
+        assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(la, lb)

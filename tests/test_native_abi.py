@@ -73,3 +73,42 @@ def test_product_never_imports_the_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(root, f)).read()
                 assert "apr_oracle" not in src and "import oracle" not in src, f
+
+
+NEUMF_HEADER = os.path.join(REPO, "include", "acf_neumf.h")
+
+
+def neumf_header_functions():
+    text = open(NEUMF_HEADER).read()
+    return set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(acf_\w+)\s*\(", text, re.M))
+
+
+def test_neumf_library_exports_every_header_symbol(native):
+    assert set(native.NEUMF_SIGNATURES) == neumf_header_functions()
+    assert native.neumf_exported_symbols() == neumf_header_functions()
+    assert b"gfx950" in open(native.NEUMF_LIB_PATH, "rb").read()
+
+
+def test_neumf_layout_matches_keras_shapes(native):
+    """The flat buffer holds the ten Keras tensors in order, 16-B aligned (host-only calls)."""
+    import ctypes
+    import numpy as np
+    import neumf_oracle as N
+    U1, I1, d = 31, 17, 12
+    lib = native.load_neumf()
+    off = (ctypes.c_int64 * 10)()
+    native.call_neumf("acf_neumf_param_offsets", U1, I1, d, off)
+    sizes = [int(np.prod(s)) for s in N.shapes(U1, I1, d).values()]
+    assert list(off) == list(np.concatenate([[0], np.cumsum(sizes)[:-1]]))
+    assert all(o % 4 == 0 for o in off)
+    assert lib.acf_neumf_param_count(U1, I1, d) == off[9] + 4
+    assert lib.acf_neumf_param_count(U1, I1, 6) == -1  # dim must be a multiple of 4
+
+
+def test_product_never_imports_the_neumf_oracle():
+    pkg = os.path.join(REPO, PKG)
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(root, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+\S*neumf_oracle", src, re.M), f
