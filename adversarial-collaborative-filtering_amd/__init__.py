@@ -17,6 +17,7 @@ from . import _native  # noqa: F401
 from .data import (OriginalDataset, SyntheticDataset, get_dataset, ml1m_like, pinterest_like,
                    synthetic_dataset, yelp_like)
 from .evaluate import evaluate, init_eval_model
+from .evaluation import evaluate_apr_mode, evaluate_model
 from .model import MF, Session
 from .neumf import AdversarialNeuMF, NeuMF
 from .recommender import APR, Recommender
@@ -28,7 +29,7 @@ _sys.modules.setdefault("acf_amd", _sys.modules[__name__])
 
 __all__ = [
     "APR", "AdversarialNeuMF", "DeviceSampler", "EpochTriplets", "MF", "NeuMF", "OriginalDataset", "Recommender", "Session",
-    "SyntheticDataset", "evaluate", "get_dataset", "init_eval_model", "ml1m_like", "output_evaluate",
+    "SyntheticDataset", "evaluate", "evaluate_apr_mode", "evaluate_model", "get_dataset", "init_eval_model", "ml1m_like", "output_evaluate",
     "pinterest_like", "prediction2file", "sampling", "shuffle", "synthetic_dataset", "training",
     "training_batch", "training_loss_acc", "write2file", "yelp_like",
 ]

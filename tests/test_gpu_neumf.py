@@ -160,3 +160,31 @@ def test_train_epoch_equals_stepwise(nm, dev):
         torch.cuda.synchronize()
         assert a.t == b.t == (n + B - 1) // B
         assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(la, lb)
+
+
+def test_neumf_ranker_in_evaluation_protocol(nm, acf, dev):
+    """run.py's evaluate_model / evaluate_apr_mode driving the GPU ranker: same
+    result as scoring with the oracle's forward (scores agree to ~1e-7; the
+    integer-free random parameters make exact ties unlikely)."""
+    P = N.init_params(41, 37, 16, 8)
+    st = _state(nm, P, dev)
+
+    class R:
+        def __init__(self):
+            self.ctx = nm.NeuMFContext(st, 64)
+
+        def rank(self, users, items):
+            return self.ctx.predict(users, items).cpu().numpy().reshape(-1, 1)
+
+    class O:
+        def rank(self, users, items):
+            return N.predict(P, np.asarray(users), np.asarray(items)).reshape(-1, 1)
+
+    rng = np.random.default_rng(1)
+    test_items = [int(x) for x in rng.integers(1, 37, 40)]
+    negs = [list(map(int, rng.integers(1, 37, 20))) for _ in range(40)]
+    got = acf.evaluate_model(R(), test_items, negs, 10)
+    want = acf.evaluate_model(O(), test_items, negs, 10)
+    assert got[0] == want[0]
+    ratings = [[u, t] for u, t in enumerate(test_items)]
+    assert acf.evaluate_apr_mode(R(), ratings, negs)[0] == acf.evaluate_apr_mode(O(), ratings, negs)[0]
