@@ -501,6 +501,38 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
   }
 }
 
+// Packed mode: per slot of every batch, (non-fused << 32) | (row stays in W
+// scratch), scanned together into the per-batch slot and write-back lists.
+__global__ void k_slot_flags(const OccRec* __restrict__ inl, int64_t n, int32_t R, int32_t gen,
+                             uint64_t* __restrict__ flags) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const OccRec* r = inl + x * R;
+  const int32_t meta = r->meta;
+  const bool valid = r->gen == gen && (meta & ACF_COUNT_MASK) != 0;
+  const uint64_t ns = (valid && !(meta & ACF_SINGLE_BIT)) ? 1 : 0;
+  const uint64_t fl = (valid && !(meta & ACF_INPLACE_BIT)) ? 1 : 0;
+  flags[x] = (ns << 32) | fl;
+}
+
+__global__ void k_slot_lists(const uint64_t* __restrict__ flags, const uint64_t* __restrict__ incl,
+                             int64_t n, int32_t S, int32_t* __restrict__ slot_list,
+                             int32_t* __restrict__ flush_list, int32_t* __restrict__ slot_cnt,
+                             int32_t* __restrict__ flush_cnt) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const int64_t t = x / S;
+  const int32_t k = (int32_t)(x - t * S);
+  const uint64_t base = t > 0 ? incl[t * S - 1] : 0;
+  const uint64_t f = flags[x], v = incl[x] - base;  // inclusive counts inside batch t
+  if (f >> 32) slot_list[t * S + (int64_t)(v >> 32) - 1] = k;
+  if (f & 0xFFFFFFFFull) flush_list[t * S + (int64_t)(v & 0xFFFFFFFFull) - 1] = k;
+  if (k == S - 1) {
+    slot_cnt[t] = (int32_t)(v >> 32);
+    flush_cnt[t] = (int32_t)(v & 0xFFFFFFFFull);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Diagnostic build only (-DACF_DIAG, libacf_apr_diag.so): per-wave
 // s_memrealtime stamps (100 MHz) to locate latency inside the step kernels.
@@ -570,6 +602,10 @@ struct StepArgs {
   int32_t use_hot;     // phase 1 reads its slot records from hot_cur
   int32_t write_hot;   // the batch's last kernel copies batch t+1's records to hot_next
   int32_t use_single;  // fused triplets run in k_single waves; their slots are skipped
+  const int32_t* slot_list;   // [nb][S] non-fused slots of each batch (list kernels)
+  const int32_t* flush_list;  // [nb][S] slots whose row stays in W scratch
+  const int32_t* slot_cnt;    // [nb]
+  const int32_t* flush_cnt;   // [nb]
   int32_t slot_waves;  // waves [0, slot_waves) are slot waves, the rest fused-triplet waves
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
@@ -869,24 +905,15 @@ __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
 // Phase 1 = sess.run([update_P, update_Q]) (APR.py:180-191) and the clean half
 // of the optimizer: clean-loss gradient of every unique row of batch t summed
 // over its occurrences, its delta (APR graph), or — BPR graph, FUSE_APPLY — the
-// Adagrad update straight away.  The team also writes back slot k of batch t-1.
-template <int LPR, int NV, bool FUSE_APPLY, int TEAM, bool SINGLE = false>
-__global__ void __launch_bounds__(256) k_clean(StepArgs a) {
-  const Geo<LPR, TEAM> q;
-  if (SINGLE && FUSE_APPLY && q.wave >= a.slot_waves) {
-    k_single<LPR, NV, false>(a, (q.wave - a.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR,
-                             q.l);
-    return;
-  }
-  const int k = q.k, m = q.m, l = q.l;
-  STAMP(a.diag_launch, q.wave, 0);
-  CLOCKSTAMP(a.diag_launch, q.wave, 6);
-  if (a.prev_valid) flush_slot(a, a.t - 1, a.wnew_prev, k, q.tl, TEAM * LPR);
+// Adagrad update straight away.  Slot k, team member m, lane l of the row-group,
+// the team leader's lane; hot ring copies only in one-slot-per-team kernels.
+template <int LPR, int NV, bool FUSE_APPLY, int TEAM>
+__device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int l, int leader, int wave) {
   HotCopy hc;
   if (FUSE_APPLY) hc = hot_load<TEAM>(a, k, m);
-  const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, q.leader);
+  const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
-  STAMP(a.diag_launch, q.wave, 1);
+  STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
     if (FUSE_APPLY) hot_store<TEAM>(a, k, m, l, hc);
     return;
@@ -926,7 +953,7 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
       if (active) axpy_row(G, role ? -gb : gb, ra);
     }
   }
-  STAMP(a.diag_launch, q.wave, 2);
+  STAMP(a.diag_launch, wave, 2);
   team_allreduce<LPR, TEAM, NV>(G);
   if (FUSE_APPLY) {
     if (m == 0) {
@@ -939,32 +966,22 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
     return;
   }
   const RowV<NV> dl = make_delta<LPR, NV>(a, G, h.is_item, h.own_row, l);
-  STAMP(a.diag_launch, q.wave, 3);
+  STAMP(a.diag_launch, wave, 3);
   if (m == 0) {
     store_row<LPR, NV>(a.g0, k, d, l, G);
     store_row<LPR, NV>(a.delta, k, d, l, dl);
   }
-  STAMP(a.diag_launch, q.wave, 4);
-  CLOCKSTAMP(a.diag_launch, q.wave, 7);
 }
 
 // Phase 2 = adversarial half of sess.run(optimizer) (APR.py:130-141,156-165)
 // and SparseApplyAdagrad: loss on p+dP[u], q+dQ[i]; G = G_clean + reg_adv*G_adv;
 // Adagrad into wnew_cur.  The tables are current (flushed by phase 1).
-template <int LPR, int NV, int TEAM, bool SINGLE = false>
-__global__ void __launch_bounds__(256) k_adv(StepArgs a) {
-  const Geo<LPR, TEAM> q;
-  if (SINGLE && q.wave >= a.slot_waves) {
-    k_single<LPR, NV, true>(a, (q.wave - a.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR,
-                            q.l);
-    return;
-  }
-  const int k = q.k, m = q.m, l = q.l;
-  STAMP(a.diag_launch, q.wave, 0);
+template <int LPR, int NV, int TEAM>
+__device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l, int leader, int wave) {
   const HotCopy hc = hot_load<TEAM>(a, k, m);
-  const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, q.leader);
+  const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
-  STAMP(a.diag_launch, q.wave, 1);
+  STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
     hot_store<TEAM>(a, k, m, l, hc);
     return;
@@ -1007,7 +1024,7 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
       if (active) axpy_row(G, role ? -gb : gb, ra);
     }
   }
-  STAMP(a.diag_launch, q.wave, 2);
+  STAMP(a.diag_launch, wave, 2);
   team_allreduce<LPR, TEAM, NV>(G);
   if (m == 0) {
     axpy_row(G0, a.reg_adv, G);
@@ -1017,7 +1034,74 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
     store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
   }
   hot_store<TEAM>(a, k, m, l, hc);
+}
+
+// One team per slot; the team also writes back slot k of batch t-1.  Waves past
+// slot_waves (SINGLE) run fused triplets.
+template <int LPR, int NV, bool FUSE_APPLY, int TEAM, bool SINGLE = false>
+__global__ void __launch_bounds__(256) k_clean(StepArgs a) {
+  const Geo<LPR, TEAM> q;
+  if (SINGLE && FUSE_APPLY && q.wave >= a.slot_waves) {
+    k_single<LPR, NV, false>(a, (q.wave - a.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR,
+                             q.l);
+    return;
+  }
+  STAMP(a.diag_launch, q.wave, 0);
+  CLOCKSTAMP(a.diag_launch, q.wave, 6);
+  if (a.prev_valid) flush_slot(a, a.t - 1, a.wnew_prev, q.k, q.tl, TEAM * LPR);
+  clean_slot<LPR, NV, FUSE_APPLY, TEAM>(a, q.k, q.m, q.l, q.leader, q.wave);
   STAMP(a.diag_launch, q.wave, 4);
+  CLOCKSTAMP(a.diag_launch, q.wave, 7);
+}
+
+template <int LPR, int NV, int TEAM, bool SINGLE = false>
+__global__ void __launch_bounds__(256) k_adv(StepArgs a) {
+  const Geo<LPR, TEAM> q;
+  if (SINGLE && q.wave >= a.slot_waves) {
+    k_single<LPR, NV, true>(a, (q.wave - a.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR,
+                            q.l);
+    return;
+  }
+  STAMP(a.diag_launch, q.wave, 0);
+  adv_slot<LPR, NV, TEAM>(a, q.k, q.m, q.l, q.leader, q.wave);
+  STAMP(a.diag_launch, q.wave, 4);
+}
+
+// Large batches with fusion (one lane-group per slot): the slot work of batch t
+// is the plan's list of its NON-fused slots and the write-back the list of the
+// rows batch t-1 left in W scratch; a fixed set of slot waves strides over both
+// (most slots belong to fused triplets and would only read their record).
+template <int LPR, int NV, bool FUSE_APPLY>
+__global__ void __launch_bounds__(256) k_clean_list(StepArgs a) {
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
+  if (FUSE_APPLY && wave >= a.slot_waves) {
+    k_single<LPR, NV, false>(a, (wave - a.slot_waves) * (64 / LPR) + g, l);
+    return;
+  }
+  const int ngroups = a.slot_waves * (64 / LPR), gid = wave * (64 / LPR) + g;
+  if (a.prev_valid) {
+    const int n = a.flush_cnt[a.t - 1];
+    const int32_t* lst = a.flush_list + (int64_t)(a.t - 1) * a.S;
+    for (int x = gid; x < n; x += ngroups) flush_slot(a, a.t - 1, a.wnew_prev, lst[x], l, LPR);
+  }
+  const int n = a.slot_cnt[a.t];
+  const int32_t* lst = a.slot_list + (int64_t)a.t * a.S;
+  for (int x = gid; x < n; x += ngroups) clean_slot<LPR, NV, FUSE_APPLY, 1>(a, lst[x], 0, l, g * LPR, wave);
+}
+
+template <int LPR, int NV>
+__global__ void __launch_bounds__(256) k_adv_list(StepArgs a) {
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
+  if (wave >= a.slot_waves) {
+    k_single<LPR, NV, true>(a, (wave - a.slot_waves) * (64 / LPR) + g, l);
+    return;
+  }
+  const int ngroups = a.slot_waves * (64 / LPR), gid = wave * (64 / LPR) + g;
+  const int n = a.slot_cnt[a.t];
+  const int32_t* lst = a.slot_list + (int64_t)a.t * a.S;
+  for (int x = gid; x < n; x += ngroups) adv_slot<LPR, NV, 1>(a, lst[x], 0, l, g * LPR, wave);
 }
 
 // Flush the pending rows of batch t (wnew_cur) to the tables (end of a call):
@@ -1319,6 +1403,8 @@ struct acf_apr_ctx {
   int32_t last_delta_batch = -1;
   int32_t mapping = 0;  // slot mapping, see get_kernels
   int32_t plan_R = 1;   // inline records per slot in the current plan (<= R)
+  int32_t lists = 0;    // the plan built slot / write-back lists (packed mode)
+  int32_t *slot_list = nullptr, *flush_list = nullptr, *slot_cnt = nullptr, *flush_cnt = nullptr;
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
   hipStream_t cap_stream = nullptr;
   std::map<GraphKey, hipGraphExec_t> graphs;
@@ -1428,6 +1514,8 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->flag, 3 * maxE); A(&c->inc, 3 * maxE);
   A(&c->uuniq, maxE); A(&c->uoff, maxE + 1); A(&c->ubs, maxNB + 1);
   A(&c->tsl, 4 * maxE); A(&c->tpos, 4 * maxE); A(&c->uinfo, maxE);
+  A(&c->slot_list, 3 * maxE); A(&c->flush_list, 3 * maxE);
+  A(&c->slot_cnt, maxNB); A(&c->flush_cnt, maxNB);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
   A(&c->iinfo, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
@@ -1438,7 +1526,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->wnew[0], S * d); A(&c->wnew[1], S * d);
   A(&c->loss_clean, maxE); A(&c->loss_adv, maxE);
   if (r != ACF_OK) { acf_apr_destroy(c); return r; }
-  size_t b1 = 0, b2 = 0, b3 = 0;
+  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
   uint32_t* k32 = reinterpret_cast<uint32_t*>(c->key_in);
   int32_t* v32 = reinterpret_cast<int32_t*>(k32 + 3 * maxE);
   if (rocprim::radix_sort_keys(nullptr, b1, c->key_in, c->key_out, (size_t)(3 * maxE), 0, 64) !=
@@ -1446,11 +1534,13 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
       rocprim::radix_sort_pairs(nullptr, b3, k32, k32, v32, v32, (size_t)(3 * maxE), 0, 32) !=
           hipSuccess ||
       rocprim::inclusive_scan(nullptr, b2, c->flag, c->inc, (size_t)(3 * maxE),
-                              rocprim::plus<int32_t>()) != hipSuccess) {
+                              rocprim::plus<int32_t>()) != hipSuccess ||
+      rocprim::inclusive_scan(nullptr, b4, c->key_in, c->key_out, (size_t)(3 * maxE),
+                              rocprim::plus<uint64_t>()) != hipSuccess) {
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "rocprim temporary-storage query failed");
   }
-  c->tmp_bytes = std::max(b1, std::max(b2, b3));
+  c->tmp_bytes = std::max(std::max(b1, b4), std::max(b2, b3));
   r = dalloc(c, reinterpret_cast<char**>(&c->tmp), c->tmp_bytes);
   if (r != ACF_OK) { acf_apr_destroy(c); return r; }
   if (hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1542,6 +1632,17 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
                                         reinterpret_cast<const int4*>(c->tpos), c->uinfo, c->iinfo,
                                         c->ubs, c->ibs, c->urec, c->irec, c->inl, c->trec, c->gen_dev);
   HIP_TRY(hipGetLastError());
+  c->lists = 0;
+  if (packed) {  // per-batch lists of non-fused slots and of rows left in W scratch
+    const int64_t n = (int64_t)nb * 3 * B;
+    k_slot_flags<<<grid_for(n), 256, 0, s>>>(c->inl, n, c->plan_R, gen, c->key_in);
+    size_t tb2 = c->tmp_bytes;
+    HIP_TRY(rocprim::inclusive_scan(c->tmp, tb2, c->key_in, c->key_out, (size_t)n, rocprim::plus<uint64_t>(), s));
+    k_slot_lists<<<grid_for(n), 256, 0, s>>>(c->key_in, c->key_out, n, 3 * B, c->slot_list, c->flush_list,
+                                             c->slot_cnt, c->flush_cnt);
+    HIP_TRY(hipGetLastError());
+    c->lists = 1;
+  }
   if (check) {
     int32_t herr = 0;
     HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1562,6 +1663,8 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.inl = c->inl; a.urec = c->urec; a.irec = c->irec; a.trec = c->trec;
   a.use_single = 0;
   a.slot_waves = 1 << 30;  // set by the launcher
+  a.slot_list = c->slot_list; a.flush_list = c->flush_list;
+  a.slot_cnt = c->slot_cnt; a.flush_cnt = c->flush_cnt;
   a.hot_cur = c->hot[t & 1];
   a.hot_next = c->hot[(t + 1) & 1];
   a.use_hot = 0;
@@ -1584,7 +1687,10 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
 struct Kernels {
   void *clean_apr = nullptr, *clean_bpr = nullptr, *adv = nullptr, *flush = nullptr;
   int slots_per_wave = 1;
+  int lists = 0;  // list kernels: slot waves stride over the plan's per-batch lists
 };
+
+#define ACF_LIST_WAVES 4096  // slot waves of a list kernel
 
 template <int LPR, int NV, int TEAM>
 static void kernel_ptrs_team(Kernels* k, int fused) {
@@ -1598,10 +1704,20 @@ static void kernel_ptrs_team(Kernels* k, int fused) {
   }
 }
 
-// fused: the phase-2 (APR) / fused-BPR kernels also run the fused-triplet waves
+// fused: the phase-2 (APR) / fused-BPR kernels also run the fused-triplet waves;
+// lists: one lane-group per slot over the plan's slot lists (packed + fused)
 template <int LPR, int NV>
-static void kernel_ptrs(Kernels* k, int packed, int fused) {
+static void kernel_ptrs(Kernels* k, int packed, int fused, int lists) {
   constexpr int OPW = 64 / LPR;
+  k->flush = reinterpret_cast<void*>(&k_flush);
+  if (packed && fused && lists) {
+    k->clean_apr = reinterpret_cast<void*>(&k_clean_list<LPR, NV, false>);
+    k->clean_bpr = reinterpret_cast<void*>(&k_clean_list<LPR, NV, true>);
+    k->adv = reinterpret_cast<void*>(&k_adv_list<LPR, NV>);
+    k->slots_per_wave = OPW;
+    k->lists = 1;
+    return;
+  }
   if (packed && OPW > 1) {
     kernel_ptrs_team<LPR, NV, 1>(k, fused);
     k->slots_per_wave = OPW;
@@ -1617,7 +1733,7 @@ static void kernel_ptrs(Kernels* k, int packed, int fused) {
 
 static int get_kernels(const acf_apr_ctx* c, Kernels* k, int fused = 0) {
   const int packed = c->mapping == 2 || (c->mapping == 0 && c->B >= ACF_PACKED_MIN_BATCH);
-  return DISPATCH_GEOM(c->d, kernel_ptrs, k, packed, fused);
+  return DISPATCH_GEOM(c->d, kernel_ptrs, k, packed, fused, c->lists);
 }
 
 typedef void (*StepKernel)(StepArgs);
@@ -1653,7 +1769,8 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   Kernels K;
   ACF_RET(get_kernels(c, &K, c->fusion));
   const int S = 3 * c->B;
-  const int SW = (S + K.slots_per_wave - 1) / K.slots_per_wave;  // slot waves of a step kernel
+  int SW = (S + K.slots_per_wave - 1) / K.slots_per_wave;  // slot waves of a step kernel
+  if (K.lists) SW = std::min(SW, ACF_LIST_WAVES);
   const int fuse = c->fusion;
   const int TW = fuse ? (c->B + 64 / c->lpr - 1) / (64 / c->lpr) : 0;  // fused-triplet waves
   int li = 0;
@@ -1668,8 +1785,8 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   for (int32_t t = first; t < first + n; ++t) {
     const int pv = t > first ? 1 : 0;
     StepArgs a = make_args(c, tb, hp, t, pv);
-    a.use_hot = pv;                       // batch t-1's last kernel copied our records
-    a.write_hot = t + 1 < first + n ? 1 : 0;
+    a.use_hot = K.lists ? 0 : pv;         // batch t-1's last kernel copied our records
+    a.write_hot = (!K.lists && t + 1 < first + n) ? 1 : 0;
     a.use_single = fuse;
     a.slot_waves = SW;
     if (hp->adver) {

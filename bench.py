@@ -120,7 +120,13 @@ def step_kernel_name(kind: str, d: int, B: int) -> str:
     while lpr < d4 and lpr < 64:
         lpr <<= 1
     nv = (d4 + lpr - 1) // lpr
-    team = 1 if B >= 4096 or lpr == 64 else 64 // lpr
+    if B >= 4096:  # packed mapping with fusion: the list kernels
+        if kind == "adv":
+            return f"k_adv_list<{lpr}, {nv}>"
+        if kind == "clean":
+            return f"k_clean_list<{lpr}, {nv}, false>"
+        return "k_flush"
+    team = 1 if lpr == 64 else 64 // lpr
     if kind == "adv":
         return f"k_adv<{lpr}, {nv}, {team}, true>"
     if kind == "clean":
