@@ -280,7 +280,7 @@ def neumf_bench(acf, dev):
             "roofline": {"bound": "hbm", "kernel": "k_nmf_adam", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "bytes_per_launch": 8 * 4 * nparam, "avg_launch_us": round(adam_us, 3),
-                         "traffic": None}}
+                         "traffic": (pmc_traffic("k_nmf_adam") or (None,))[0]}}
 
 
 def main():

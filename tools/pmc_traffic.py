@@ -43,7 +43,8 @@ def main(src, dst):
             continue
         f, w = statistics.median(fetch[k]), statistics.median(write.get(k, [0.0]))
         calls, avg = stats.get(k, (0, None))
-        out[k.replace("void ", "").replace("(StepArgs)", "")] = {
+        name = k.replace("void ", "")
+        out[name[: name.index("(")] if "(" in name else name] = {
             "launches": len(fetch[k]), "fetch_kib_median": round(f, 2), "write_kib_median": round(w, 2),
             "traffic_bytes_per_launch": int((2 * f + w) * 1024),
             "trace_avg_us": None if avg is None else round(avg, 3)}
