@@ -584,8 +584,6 @@ struct StepArgs {
   float* accP;
   float* accQ;
   const OccRec* inl;   // [nb][S][R]
-  const OccRec* hot_cur;  // [S][R] batch t's inline records, copied warm by batch t-1
-  OccRec* hot_next;       // [S][R] where this batch's last kernel copies batch t+1's
   const OccRec* urec;  // CSR, user occurrences
   const OccRec* irec;  // CSR, item occurrences
   const OccRec* trec;  // [E] fused-triplet records (see fuse_info)
@@ -599,8 +597,6 @@ struct StepArgs {
   int32_t d, B, S, R, t;
   int32_t prev_valid;  // 1: rows of batch t-1 are still pending in wnew_prev
   int32_t diag_launch; // diagnostic build: stamp slot of this launch
-  int32_t use_hot;     // phase 1 reads its slot records from hot_cur
-  int32_t write_hot;   // the batch's last kernel copies batch t+1's records to hot_next
   int32_t use_single;  // fused triplets run in k_single waves; their slots are skipped
   const int32_t* slot_list;   // [nb][S] non-fused slots of each batch (list kernels)
   const int32_t* flush_list;  // [nb][S] slots whose row stays in W scratch
@@ -689,8 +685,7 @@ __device__ __forceinline__ SlotRec slot_header(const StepArgs& a, int k, int m, 
   SlotRec s;
   s.r0.a = s.r0.b = s.r0.c = make_int4(0, 0, 0, -1);
   if (m < a.R && k < a.S)
-    s.r0 = load_rec(a.use_hot ? a.hot_cur + (int64_t)k * a.R + m
-                              : a.inl + ((int64_t)a.t * a.S + k) * a.R + m);
+    s.r0 = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R + m);
   s.r0_valid = s.r0.gen() == gen;
   const int32_t meta = __shfl(s.r0_valid ? s.r0.meta() : 0, leader_lane, 64);
   // a fused triplet's slots are handled by its k_single lane-group
@@ -709,32 +704,6 @@ __device__ __forceinline__ RecV occ_rec(const StepArgs& a, const SlotRec& s, int
   return load_rec((s.h.is_item ? a.irec : a.urec) + s.h.ovf + idx);
 }
 
-// Warm copy of batch t+1's inline records of slot k (issued early by the
-// batch's last kernel, stored at its end): the next batch's first kernel then
-// finds them in the Infinity Cache instead of HBM.  Member m copies record m
-// (m < R); in packed mode that is the slot's first record only.
-struct HotCopy {
-  int4 a, b, c;
-};
-
-template <int TEAM>
-__device__ __forceinline__ HotCopy hot_load(const StepArgs& a, int k, int m) {
-  HotCopy h;
-  if (a.write_hot && k < a.S && m < a.R) {
-    const int4* p = reinterpret_cast<const int4*>(a.inl + ((int64_t)(a.t + 1) * a.S + k) * a.R + m);
-    h.a = p[0]; h.b = p[1]; h.c = p[2];
-  }
-  return h;
-}
-
-template <int TEAM>
-__device__ __forceinline__ void hot_store(const StepArgs& a, int k, int m, int l, const HotCopy& h) {
-  if (a.write_hot && k < a.S && m < a.R && l == 0) {
-    int4* p = reinterpret_cast<int4*>(a.hot_next + (int64_t)k * a.R + m);
-    p[0] = h.a; p[1] = h.b; p[2] = h.c;
-  }
-}
-
 // copy the pending row of slot k of batch tb (in wsrc) to its table; the
 // team's tl-th lane of tn copies float4 chunks tl, tl+tn, ...
 __device__ __forceinline__ void flush_slot(const StepArgs& a, int tb, const float* __restrict__ wsrc,
@@ -747,6 +716,38 @@ __device__ __forceinline__ void flush_slot(const StepArgs& a, int tb, const floa
   const float* src = wsrc + (int64_t)k * a.d;
   for (int c = tl; c * 4 < a.d; c += tn)
     *reinterpret_cast<float4*>(dst + c * 4) = *reinterpret_cast<const float4*>(src + c * 4);
+}
+
+// The write-back of slot k of batch t-1 split in two so that it never sits in
+// front of the wave's own loads: begin() loads the record, then (once the
+// record is there) the pending row chunk this lane copies; end() stores it.
+struct FlushOp {
+  float4 v;
+  float* dst;
+};
+
+__device__ __forceinline__ RecV flush_rec(const StepArgs& a, int tb, int k) {
+  RecV r;
+  r.a = r.b = r.c = make_int4(0, 0, 0, -1);
+  if (k < a.S) r = load_rec(a.inl + ((int64_t)tb * a.S + k) * a.R);
+  return r;
+}
+
+// lane tl of a team of tn lanes copies float4 chunk tl (d/4 <= tn) of the row
+__device__ __forceinline__ FlushOp flush_load(const StepArgs& a, const RecV& r, const float* __restrict__ wsrc,
+                                              int k, int tl, int tn) {
+  FlushOp f;
+  f.dst = nullptr;
+  if (r.gen() != *a.gen_ptr || (r.meta() & ACF_COUNT_MASK) == 0) return f;
+  if (a.use_single && (r.meta() & ACF_INPLACE_BIT)) return f;
+  if (tl * 4 >= a.d) return f;
+  f.dst = ((r.meta() & ACF_ITEM_BIT) ? a.Q : a.P) + (int64_t)r.own_row() * a.d + tl * 4;
+  f.v = *reinterpret_cast<const float4*>(wsrc + (int64_t)k * a.d + tl * 4);
+  return f;
+}
+
+__device__ __forceinline__ void flush_store(const FlushOp& f) {
+  if (f.dst) *reinterpret_cast<float4*>(f.dst) = f.v;
 }
 
 // Adagrad (TF SparseApplyAdagrad after the dedup) for one row held by a
@@ -906,16 +907,20 @@ __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
 // of the optimizer: clean-loss gradient of every unique row of batch t summed
 // over its occurrences, its delta (APR graph), or — BPR graph, FUSE_APPLY — the
 // Adagrad update straight away.  Slot k, team member m, lane l of the row-group,
-// the team leader's lane; hot ring copies only in one-slot-per-team kernels.
-template <int LPR, int NV, bool FUSE_APPLY, int TEAM>
-__device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int l, int leader, int wave) {
-  HotCopy hc;
-  if (FUSE_APPLY) hc = hot_load<TEAM>(a, k, m);
+// the team leader's lane.
+template <int LPR, int NV, bool FUSE_APPLY, int TEAM, bool FLUSH = false>
+__device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int l, int leader, int wave,
+                                           int tl = 0) {
+  // write-back of slot k of batch t-1: its record is loaded next to our header
+  RecV frec;
+  if (FLUSH) frec = flush_rec(a, a.t - 1, k);
   const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
+  FlushOp fo;
+  if (FLUSH) fo = flush_load(a, frec, a.wnew_prev, k, tl, TEAM * LPR);
   STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
-    if (FUSE_APPLY) hot_store<TEAM>(a, k, m, l, hc);
+    if (FLUSH) flush_store(fo);
     return;
   }
   const int d = a.d;
@@ -955,6 +960,7 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
   }
   STAMP(a.diag_launch, wave, 2);
   team_allreduce<LPR, TEAM, NV>(G);
+  if (FLUSH) flush_store(fo);
   if (FUSE_APPLY) {
     if (m == 0) {
       RowV<NV> wout;
@@ -962,7 +968,6 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
       store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
       store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
     }
-    hot_store<TEAM>(a, k, m, l, hc);
     return;
   }
   const RowV<NV> dl = make_delta<LPR, NV>(a, G, h.is_item, h.own_row, l);
@@ -978,14 +983,10 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
 // Adagrad into wnew_cur.  The tables are current (flushed by phase 1).
 template <int LPR, int NV, int TEAM>
 __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l, int leader, int wave) {
-  const HotCopy hc = hot_load<TEAM>(a, k, m);
   const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
   STAMP(a.diag_launch, wave, 1);
-  if (h.count == 0) {
-    hot_store<TEAM>(a, k, m, l, hc);
-    return;
-  }
+  if (h.count == 0) return;
   const int d = a.d;
   const RowV<NV> own = load_row<LPR, NV>(h.is_item ? a.Q : a.P, h.own_row, d, l);
   const RowV<NV> ownp = add_row(own, load_row<LPR, NV>(a.delta, k, d, l));
@@ -1033,7 +1034,6 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
     store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
     store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
   }
-  hot_store<TEAM>(a, k, m, l, hc);
 }
 
 // One team per slot; the team also writes back slot k of batch t-1.  Waves past
@@ -1048,8 +1048,13 @@ __global__ void __launch_bounds__(256) k_clean(StepArgs a) {
   }
   STAMP(a.diag_launch, q.wave, 0);
   CLOCKSTAMP(a.diag_launch, q.wave, 6);
-  if (a.prev_valid) flush_slot(a, a.t - 1, a.wnew_prev, q.k, q.tl, TEAM * LPR);
-  clean_slot<LPR, NV, FUSE_APPLY, TEAM>(a, q.k, q.m, q.l, q.leader, q.wave);
+  // one wave per slot and a row of <= 64 float4: the write-back overlaps the slot's loads
+  if (TEAM * LPR >= 64 && a.d <= 4 * TEAM * LPR && a.prev_valid) {
+    clean_slot<LPR, NV, FUSE_APPLY, TEAM, true>(a, q.k, q.m, q.l, q.leader, q.wave, q.tl);
+  } else {
+    if (a.prev_valid) flush_slot(a, a.t - 1, a.wnew_prev, q.k, q.tl, TEAM * LPR);
+    clean_slot<LPR, NV, FUSE_APPLY, TEAM>(a, q.k, q.m, q.l, q.leader, q.wave);
+  }
   STAMP(a.diag_launch, q.wave, 4);
   CLOCKSTAMP(a.diag_launch, q.wave, 7);
 }
@@ -1391,7 +1396,7 @@ struct acf_apr_ctx {
   int4 *uinfo = nullptr, *iinfo = nullptr;   // per unique row, see k_slot_info
   int32_t *iuniq = nullptr, *ioff = nullptr, *ibs = nullptr;
   OccRec* trec = nullptr;
-  OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr, *hot[2] = {nullptr, nullptr};
+  OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr;
   int32_t *err = nullptr, *gen_dev = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -1520,7 +1525,6 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->iinfo, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
-  A(&c->hot[0], S * c->R); A(&c->hot[1], S * c->R);
   A(&c->err, 4); A(&c->gen_dev, 4);
   A(&c->g0, S * d); A(&c->delta, S * d);
   A(&c->wnew[0], S * d); A(&c->wnew[1], S * d);
@@ -1665,10 +1669,6 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.slot_waves = 1 << 30;  // set by the launcher
   a.slot_list = c->slot_list; a.flush_list = c->flush_list;
   a.slot_cnt = c->slot_cnt; a.flush_cnt = c->flush_cnt;
-  a.hot_cur = c->hot[t & 1];
-  a.hot_next = c->hot[(t + 1) & 1];
-  a.use_hot = 0;
-  a.write_hot = 0;
   a.g0 = c->g0; a.delta = c->delta;
   a.wnew_cur = c->wnew[t & 1];
   a.wnew_prev = c->wnew[(t + 1) & 1];
@@ -1785,14 +1785,10 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   for (int32_t t = first; t < first + n; ++t) {
     const int pv = t > first ? 1 : 0;
     StepArgs a = make_args(c, tb, hp, t, pv);
-    a.use_hot = K.lists ? 0 : pv;         // batch t-1's last kernel copied our records
-    a.write_hot = (!K.lists && t + 1 < first + n) ? 1 : 0;
     a.use_single = fuse;
     a.slot_waves = SW;
     if (hp->adver) {
-      StepArgs a1 = a;
-      a1.write_hot = 0;
-      ACF_RET(L(K.clean_apr, a1, SW, 0));
+      ACF_RET(L(K.clean_apr, a, SW, 0));
       ACF_RET(L(K.adv, a, SW + TW, 1));
     } else {
       ACF_RET(L(K.clean_bpr, a, SW + TW, 0));

@@ -99,6 +99,27 @@ def main():
             clk.append(np.median((w[ok, 7] - w[ok, 6]) / np.maximum(w[ok, 4] - w[ok, 0], 1)) * 100.0)
     if clk:
         summary["shader_clock_MHz_median"] = float(np.median(clk))
+    # tail: the longest waves of each kind and the occurrence counts of their slots
+    u0 = ep.user[:B].cpu().numpy()
+    it0 = np.concatenate([ep.item_pos[:B].cpu().numpy(), ep.item_neg[:B].cpu().numpy()])
+    cu = np.unique(u0, return_counts=True)[1]
+    ci = np.unique(it0, return_counts=True)[1]
+    counts = np.concatenate([cu, ci])
+    for par, name in ((0, "clean"), (1, "adv")):
+        durs, tops = [], []
+        for li in range(par, n_launch - 1, 2):
+            w = st[li]
+            full = w[:, 4] > 0
+            dd = np.where(full, w[:, 4] - w[:, 0], 0) * 10
+            durs.append(dd[full])
+            if li < 2:  # batch 0: slot counts known
+                top = np.argsort(dd)[-5:][::-1]
+                tops = [(int(k), float(dd[k]), int(counts[k]) if k < len(counts) else -1) for k in top]
+        allv = np.concatenate(durs) if durs else np.zeros(1)
+        summary[f"wave_ns_{name}"] = {q: float(np.percentile(allv, p)) for q, p in
+                                      (("p50", 50), ("p90", 90), ("p99", 99), ("max", 100))}
+        summary[f"longest_waves_batch0_{name}"] = tops
+    summary["max_slot_count_batch0"] = int(counts.max())
     print(json.dumps(summary, indent=1))
     with open(os.path.join(REPO, "gpurun_out", f"diag_g{int(graph)}_a{hp.adver}.json"), "w") as f:
         json.dump(out, f, indent=1)
