@@ -37,6 +37,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -598,6 +599,7 @@ struct StepArgs {
   int32_t prev_valid;  // 1: rows of batch t-1 are still pending in wnew_prev
   int32_t diag_launch; // diagnostic build: stamp slot of this launch
   int32_t use_single;  // fused triplets run in k_single waves; their slots are skipped
+  int32_t touch_next;  // phase 2 reads batch t+1's inline records (brings them on-die)
   const int32_t* slot_list;   // [nb][S] non-fused slots of each batch (list kernels)
   const int32_t* flush_list;  // [nb][S] slots whose row stays in W scratch
   const int32_t* slot_cnt;    // [nb]
@@ -983,10 +985,18 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
 // Adagrad into wnew_cur.  The tables are current (flushed by phase 1).
 template <int LPR, int NV, int TEAM>
 __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l, int leader, int wave) {
+  // read (not copy) batch t+1's record of this slot: phase 1 of the next batch
+  // then finds it in the Infinity Cache instead of HBM
+  int4 nxt = make_int4(0, 0, 0, 0);
+  if (a.touch_next && m < a.R && k < a.S)
+    nxt = *reinterpret_cast<const int4*>(a.inl + ((int64_t)(a.t + 1) * a.S + k) * a.R + m);
   const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
   STAMP(a.diag_launch, wave, 1);
-  if (h.count == 0) return;
+  if (h.count == 0) {
+    if (nxt.x == -0x7fffffff && nxt.y == 0x7fffffff) a.loss_adv[0] = 0.f;
+    return;
+  }
   const int d = a.d;
   const RowV<NV> own = load_row<LPR, NV>(h.is_item ? a.Q : a.P, h.own_row, d, l);
   const RowV<NV> ownp = add_row(own, load_row<LPR, NV>(a.delta, k, d, l));
@@ -1034,6 +1044,7 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
     store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
     store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
   }
+  if (nxt.x == -0x7fffffff && nxt.y == 0x7fffffff) a.loss_adv[0] = 0.f;  // keeps the read alive; never true
 }
 
 // One team per slot; the team also writes back slot k of batch t-1.  Waves past
@@ -1409,6 +1420,7 @@ struct acf_apr_ctx {
   int32_t mapping = 0;  // slot mapping, see get_kernels
   int32_t plan_R = 1;   // inline records per slot in the current plan (<= R)
   int32_t lists = 0;    // the plan built slot / write-back lists (packed mode)
+  int32_t touch_next = 1;  // phase 2 reads the next batch's records (ACF_TOUCH_NEXT=0 disables)
   int32_t *slot_list = nullptr, *flush_list = nullptr, *slot_cnt = nullptr, *flush_cnt = nullptr;
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
   hipStream_t cap_stream = nullptr;
@@ -1512,6 +1524,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB; c->maxNB = maxNB; c->maxE = maxE;
   geometry(d, &c->lpr, &c->nv);
   c->R = std::min(64 / c->lpr, 4);
+  if (const char* e = getenv("ACF_TOUCH_NEXT")) c->touch_next = atoi(e) != 0;
   const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
   auto A = [&](auto** p, size_t n) { if (r == ACF_OK) r = dalloc(c, p, n); };
@@ -1666,6 +1679,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.P = tb->P; a.Q = tb->Q; a.accP = tb->accP; a.accQ = tb->accQ;
   a.inl = c->inl; a.urec = c->urec; a.irec = c->irec; a.trec = c->trec;
   a.use_single = 0;
+  a.touch_next = 0;
   a.slot_waves = 1 << 30;  // set by the launcher
   a.slot_list = c->slot_list; a.flush_list = c->flush_list;
   a.slot_cnt = c->slot_cnt; a.flush_cnt = c->flush_cnt;
@@ -1787,6 +1801,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     StepArgs a = make_args(c, tb, hp, t, pv);
     a.use_single = fuse;
     a.slot_waves = SW;
+    a.touch_next = (c->touch_next && !K.lists && t + 1 < first + n) ? 1 : 0;
     if (hp->adver) {
       ACF_RET(L(K.clean_apr, a, SW, 0));
       ACF_RET(L(K.adv, a, SW + TW, 1));
