@@ -59,7 +59,7 @@ def _as_epoch(model, batches) -> EpochTriplets:
 
 
 def training_batch(model, sess, batches, adver=False, graph=True):
-    """utils.py:106-140.  dns == 1: the epoch is planned in chunks of 512 batches,
+    """utils.py:106-140.  dns == 1: the epoch is planned in chunks (plan_chunk),
     each replayed as one hipGraph (delta_update + optimizer_step per batch, in
     batch order) while the next chunk is planned on a side stream.
     dns > 1: per batch, the highest-scoring of dns negatives under the current
@@ -69,7 +69,7 @@ def training_batch(model, sess, batches, adver=False, graph=True):
         ep = _as_epoch(model, batches)
         B, nb = ep.batch_size, ep.n_batches
         hp = model.hparams(adver=int(bool(adver)))
-        pipe = model.pipeline(B, min(nb, _PLAN_CHUNK))
+        pipe = model.pipeline(B, min(nb, plan_chunk(B)))
         pipe.run(model.tables, hp, ep.user, ep.item_pos, ep.item_neg, graph=graph, check=True)
         return ep
     user_input, item_input_pos, user_dns_list, item_dns_list = batches
@@ -91,7 +91,11 @@ def training_batch(model, sess, batches, adver=False, graph=True):
     return user_input, item_input_pos, negs
 
 
-_PLAN_CHUNK = 512  # batches per plan / graph; the next chunk is planned during this one
+def plan_chunk(batch_size: int) -> int:
+    """Batches per plan / hipGraph; the next chunk is planned during this one.
+    Small batches: 512 (the chunk's inline records stay in the Infinity Cache);
+    large batches: 2M triplets (the plan's fixed sort cost amortised)."""
+    return 512 if batch_size < 4096 else max(1, (1 << 21) // batch_size)
 
 
 def training_loss_acc(model, sess, train_batches, output_adv=0):

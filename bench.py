@@ -203,7 +203,7 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
 def large_batch_roofline(acf, ops, dev, d=128):
     """Batch 65,536 on 10M x 5M tables (d = 128: ~15 GB incl. Adagrad slots):
     tables far beyond the 256 MB Infinity Cache, so rows come from HBM."""
-    U1, I1, B, nb, chunk = 10_000_001, 5_000_001, 65536, 32, 8
+    U1, I1, B, nb, chunk = 10_000_001, 5_000_001, 65536, 64, 32
     g = torch.Generator(device=dev).manual_seed(5)
     u = torch.randint(0, U1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
     i = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)

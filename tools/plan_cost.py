@@ -63,6 +63,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--large", action="store_true")
     ap.add_argument("--ml-chunks", type=int, nargs="*", default=None)
+    ap.add_argument("--large-chunks", type=int, nargs="*", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ops = importlib.import_module(PKG + ".ops")
@@ -77,8 +78,8 @@ def main():
              [x[: 3 * 1941 * 512] for x in st])
     if a.large:
         for d in (64, 128):
-            for chunk in (1, 2, 8):
-                case(ops, acf, "10Mx5M", 10_000_001, 5_000_001, d, 65536, 16, chunk, dev)
+            for chunk in (a.large_chunks or [1, 2, 8]):
+                case(ops, acf, "10Mx5M", 10_000_001, 5_000_001, d, 65536, max(16, 2 * chunk), chunk, dev)
     del nb_ml
 
 
