@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--time-batches", type=int, default=400, help="batches in the kernel-timing pass")
     p.add_argument("--large", action="store_true", help="also measure batch 65536 on 10M x 5M x d128")
     p.add_argument("--no-neumf", action="store_true", help="skip the adversarial-NeuMF line (configs[3])")
+    p.add_argument("--mapping", default="auto", choices=["auto", "wave", "group"],
+                   help="slot mapping of the step kernels (auto: by batch size)")
     return p.parse_args()
 
 
@@ -307,6 +309,7 @@ def main():
     chunk = min(a.chunk, a.steps)
     # B = 512 steps are latency-bound: planning concurrently slows them
     pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False)
+    pipe.set_slot_mapping(a.mapping)
     hp = ops.StepHParams(lr=0.05, eps=0.5, reg=0.0, reg_adv=1.0, adver=1)
     graph = not a.eager
     # warmup: W steps plus every chunk size the timed region uses on both contexts
