@@ -675,20 +675,24 @@ struct SlotHdr {
 // wave (large batches, where almost every slot has one occurrence).
 struct SlotRec {
   SlotHdr h;
-  RecV r0;
-  bool r0_valid;
+  RecV r0, r1;  // inline records of occurrences m and m + TEAM
+  bool r0_valid, r1_valid;
 };
 
-// Record m of slot k (members m < R) and the slot header broadcast from the
-// team leader's lane.
+// Records m and m + TEAM of slot k (those < R; both addresses are known up
+// front, so a slot of up to 2 TEAM occurrences needs no CSR hop) and the slot
+// header broadcast from the team leader's lane.
 template <int LPR, int TEAM>
 __device__ __forceinline__ SlotRec slot_header(const StepArgs& a, int k, int m, int leader_lane) {
   const int32_t gen = *a.gen_ptr;
   SlotRec s;
   s.r0.a = s.r0.b = s.r0.c = make_int4(0, 0, 0, -1);
-  if (m < a.R && k < a.S)
-    s.r0 = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R + m);
+  s.r1 = s.r0;
+  const OccRec* base = a.inl + ((int64_t)a.t * a.S + k) * a.R;
+  if (m < a.R && k < a.S) s.r0 = load_rec(base + m);
+  if (m + TEAM < a.R && k < a.S) s.r1 = load_rec(base + m + TEAM);
   s.r0_valid = s.r0.gen() == gen;
+  s.r1_valid = s.r1.gen() == gen;
   const int32_t meta = __shfl(s.r0_valid ? s.r0.meta() : 0, leader_lane, 64);
   // a fused triplet's slots are handled by its k_single lane-group
   s.h.count = (a.use_single && (meta & ACF_SINGLE_BIT)) ? 0 : (meta & ACF_COUNT_MASK);
@@ -700,10 +704,37 @@ __device__ __forceinline__ SlotRec slot_header(const StepArgs& a, int k, int m, 
 }
 
 // record of occurrence idx of the slot (idx < count): the member's inline
-// record for its first occurrence, the CSR records otherwise
+// records for occurrences m and m + TEAM, the CSR records otherwise
+template <int TEAM>
 __device__ __forceinline__ RecV occ_rec(const StepArgs& a, const SlotRec& s, int idx, int m) {
   if (idx == m && m < a.R && s.r0_valid) return s.r0;
+  if (idx == m + TEAM && m + TEAM < a.R && s.r1_valid) return s.r1;
   return load_rec((s.h.is_item ? a.irec : a.urec) + s.h.ovf + idx);
+}
+
+// One occurrence's BPR term (APR.py:127-150) against the slot's own row (clean,
+// or own + delta for the adversarial loss) and the partner rows ra / rb; the
+// gradient w.r.t. the own row goes into G, the loss to loss[e].
+template <int LPR, int NV>
+__device__ __forceinline__ void occ_term(const StepArgs& a, int is_item, const RowV<NV>& own, const RecV& r,
+                                         const RowV<NV>& ra, const RowV<NV>& rb, bool active, int l,
+                                         float* __restrict__ loss_out, RowV<NV>& G) {
+  float gb, loss;
+  if (!is_item) {
+    const float x = dot_row<LPR, NV>(own, ra) - dot_row<LPR, NV>(own, rb);
+    bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
+    if (active) {
+      axpy_row(G, gb, ra);   // pos branch: dx+/dp = q_i
+      axpy_row(G, -gb, rb);  // neg branch: dx-/dp = q_j
+      if (l == 0) loss_out[r.e_role()] = loss;
+    }
+  } else {
+    const float dq = dot_row<LPR, NV>(ra, own), dqo = dot_row<LPR, NV>(ra, rb);
+    const int role = active ? (r.e_role() & 1) : 0;
+    const float x = role ? (dqo - dq) : (dq - dqo);
+    bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
+    if (active) axpy_row(G, role ? -gb : gb, ra);
+  }
 }
 
 // copy the pending row of slot k of batch tb (in wsrc) to its table; the
@@ -932,33 +963,26 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
   if (FUSE_APPLY && m == 0)
     acc = load_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l);
   RowV<NV> G = zero_row<NV>();
-  for (int base = 0; base < h.count; base += TEAM) {
-    const int idx = base + m;
-    const bool active = idx < h.count;
-    RowV<NV> ra = zero_row<NV>(), rb = zero_row<NV>();
-    RecV r;
-    if (active) {
-      r = occ_rec(a, sr, idx, m);
-      // user slot: ra = Q[i], rb = Q[j];  item slot: ra = P[u], rb = Q[other]
-      ra = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r.pa_row(), r.pa_src()), d, l);
-      rb = load_at<LPR, NV>(row_src(a, a.Q, r.pb_row(), r.pb_src()), d, l);
+  // member m takes occurrences m, m + TEAM, m + 2 TEAM, ... (in that order into
+  // G); two per pass, all their loads in flight before either is used
+  for (int base = 0; base < h.count; base += 2 * TEAM) {
+    const int i0 = base + m, i1 = base + TEAM + m;
+    const bool a0 = i0 < h.count, a1 = i1 < h.count;
+    RowV<NV> ra0 = zero_row<NV>(), rb0 = zero_row<NV>(), ra1 = zero_row<NV>(), rb1 = zero_row<NV>();
+    RecV r0, r1;
+    if (a0) r0 = occ_rec<TEAM>(a, sr, i0, m);
+    if (a1) r1 = occ_rec<TEAM>(a, sr, i1, m);
+    // user slot: ra = Q[i], rb = Q[j];  item slot: ra = P[u], rb = Q[other]
+    if (a0) {
+      ra0 = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r0.pa_row(), r0.pa_src()), d, l);
+      rb0 = load_at<LPR, NV>(row_src(a, a.Q, r0.pb_row(), r0.pb_src()), d, l);
     }
-    float gb, loss;
-    if (!h.is_item) {
-      const float x = dot_row<LPR, NV>(own, ra) - dot_row<LPR, NV>(own, rb);
-      bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
-      if (active) {
-        axpy_row(G, gb, ra);   // pos branch: dx+/dp = q_i
-        axpy_row(G, -gb, rb);  // neg branch: dx-/dp = q_j
-        if (l == 0) a.loss_clean[r.e_role()] = loss;
-      }
-    } else {
-      const float dq = dot_row<LPR, NV>(ra, own), dqo = dot_row<LPR, NV>(ra, rb);
-      const int role = active ? (r.e_role() & 1) : 0;
-      const float x = role ? (dqo - dq) : (dq - dqo);
-      bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
-      if (active) axpy_row(G, role ? -gb : gb, ra);
+    if (a1) {
+      ra1 = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r1.pa_row(), r1.pa_src()), d, l);
+      rb1 = load_at<LPR, NV>(row_src(a, a.Q, r1.pb_row(), r1.pb_src()), d, l);
     }
+    occ_term<LPR, NV>(a, h.is_item, own, r0, ra0, rb0, a0, l, a.loss_clean, G);
+    if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, own, r1, ra1, rb1, a1, l, a.loss_clean, G);
   }
   STAMP(a.diag_launch, wave, 2);
   team_allreduce<LPR, TEAM, NV>(G);
@@ -987,14 +1011,17 @@ template <int LPR, int NV, int TEAM>
 __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l, int leader, int wave) {
   // read (not copy) batch t+1's record of this slot: phase 1 of the next batch
   // then finds it in the Infinity Cache instead of HBM
-  int4 nxt = make_int4(0, 0, 0, 0);
-  if (a.touch_next && m < a.R && k < a.S)
-    nxt = *reinterpret_cast<const int4*>(a.inl + ((int64_t)(a.t + 1) * a.S + k) * a.R + m);
+  int4 nxt = make_int4(0, 0, 0, 0), nxt1 = nxt;
+  if (a.touch_next && k < a.S) {
+    const OccRec* nb = a.inl + ((int64_t)(a.t + 1) * a.S + k) * a.R;
+    if (m < a.R) nxt = *reinterpret_cast<const int4*>(nb + m);
+    if (m + TEAM < a.R) nxt1 = *reinterpret_cast<const int4*>(nb + m + TEAM);
+  }
   const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
   STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
-    if (nxt.x == -0x7fffffff && nxt.y == 0x7fffffff) a.loss_adv[0] = 0.f;
+    if (nxt.x == -0x7fffffff && nxt1.y == 0x7fffffff) a.loss_adv[0] = 0.f;
     return;
   }
   const int d = a.d;
@@ -1006,34 +1033,27 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
     G0 = load_row<LPR, NV>(a.g0, k, d, l);
   }
   RowV<NV> G = zero_row<NV>();
-  for (int base = 0; base < h.count; base += TEAM) {
-    const int idx = base + m;
-    const bool active = idx < h.count;
-    RowV<NV> ra = zero_row<NV>(), rb = zero_row<NV>();
-    RecV r;
-    if (active) {
-      r = occ_rec(a, sr, idx, m);
-      ra = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r.pa_row(), d, l),
-                   load_row<LPR, NV>(a.delta, r.pa_slot(), d, l));
-      rb = add_row(load_row<LPR, NV>(a.Q, r.pb_row(), d, l),
-                   load_row<LPR, NV>(a.delta, r.pb_slot(), d, l));
+  for (int base = 0; base < h.count; base += 2 * TEAM) {  // as in clean_slot
+    const int i0 = base + m, i1 = base + TEAM + m;
+    const bool a0 = i0 < h.count, a1 = i1 < h.count;
+    RowV<NV> ra0 = zero_row<NV>(), rb0 = zero_row<NV>(), ra1 = zero_row<NV>(), rb1 = zero_row<NV>();
+    RecV r0, r1;
+    if (a0) r0 = occ_rec<TEAM>(a, sr, i0, m);
+    if (a1) r1 = occ_rec<TEAM>(a, sr, i1, m);
+    if (a0) {
+      ra0 = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r0.pa_row(), d, l),
+                    load_row<LPR, NV>(a.delta, r0.pa_slot(), d, l));
+      rb0 = add_row(load_row<LPR, NV>(a.Q, r0.pb_row(), d, l),
+                    load_row<LPR, NV>(a.delta, r0.pb_slot(), d, l));
     }
-    float gb, loss;
-    if (!h.is_item) {
-      const float x = dot_row<LPR, NV>(ownp, ra) - dot_row<LPR, NV>(ownp, rb);
-      bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
-      if (active) {
-        axpy_row(G, gb, ra);
-        axpy_row(G, -gb, rb);
-        if (l == 0) a.loss_adv[r.e_role()] = loss;
-      }
-    } else {
-      const float dq = dot_row<LPR, NV>(ra, ownp), dqo = dot_row<LPR, NV>(ra, rb);
-      const int role = active ? (r.e_role() & 1) : 0;
-      const float x = role ? (dqo - dq) : (dq - dqo);
-      bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
-      if (active) axpy_row(G, role ? -gb : gb, ra);
+    if (a1) {
+      ra1 = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r1.pa_row(), d, l),
+                    load_row<LPR, NV>(a.delta, r1.pa_slot(), d, l));
+      rb1 = add_row(load_row<LPR, NV>(a.Q, r1.pb_row(), d, l),
+                    load_row<LPR, NV>(a.delta, r1.pb_slot(), d, l));
     }
+    occ_term<LPR, NV>(a, h.is_item, ownp, r0, ra0, rb0, a0, l, a.loss_adv, G);
+    if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, ownp, r1, ra1, rb1, a1, l, a.loss_adv, G);
   }
   STAMP(a.diag_launch, wave, 2);
   team_allreduce<LPR, TEAM, NV>(G);
@@ -1044,7 +1064,7 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
     store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
     store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
   }
-  if (nxt.x == -0x7fffffff && nxt.y == 0x7fffffff) a.loss_adv[0] = 0.f;  // keeps the read alive; never true
+  if (nxt.x == -0x7fffffff && nxt1.y == 0x7fffffff) a.loss_adv[0] = 0.f;  // keeps the reads alive; never true
 }
 
 // One team per slot; the team also writes back slot k of batch t-1.  Waves past
@@ -1523,7 +1543,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   acf_apr_ctx* c = new acf_apr_ctx();
   c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB; c->maxNB = maxNB; c->maxE = maxE;
   geometry(d, &c->lpr, &c->nv);
-  c->R = std::min(64 / c->lpr, 4);
+  c->R = std::min(128 / c->lpr, 8);  // 2 records per team member (see slot_header)
   if (const char* e = getenv("ACF_TOUCH_NEXT")) c->touch_next = atoi(e) != 0;
   const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
