@@ -110,6 +110,24 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, int64_t row,
   }
 }
 
+// store_row with device-scope write-through stores (sc1): once the wave's
+// vmcnt drains they are visible to every XCD, with no L2 write-back (the
+// release fence a flag would otherwise need writes back the whole L2).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <int LPR, int NV>
+__device__ __forceinline__ void store_row_wt(float* __restrict__ base, int64_t row, int d, int l,
+                                             const RowV<NV>& r) {
+  float* p = base + row * (int64_t)d;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    int c = l + LPR * v;
+    if (c * 4 < d) {
+      const f32x4 x = {r.v[v].x, r.v[v].y, r.v[v].z, r.v[v].w};
+      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p + c * 4), "v"(x) : "memory");
+    }
+  }
+}
+
 template <int NV>
 __device__ __forceinline__ RowV<NV> zero_row() {
   RowV<NV> r;
@@ -332,14 +350,40 @@ __global__ void k_compact(KT key, const int32_t* __restrict__ inc, const int32_t
 // For every unique row of batch t: where its current value lives when batch t
 // starts.  Rows updated by batch t-1 are still in that batch's W scratch (the
 // flush to the table happens inside batch t's first kernel), so the plan encodes
-// src = ~(local slot in batch t-1) for them and src = row otherwise.
+// src = ~(local slot in batch t-1) for them and src = row otherwise.  With
+// `kind2`, rows updated by batch t-2 but not t-1 get src = ~(local slot in
+// batch t-2 | ACF_SRC_KIND2): the overlapped step (k_ovl) reads them from
+// W(t-2) while W(t-1) is being flushed; every other kernel treats them as
+// "in the table" (pend1).
 // user local slot = g - ubs[t]; item local slot = nU(t) + g - ibs[t].
 // info[g] = {row, src, occurrence count | NEXT (batch t+1 touches the row too),
 //            CSR offset of the first occurrence}.
 #define ACF_INFO_NEXT (1 << 30)
+#define ACF_SRC_KIND2 (1 << 29)
+
+// src names W scratch of batch t-1 (not t-2, not the table)
+__device__ __forceinline__ bool pend1(int32_t src) { return src < 0 && !((~src) & ACF_SRC_KIND2); }
+
+// local slot in batch tb of the row (binary search of tb's sorted unique rows), or -1
+__device__ __forceinline__ int find_local(const int32_t* __restrict__ uniq, const int32_t* __restrict__ ubs,
+                                          const int32_t* __restrict__ bstart, int tb, int32_t row,
+                                          int item_side) {
+  int a = bstart[tb], b = bstart[tb + 1];
+  while (a < b) {
+    int mid = (a + b) >> 1;
+    if (uniq[mid] < row) a = mid + 1; else b = mid;
+  }
+  if (a < bstart[tb + 1] && uniq[a] == row) {
+    const int nU = ubs[tb + 1] - ubs[tb];
+    return item_side ? nU + (a - bstart[tb]) : (a - bstart[tb]);
+  }
+  return -1;
+}
+
 __global__ void k_slot_info(const int32_t* __restrict__ uniq, const int32_t* __restrict__ off,
                             const int32_t* __restrict__ ubs, const int32_t* __restrict__ bstart,
-                            int32_t n_uniq, int32_t nb, int32_t item_side, int4* __restrict__ info) {
+                            int32_t n_uniq, int32_t nb, int32_t item_side, int32_t kind2,
+                            int4* __restrict__ info) {
   int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (g >= n_uniq || g >= bstart[nb]) return;  // bstart[nb] = unique rows of the plan
   // batch of g: last t with bstart[t] <= g
@@ -352,15 +396,12 @@ __global__ void k_slot_info(const int32_t* __restrict__ uniq, const int32_t* __r
   const int32_t row = uniq[g];
   int32_t s = row;
   if (t > 0) {
-    int a = bstart[t - 1], b = bstart[t];
-    while (a < b) {
-      int mid = (a + b) >> 1;
-      if (uniq[mid] < row) a = mid + 1; else b = mid;
-    }
-    if (a < bstart[t] && uniq[a] == row) {
-      const int nU_prev = ubs[t] - ubs[t - 1];
-      const int local = item_side ? nU_prev + (a - bstart[t - 1]) : (a - bstart[t - 1]);
+    const int local = find_local(uniq, ubs, bstart, t - 1, row, item_side);
+    if (local >= 0) {
       s = ~local;
+    } else if (kind2 && t > 1) {
+      const int local2 = find_local(uniq, ubs, bstart, t - 2, row, item_side);
+      if (local2 >= 0) s = ~(local2 | ACF_SRC_KIND2);
     }
   }
   int32_t in_next = 0;
@@ -416,9 +457,9 @@ __device__ __forceinline__ int info_count(const int4& f) { return f.z & (ACF_INF
 __device__ __forceinline__ FuseInfo fuse_info(const int4& U, const int4& I, const int4& J) {
   FuseInfo f;
   f.fused = info_count(U) == 1 && info_count(I) == 1 && info_count(J) == 1;
-  f.in_u = f.fused && U.y >= 0 && !(U.z & ACF_INFO_NEXT);
-  f.in_i = f.fused && I.y >= 0 && !(I.z & ACF_INFO_NEXT);
-  f.in_j = f.fused && J.y >= 0 && !(J.z & ACF_INFO_NEXT);
+  f.in_u = f.fused && !pend1(U.y) && !(U.z & ACF_INFO_NEXT);
+  f.in_i = f.fused && !pend1(I.y) && !(I.z & ACF_INFO_NEXT);
+  f.in_j = f.fused && !pend1(J.y) && !(J.z & ACF_INFO_NEXT);
   return f;
 }
 
@@ -605,6 +646,14 @@ struct StepArgs {
   const int32_t* slot_cnt;    // [nb]
   const int32_t* flush_cnt;   // [nb]
   int32_t slot_waves;  // waves [0, slot_waves) are slot waves, the rest fused-triplet waves
+  // overlapped step (k_ovl): adv(t) publishes flags[t][slot] once W(t)[slot] is
+  // stored; clean(t+1) in the same launch waits for the rows it reads from W(t)
+  int32_t* flags;       // [nb][S]
+  int32_t* step_err;    // bit 0: a wait gave up (ACF_SPIN_LIMIT)
+  float* wnew_prev2;    // [S, d] updated rows of batch t-2 (clean half of k_ovl)
+  int32_t prev2_valid;  // 1: batch t-2 ran in this call (its W scratch is live)
+  int32_t ovl_flush;    // adv half writes back W(t-1) (the launch has no clean half)
+  int32_t ovl_delay;    // clean half: s_sleep(8) rounds before starting (ACF_OVL_DELAY, tuning)
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -640,8 +689,86 @@ __device__ __forceinline__ RecV load_rec(const OccRec* __restrict__ p) {
 // current value of a row at batch start: pending scratch or the table
 __device__ __forceinline__ const float* row_src(const StepArgs& a, const float* table, int32_t row,
                                                 int32_t src) {
-  return (src < 0 && a.prev_valid) ? a.wnew_prev + (int64_t)(~src) * a.d
-                                   : table + (int64_t)row * a.d;
+  return (pend1(src) && a.prev_valid) ? a.wnew_prev + (int64_t)(~src) * a.d
+                                      : table + (int64_t)row * a.d;
+}
+
+// --- overlapped step: sources, waits and publication ------------------------
+// The clean half of k_ovl (batch t) runs beside adv(t-1): a row batch t-1
+// updates comes from W(t-1) once adv(t-1) has published it, a row last updated
+// by batch t-2 from W(t-2) (its flush to the table is running in this launch).
+#define ACF_SPIN_LIMIT (1 << 16)
+
+__device__ __forceinline__ const float* row_src_ovl(const StepArgs& a, const float* table, int32_t row,
+                                                    int32_t src) {
+  if (src < 0 && a.prev_valid) {
+    const int32_t v = ~src;
+    if (!(v & ACF_SRC_KIND2)) return a.wnew_prev + (int64_t)v * a.d;
+    if (a.prev2_valid) return a.wnew_prev2 + (int64_t)(v & ~ACF_SRC_KIND2) * a.d;
+  }
+  return table + (int64_t)row * a.d;
+}
+
+__device__ __forceinline__ bool src_waits(const StepArgs& a, int32_t src) {
+  return a.prev_valid && pend1(src);
+}
+
+
+// Wave-wide: wait until every listed source row (0 = none) that batch t-1
+// updates is published.  Bounded: after ACF_SPIN_LIMIT polls the wave records
+// bit 0 in step_err and goes on (the call then reports an error).
+// No L2 invalidate is needed after the flag: the flag load is device-coherent
+// (sc1), the rows were stored write-through before it (publish), and no L2 can
+// hold a stale copy of them — every launch starts with invalidated L2s and a W(t)
+// row is read in this launch only after its flag.  The compiler barrier keeps
+// the row loads behind the wait.
+// Lane x of each lane-group polls the group's x-th source (x < 5, LPR >= 8;
+// narrower groups poll their sources in turn), so one poll is one round trip.
+template <int LPR>
+__device__ __forceinline__ void wait_srcs(const StepArgs& a, int32_t s0, int32_t s1, int32_t s2, int32_t s3,
+                                          int32_t s4) {
+  const int l = (int)(threadIdx.x & (LPR - 1));
+  const int32_t* fl = a.flags + (int64_t)(a.t - 1) * a.S;
+  const int32_t src[5] = {s0, s1, s2, s3, s4};
+  constexpr int PER = LPR >= 8 ? 1 : (5 + LPR - 1) / LPR;  // sources per lane
+  int32_t mine[PER];
+  bool need = false;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int x = l + p * LPR;
+    int32_t v = 0;
+#pragma unroll
+    for (int y = 0; y < 5; ++y) v = x == y ? src[y] : v;
+    mine[p] = src_waits(a, v) ? ~v : -1;  // flag index, or -1
+    need = need || mine[p] >= 0;
+  }
+  if (!__any(need)) return;
+  for (int it = 0;; ++it) {
+    bool ok = true;
+#pragma unroll
+    for (int p = 0; p < PER; ++p)
+      if (mine[p] >= 0)
+        ok = ok && __hip_atomic_load(fl + mine[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (__all(ok)) break;
+    if (it >= ACF_SPIN_LIMIT) {
+      atomicOr(a.step_err, 1);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// after this wave stored W(t)[k] (and k2, k3) with store_row_wt: wait for the
+// stores to complete at device scope, then set the flags
+__device__ __forceinline__ void publish(const StepArgs& a, bool leader, int k, int k2 = -1, int k3 = -1) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (leader) {
+    int32_t* f = a.flags + (int64_t)a.t * a.S;
+    __hip_atomic_store(f + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k2 >= 0) __hip_atomic_store(f + k2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k3 >= 0) __hip_atomic_store(f + k3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <int LPR, int NV>
@@ -878,7 +1005,10 @@ __device__ __forceinline__ RowV<NV> make_delta(const StepArgs& a, const RowV<NV>
 // the row goes clean -> delta -> adversarial -> Adagrad; otherwise (BPR graph,
 // inside k_clean<FUSE_APPLY>) rows are read through their batch-start source and
 // the clean gradient is applied.
-template <int LPR, int NV, bool ADV>
+// OVL (inside k_ovl): rows are read through their batch-start source (W(t-1)
+// is being flushed beside it) and every row also goes to W(t), where clean(t+2)
+// finds a row batch t+1 does not touch; its flags are published.
+template <int LPR, int NV, bool ADV, bool OVL = false>
 __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
   if (b >= a.B) return;
   const int64_t e = (int64_t)a.t * a.B + b;
@@ -887,7 +1017,7 @@ __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
   const int d = a.d;
   const int32_t u = r.a.x, i = r.a.y, j = r.a.z, flags = r.c.y;
   RowV<NV> p, qi, qj;
-  if (ADV) {
+  if (ADV && !OVL) {
     p = load_row<LPR, NV>(a.P, u, d, l);
     qi = load_row<LPR, NV>(a.Q, i, d, l);
     qj = load_row<LPR, NV>(a.Q, j, d, l);
@@ -927,9 +1057,19 @@ __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
   adagrad_row(a, Gu, p, cu, 1, wu);
   adagrad_row(a, Gi, qi, ci, 1, wi);
   adagrad_row(a, Gj, qj, cj, 1, wj);
+  if (OVL) {  // publish first: the flags wait only for the W rows
+    store_row_wt<LPR, NV>(a.wnew_cur, r.a.w, d, l, wu);
+    store_row_wt<LPR, NV>(a.wnew_cur, r.b.x, d, l, wi);
+    store_row_wt<LPR, NV>(a.wnew_cur, r.b.y, d, l, wj);
+    publish(a, l == 0, r.a.w, r.b.x, r.b.y);
+    if (flags & 2) store_row<LPR, NV>(a.P, u, d, l, wu);
+    if (flags & 4) store_row<LPR, NV>(a.Q, i, d, l, wi);
+    if (flags & 8) store_row<LPR, NV>(a.Q, j, d, l, wj);
+  }
   store_row<LPR, NV>(a.accP, u, d, l, cu);
   store_row<LPR, NV>(a.accQ, i, d, l, ci);
   store_row<LPR, NV>(a.accQ, j, d, l, cj);
+  if (OVL) return;
   // in place unless the row is pending from batch t-1 or read by batch t+1
   store_row<LPR, NV>((flags & 2) ? a.P : a.wnew_cur, (flags & 2) ? u : r.a.w, d, l, wu);
   store_row<LPR, NV>((flags & 4) ? a.Q : a.wnew_cur, (flags & 4) ? i : r.b.x, d, l, wi);
@@ -941,16 +1081,20 @@ __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
 // over its occurrences, its delta (APR graph), or — BPR graph, FUSE_APPLY — the
 // Adagrad update straight away.  Slot k, team member m, lane l of the row-group,
 // the team leader's lane.
-template <int LPR, int NV, bool FUSE_APPLY, int TEAM, bool FLUSH = false>
+// OVL: the clean half of k_ovl (one wave per slot, APR graph): sources via
+// row_src_ovl, waiting for rows adv(t-1) is still producing.
+template <int LPR, int NV, bool FUSE_APPLY, int TEAM, bool FLUSH = false, bool OVL = false>
 __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int l, int leader, int wave,
                                            int tl = 0) {
-  // write-back of slot k of batch t-1: its record is loaded next to our header
+  static_assert(!OVL || (!FUSE_APPLY && TEAM * LPR == 64), "k_ovl: one wave per slot, APR");
+  // write-back of slot k of batch t-1 (OVL: of t-2, whose adv half runs beside
+  // us): its record is loaded next to our header
   RecV frec;
-  if (FLUSH) frec = flush_rec(a, a.t - 1, k);
+  if (FLUSH) frec = flush_rec(a, OVL ? a.t - 2 : a.t - 1, k);
   const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
   FlushOp fo;
-  if (FLUSH) fo = flush_load(a, frec, a.wnew_prev, k, tl, TEAM * LPR);
+  if (FLUSH) fo = flush_load(a, frec, OVL ? a.wnew_prev2 : a.wnew_prev, k, tl, TEAM * LPR);
   STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
     if (FLUSH) flush_store(fo);
@@ -958,7 +1102,8 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
   }
   const int d = a.d;
   const float* own_tab = h.is_item ? a.Q : a.P;
-  const RowV<NV> own = load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l);
+  RowV<NV> own;
+  if (!OVL) own = load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l);
   RowV<NV> acc;
   if (FUSE_APPLY && m == 0)
     acc = load_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l);
@@ -972,6 +1117,20 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
     RecV r0, r1;
     if (a0) r0 = occ_rec<TEAM>(a, sr, i0, m);
     if (a1) r1 = occ_rec<TEAM>(a, sr, i1, m);
+    if (OVL) {  // the pass is wave-uniform (one team per wave)
+      wait_srcs<LPR>(a, base == 0 ? h.own_src : 0, a0 ? r0.pa_src() : 0, a0 ? r0.pb_src() : 0,
+                a1 ? r1.pa_src() : 0, a1 ? r1.pb_src() : 0);
+      if (base == 0) STAMP(a.diag_launch, wave, 5);
+      if (base == 0) own = load_at<LPR, NV>(row_src_ovl(a, own_tab, h.own_row, h.own_src), d, l);
+      if (a0) {
+        ra0 = load_at<LPR, NV>(row_src_ovl(a, h.is_item ? a.P : a.Q, r0.pa_row(), r0.pa_src()), d, l);
+        rb0 = load_at<LPR, NV>(row_src_ovl(a, a.Q, r0.pb_row(), r0.pb_src()), d, l);
+      }
+      if (a1) {
+        ra1 = load_at<LPR, NV>(row_src_ovl(a, h.is_item ? a.P : a.Q, r1.pa_row(), r1.pa_src()), d, l);
+        rb1 = load_at<LPR, NV>(row_src_ovl(a, a.Q, r1.pb_row(), r1.pb_src()), d, l);
+      }
+    } else {
     // user slot: ra = Q[i], rb = Q[j];  item slot: ra = P[u], rb = Q[other]
     if (a0) {
       ra0 = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r0.pa_row(), r0.pa_src()), d, l);
@@ -980,6 +1139,7 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
     if (a1) {
       ra1 = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r1.pa_row(), r1.pa_src()), d, l);
       rb1 = load_at<LPR, NV>(row_src(a, a.Q, r1.pb_row(), r1.pb_src()), d, l);
+    }
     }
     occ_term<LPR, NV>(a, h.is_item, own, r0, ra0, rb0, a0, l, a.loss_clean, G);
     if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, own, r1, ra1, rb1, a1, l, a.loss_clean, G);
@@ -1007,8 +1167,20 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
 // Phase 2 = adversarial half of sess.run(optimizer) (APR.py:130-141,156-165)
 // and SparseApplyAdagrad: loss on p+dP[u], q+dQ[i]; G = G_clean + reg_adv*G_adv;
 // Adagrad into wnew_cur.  The tables are current (flushed by phase 1).
-template <int LPR, int NV, int TEAM>
-__device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l, int leader, int wave) {
+// OVL (adv half of k_ovl): batch t-1's rows were not flushed by a phase 1, so
+// this wave writes back slot k of W(t-1) (its loads overlap the slot's own) and
+// reads rows through their batch-start source; W(t)[k] is then published.
+template <int LPR, int NV, int TEAM, bool OVL = false>
+__device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l, int leader, int wave,
+                                         int tl = 0) {
+  constexpr bool OFL = OVL && TEAM * LPR >= 64;  // write-back overlapped with the loads (d <= 256)
+  RecV frec;
+  FlushOp fo;
+  fo.dst = nullptr;
+  if (OVL && a.prev_valid && a.ovl_flush) {
+    if (OFL && a.d <= 4 * TEAM * LPR) frec = flush_rec(a, a.t - 1, k);
+    else flush_slot(a, a.t - 1, a.wnew_prev, k, tl, TEAM * LPR);
+  }
   // read (not copy) batch t+1's record of this slot: phase 1 of the next batch
   // then finds it in the Infinity Cache instead of HBM
   int4 nxt = make_int4(0, 0, 0, 0), nxt1 = nxt;
@@ -1019,13 +1191,18 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
   }
   const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
+  if (OFL && a.prev_valid && a.ovl_flush && a.d <= 4 * TEAM * LPR)
+    fo = flush_load(a, frec, a.wnew_prev, k, tl, TEAM * LPR);
   STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
+    if (OFL) flush_store(fo);
     if (nxt.x == -0x7fffffff && nxt1.y == 0x7fffffff) a.loss_adv[0] = 0.f;
     return;
   }
   const int d = a.d;
-  const RowV<NV> own = load_row<LPR, NV>(h.is_item ? a.Q : a.P, h.own_row, d, l);
+  const float* own_tab = h.is_item ? a.Q : a.P;
+  const RowV<NV> own = OVL ? load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l)
+                           : load_row<LPR, NV>(own_tab, h.own_row, d, l);
   const RowV<NV> ownp = add_row(own, load_row<LPR, NV>(a.delta, k, d, l));
   RowV<NV> acc, G0;
   if (m == 0) {
@@ -1040,16 +1217,21 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
     RecV r0, r1;
     if (a0) r0 = occ_rec<TEAM>(a, sr, i0, m);
     if (a1) r1 = occ_rec<TEAM>(a, sr, i1, m);
+    const float* ptab = h.is_item ? a.P : a.Q;
     if (a0) {
-      ra0 = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r0.pa_row(), d, l),
+      ra0 = add_row(OVL ? load_at<LPR, NV>(row_src(a, ptab, r0.pa_row(), r0.pa_src()), d, l)
+                        : load_row<LPR, NV>(ptab, r0.pa_row(), d, l),
                     load_row<LPR, NV>(a.delta, r0.pa_slot(), d, l));
-      rb0 = add_row(load_row<LPR, NV>(a.Q, r0.pb_row(), d, l),
+      rb0 = add_row(OVL ? load_at<LPR, NV>(row_src(a, a.Q, r0.pb_row(), r0.pb_src()), d, l)
+                        : load_row<LPR, NV>(a.Q, r0.pb_row(), d, l),
                     load_row<LPR, NV>(a.delta, r0.pb_slot(), d, l));
     }
     if (a1) {
-      ra1 = add_row(load_row<LPR, NV>(h.is_item ? a.P : a.Q, r1.pa_row(), d, l),
+      ra1 = add_row(OVL ? load_at<LPR, NV>(row_src(a, ptab, r1.pa_row(), r1.pa_src()), d, l)
+                        : load_row<LPR, NV>(ptab, r1.pa_row(), d, l),
                     load_row<LPR, NV>(a.delta, r1.pa_slot(), d, l));
-      rb1 = add_row(load_row<LPR, NV>(a.Q, r1.pb_row(), d, l),
+      rb1 = add_row(OVL ? load_at<LPR, NV>(row_src(a, a.Q, r1.pb_row(), r1.pb_src()), d, l)
+                        : load_row<LPR, NV>(a.Q, r1.pb_row(), d, l),
                     load_row<LPR, NV>(a.delta, r1.pb_slot(), d, l));
     }
     occ_term<LPR, NV>(a, h.is_item, ownp, r0, ra0, rb0, a0, l, a.loss_adv, G);
@@ -1057,12 +1239,19 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
   }
   STAMP(a.diag_launch, wave, 2);
   team_allreduce<LPR, TEAM, NV>(G);
+  if (OFL) flush_store(fo);
   if (m == 0) {
     axpy_row(G0, a.reg_adv, G);
     RowV<NV> wout;
     adagrad_row(a, G0, own, acc, h.count, wout);
-    store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
-    store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+    if (OVL) {  // publish first: the flag waits only for the W row
+      store_row_wt<LPR, NV>(a.wnew_cur, k, d, l, wout);
+      publish(a, l == 0, k);
+      store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
+    } else {
+      store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
+      store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+    }
   }
   if (nxt.x == -0x7fffffff && nxt1.y == 0x7fffffff) a.loss_adv[0] = 0.f;  // keeps the reads alive; never true
 }
@@ -1101,6 +1290,40 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
   STAMP(a.diag_launch, q.wave, 0);
   adv_slot<LPR, NV, TEAM>(a, q.k, q.m, q.l, q.leader, q.wave);
   STAMP(a.diag_launch, q.wave, 4);
+}
+
+// Overlapped APR step (small batches, one wave per slot): adv(t) of `aa` on
+// waves [0, adv_waves) — slot waves, then fused-triplet waves — and clean(t+1)
+// of `ac` on the waves after them.  A clean wave only waits for flags of adv
+// waves; those come first in dispatch order and never wait, so the launch
+// always drains.  Saves one kernel boundary and the slowest waves' tail per
+// batch against k_clean + k_adv, with identical arithmetic.
+template <int LPR, int NV, int TEAM>
+__global__ void __launch_bounds__(256) k_ovl(StepArgs aa, StepArgs ac, int32_t adv_waves) {
+  static_assert(TEAM * LPR == 64, "k_ovl: one wave per slot");
+  const Geo<LPR, TEAM> q;
+  STAMP(aa.diag_launch, q.wave, 0);
+  if (q.wave < adv_waves) {
+    if (q.wave >= aa.slot_waves) {
+      if (aa.use_single)
+        k_single<LPR, NV, true, true>(aa, (q.wave - aa.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR,
+                                      q.l);
+    } else {
+      adv_slot<LPR, NV, TEAM, true>(aa, q.k, q.m, q.l, q.leader, q.wave, q.tl);
+    }
+  } else {
+    const int w = q.wave - adv_waves;  // slot of batch t+1
+    for (int x = 0; x < ac.ovl_delay; ++x) __builtin_amdgcn_s_sleep(8);
+    // the clean half writes back W(t-1) (= W(t+1-2)): nothing in this launch
+    // reads those rows from the tables
+    if (ac.prev2_valid && ac.d <= 4 * TEAM * LPR) {
+      clean_slot<LPR, NV, false, TEAM, true, true>(ac, w, q.m, q.l, q.leader, q.wave, q.tl);
+    } else {
+      if (ac.prev2_valid) flush_slot(ac, ac.t - 2, ac.wnew_prev2, w, q.tl, TEAM * LPR);
+      clean_slot<LPR, NV, false, TEAM, false, true>(ac, w, q.m, q.l, q.leader, q.wave, q.tl);
+    }
+  }
+  STAMP(aa.diag_launch, q.wave, 4);
 }
 
 // Large batches with fusion (one lane-group per slot): the slot work of batch t
@@ -1410,7 +1633,7 @@ __global__ void __launch_bounds__(256) k_dns_select(const float* __restrict__ P,
 struct GraphKey {
   const void* ptrs[4];
   acf_apr_hparams hp;
-  int32_t first, n, B, d, mapping, fusion;
+  int32_t first, n, B, d, mapping, fusion, ovl;
   bool operator<(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
 
@@ -1443,6 +1666,10 @@ struct acf_apr_ctx {
   int32_t touch_next = 1;  // phase 2 reads the next batch's records (ACF_TOUCH_NEXT=0 disables)
   int32_t *slot_list = nullptr, *flush_list = nullptr, *slot_cnt = nullptr, *flush_cnt = nullptr;
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
+  int32_t overlap = 1;  // k_ovl for APR runs of one-wave-per-slot plans (ACF_STEP_OVERLAP=0 disables)
+  int32_t plan_kind2 = 0;  // the plan encodes batch t-2 sources (k_slot_info kind2)
+  int32_t ovl_delay = 0;   // ACF_OVL_DELAY (tuning only)
+  int32_t* flags = nullptr;  // [maxNB][S] k_ovl publication flags
   hipStream_t cap_stream = nullptr;
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<void*> allocs;
@@ -1545,6 +1772,8 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   geometry(d, &c->lpr, &c->nv);
   c->R = std::min(128 / c->lpr, 8);  // 2 records per team member (see slot_header)
   if (const char* e = getenv("ACF_TOUCH_NEXT")) c->touch_next = atoi(e) != 0;
+  if (const char* e = getenv("ACF_STEP_OVERLAP")) c->overlap = atoi(e) != 0;
+  if (const char* e = getenv("ACF_OVL_DELAY")) c->ovl_delay = std::max(0, atoi(e));
   const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
   auto A = [&](auto** p, size_t n) { if (r == ACF_OK) r = dalloc(c, p, n); };
@@ -1559,7 +1788,8 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
   A(&c->err, 4); A(&c->gen_dev, 4);
-  A(&c->g0, S * d); A(&c->delta, S * d);
+  A(&c->g0, 2 * S * d); A(&c->delta, 2 * S * d);  // by batch parity (k_ovl: clean(t+1) beside adv(t))
+  A(&c->flags, 3 * maxE);
   A(&c->wnew[0], S * d); A(&c->wnew[1], S * d);
   A(&c->loss_clean, maxE); A(&c->loss_adv, maxE);
   if (r != ACF_OK) { acf_apr_destroy(c); return r; }
@@ -1656,14 +1886,17 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
     const Key64 ku{c->key_out, ob_u, ~0ull}, ki{c->key_out + E, ob_i, ~item_bit};
     ACF_RET(plan_groups(c, ku, ki, E, nb, s));
   }
-  // where each unique row's value lives at batch start, then the records
-  k_slot_info<<<grid_for(E), 256, 0, s>>>(c->uuniq, c->uoff, c->ubs, c->ubs, (int32_t)E, nb, 0,
+  // where each unique row's value lives at batch start, then the records; one
+  // lane-group per slot (large batches) reads only a slot's first record inline
+  // and never runs k_ovl, so only one-wave-per-slot plans encode t-2 sources
+  const int packed = c->mapping == 2 || (c->mapping == 0 && B >= ACF_PACKED_MIN_BATCH);
+  const int kind2 = !packed && 3 * (int64_t)B < ACF_SRC_KIND2;
+  k_slot_info<<<grid_for(E), 256, 0, s>>>(c->uuniq, c->uoff, c->ubs, c->ubs, (int32_t)E, nb, 0, kind2,
                                           c->uinfo);
   k_slot_info<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, c->ioff, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
-                                              c->iinfo);
-  // one lane-group per slot (large batches) reads only a slot's first record inline
-  const int packed = c->mapping == 2 || (c->mapping == 0 && B >= ACF_PACKED_MIN_BATCH);
+                                              kind2, c->iinfo);
   c->plan_R = packed ? 1 : c->R;
+  c->plan_kind2 = kind2;
   k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen,
                                         reinterpret_cast<const int4*>(c->tsl),
                                         reinterpret_cast<const int4*>(c->tpos), c->uinfo, c->iinfo,
@@ -1703,9 +1936,16 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.slot_waves = 1 << 30;  // set by the launcher
   a.slot_list = c->slot_list; a.flush_list = c->flush_list;
   a.slot_cnt = c->slot_cnt; a.flush_cnt = c->flush_cnt;
-  a.g0 = c->g0; a.delta = c->delta;
+  const size_t par = (size_t)(t & 1) * 3 * c->B * c->d;
+  a.g0 = c->g0 + par; a.delta = c->delta + par;
   a.wnew_cur = c->wnew[t & 1];
   a.wnew_prev = c->wnew[(t + 1) & 1];
+  a.wnew_prev2 = c->wnew[t & 1];  // W(t-2) shares W(t)'s buffer (read only by k_ovl's clean half)
+  a.prev2_valid = 0;
+  a.ovl_flush = 0;
+  a.ovl_delay = c->ovl_delay;
+  a.flags = c->flags;
+  a.step_err = c->err + 1;
   a.loss_clean = c->loss_clean; a.loss_adv = c->loss_adv;
   a.gen_ptr = c->gen_dev;
   a.d = c->d; a.B = c->B; a.S = 3 * c->B; a.R = c->plan_R; a.t = t;
@@ -1720,6 +1960,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
 // kernel kinds for timing: 0 = phase-1 (clean, or fused BPR), 1 = adversarial, 2 = flush
 struct Kernels {
   void *clean_apr = nullptr, *clean_bpr = nullptr, *adv = nullptr, *flush = nullptr;
+  void* ovl = nullptr;  // k_ovl (one wave per slot only)
   int slots_per_wave = 1;
   int lists = 0;  // list kernels: slot waves stride over the plan's per-batch lists
 };
@@ -1757,6 +1998,7 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists) {
     k->slots_per_wave = OPW;
   } else {
     kernel_ptrs_team<LPR, NV, OPW>(k, fused);
+    k->ovl = reinterpret_cast<void*>(&k_ovl<LPR, NV, OPW>);
     k->slots_per_wave = 1;
   }
   k->flush = reinterpret_cast<void*>(&k_flush);
@@ -1786,6 +2028,22 @@ static int launch(void* fn, const StepArgs& a, int waves, hipStream_t s, hipEven
   return ACF_OK;
 }
 
+typedef void (*OvlKernel)(StepArgs, StepArgs, int32_t);
+
+static int launch_ovl(void* fn, const StepArgs& aa, const StepArgs& ac, int adv_waves, int clean_waves,
+                      hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+  if (aa.slot_waves > adv_waves || clean_waves < 0 || (clean_waves > 0 && clean_waves != ac.S))
+    return set_error(ACF_E_STATE, "bad overlapped step geometry");
+  const int waves = adv_waves + clean_waves;
+  const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+  if (e0)
+    hipExtLaunchKernelGGL(reinterpret_cast<OvlKernel>(fn), grid, block, 0, s, e0, e1, 0, aa, ac, adv_waves);
+  else
+    hipLaunchKernelGGL(reinterpret_cast<OvlKernel>(fn), grid, block, 0, s, aa, ac, adv_waves);
+  HIP_TRY(hipGetLastError());
+  return ACF_OK;
+}
+
 static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                       int32_t t) {
   ACF_CHECK(c && tb && hp, ACF_E_INVALID, "NULL ctx/tables/hparams");
@@ -1798,8 +2056,16 @@ static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hp
 // training_batch over planned batches [first, first+n): per batch phase 1
 // (+ flush of the previous batch) and, for APR, phase 2; a final flush.
 // events != nullptr: timing mode, 2 events per launch, kinds[] per launch.
+// The APR graph of a one-wave-per-slot plan runs overlapped: clean(first),
+// then k_ovl = adv(t) + clean(t+1) for t < last, k_ovl = adv(last) alone, flush.
+static bool use_overlap(const acf_apr_ctx* c, const Kernels& K, const acf_apr_hparams* hp) {
+  return c->overlap && hp->adver && K.ovl && !K.lists && K.slots_per_wave == 1 && c->plan_kind2;
+}
+
+// kinds: 0 phase 1 / fused BPR, 1 phase 2, 2 flush, 3 k_ovl with both halves
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
-                    int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds) {
+                    int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds,
+                    int allow_overlap = 1) {
   Kernels K;
   ACF_RET(get_kernels(c, &K, c->fusion));
   const int S = 3 * c->B;
@@ -1816,6 +2082,30 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     ++li;
     return launch(fn, b, waves, s, e0, e1);
   };
+  if (allow_overlap && use_overlap(c, K, hp)) {
+    HIP_TRY(hipMemsetAsync(c->flags + (size_t)first * S, 0, (size_t)n * S * sizeof(int32_t), s));
+    auto args = [&](int32_t t, int pv) {
+      StepArgs a = make_args(c, tb, hp, t, pv);
+      a.use_single = fuse;
+      a.slot_waves = SW;
+      a.touch_next = 0;
+      a.prev2_valid = t - 2 >= first ? 1 : 0;
+      return a;
+    };
+    ACF_RET(L(K.clean_apr, args(first, 0), SW, 0));
+    for (int32_t t = first; t < first + n; ++t) {
+      const bool both = t + 1 < first + n;
+      StepArgs aa = args(t, t > first ? 1 : 0);
+      aa.ovl_flush = both ? 0 : 1;  // otherwise the clean half writes W(t-1) back
+      const StepArgs ac = both ? args(t + 1, 1) : aa;
+      hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
+      if (kinds) kinds[li] = both ? 3 : 1;
+      StepArgs xa = aa, xc = ac;
+      xa.diag_launch = xc.diag_launch = li;
+      ++li;
+      ACF_RET(launch_ovl(K.ovl, xa, xc, SW + TW, both ? SW : 0, s, e0, e1));
+    }
+  } else {
   for (int32_t t = first; t < first + n; ++t) {
     const int pv = t > first ? 1 : 0;
     StepArgs a = make_args(c, tb, hp, t, pv);
@@ -1828,6 +2118,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     } else {
       ACF_RET(L(K.clean_bpr, a, SW + TW, 0));
     }
+  }
   }
   StepArgs af = make_args(c, tb, hp, first + n - 1, 0);
   af.use_single = fuse;
@@ -1888,6 +2179,7 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   key.hp = *hp;
   key.first = first; key.n = n; key.B = c->B; key.d = c->d; key.mapping = c->mapping;
   key.fusion = c->fusion;
+  key.ovl = c->overlap;
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -1910,9 +2202,8 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   return ACF_OK;
 }
 
-extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
-                                    const acf_apr_hparams* hp, int32_t first, int32_t n,
-                                    double* ms_out, int32_t* launches_out, void* stream_) {
+static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp, int32_t first,
+                        int32_t n, double* ms_out, int32_t* launches_out, void* stream_, int nkinds) {
   ACF_CHECK(c && tb && hp && ms_out && launches_out, ACF_E_INVALID, "NULL argument");
   ACF_CHECK(n > 0 && first >= 0 && first + n <= c->nb, ACF_E_INVALID,
             "batch range [%d, %d) outside planned range [0, %d)", first, first + n, c->nb);
@@ -1922,11 +2213,11 @@ extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
   std::vector<hipEvent_t> ev((size_t)2 * nl, nullptr);
   std::vector<int> kinds(nl, -1);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
-  int r = run_loop(c, tb, hp, first, n, s, ev.data(), kinds.data());
+  int r = run_loop(c, tb, hp, first, n, s, ev.data(), kinds.data(), nkinds > 3);
   if (r == ACF_OK && hipStreamSynchronize(s) != hipSuccess) r = set_error(ACF_E_HIP, "sync failed");
-  for (int k = 0; k < 3; ++k) { ms_out[k] = 0.0; launches_out[k] = 0; }
+  for (int k = 0; k < nkinds; ++k) { ms_out[k] = 0.0; launches_out[k] = 0; }
   for (int x = 0; r == ACF_OK && x < nl; ++x) {
-    if (kinds[x] < 0) continue;
+    if (kinds[x] < 0 || kinds[x] >= nkinds) continue;
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, ev[2 * x], ev[2 * x + 1]) != hipSuccess) {
       r = set_error(ACF_E_HIP, "hipEventElapsedTime failed");
@@ -1940,6 +2231,21 @@ extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
   return r;
 }
 
+// v1: kinds clean / adv / flush, the two-kernel step (no k_ovl)
+extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
+                                    const acf_apr_hparams* hp, int32_t first, int32_t n,
+                                    double* ms_out, int32_t* launches_out, void* stream_) {
+  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 3);
+}
+
+// v2: kinds clean / adv / flush / overlapped (k_ovl = adv(t) + clean(t+1)), the
+// launch sequence acf_apr_train_planned runs
+extern "C" int acf_apr_time_kernels_v2(acf_apr_ctx* c, const acf_apr_tables* tb,
+                                       const acf_apr_hparams* hp, int32_t first, int32_t n,
+                                       double* ms_out, int32_t* launches_out, void* stream_) {
+  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 4);
+}
+
 extern "C" int acf_apr_set_slot_mapping(acf_apr_ctx* c, int32_t mode) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_CHECK(mode >= 0 && mode <= 2, ACF_E_INVALID, "slot mapping must be 0 (auto), 1 or 2, got %d", mode);
@@ -1951,6 +2257,22 @@ extern "C" int acf_apr_set_fusion(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "fusion must be 0 or 1, got %d", on);
   c->fusion = on;
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);
+  c->overlap = on;
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_step_errors(acf_apr_ctx* c, int32_t* out, void* stream_) {
+  ACF_CHECK(c && out, ACF_E_INVALID, "NULL argument");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemcpyAsync(out, c->err + 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemsetAsync(c->err + 1, 0, sizeof(int32_t), s));
+  HIP_TRY(hipStreamSynchronize(s));
   return ACF_OK;
 }
 

@@ -159,17 +159,31 @@ class APRContext:
 
     def time_kernels(self, tables, hp: StepHParams, first: int = 0, n: int | None = None):
         """Per-kernel-kind device time (ms) and launch counts over planned batches,
-        measured with start/stop events attached to each launch (tables are
-        trained exactly as by train_planned).  Kinds: clean (phase 1, or the fused
-        BPR step), adv (phase 2 + Adagrad), flush (end-of-call write-back)."""
+        measured with start/stop events attached to each launch of the sequence
+        train_planned runs (tables are trained exactly as by it).  Kinds: clean
+        (phase 1, or the fused BPR step), adv (phase 2 + Adagrad), flush
+        (end-of-call write-back), ovl (overlapped adv(t) + clean(t+1), k_ovl)."""
         n = self.n_batches - first if n is None else n
         tb, h = self._tables(*tables), hp.to_c()
-        ms = (ctypes.c_double * 3)()
-        cnt = (ctypes.c_int32 * 3)()
+        ms = (ctypes.c_double * 4)()
+        cnt = (ctypes.c_int32 * 4)()
         with torch.cuda.device(self.device):
-            call("acf_apr_time_kernels", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
+            call("acf_apr_time_kernels_v2", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
                  _stream_ptr(self.device))
-        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush"))}
+        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush", "ovl"))}
+
+    def set_step_overlap(self, on: bool) -> None:
+        """Overlapped APR steps (default on; identical results either way): the
+        adversarial pass of batch t and the clean pass of batch t+1 in one launch."""
+        call("acf_apr_set_step_overlap", self._ptr, int(bool(on)))
+
+    def step_errors(self) -> int:
+        """Read and clear the step error word (bit 0: an overlapped step gave up
+        waiting for a row)."""
+        out = ctypes.c_int32(0)
+        with torch.cuda.device(self.device):
+            call("acf_apr_step_errors", self._ptr, ctypes.byref(out), _stream_ptr(self.device))
+        return int(out.value)
 
     def losses(self):
         """Per-triplet (clean, adversarial) softplus terms of the last steps."""
@@ -218,6 +232,16 @@ class PlanPipeline:
     def set_fusion(self, on: bool) -> None:
         for c in self.ctx:
             c.set_fusion(on)
+
+    def set_step_overlap(self, on: bool) -> None:
+        for c in self.ctx:
+            c.set_step_overlap(on)
+
+    def step_errors(self) -> int:
+        e = 0
+        for c in self.ctx:
+            e |= c.step_errors()
+        return e
 
     def set_slot_mapping(self, mode) -> None:
         for c in self.ctx:

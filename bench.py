@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--time-batches", type=int, default=400, help="batches in the kernel-timing pass")
     p.add_argument("--large", action="store_true", help="also measure batch 65536 on 10M x 5M x d128")
     p.add_argument("--no-neumf", action="store_true", help="skip the adversarial-NeuMF line (configs[3])")
+    p.add_argument("--no-step-overlap", action="store_true",
+                   help="two kernels per APR step instead of the overlapped k_ovl (A/B)")
     p.add_argument("--mapping", default="auto", choices=["auto", "wave", "group"],
                    help="slot mapping of the step kernels (auto: by batch size)")
     return p.parse_args()
@@ -81,11 +83,11 @@ def bytes_per_launch(kind: int, d: int, B: int, st: dict) -> float:
       per triplet, reads of P[u], Q[i], Q[j] and their 3 Adagrad rows + 12 B of indices;
     clean (phase 1): P[u], Q[i], Q[j] + indices per triplet that is not fused;
     flush: read the scratch row + write the table row, per unique row (upper bound:
-      rows a fused triplet wrote in place are not flushed)."""
+      rows a fused triplet wrote in place are not flushed);
+    ovl (k_ovl = adv of batch t + clean of batch t+1 in one launch): adv + clean."""
     rows = st["unique_user_rows"] + st["unique_item_rows"]
-    return {0: (3 * d * 4 + 12) * (B - st["fused_triplets"]),
-            1: (6 * d * 4 + 12) * B,
-            2: 2 * d * 4 * rows}[kind]
+    clean, adv = (3 * d * 4 + 12) * (B - st["fused_triplets"]), (6 * d * 4 + 12) * B
+    return {0: clean, 1: adv, 2: 2 * d * 4 * rows, 3: adv + clean}[kind]
 
 
 def unique_rw_bytes(d: int, B: int, st: dict) -> float:
@@ -129,6 +131,8 @@ def step_kernel_name(kind: str, d: int, B: int) -> str:
             return f"k_clean_list<{lpr}, {nv}, false>"
         return "k_flush"
     team = 1 if lpr == 64 else 64 // lpr
+    if kind == "ovl":
+        return f"k_ovl<{lpr}, {nv}, {team}>"
     if kind == "adv":
         return f"k_adv<{lpr}, {nv}, {team}, true>"
     if kind == "clean":
@@ -154,14 +158,14 @@ def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb, st):
     s = slice(0, nb * B)
     ctx.plan(u[s], i[s], j[s], B, check=False)
     t = ctx.time_kernels(tabs, hp, 0, nb)
-    kinds = ["clean", "adv", "flush"]
+    kinds = ["clean", "adv", "flush", "ovl"]
     tot = {k: t[k][0] for k in kinds}
     dom = max(kinds, key=lambda k: tot[k])
     kid = kinds.index(dom)
     avg_ms = t[dom][0] / max(t[dom][1], 1)
     alg_bytes = bytes_per_launch(kid, d, B, st)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-    rw = unique_rw_bytes(d, B, st) / (avg_ms * 1e-3) / 1e9 if kid == 1 else None
+    rw = unique_rw_bytes(d, B, st) / (avg_ms * 1e-3) / 1e9 if kid in (1, 3) else None
     per_kernel_us = {k: round(1e3 * t[k][0] / max(t[k][1], 1), 3) for k in kinds if t[k][1]}
     name = step_kernel_name(dom, d, B)
     tr = pmc_traffic(name)
@@ -310,6 +314,7 @@ def main():
     # B = 512 steps are latency-bound: planning concurrently slows them
     pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False)
     pipe.set_slot_mapping(a.mapping)
+    pipe.set_step_overlap(not a.no_step_overlap)
     hp = ops.StepHParams(lr=0.05, eps=0.5, reg=0.0, reg_adv=1.0, adver=1)
     graph = not a.eager
     # warmup: W steps plus every chunk size the timed region uses on both contexts
@@ -333,8 +338,11 @@ def main():
         elapsed = float(t.item())
     value = world * a.steps * B / elapsed
     finite = bool(torch.isfinite(tabs[0]).all() and torch.isfinite(tabs[1]).all())
+    step_errors = pipe.step_errors()
     # roofline of the dominant kernel (separate eager pass with per-launch events)
     tctx = ops.APRContext(U1, I1, d, B, a.time_batches, dev)
+    tctx.set_slot_mapping(a.mapping)
+    tctx.set_step_overlap(not a.no_step_overlap)
     st = batch_stats(u, i, j, B, a.time_batches, U1, I1)
     roof = kernel_roofline(ops, tctx, tabs, hp, u, i, j, B, d, a.time_batches, st)
 
@@ -360,6 +368,8 @@ def main():
         "step_bandwidth": step_bandwidth(d, B, st, value / world),
         "batch_stats": {k: round(v, 1) for k, v in st.items()},
         "tables_finite": finite,
+        "step_errors": step_errors,
+        "step_overlap": not a.no_step_overlap,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(u, i, j, P0, Q0, B, a.cpu_batches)

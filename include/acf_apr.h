@@ -129,6 +129,15 @@ int acf_apr_time_kernels(acf_apr_ctx* ctx, const acf_apr_tables* tables,
                          int32_t n_batches, double* ms_out, int32_t* launches_out,
                          void* stream);
 
+/* As acf_apr_time_kernels, with the launch sequence acf_apr_train_planned
+ * really runs (see acf_apr_set_step_overlap): ms_out / launches_out hold 4 kinds,
+ * the fourth being the overlapped step kernel (adversarial pass of batch t +
+ * clean pass of batch t+1 in one launch).  Not part of the reference surface. */
+int acf_apr_time_kernels_v2(acf_apr_ctx* ctx, const acf_apr_tables* tables,
+                            const acf_apr_hparams* hp, int32_t first_batch,
+                            int32_t n_batches, double* ms_out, int32_t* launches_out,
+                            void* stream);
+
 /* How step kernels map unique rows ("slots") to lanes: 0 = auto (default: one
  * wavefront per slot below 4,096 triplets per batch, where hot rows have many
  * occurrences; one lane-group of dim/4 lanes per slot at and above it, where
@@ -144,6 +153,20 @@ int acf_apr_set_slot_mapping(acf_apr_ctx* ctx, int32_t mode);
  * kernels' own, so on and off give identical bits.  The split per-batch calls
  * (delta_update / optimizer_step) never fuse.  Not part of the reference surface. */
 int acf_apr_set_fusion(acf_apr_ctx* ctx, int32_t on);
+
+/* Overlapped APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
+ * environment ACF_STEP_OVERLAP=0 sets the default off).  For plans with one
+ * wavefront per slot, the adversarial pass of batch t and the clean pass of
+ * batch t+1 run in one launch: a t+1 row waits (bounded spin on a per-row flag)
+ * only for the rows batch t is still updating.  Arithmetic and order of every
+ * sum are unchanged, so on and off give identical bits.  Not part of the
+ * reference surface. */
+int acf_apr_set_step_overlap(acf_apr_ctx* ctx, int32_t on);
+
+/* Reads into *out and clears the step error word: bit 0 = an overlapped step
+ * gave up waiting for a row (results of that call are not trustworthy).
+ * Synchronous on `stream`.  Not part of the reference surface. */
+int acf_apr_step_errors(acf_apr_ctx* ctx, int32_t* out, void* stream);
 
 /* Per-triplet clean / adversarial losses computed by the last step of each
  * planned batch (softplus(-clip(x)) terms of APR.py:150,162), for the staged

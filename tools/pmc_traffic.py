@@ -39,6 +39,7 @@ def main(src, dst):
                     "dispatches (MI355X_MICROARCH.md: FETCH_SIZE counts half of 16-B/lane reads on gfx950)"}
     for k in sorted(fetch):
         if not (k.startswith("void k_adv") or k.startswith("void k_clean") or k.startswith("k_flush")
+                or k.startswith("void k_ovl")
                 or k.startswith("void k_nmf") or k.startswith("k_nmf")):
             continue
         f, w = statistics.median(fetch[k]), statistics.median(write.get(k, [0.0]))
