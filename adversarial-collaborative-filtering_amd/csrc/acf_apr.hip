@@ -969,6 +969,29 @@ struct Geo {
   }
 };
 
+// "random" delta: l2_normalize(truncated_normal(0, 0.01)) * eps, redrawn every
+// run (APR.py:180-191, adv == "random").  Out of line: the gradient mode never
+// runs it and it would otherwise bloat every step kernel's instruction stream.
+template <int LPR, int NV>
+__device__ __noinline__ RowV<NV> random_delta(uint64_t seed, int32_t t, int32_t d, float eps, int is_item,
+                                              int32_t row, int l) {
+  RowV<NV> z;
+  const uint64_t rk = mix64(seed ^ mix64(((uint64_t)t << 1) | (is_item ? 1 : 0))) ^
+                      mix64((uint64_t)row * 0x100000001B3ull);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = l + LPR * v;
+    float e4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      e4[e] = (c * 4 + e < d) ? trunc_normal(rk ^ mix64((uint64_t)(c * 4 + e)), 0.01f) : 0.f;
+    z.v[v] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+  }
+  const float ss = dot_row<LPR, NV>(z, z);
+  const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
+  return scale_row(scale_row(z, inv), eps);
+}
+
 // delta of one row from its batch-summed clean gradient G (APR.py:180-191)
 template <int LPR, int NV>
 __device__ __forceinline__ RowV<NV> make_delta(const StepArgs& a, const RowV<NV>& G, int is_item,
@@ -980,22 +1003,7 @@ __device__ __forceinline__ RowV<NV> make_delta(const StepArgs& a, const RowV<NV>
     const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
     return scale_row(scale_row(G, inv), a.eps);
   }
-  // "random": l2_normalize(truncated_normal(0, 0.01)) * eps, redrawn every run
-  RowV<NV> z;
-  const uint64_t rk = mix64(a.seed ^ mix64(((uint64_t)a.t << 1) | (is_item ? 1 : 0))) ^
-                      mix64((uint64_t)row * 0x100000001B3ull);
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int c = l + LPR * v;
-    float e4[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      e4[e] = (c * 4 + e < a.d) ? trunc_normal(rk ^ mix64((uint64_t)(c * 4 + e)), 0.01f) : 0.f;
-    z.v[v] = make_float4(e4[0], e4[1], e4[2], e4[3]);
-  }
-  const float ss = dot_row<LPR, NV>(z, z);
-  const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
-  return scale_row(scale_row(z, inv), a.eps);
+  return random_delta<LPR, NV>(a.seed, a.t, a.d, a.eps, is_item, row, l);
 }
 
 // A fused triplet (fuse_info): its whole step in one lane-group.  The operation
@@ -1771,6 +1779,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB; c->maxNB = maxNB; c->maxE = maxE;
   geometry(d, &c->lpr, &c->nv);
   c->R = std::min(128 / c->lpr, 8);  // 2 records per team member (see slot_header)
+  if (const char* e = getenv("ACF_INLINE_R")) c->R = std::max(1, std::min(c->R, atoi(e)));  // tuning
   if (const char* e = getenv("ACF_TOUCH_NEXT")) c->touch_next = atoi(e) != 0;
   if (const char* e = getenv("ACF_STEP_OVERLAP")) c->overlap = atoi(e) != 0;
   if (const char* e = getenv("ACF_OVL_DELAY")) c->ovl_delay = std::max(0, atoi(e));
