@@ -348,21 +348,30 @@ __global__ void k_compact(KT key, const int32_t* __restrict__ inc, const int32_t
 }
 
 // For every unique row of batch t: where its current value lives when batch t
-// starts.  Rows updated by batch t-1 are still in that batch's W scratch (the
-// flush to the table happens inside batch t's first kernel), so the plan encodes
-// src = ~(local slot in batch t-1) for them and src = row otherwise.  With
-// `kind2`, rows updated by batch t-2 but not t-1 get src = ~(local slot in
-// batch t-2 | ACF_SRC_KIND2): the overlapped step (k_ovl) reads them from
-// W(t-2) while W(t-1) is being flushed; every other kernel treats them as
-// "in the table" (pend1).
+// starts ("src").  src = row (>= 0) when no earlier batch of the plan touches
+// the row; otherwise src = ~((dt << kb) | k): the row was last updated dt >= 1
+// batches earlier, in that batch's local slot k (kb = slot bits of the plan).
+//  - the two-kernel step reads dt = 1 rows from W scratch of batch t-1 (the
+//    flush to the table happens inside batch t's first kernel) and every other
+//    row from the table (pend1);
+//  - the overlapped step (k_ovl) also reads dt = 2 rows from W(t-2), while
+//    W(t-1) is being flushed beside it;
+//  - the streamed step (k_stream) reads any dt from that batch's row version.
+// Plans with one lane-group per slot (packed) encode dt = 1 only (binary
+// search of batch t-1); one-wave-per-slot plans encode every dt (k_prev_next).
 // user local slot = g - ubs[t]; item local slot = nU(t) + g - ibs[t].
 // info[g] = {row, src, occurrence count | NEXT (batch t+1 touches the row too),
 //            CSR offset of the first occurrence}.
 #define ACF_INFO_NEXT (1 << 30)
-#define ACF_SRC_KIND2 (1 << 29)
 
-// src names W scratch of batch t-1 (not t-2, not the table)
-__device__ __forceinline__ bool pend1(int32_t src) { return src < 0 && !((~src) & ACF_SRC_KIND2); }
+__device__ __forceinline__ int32_t src_dt(int32_t src, int kb) {
+  return src < 0 ? (int32_t)((uint32_t)(~src) >> kb) : 0;
+}
+__device__ __forceinline__ int32_t src_slot(int32_t src, int kb) { return (~src) & ((1 << kb) - 1); }
+__device__ __forceinline__ int32_t make_src(int32_t dt, int32_t k, int kb) { return ~((dt << kb) | k); }
+
+// src names W scratch of batch t-1 (not an older batch, not the table)
+__device__ __forceinline__ bool pend1(int32_t src, int kb) { return src_dt(src, kb) == 1; }
 
 // local slot in batch tb of the row (binary search of tb's sorted unique rows), or -1
 __device__ __forceinline__ int find_local(const int32_t* __restrict__ uniq, const int32_t* __restrict__ ubs,
@@ -382,7 +391,7 @@ __device__ __forceinline__ int find_local(const int32_t* __restrict__ uniq, cons
 
 __global__ void k_slot_info(const int32_t* __restrict__ uniq, const int32_t* __restrict__ off,
                             const int32_t* __restrict__ ubs, const int32_t* __restrict__ bstart,
-                            int32_t n_uniq, int32_t nb, int32_t item_side, int32_t kind2,
+                            int32_t n_uniq, int32_t nb, int32_t item_side, int32_t kb,
                             int4* __restrict__ info) {
   int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (g >= n_uniq || g >= bstart[nb]) return;  // bstart[nb] = unique rows of the plan
@@ -397,12 +406,7 @@ __global__ void k_slot_info(const int32_t* __restrict__ uniq, const int32_t* __r
   int32_t s = row;
   if (t > 0) {
     const int local = find_local(uniq, ubs, bstart, t - 1, row, item_side);
-    if (local >= 0) {
-      s = ~local;
-    } else if (kind2 && t > 1) {
-      const int local2 = find_local(uniq, ubs, bstart, t - 2, row, item_side);
-      if (local2 >= 0) s = ~(local2 | ACF_SRC_KIND2);
-    }
+    if (local >= 0) s = make_src(1, local, kb);
   }
   int32_t in_next = 0;
   if (t + 1 < nb) {
@@ -415,6 +419,104 @@ __global__ void k_slot_info(const int32_t* __restrict__ uniq, const int32_t* __r
   }
   const int32_t o = off[g];
   info[g] = make_int4(row, s, (off[g + 1] - o) | (in_next ? ACF_INFO_NEXT : 0), o);
+}
+
+// One-wave-per-slot plans: the previous and next batch that touch each unique
+// row, at any distance, from one sort of the unique (side, row, batch) keys.
+// Entry x < E names user unique x, entry E + x item unique x; entries past a
+// side's unique count sort last (all-ones key).  The key layout:
+//   32-bit (VK32): side << (rb + tb) | row << tb | t, the entry as the value;
+//   64-bit: (side << (rb + tb) | row << tb | t) << 30 | entry.
+struct VKeys {
+  int32_t rb, tb, k32;
+  __device__ uint64_t key(int32_t side, int32_t row, int32_t t) const {
+    return ((uint64_t)side << (rb + tb)) | ((uint64_t)row << tb) | (uint64_t)t;
+  }
+};
+
+__device__ __forceinline__ int batch_of(const int32_t* __restrict__ bstart, int nb, int64_t g) {
+  int lo = 0, hi = nb;  // last t with bstart[t] <= g
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (bstart[mid] <= g) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void k_vkeys(const int32_t* __restrict__ uuniq, const int32_t* __restrict__ iuniq,
+                        const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs, int64_t E,
+                        int32_t nb, VKeys vk, void* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= 3 * E) return;
+  const int32_t side = x >= E ? 1 : 0;
+  const int64_t g = side ? x - E : x;
+  const int32_t* bs = side ? ibs : ubs;
+  const bool valid = g < bs[nb];
+  uint64_t k = ~0ull;
+  if (valid) k = vk.key(side, (side ? iuniq : uuniq)[g], batch_of(bs, nb, g));
+  if (vk.k32) {
+    static_cast<uint32_t*>(keys)[x] = valid ? (uint32_t)k : ~0u;
+    vals[x] = (int32_t)x;
+  } else {
+    static_cast<uint64_t*>(keys)[x] = valid ? (k << 30) | (uint64_t)x : ~0ull;
+  }
+}
+
+// Over the sorted keys: info[g] of each unique row (src from the previous batch
+// that touches it, NEXT when batch t+1 does) and nextt[t][slot] = the next batch
+// that touches it (0x7fffffff: none in the plan).
+__global__ void k_prev_next(const void* __restrict__ keys, const int32_t* __restrict__ vals, int64_t E,
+                            VKeys vk, const int32_t* __restrict__ uoff, const int32_t* __restrict__ ioff,
+                            const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs, int32_t S,
+                            int32_t kb, int4* __restrict__ uinfo, int4* __restrict__ iinfo,
+                            int32_t* __restrict__ nextt) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= 3 * E) return;
+  const uint64_t tmask = (1ull << vk.tb) - 1;
+  auto rd = [&](int64_t q, uint64_t& k, int64_t& x) {  // (side,row,t) key and entry at sorted q
+    if (vk.k32) {
+      const uint32_t v = static_cast<const uint32_t*>(keys)[q];
+      k = v == ~0u ? ~0ull : (uint64_t)v;
+      x = vals[q];
+    } else {
+      const uint64_t v = static_cast<const uint64_t*>(keys)[q];
+      k = v == ~0ull ? ~0ull : (v >> 30);
+      x = (int64_t)(v & ((1ull << 30) - 1));
+    }
+  };
+  uint64_t k;
+  int64_t x;
+  rd(p, k, x);
+  if (k == ~0ull) return;
+  const int32_t side = x >= E ? 1 : 0;
+  const int64_t g = side ? x - E : x;
+  const int32_t t = (int32_t)(k & tmask);
+  const uint64_t rowkey = k >> vk.tb;  // side | row
+  const int32_t row = (int32_t)(rowkey & ((1ull << vk.rb) - 1));
+  auto local = [&](int32_t s, int64_t gg, int32_t tt) -> int32_t {
+    return s ? (ubs[tt + 1] - ubs[tt]) + (int32_t)(gg - ibs[tt]) : (int32_t)(gg - ubs[tt]);
+  };
+  int32_t src = row;
+  if (p > 0) {
+    uint64_t kp;
+    int64_t xp;
+    rd(p - 1, kp, xp);
+    if (kp != ~0ull && (kp >> vk.tb) == rowkey) {
+      const int32_t tp = (int32_t)(kp & tmask);
+      src = make_src(t - tp, local(side, side ? xp - E : xp, tp), kb);
+    }
+  }
+  int32_t tn = 0x7fffffff;
+  if (p + 1 < 3 * E) {
+    uint64_t kn;
+    int64_t xn;
+    rd(p + 1, kn, xn);
+    if (kn != ~0ull && (kn >> vk.tb) == rowkey) tn = (int32_t)(kn & tmask);
+  }
+  const int32_t* off = side ? ioff : uoff;
+  const int32_t o = off[g];
+  (side ? iinfo : uinfo)[g] = make_int4(row, src, (off[g + 1] - o) | (tn == t + 1 ? ACF_INFO_NEXT : 0), o);
+  nextt[(int64_t)t * S + local(side, g, t)] = tn;
 }
 
 // Occurrence record: everything one lane-group needs to process one occurrence
@@ -454,12 +556,12 @@ struct FuseInfo {
 
 __device__ __forceinline__ int info_count(const int4& f) { return f.z & (ACF_INFO_NEXT - 1); }
 
-__device__ __forceinline__ FuseInfo fuse_info(const int4& U, const int4& I, const int4& J) {
+__device__ __forceinline__ FuseInfo fuse_info(const int4& U, const int4& I, const int4& J, int kb) {
   FuseInfo f;
   f.fused = info_count(U) == 1 && info_count(I) == 1 && info_count(J) == 1;
-  f.in_u = f.fused && !pend1(U.y) && !(U.z & ACF_INFO_NEXT);
-  f.in_i = f.fused && !pend1(I.y) && !(I.z & ACF_INFO_NEXT);
-  f.in_j = f.fused && !pend1(J.y) && !(J.z & ACF_INFO_NEXT);
+  f.in_u = f.fused && !pend1(U.y, kb) && !(U.z & ACF_INFO_NEXT);
+  f.in_i = f.fused && !pend1(I.y, kb) && !(I.z & ACF_INFO_NEXT);
+  f.in_j = f.fused && !pend1(J.y, kb) && !(J.z & ACF_INFO_NEXT);
   return f;
 }
 
@@ -491,7 +593,7 @@ __device__ __forceinline__ OccRec item_rec(const int4& own, const int4& oth, con
 // One thread per triplet: its user and two item occurrence records and, when
 // fused, its fused-triplet record.  The first R records of a slot go inline
 // only (that is the only place they are read from), later ones to the CSR.
-__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen,
+__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb,
                           const int4* __restrict__ tsl, const int4* __restrict__ tpos,
                           const int4* __restrict__ uinfo, const int4* __restrict__ iinfo,
                           const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
@@ -506,7 +608,7 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
   const int32_t t = (int32_t)(e / B);
   const int32_t nU = ubs[t + 1] - ubs[t];
   const int32_t k = sl.x - ubs[t], ki = nU + (sl.y - ibs[t]), kj = nU + (sl.z - ibs[t]);
-  const FuseInfo f = fuse_info(U, I, J);
+  const FuseInfo f = fuse_info(U, I, J, kb);
   OccRec r;
   r.own_row = U.x;
   r.own_src = U.y;
@@ -637,6 +739,7 @@ struct StepArgs {
   float* loss_adv;     // [E]
   const int32_t* gen_ptr;  // plan generation (device: graphs stay valid across plans)
   int32_t d, B, S, R, t;
+  int32_t kb;          // slot bits of the plan's src encoding
   int32_t prev_valid;  // 1: rows of batch t-1 are still pending in wnew_prev
   int32_t diag_launch; // diagnostic build: stamp slot of this launch
   int32_t use_single;  // fused triplets run in k_single waves; their slots are skipped
@@ -654,6 +757,15 @@ struct StepArgs {
   int32_t prev2_valid;  // 1: batch t-2 ran in this call (its W scratch is live)
   int32_t ovl_flush;    // adv half writes back W(t-1) (the launch has no clean half)
   int32_t ovl_delay;    // clean half: s_sleep(8) rounds before starting (ACF_OVL_DELAY, tuning)
+  // streamed step (k_stream): one launch runs batches [first, t_end); every row a
+  // batch updates becomes a VERSION at [batch][slot] (weights ver_w, Adagrad slot
+  // ver_a) and every delta too (ver_d), as tagged granules (tag = *epoch)
+  int32_t first, t_end;
+  unsigned long long* ver_w;
+  unsigned long long* ver_a;
+  unsigned long long* ver_d;
+  const uint32_t* epoch;
+  const int32_t* nextt;  // [nb][S] next batch touching the slot's row (flush)
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -689,8 +801,8 @@ __device__ __forceinline__ RecV load_rec(const OccRec* __restrict__ p) {
 // current value of a row at batch start: pending scratch or the table
 __device__ __forceinline__ const float* row_src(const StepArgs& a, const float* table, int32_t row,
                                                 int32_t src) {
-  return (pend1(src) && a.prev_valid) ? a.wnew_prev + (int64_t)(~src) * a.d
-                                      : table + (int64_t)row * a.d;
+  return (pend1(src, a.kb) && a.prev_valid) ? a.wnew_prev + (int64_t)src_slot(src, a.kb) * a.d
+                                            : table + (int64_t)row * a.d;
 }
 
 // --- overlapped step: sources, waits and publication ------------------------
@@ -702,15 +814,15 @@ __device__ __forceinline__ const float* row_src(const StepArgs& a, const float* 
 __device__ __forceinline__ const float* row_src_ovl(const StepArgs& a, const float* table, int32_t row,
                                                     int32_t src) {
   if (src < 0 && a.prev_valid) {
-    const int32_t v = ~src;
-    if (!(v & ACF_SRC_KIND2)) return a.wnew_prev + (int64_t)v * a.d;
-    if (a.prev2_valid) return a.wnew_prev2 + (int64_t)(v & ~ACF_SRC_KIND2) * a.d;
+    const int32_t dt = src_dt(src, a.kb);
+    if (dt == 1) return a.wnew_prev + (int64_t)src_slot(src, a.kb) * a.d;
+    if (dt == 2 && a.prev2_valid) return a.wnew_prev2 + (int64_t)src_slot(src, a.kb) * a.d;
   }
   return table + (int64_t)row * a.d;
 }
 
 __device__ __forceinline__ bool src_waits(const StepArgs& a, int32_t src) {
-  return a.prev_valid && pend1(src);
+  return a.prev_valid && pend1(src, a.kb);
 }
 
 
@@ -739,7 +851,7 @@ __device__ __forceinline__ void wait_srcs(const StepArgs& a, int32_t s0, int32_t
     int32_t v = 0;
 #pragma unroll
     for (int y = 0; y < 5; ++y) v = x == y ? src[y] : v;
-    mine[p] = src_waits(a, v) ? ~v : -1;  // flag index, or -1
+    mine[p] = src_waits(a, v) ? src_slot(v, a.kb) : -1;  // flag index, or -1
     need = need || mine[p] >= 0;
   }
   if (!__any(need)) return;
@@ -837,6 +949,13 @@ __device__ __forceinline__ RecV occ_rec(const StepArgs& a, const SlotRec& s, int
   if (idx == m && m < a.R && s.r0_valid) return s.r0;
   if (idx == m + TEAM && m + TEAM < a.R && s.r1_valid) return s.r1;
   return load_rec((s.h.is_item ? a.irec : a.urec) + s.h.ovf + idx);
+}
+
+// record of occurrence idx of slot k re-read from memory (inline or CSR): the
+// streamed step's hot-row passes, which keep no records in registers
+__device__ __forceinline__ RecV occ_rec_mem(const StepArgs& a, const SlotHdr& h, int k, int idx) {
+  if (idx < a.R) return load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R + idx);
+  return load_rec((h.is_item ? a.irec : a.urec) + h.ovf + idx);
 }
 
 // One occurrence's BPR term (APR.py:127-150) against the slot's own row (clean,
@@ -1334,6 +1453,378 @@ __global__ void __launch_bounds__(256) k_ovl(StepArgs aa, StepArgs ac, int32_t a
   STAMP(aa.diag_launch, q.wave, 4);
 }
 
+// ---------------------------------------------------------------------------
+// Streamed APR step (small batches, one wave per slot): ONE launch runs a whole
+// range of batches.  Nothing is written to the tables inside it: the Adagrad
+// result of row r in batch t becomes the version [t][slot] of r (weights in
+// ver_w, accumulator in ver_a), and a reader at batch t' > t finds it through
+// the plan's src (dt = t' - t at any distance, k_prev_next).  Versions are never
+// overwritten inside a launch, so there is no write-after-read hazard; a reader
+// only has to wait until the version exists.
+//
+// Hand-off (MI355X guide, Guideline 16 R2): a version row is a run of 8-B
+// granules {value, tag = epoch of this launch}, each written by a device-scope
+// write-through (sc1) store and read by sc1 loads; the reader re-reads the
+// granules whose tag is not yet this launch's until every one matches.  No flag,
+// no fence, no drain: the data is the flag.  The epoch is bumped by the flush
+// kernel after every launch, so a granule left by an earlier launch never
+// matches.
+//
+// Schedule: wave w takes position p = w % P of batches t = first + w / P,
+// + D, + 2D, ... (P = slot waves + fused-triplet waves of a batch, D = waves / P).
+// A position is one unique row (clean half -> delta -> adversarial half ->
+// Adagrad, all in the same wave, so G_clean and the own row stay in registers)
+// or a group of fused triplets.  No deadlock while every wave is resident (the
+// launcher checks occupancy): a clean half waits only for versions of earlier
+// batches; an adversarial half waits only for deltas of the same batch, which
+// clean halves produce before they wait for anything of that batch, and a wave
+// holds at most one position of any batch.  Every wait is bounded; a give-up
+// sets step_err bit 0 and makes every other waiting wave give up too.
+// ---------------------------------------------------------------------------
+typedef unsigned long long u64;
+
+__device__ __forceinline__ const u64* vrow(const u64* base, const StepArgs& a, int32_t t, int32_t k) {
+  return base + ((int64_t)t * a.S + k) * a.d;
+}
+
+// where the value of a row at the start of batch a.t lives, as ONE 64-bit word:
+// the table row's address, or a version row's address | 1 (a version of an
+// earlier batch of this launch)
+typedef uint64_t VSrc;
+
+__device__ __forceinline__ VSrc ver_src(const StepArgs& a, const float* table, const u64* vbase, int32_t row,
+                                        int32_t src) {
+  if (src < 0) {
+    const int32_t tp = a.t - src_dt(src, a.kb);
+    if (tp >= a.first) return (VSrc)(uintptr_t)vrow(vbase, a, tp, src_slot(src, a.kb)) | 1ull;
+  }
+  return (VSrc)(uintptr_t)(table + (int64_t)row * a.d);
+}
+
+__device__ __forceinline__ VSrc ver_at(const u64* p) { return (VSrc)(uintptr_t)p | 1ull; }
+
+// One attempt at a row: tables are read plainly (nothing writes them in this
+// launch); a version's granules with sc1 loads, ok once every tag is this
+// launch's.  A row already ok is not re-read.
+template <int LPR, int NV>
+__device__ __forceinline__ void try_row(VSrc s, int d, int l, uint32_t tag, RowV<NV>& r, bool& ok) {
+  if (ok) return;
+  if (!(s & 1ull)) {
+    r = load_at<LPR, NV>(reinterpret_cast<const float*>((uintptr_t)s), d, l);
+    ok = true;
+    return;
+  }
+  const u64* base = reinterpret_cast<const u64*>((uintptr_t)(s & ~1ull));
+  bool all = true;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = l + LPR * v;
+    if (c * 4 < d) {
+      const u64* g = base + c * 4;
+      u64 x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = __hip_atomic_load(g + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r.v[v] = make_float4(__uint_as_float((uint32_t)x[0]), __uint_as_float((uint32_t)x[1]),
+                           __uint_as_float((uint32_t)x[2]), __uint_as_float((uint32_t)x[3]));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) all = all && (uint32_t)(x[e] >> 32) == tag;
+    } else {
+      r.v[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  ok = all;
+}
+
+// a row as version granules: one aligned 8-B device-scope store per granule
+// (write-through, sc1).  Two granules per 16-B store tore under load (reads saw
+// a granule's tag before its value), so every granule is its own store.
+template <int LPR, int NV>
+__device__ __forceinline__ void store_ver(u64* dst, int d, int l, const RowV<NV>& r, uint32_t tag) {
+  const u64 hi = (u64)tag << 32;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = l + LPR * v;
+    if (c * 4 < d) {
+      u64* g = dst + c * 4;
+      __hip_atomic_store(g + 0, hi | __float_as_uint(r.v[v].x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 1, hi | __float_as_uint(r.v[v].y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 2, hi | __float_as_uint(r.v[v].z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 3, hi | __float_as_uint(r.v[v].w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// wave-uniform end of a wait round: true = stop (all there, or give up)
+__device__ __forceinline__ bool wait_round(const StepArgs& a, bool ok, int it) {
+  if (__all(ok)) return true;
+  if (it >= ACF_SPIN_LIMIT) {
+    if ((threadIdx.x & 63) == 0) atomicOr(a.step_err, 1);
+    return true;
+  }
+  if ((it & 31) == 31 &&
+      __any(__hip_atomic_load(a.step_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
+    return true;  // another wave gave up: the launch is failing, drain it
+  __builtin_amdgcn_s_sleep(2);
+  return false;
+}
+
+// Partner rows of the member's two occurrences of a pass (batch-start values)
+template <int LPR, int NV>
+__device__ __forceinline__ void stream_partners(const StepArgs& a, int is_item, const RecV& r0, const RecV& r1,
+                                                bool a0, bool a1, uint32_t tag, int l, RowV<NV>& ra0,
+                                                RowV<NV>& rb0, RowV<NV>& ra1, RowV<NV>& rb1) {
+  const float* ptab = is_item ? a.P : a.Q;
+  const VSrc sa0 = a0 ? ver_src(a, ptab, a.ver_w, r0.pa_row(), r0.pa_src()) : 0;
+  const VSrc sb0 = a0 ? ver_src(a, a.Q, a.ver_w, r0.pb_row(), r0.pb_src()) : 0;
+  const VSrc sa1 = a1 ? ver_src(a, ptab, a.ver_w, r1.pa_row(), r1.pa_src()) : 0;
+  const VSrc sb1 = a1 ? ver_src(a, a.Q, a.ver_w, r1.pb_row(), r1.pb_src()) : 0;
+  bool oa0 = !a0, ob0 = !a0, oa1 = !a1, ob1 = !a1;
+  for (int it = 0;; ++it) {
+    try_row<LPR, NV>(sa0, a.d, l, tag, ra0, oa0);
+    try_row<LPR, NV>(sb0, a.d, l, tag, rb0, ob0);
+    try_row<LPR, NV>(sa1, a.d, l, tag, ra1, oa1);
+    try_row<LPR, NV>(sb1, a.d, l, tag, rb1, ob1);
+    if (wait_round(a, oa0 && ob0 && oa1 && ob1, it)) break;
+  }
+}
+
+// Adversarial terms of one pass: partner rows (batch-start values) plus the
+// deltas their clean halves publish in this batch (wait for them).
+template <int LPR, int NV>
+__device__ __forceinline__ void stream_adv_pass(const StepArgs& a, int is_item, const RowV<NV>& ownp,
+                                                const RecV& r0, const RecV& r1, bool a0, bool a1,
+                                                RowV<NV> ra0, RowV<NV> rb0, RowV<NV> ra1, RowV<NV> rb1,
+                                                uint32_t tag, int l, RowV<NV>& GA) {
+  RowV<NV> da0 = zero_row<NV>(), db0 = da0, da1 = da0, db1 = da0;
+  const VSrc ta0 = a0 ? ver_at(vrow(a.ver_d, a, a.t, r0.pa_slot())) : 0;
+  const VSrc tb0 = a0 ? ver_at(vrow(a.ver_d, a, a.t, r0.pb_slot())) : 0;
+  const VSrc ta1 = a1 ? ver_at(vrow(a.ver_d, a, a.t, r1.pa_slot())) : 0;
+  const VSrc tb1 = a1 ? ver_at(vrow(a.ver_d, a, a.t, r1.pb_slot())) : 0;
+  bool pa0 = !a0, pb0 = !a0, pa1 = !a1, pb1 = !a1;
+  for (int it = 0;; ++it) {
+    try_row<LPR, NV>(ta0, a.d, l, tag, da0, pa0);
+    try_row<LPR, NV>(tb0, a.d, l, tag, db0, pb0);
+    try_row<LPR, NV>(ta1, a.d, l, tag, da1, pa1);
+    try_row<LPR, NV>(tb1, a.d, l, tag, db1, pb1);
+    if (wait_round(a, pa0 && pb0 && pa1 && pb1, it)) break;
+  }
+  ra0 = add_row(ra0, da0);
+  rb0 = add_row(rb0, db0);
+  ra1 = add_row(ra1, da1);
+  rb1 = add_row(rb1, db1);
+  occ_term<LPR, NV>(a, is_item, ownp, r0, ra0, rb0, a0, l, a.loss_adv, GA);
+  if (__any(a1)) occ_term<LPR, NV>(a, is_item, ownp, r1, ra1, rb1, a1, l, a.loss_adv, GA);
+}
+
+// One unique row of batch a.t: clean half (utils.py:117, APR.py:180-191), its
+// delta published as a version, then the adversarial half and Adagrad
+// (APR.py:130-165,193-195).  The operation sequence is clean_slot's followed by
+// adv_slot's, so the bits equal the two-kernel step's.  A slot of at most
+// 2 TEAM occurrences (one pass) keeps its partner rows for the adversarial half;
+// the Adagrad slot is fetched with the first gathers.
+template <int LPR, int NV, int TEAM>
+__device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int l, int leader, uint32_t tag) {
+  const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
+  const SlotHdr& h = sr.h;
+  if (h.count == 0) return;
+  const int d = a.d;
+  const VSrc own_s = ver_src(a, h.is_item ? a.Q : a.P, a.ver_w, h.own_row, h.own_src);
+  const VSrc acc_s = m == 0 ? ver_src(a, h.is_item ? a.accQ : a.accP, a.ver_a, h.own_row, h.own_src) : 0;
+  RowV<NV> own = zero_row<NV>(), acc = own, G = own;
+  RowV<NV> ra0 = own, rb0 = own, ra1 = own, rb1 = own;
+  RecV r0, r1;
+  bool a0 = false, a1 = false;
+  {  // first pass: own row, Adagrad slot, partners in one wait
+    a0 = m < h.count;
+    a1 = TEAM + m < h.count;
+    if (a0) r0 = occ_rec<TEAM>(a, sr, m, m);
+    if (a1) r1 = occ_rec<TEAM>(a, sr, TEAM + m, m);
+    const float* ptab = h.is_item ? a.P : a.Q;
+    const VSrc sa0 = a0 ? ver_src(a, ptab, a.ver_w, r0.pa_row(), r0.pa_src()) : 0;
+    const VSrc sb0 = a0 ? ver_src(a, a.Q, a.ver_w, r0.pb_row(), r0.pb_src()) : 0;
+    const VSrc sa1 = a1 ? ver_src(a, ptab, a.ver_w, r1.pa_row(), r1.pa_src()) : 0;
+    const VSrc sb1 = a1 ? ver_src(a, a.Q, a.ver_w, r1.pb_row(), r1.pb_src()) : 0;
+    bool oo = false, oc = m != 0, oa0 = !a0, ob0 = !a0, oa1 = !a1, ob1 = !a1;
+    for (int it = 0;; ++it) {
+      try_row<LPR, NV>(own_s, d, l, tag, own, oo);
+      try_row<LPR, NV>(acc_s, d, l, tag, acc, oc);
+      try_row<LPR, NV>(sa0, d, l, tag, ra0, oa0);
+      try_row<LPR, NV>(sb0, d, l, tag, rb0, ob0);
+      try_row<LPR, NV>(sa1, d, l, tag, ra1, oa1);
+      try_row<LPR, NV>(sb1, d, l, tag, rb1, ob1);
+      if (wait_round(a, oo && oc && oa0 && ob0 && oa1 && ob1, it)) break;
+    }
+    occ_term<LPR, NV>(a, h.is_item, own, r0, ra0, rb0, a0, l, a.loss_clean, G);
+    if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, own, r1, ra1, rb1, a1, l, a.loss_clean, G);
+  }
+  // the clean half's end: batch-summed gradient, delta, delta published
+  auto finish_clean = [&](RowV<NV>& Gc) -> RowV<NV> {
+    team_allreduce<LPR, TEAM, NV>(Gc);
+    const RowV<NV> dl = make_delta<LPR, NV>(a, Gc, h.is_item, h.own_row, l);
+    if (m == 0) store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_d, a, a.t, k)), d, l, dl, tag);
+    return add_row(own, dl);
+  };
+  RowV<NV> GA = zero_row<NV>();
+  if (h.count <= 2 * TEAM) {  // one pass (wave-uniform): partner rows kept for the adversarial half
+    const RowV<NV> ownp = finish_clean(G);
+    stream_adv_pass<LPR, NV>(a, h.is_item, ownp, r0, r1, a0, a1, ra0, rb0, ra1, rb1, tag, l, GA);
+  } else {  // hot rows: more passes, partner rows re-read (versions never change)
+    for (int base = 2 * TEAM; base < h.count; base += 2 * TEAM) {
+      const int i0 = base + m, i1 = base + TEAM + m;
+      const bool b0 = i0 < h.count, b1 = i1 < h.count;
+      RecV q0, q1;
+      if (b0) q0 = occ_rec_mem(a, h, k, i0);
+      if (b1) q1 = occ_rec_mem(a, h, k, i1);
+      RowV<NV> xa0 = zero_row<NV>(), xb0 = xa0, xa1 = xa0, xb1 = xa0;
+      stream_partners<LPR, NV>(a, h.is_item, q0, q1, b0, b1, tag, l, xa0, xb0, xa1, xb1);
+      occ_term<LPR, NV>(a, h.is_item, own, q0, xa0, xb0, b0, l, a.loss_clean, G);
+      if (__any(b1)) occ_term<LPR, NV>(a, h.is_item, own, q1, xa1, xb1, b1, l, a.loss_clean, G);
+    }
+    const RowV<NV> ownp = finish_clean(G);
+    for (int base = 0; base < h.count; base += 2 * TEAM) {
+      const int i0 = base + m, i1 = base + TEAM + m;
+      const bool b0 = i0 < h.count, b1 = i1 < h.count;
+      RecV q0, q1;
+      if (b0) q0 = occ_rec_mem(a, h, k, i0);
+      if (b1) q1 = occ_rec_mem(a, h, k, i1);
+      RowV<NV> xa0 = zero_row<NV>(), xb0 = xa0, xa1 = xa0, xb1 = xa0;
+      stream_partners<LPR, NV>(a, h.is_item, q0, q1, b0, b1, tag, l, xa0, xb0, xa1, xb1);
+      stream_adv_pass<LPR, NV>(a, h.is_item, ownp, q0, q1, b0, b1, xa0, xb0, xa1, xb1, tag, l, GA);
+    }
+  }
+  team_allreduce<LPR, TEAM, NV>(GA);
+  if (m == 0) {
+    axpy_row(G, a.reg_adv, GA);
+    RowV<NV> wout;
+    adagrad_row(a, G, own, acc, h.count, wout);
+    store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_w, a, a.t, k)), d, l, wout, tag);
+    store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_a, a, a.t, k)), d, l, acc, tag);
+  }
+}
+
+// A fused triplet of batch a.t (k_single's APR sequence): rows and Adagrad
+// slots from their versions or the tables, results as versions of its 3 slots.
+template <int LPR, int NV>
+__device__ __forceinline__ void stream_single(const StepArgs& a, int b, int l, uint32_t tag) {
+  const int64_t e = (int64_t)a.t * a.B + b;
+  RecV r;
+  r.a = r.b = r.c = make_int4(0, 0, 0, -1);
+  if (b < a.B) r = load_rec(a.trec + e);
+  const bool act = r.c.w == *a.gen_ptr && (r.c.y & 1);
+  const int d = a.d;
+  const int32_t u = r.a.x, i = r.a.y, j = r.a.z;
+  const VSrc su = act ? ver_src(a, a.P, a.ver_w, u, r.b.z) : 0;
+  const VSrc si = act ? ver_src(a, a.Q, a.ver_w, i, r.b.w) : 0;
+  const VSrc sj = act ? ver_src(a, a.Q, a.ver_w, j, r.c.x) : 0;
+  const VSrc cu_s = act ? ver_src(a, a.accP, a.ver_a, u, r.b.z) : 0;
+  const VSrc ci_s = act ? ver_src(a, a.accQ, a.ver_a, i, r.b.w) : 0;
+  const VSrc cj_s = act ? ver_src(a, a.accQ, a.ver_a, j, r.c.x) : 0;
+  RowV<NV> p = zero_row<NV>(), qi = p, qj = p, cu = p, ci = p, cj = p;
+  bool op = !act, oi = !act, oj = !act, ou = !act, oci = !act, ocj = !act;
+  for (int it = 0;; ++it) {
+    try_row<LPR, NV>(su, d, l, tag, p, op);
+    try_row<LPR, NV>(si, d, l, tag, qi, oi);
+    try_row<LPR, NV>(sj, d, l, tag, qj, oj);
+    try_row<LPR, NV>(cu_s, d, l, tag, cu, ou);
+    try_row<LPR, NV>(ci_s, d, l, tag, ci, oci);
+    try_row<LPR, NV>(cj_s, d, l, tag, cj, ocj);
+    if (wait_round(a, op && oi && oj && ou && oci && ocj, it)) break;
+  }
+  if (!act) return;
+  float g, loss;
+  bpr_term(dot_row<LPR, NV>(p, qi) - dot_row<LPR, NV>(p, qj), a.clip_lo, a.clip_hi, g, loss);
+  if (l == 0) a.loss_clean[e] = loss;
+  RowV<NV> Gu = zero_row<NV>(), Gi = zero_row<NV>(), Gj = zero_row<NV>();
+  axpy_row(Gu, g, qi);
+  axpy_row(Gu, -g, qj);
+  axpy_row(Gi, g, p);
+  axpy_row(Gj, -g, p);
+  const RowV<NV> pp = add_row(p, make_delta<LPR, NV>(a, Gu, 0, u, l));
+  const RowV<NV> qip = add_row(qi, make_delta<LPR, NV>(a, Gi, 1, i, l));
+  const RowV<NV> qjp = add_row(qj, make_delta<LPR, NV>(a, Gj, 1, j, l));
+  float ga, la;
+  bpr_term(dot_row<LPR, NV>(pp, qip) - dot_row<LPR, NV>(pp, qjp), a.clip_lo, a.clip_hi, ga, la);
+  if (l == 0) a.loss_adv[e] = la;
+  RowV<NV> Au = zero_row<NV>(), Ai = zero_row<NV>(), Aj = zero_row<NV>();
+  axpy_row(Au, ga, qip);
+  axpy_row(Au, -ga, qjp);
+  axpy_row(Ai, ga, pp);
+  axpy_row(Aj, -ga, pp);
+  axpy_row(Gu, a.reg_adv, Au);
+  axpy_row(Gi, a.reg_adv, Ai);
+  axpy_row(Gj, a.reg_adv, Aj);
+  RowV<NV> wu, wi, wj;
+  adagrad_row(a, Gu, p, cu, 1, wu);
+  adagrad_row(a, Gi, qi, ci, 1, wi);
+  adagrad_row(a, Gj, qj, cj, 1, wj);
+  store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_w, a, a.t, r.a.w)), d, l, wu, tag);
+  store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_w, a, a.t, r.b.x)), d, l, wi, tag);
+  store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_w, a, a.t, r.b.y)), d, l, wj, tag);
+  store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_a, a, a.t, r.a.w)), d, l, cu, tag);
+  store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_a, a, a.t, r.b.x)), d, l, ci, tag);
+  store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_a, a, a.t, r.b.y)), d, l, cj, tag);
+}
+
+// positions [0, slot_waves) are slots, the rest fused-triplet groups; `depth`
+// waves share a position, taking every depth-th batch
+template <int LPR, int NV, int TEAM>
+__global__ void __launch_bounds__(256, 4) k_stream(StepArgs a, int32_t positions) {
+  static_assert(TEAM * LPR == 64, "k_stream: one wave per slot");
+  const Geo<LPR, TEAM> q;
+  const int pos = q.wave % positions;
+  const int depth = (int)((gridDim.x * (int64_t)blockDim.x) >> 6) / positions;
+  const int phase = q.wave / positions;
+  if (phase >= depth) return;
+  const uint32_t tag = *a.epoch;
+  for (int32_t t = a.first + phase; t < a.t_end; t += depth) {
+    StepArgs b = a;
+    b.t = t;
+    if (pos < a.slot_waves)
+      stream_slot<LPR, NV, TEAM>(b, pos, q.m, q.l, q.leader, tag);
+    else
+      stream_single<LPR, NV>(b, (pos - a.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR, q.l, tag);
+  }
+}
+
+// After k_stream: the last version of every row the launch updated goes to the
+// tables (weights and Adagrad slot); then the epoch moves on.  One thread per
+// slot of the range finds the rows to write back, the wave copies them.
+__global__ void __launch_bounds__(256) k_stream_flush(StepArgs a, uint32_t* __restrict__ epoch) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)(a.t_end - a.first) * a.S;
+  const int lane = threadIdx.x & 63;
+  if (x == 0) atomicAdd(epoch, 1u);  // every k_stream wave has read it (kernel boundary)
+  bool need = false;
+  int32_t t = 0, k = 0;
+  if (x < n) {
+    t = a.first + (int32_t)(x / a.S);
+    k = (int32_t)(x - (int64_t)(t - a.first) * a.S);
+    need = a.nextt[(int64_t)t * a.S + k] >= a.t_end;
+  }
+  RecV r;
+  r.a = r.b = r.c = make_int4(0, 0, 0, -1);
+  if (need) {
+    r = load_rec(a.inl + ((int64_t)t * a.S + k) * a.R);
+    need = r.gen() == *a.gen_ptr && (r.meta() & ACF_COUNT_MASK) != 0;
+  }
+  uint64_t mask = __ballot(need);
+  while (mask) {
+    const int src_lane = __ffsll((long long)mask) - 1;
+    mask &= mask - 1;
+    const int32_t tt = __shfl(t, src_lane, 64), kk = __shfl(k, src_lane, 64);
+    const int32_t row = __shfl(r.own_row(), src_lane, 64);
+    const int item = (__shfl(r.meta(), src_lane, 64) & ACF_ITEM_BIT) != 0;
+    float* w = (item ? a.Q : a.P) + (int64_t)row * a.d;
+    float* c = (item ? a.accQ : a.accP) + (int64_t)row * a.d;
+    const u64* vw = vrow(a.ver_w, a, tt, kk);
+    const u64* va = vrow(a.ver_a, a, tt, kk);
+    for (int e = lane; e < a.d; e += 64) {
+      w[e] = __uint_as_float((uint32_t)vw[e]);
+      c[e] = __uint_as_float((uint32_t)va[e]);
+    }
+  }
+}
+
 // Large batches with fusion (one lane-group per slot): the slot work of batch t
 // is the plan's list of its NON-fused slots and the write-back the list of the
 // rows batch t-1 left in W scratch; a fixed set of slot waves strides over both
@@ -1675,9 +2166,18 @@ struct acf_apr_ctx {
   int32_t *slot_list = nullptr, *flush_list = nullptr, *slot_cnt = nullptr, *flush_cnt = nullptr;
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
   int32_t overlap = 1;  // k_ovl for APR runs of one-wave-per-slot plans (ACF_STEP_OVERLAP=0 disables)
-  int32_t plan_kind2 = 0;  // the plan encodes batch t-2 sources (k_slot_info kind2)
+  int32_t plan_kind2 = 0;  // the plan encodes sources at every distance (k_prev_next)
+  int32_t plan_kb = 1;     // slot bits of the plan's src encoding
+  int32_t* nextt = nullptr;  // [maxNB][S] next batch touching each slot's row (k_prev_next)
   int32_t ovl_delay = 0;   // ACF_OVL_DELAY (tuning only)
   int32_t* flags = nullptr;  // [maxNB][S] k_ovl publication flags
+  // streamed step (k_stream): row versions of every batch of a launch
+  int32_t stream = 1;        // ACF_STREAM=0 disables
+  int32_t stream_depth = 2;  // ACF_STREAM_DEPTH: waves per position (batches in flight)
+  int32_t stream_ok = -1;    // -1 unknown, 0 unavailable (allocation / occupancy), 1 ready
+  int64_t stream_max_waves = 0;
+  unsigned long long *ver_w = nullptr, *ver_a = nullptr, *ver_d = nullptr;
+  uint32_t* epoch = nullptr;
   hipStream_t cap_stream = nullptr;
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<void*> allocs;
@@ -1783,6 +2283,8 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (const char* e = getenv("ACF_TOUCH_NEXT")) c->touch_next = atoi(e) != 0;
   if (const char* e = getenv("ACF_STEP_OVERLAP")) c->overlap = atoi(e) != 0;
   if (const char* e = getenv("ACF_OVL_DELAY")) c->ovl_delay = std::max(0, atoi(e));
+  if (const char* e = getenv("ACF_STREAM")) c->stream = atoi(e) != 0;
+  if (const char* e = getenv("ACF_STREAM_DEPTH")) c->stream_depth = std::max(1, std::min(8, atoi(e)));
   const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
   auto A = [&](auto** p, size_t n) { if (r == ACF_OK) r = dalloc(c, p, n); };
@@ -1796,9 +2298,10 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->iinfo, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
-  A(&c->err, 4); A(&c->gen_dev, 4);
+  A(&c->err, 4); A(&c->gen_dev, 4); A(&c->epoch, 4);
   A(&c->g0, 2 * S * d); A(&c->delta, 2 * S * d);  // by batch parity (k_ovl: clean(t+1) beside adv(t))
   A(&c->flags, 3 * maxE);
+  A(&c->nextt, 3 * maxE);
   A(&c->wnew[0], S * d); A(&c->wnew[1], S * d);
   A(&c->loss_clean, maxE); A(&c->loss_adv, maxE);
   if (r != ACF_OK) { acf_apr_destroy(c); return r; }
@@ -1827,6 +2330,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (hipMemset(c->inl, 0, (size_t)maxNB * S * c->R * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->trec, 0, (size_t)maxE * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->gen_dev, 0, 16) != hipSuccess ||
+      hipMemset(c->epoch, 0, 16) != hipSuccess || hipMemset(c->nextt, 0, 3 * maxE * sizeof(int32_t)) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipMemset failed");
@@ -1899,14 +2403,44 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   // lane-group per slot (large batches) reads only a slot's first record inline
   // and never runs k_ovl, so only one-wave-per-slot plans encode t-2 sources
   const int packed = c->mapping == 2 || (c->mapping == 0 && B >= ACF_PACKED_MIN_BATCH);
-  const int kind2 = !packed && 3 * (int64_t)B < ACF_SRC_KIND2;
-  k_slot_info<<<grid_for(E), 256, 0, s>>>(c->uuniq, c->uoff, c->ubs, c->ubs, (int32_t)E, nb, 0, kind2,
-                                          c->uinfo);
-  k_slot_info<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, c->ioff, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
-                                              kind2, c->iinfo);
+  const int32_t kb = (int32_t)bits_for((uint64_t)3 * B + 1);
+  // one-wave-per-slot plans encode every earlier batch (dt < nb must fit the src)
+  const VKeys vk{(int32_t)bits_for((uint64_t)std::max(c->U1, c->I1)), (int32_t)bits_for((uint64_t)nb), 0};
+  const int all_dt = !packed && kb + bits_for((uint64_t)nb + 1) <= 31 && vk.rb + vk.tb <= 32;
+  if (all_dt) {
+    // slots k_prev_next does not name (no row) read as "next batch 0": never flushed
+    HIP_TRY(hipMemsetAsync(c->nextt, 0, (size_t)n3 * sizeof(int32_t), s));
+    VKeys v = vk;
+    v.k32 = 1 + vk.rb + vk.tb <= 31;
+    uint32_t* k32 = reinterpret_cast<uint32_t*>(c->key_in);
+    int32_t* v32 = reinterpret_cast<int32_t*>(k32 + n3);
+    uint32_t* o32 = reinterpret_cast<uint32_t*>(c->key_out);
+    int32_t* w32 = reinterpret_cast<int32_t*>(o32 + n3);
+    k_vkeys<<<grid_for(n3), 256, 0, s>>>(c->uuniq, c->iuniq, c->ubs, c->ibs, E, nb, v,
+                                         v.k32 ? (void*)k32 : (void*)c->key_in, v32);
+    HIP_TRY(hipGetLastError());
+    size_t tb3 = c->tmp_bytes;
+    const int bits = 1 + vk.rb + vk.tb;
+    if (v.k32) {
+      // padding keys are all ones: past every valid key in the sorted bits (ties keep input order)
+      HIP_TRY(rocprim::radix_sort_pairs(c->tmp, tb3, k32, o32, v32, w32, (size_t)n3, 0, bits, s));
+    } else {
+      HIP_TRY(rocprim::radix_sort_keys(c->tmp, tb3, c->key_in, c->key_out, (size_t)n3, 0, bits + 30, s));
+    }
+    k_prev_next<<<grid_for(n3), 256, 0, s>>>(v.k32 ? (const void*)o32 : (const void*)c->key_out, w32, E, v,
+                                             c->uoff, c->ioff, c->ubs, c->ibs, 3 * B, kb, c->uinfo, c->iinfo,
+                                             c->nextt);
+  } else {
+    k_slot_info<<<grid_for(E), 256, 0, s>>>(c->uuniq, c->uoff, c->ubs, c->ubs, (int32_t)E, nb, 0, kb,
+                                            c->uinfo);
+    k_slot_info<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, c->ioff, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
+                                                kb, c->iinfo);
+  }
+  HIP_TRY(hipGetLastError());
   c->plan_R = packed ? 1 : c->R;
-  c->plan_kind2 = kind2;
-  k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen,
+  c->plan_kind2 = all_dt;
+  c->plan_kb = kb;
+  k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen, kb,
                                         reinterpret_cast<const int4*>(c->tsl),
                                         reinterpret_cast<const int4*>(c->tpos), c->uinfo, c->iinfo,
                                         c->ubs, c->ibs, c->urec, c->irec, c->inl, c->trec, c->gen_dev);
@@ -1957,9 +2491,12 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.step_err = c->err + 1;
   a.loss_clean = c->loss_clean; a.loss_adv = c->loss_adv;
   a.gen_ptr = c->gen_dev;
-  a.d = c->d; a.B = c->B; a.S = 3 * c->B; a.R = c->plan_R; a.t = t;
+  a.d = c->d; a.B = c->B; a.S = 3 * c->B; a.R = c->plan_R; a.t = t; a.kb = c->plan_kb;
   a.prev_valid = prev_valid;
   a.diag_launch = 0;
+  a.first = 0; a.t_end = 0;
+  a.ver_w = c->ver_w; a.ver_a = c->ver_a; a.ver_d = c->ver_d;
+  a.epoch = c->epoch; a.nextt = c->nextt;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -1970,6 +2507,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
 struct Kernels {
   void *clean_apr = nullptr, *clean_bpr = nullptr, *adv = nullptr, *flush = nullptr;
   void* ovl = nullptr;  // k_ovl (one wave per slot only)
+  void* stream = nullptr;  // k_stream (one wave per slot, d <= 256)
   int slots_per_wave = 1;
   int lists = 0;  // list kernels: slot waves stride over the plan's per-batch lists
 };
@@ -2008,6 +2546,7 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists) {
   } else {
     kernel_ptrs_team<LPR, NV, OPW>(k, fused);
     k->ovl = reinterpret_cast<void*>(&k_ovl<LPR, NV, OPW>);
+    if constexpr (NV == 1) k->stream = reinterpret_cast<void*>(&k_stream<LPR, NV, OPW>);
     k->slots_per_wave = 1;
   }
   k->flush = reinterpret_cast<void*>(&k_flush);
@@ -2071,10 +2610,61 @@ static bool use_overlap(const acf_apr_ctx* c, const Kernels& K, const acf_apr_hp
   return c->overlap && hp->adver && K.ovl && !K.lists && K.slots_per_wave == 1 && c->plan_kind2;
 }
 
-// kinds: 0 phase 1 / fused BPR, 1 phase 2, 2 flush, 3 k_ovl with both halves
+// Streamed step: version buffers (allocated at first use: 3 x maxNB x S x d
+// granules) and the resident-wave budget of k_stream.
+static int stream_ready(acf_apr_ctx* c, const Kernels& K) {
+  if (c->stream_ok >= 0) return c->stream_ok;
+  c->stream_ok = 0;
+  if (!K.stream) return 0;
+  int dev = 0, cus = 0, blocks = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(K.stream), 256, 0) !=
+          hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  // MI355X guide (residency): 256-thread blocks admitted per CU = min(API, 8,
+  // 800 / (ceil(sgpr/16)*16 + 16)); k_stream's SGPR count (< 144) caps it at 5
+  c->stream_max_waves = (int64_t)std::max(0, std::min(blocks, 5)) * cus * 4;
+  const size_t n = (size_t)c->maxNB * 3 * c->maxB * c->d;
+  if (dalloc(c, &c->ver_w, n) != ACF_OK || dalloc(c, &c->ver_a, n) != ACF_OK ||
+      dalloc(c, &c->ver_d, n) != ACF_OK)
+    return 0;
+  // tag 0 never matches: the epoch starts at 1
+  const uint32_t one = 1;
+  if (hipMemset(c->ver_w, 0, n * 8) != hipSuccess || hipMemset(c->ver_a, 0, n * 8) != hipSuccess ||
+      hipMemset(c->ver_d, 0, n * 8) != hipSuccess ||
+      hipMemcpy(c->epoch, &one, sizeof(one), hipMemcpyHostToDevice) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  c->stream_ok = 1;
+  return 1;
+}
+
+static int stream_positions(const acf_apr_ctx* c, const Kernels& K, int fuse) {
+  const int TW = fuse ? (c->B + 64 / c->lpr - 1) / (64 / c->lpr) : 0;
+  return 3 * c->B + TW;
+}
+
+// (stream_ready allocates: call prepare_stream before any capture)
+static bool use_stream(acf_apr_ctx* c, const Kernels& K, const acf_apr_hparams* hp) {
+  if (!(c->stream && hp->adver && K.stream && !K.lists && K.slots_per_wave == 1 && c->plan_kind2)) return false;
+  if (c->stream_ok != 1) return false;
+  return stream_positions(c, K, c->fusion) <= c->stream_max_waves;
+}
+
+static void prepare_stream(acf_apr_ctx* c, const acf_apr_hparams* hp) {
+  Kernels K;
+  if (c->stream && hp->adver && c->stream_ok < 0 && get_kernels(c, &K, c->fusion) == ACF_OK) (void)stream_ready(c, K);
+}
+
+// kinds: 0 phase 1 / fused BPR, 1 phase 2, 2 flush, 3 k_ovl with both halves, 4 k_stream
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                     int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds,
-                    int allow_overlap = 1) {
+                    int allow_overlap = 2) {
   Kernels K;
   ACF_RET(get_kernels(c, &K, c->fusion));
   const int S = 3 * c->B;
@@ -2091,6 +2681,36 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     ++li;
     return launch(fn, b, waves, s, e0, e1);
   };
+  if (allow_overlap >= 2 && use_stream(c, K, hp)) {
+    const int P = stream_positions(c, K, fuse);
+    const int depth = (int)std::max<int64_t>(1, std::min<int64_t>(c->stream_depth, c->stream_max_waves / P));
+    StepArgs a = make_args(c, tb, hp, first, 0);
+    a.use_single = fuse;
+    a.slot_waves = S;
+    a.first = first;
+    a.t_end = first + n;
+    hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
+    if (kinds) kinds[li] = 4;
+    ++li;
+    typedef void (*SK)(StepArgs, int32_t);
+    const dim3 grid((unsigned)(((int64_t)P * depth + 3) / 4)), block(256);
+    if (e0)
+      hipExtLaunchKernelGGL(reinterpret_cast<SK>(K.stream), grid, block, 0, s, e0, e1, 0, a, (int32_t)P);
+    else
+      hipLaunchKernelGGL(reinterpret_cast<SK>(K.stream), grid, block, 0, s, a, (int32_t)P);
+    HIP_TRY(hipGetLastError());
+    e0 = events ? events[2 * li] : nullptr;
+    e1 = events ? events[2 * li + 1] : nullptr;
+    if (kinds) kinds[li] = 2;
+    ++li;
+    const dim3 fgrid(grid_for((int64_t)n * S));
+    if (e0)
+      hipExtLaunchKernelGGL(k_stream_flush, fgrid, block, 0, s, e0, e1, 0, a, c->epoch);
+    else
+      hipLaunchKernelGGL(k_stream_flush, fgrid, block, 0, s, a, c->epoch);
+    HIP_TRY(hipGetLastError());
+    return ACF_OK;
+  }
   if (allow_overlap && use_overlap(c, K, hp)) {
     HIP_TRY(hipMemsetAsync(c->flags + (size_t)first * S, 0, (size_t)n * S * sizeof(int32_t), s));
     auto args = [&](int32_t t, int pv) {
@@ -2181,6 +2801,7 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   ACF_RET(check_step(c, tb, hp, first));
   hipStream_t s = static_cast<hipStream_t>(stream_);
   c->last_delta_batch = -1;
+  prepare_stream(c, hp);
   if (!graph_mode) return run_loop(c, tb, hp, first, n, s, nullptr, nullptr);
   GraphKey key;
   memset(&key, 0, sizeof(key));
@@ -2188,7 +2809,7 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   key.hp = *hp;
   key.first = first; key.n = n; key.B = c->B; key.d = c->d; key.mapping = c->mapping;
   key.fusion = c->fusion;
-  key.ovl = c->overlap;
+  key.ovl = c->overlap | (c->stream << 1);
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -2218,11 +2839,12 @@ static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_
             "batch range [%d, %d) outside planned range [0, %d)", first, first + n, c->nb);
   ACF_RET(check_step(c, tb, hp, first));
   hipStream_t s = static_cast<hipStream_t>(stream_);
+  prepare_stream(c, hp);
   const int nl = 2 * n + 1;
   std::vector<hipEvent_t> ev((size_t)2 * nl, nullptr);
   std::vector<int> kinds(nl, -1);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
-  int r = run_loop(c, tb, hp, first, n, s, ev.data(), kinds.data(), nkinds > 3);
+  int r = run_loop(c, tb, hp, first, n, s, ev.data(), kinds.data(), nkinds > 4 ? 2 : (nkinds > 3 ? 1 : 0));
   if (r == ACF_OK && hipStreamSynchronize(s) != hipSuccess) r = set_error(ACF_E_HIP, "sync failed");
   for (int k = 0; k < nkinds; ++k) { ms_out[k] = 0.0; launches_out[k] = 0; }
   for (int x = 0; r == ACF_OK && x < nl; ++x) {
@@ -2267,6 +2889,20 @@ extern "C" int acf_apr_set_fusion(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "fusion must be 0 or 1, got %d", on);
   c->fusion = on;
   return ACF_OK;
+}
+
+extern "C" int acf_apr_set_stream(acf_apr_ctx* c, int32_t on) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  c->stream = on != 0;
+  return ACF_OK;
+}
+
+// v3: kinds clean / adv / flush / overlapped / streamed (k_stream), the launch
+// sequence acf_apr_train_planned runs
+extern "C" int acf_apr_time_kernels_v3(acf_apr_ctx* c, const acf_apr_tables* tb,
+                                       const acf_apr_hparams* hp, int32_t first, int32_t n,
+                                       double* ms_out, int32_t* launches_out, void* stream_) {
+  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 5);
 }
 
 extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {

@@ -162,15 +162,21 @@ class APRContext:
         measured with start/stop events attached to each launch of the sequence
         train_planned runs (tables are trained exactly as by it).  Kinds: clean
         (phase 1, or the fused BPR step), adv (phase 2 + Adagrad), flush
-        (end-of-call write-back), ovl (overlapped adv(t) + clean(t+1), k_ovl)."""
+        (end-of-call write-back), ovl (overlapped adv(t) + clean(t+1), k_ovl),
+        stream (the whole range in one launch, k_stream)."""
         n = self.n_batches - first if n is None else n
         tb, h = self._tables(*tables), hp.to_c()
-        ms = (ctypes.c_double * 4)()
-        cnt = (ctypes.c_int32 * 4)()
+        ms = (ctypes.c_double * 5)()
+        cnt = (ctypes.c_int32 * 5)()
         with torch.cuda.device(self.device):
-            call("acf_apr_time_kernels_v2", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
+            call("acf_apr_time_kernels_v3", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
                  _stream_ptr(self.device))
-        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush", "ovl"))}
+        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush", "ovl", "stream"))}
+
+    def set_stream(self, on: bool) -> None:
+        """Streamed APR steps (default on; identical results either way): one
+        launch runs the whole batch range through tagged row versions."""
+        call("acf_apr_set_stream", self._ptr, int(bool(on)))
 
     def set_step_overlap(self, on: bool) -> None:
         """Overlapped APR steps (default on; identical results either way): the
@@ -236,6 +242,10 @@ class PlanPipeline:
     def set_step_overlap(self, on: bool) -> None:
         for c in self.ctx:
             c.set_step_overlap(on)
+
+    def set_stream(self, on: bool) -> None:
+        for c in self.ctx:
+            c.set_stream(on)
 
     def step_errors(self) -> int:
         e = 0

@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--no-neumf", action="store_true", help="skip the adversarial-NeuMF line (configs[3])")
     p.add_argument("--no-step-overlap", action="store_true",
                    help="two kernels per APR step instead of the overlapped k_ovl (A/B)")
+    p.add_argument("--no-stream", action="store_true",
+                   help="per-batch launches (k_ovl) instead of the streamed step k_stream (A/B)")
     p.add_argument("--mapping", default="auto", choices=["auto", "wave", "group"],
                    help="slot mapping of the step kernels (auto: by batch size)")
     return p.parse_args()
@@ -77,17 +79,19 @@ def batch_stats(u, i, j, B, nb, U1, I1):
             "fused_triplets": float(fused.sum()) / nb}
 
 
-def bytes_per_launch(kind: int, d: int, B: int, st: dict) -> float:
+def bytes_per_launch(kind: int, d: int, B: int, st: dict, nb: int = 1) -> float:
     """Algorithmic HBM bytes of one launch, fp32 rows of 4d bytes.
     adv (phase 2 + fused triplets + Adagrad) uses SURVEY.md §8(d)'s official figure:
       per triplet, reads of P[u], Q[i], Q[j] and their 3 Adagrad rows + 12 B of indices;
     clean (phase 1): P[u], Q[i], Q[j] + indices per triplet that is not fused;
     flush: read the scratch row + write the table row, per unique row (upper bound:
       rows a fused triplet wrote in place are not flushed);
-    ovl (k_ovl = adv of batch t + clean of batch t+1 in one launch): adv + clean."""
+    ovl (k_ovl = adv of batch t + clean of batch t+1 in one launch): adv + clean;
+    stream (k_stream = the whole APR step of all nb batches of a call in one launch):
+      the official figure per triplet x every triplet of the launch."""
     rows = st["unique_user_rows"] + st["unique_item_rows"]
     clean, adv = (3 * d * 4 + 12) * (B - st["fused_triplets"]), (6 * d * 4 + 12) * B
-    return {0: clean, 1: adv, 2: 2 * d * 4 * rows, 3: adv + clean}[kind]
+    return {0: clean, 1: adv, 2: 2 * d * 4 * rows, 3: adv + clean, 4: adv * nb}[kind]
 
 
 def unique_rw_bytes(d: int, B: int, st: dict) -> float:
@@ -131,6 +135,10 @@ def step_kernel_name(kind: str, d: int, B: int) -> str:
             return f"k_clean_list<{lpr}, {nv}, false>"
         return "k_flush"
     team = 1 if lpr == 64 else 64 // lpr
+    if kind == "stream":
+        return f"k_stream<{lpr}, {nv}, {team}>"
+    if kind == "stream_flush":
+        return "k_stream_flush"
     if kind == "ovl":
         return f"k_ovl<{lpr}, {nv}, {team}>"
     if kind == "adv":
@@ -158,22 +166,29 @@ def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb, st):
     s = slice(0, nb * B)
     ctx.plan(u[s], i[s], j[s], B, check=False)
     t = ctx.time_kernels(tabs, hp, 0, nb)
-    kinds = ["clean", "adv", "flush", "ovl"]
+    kinds = ["clean", "adv", "flush", "ovl", "stream"]
     tot = {k: t[k][0] for k in kinds}
     dom = max(kinds, key=lambda k: tot[k])
     kid = kinds.index(dom)
     avg_ms = t[dom][0] / max(t[dom][1], 1)
-    alg_bytes = bytes_per_launch(kid, d, B, st)
+    alg_bytes = bytes_per_launch(kid, d, B, st, nb)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
-    rw = unique_rw_bytes(d, B, st) / (avg_ms * 1e-3) / 1e9 if kid in (1, 3) else None
+    rw = None
+    if kid in (1, 3):
+        rw = unique_rw_bytes(d, B, st) / (avg_ms * 1e-3) / 1e9
+    elif kid == 4:
+        rw = unique_rw_bytes(d, B, st) * nb / (avg_ms * 1e-3) / 1e9
     per_kernel_us = {k: round(1e3 * t[k][0] / max(t[k][1], 1), 3) for k in kinds if t[k][1]}
     name = step_kernel_name(dom, d, B)
+    if t["stream"][1]:
+        per_kernel_us["stream_per_batch"] = round(1e3 * t["stream"][0] / t["stream"][1] / nb, 3)
     tr = pmc_traffic(name)
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": None if tr is None else tr[0],
             "traffic_source": None if tr is None else tr[1],
             "bytes_per_launch": int(alg_bytes), "avg_launch_us": round(avg_ms * 1e3, 3),
+            "batches_per_launch": nb if kid == 4 else 1,
             "per_kernel_avg_us": per_kernel_us,
             "achieved_unique_rw_GBs": None if rw is None else round(rw, 2)}
 
@@ -315,6 +330,7 @@ def main():
     pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False)
     pipe.set_slot_mapping(a.mapping)
     pipe.set_step_overlap(not a.no_step_overlap)
+    pipe.set_stream(not a.no_stream)
     hp = ops.StepHParams(lr=0.05, eps=0.5, reg=0.0, reg_adv=1.0, adver=1)
     graph = not a.eager
     # warmup: W steps plus every chunk size the timed region uses on both contexts
@@ -343,6 +359,7 @@ def main():
     tctx = ops.APRContext(U1, I1, d, B, a.time_batches, dev)
     tctx.set_slot_mapping(a.mapping)
     tctx.set_step_overlap(not a.no_step_overlap)
+    tctx.set_stream(not a.no_stream)
     st = batch_stats(u, i, j, B, a.time_batches, U1, I1)
     roof = kernel_roofline(ops, tctx, tabs, hp, u, i, j, B, d, a.time_batches, st)
 
@@ -370,6 +387,7 @@ def main():
         "tables_finite": finite,
         "step_errors": step_errors,
         "step_overlap": not a.no_step_overlap,
+        "step_stream": roof["kernel"].startswith("k_stream"),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(u, i, j, P0, Q0, B, a.cpu_batches)

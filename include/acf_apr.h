@@ -138,6 +138,14 @@ int acf_apr_time_kernels_v2(acf_apr_ctx* ctx, const acf_apr_tables* tables,
                             int32_t n_batches, double* ms_out, int32_t* launches_out,
                             void* stream);
 
+/* As acf_apr_time_kernels_v2 with a fifth kind, the streamed step kernel
+ * (see acf_apr_set_stream); its write-back kernel counts as kind 2.  Not part
+ * of the reference surface. */
+int acf_apr_time_kernels_v3(acf_apr_ctx* ctx, const acf_apr_tables* tables,
+                            const acf_apr_hparams* hp, int32_t first_batch,
+                            int32_t n_batches, double* ms_out, int32_t* launches_out,
+                            void* stream);
+
 /* How step kernels map unique rows ("slots") to lanes: 0 = auto (default: one
  * wavefront per slot below 4,096 triplets per batch, where hot rows have many
  * occurrences; one lane-group of dim/4 lanes per slot at and above it, where
@@ -162,6 +170,17 @@ int acf_apr_set_fusion(acf_apr_ctx* ctx, int32_t on);
  * sum are unchanged, so on and off give identical bits.  Not part of the
  * reference surface. */
 int acf_apr_set_step_overlap(acf_apr_ctx* ctx, int32_t on);
+
+/* Streamed APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
+ * environment ACF_STREAM=0 sets the default off).  For plans with one wavefront
+ * per slot and dim <= 256, ONE launch runs the whole batch range: every row a
+ * batch updates becomes a tagged version that later batches read (bounded spin
+ * until it exists), and one write-back kernel moves the last versions to the
+ * tables.  Arithmetic and order of every sum are unchanged, so on and off give
+ * identical bits.  Uses 3 x max_batches x 3 x max_batch_size x dim x 8 bytes of
+ * device memory, allocated at first use (off when that fails, or when the
+ * device cannot keep the launch resident).  Not part of the reference surface. */
+int acf_apr_set_stream(acf_apr_ctx* ctx, int32_t on);
 
 /* Reads into *out and clears the step error word: bit 0 = an overlapped step
  * gave up waiting for a row (results of that call are not trustworthy).

@@ -499,9 +499,10 @@ def _overlap_stream(shape, acf, dev, B, nb, seed):
 @pytest.mark.parametrize("fuse", [False, True])
 def test_step_overlap_bit_identical(ops, acf, dev, d, shape, fuse):
     """Overlapped APR steps (k_ovl: adv(t) + clean(t+1) in one launch, clean
-    rows waiting on adv(t)'s flags) vs two kernels per step: identical bits for
-    tables, accumulators and both losses, over one call (graph and eager) and
-    over piecewise calls; no wait gave up."""
+    rows waiting on adv(t)'s flags) and streamed steps (k_stream: the whole range
+    in one launch through tagged row versions) vs two kernels per step:
+    identical bits for tables, accumulators and both losses, over one call
+    (graph and eager) and over piecewise calls; no wait gave up."""
     if shape == "ml1m" and d not in (32, 64):
         pytest.skip("ml1m shape at the headline dims only")
     B, nb = {"hot": (64, 12), "sparse": (256, 8), "ml1m": (512, 24)}[shape]
@@ -514,9 +515,13 @@ def test_step_overlap_bit_identical(ops, acf, dev, d, shape, fuse):
     ctx.set_fusion(fuse)
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     runs = []
-    for ovl, pieces, graph in ((False, [(0, nb)], True), (True, [(0, nb)], True), (True, [(0, nb)], False),
-                               (True, [(0, 1), (1, 2), (3, 4), (7, nb - 7)], True)):
+    split = [(0, 1), (1, 2), (3, 4), (7, nb - 7)]
+    for ovl, stream, pieces, graph in ((False, False, [(0, nb)], True), (True, False, [(0, nb)], True),
+                                       (True, False, [(0, nb)], False), (True, False, split, True),
+                                       (False, True, [(0, nb)], True), (False, True, [(0, nb)], False),
+                                       (False, True, split, True), (False, True, split, False)):
         ctx.set_step_overlap(ovl)
+        ctx.set_stream(stream)
         tabs = _gpu_tables(P, Q, dev)
         for first, n in pieces:
             ctx.train_planned(tabs, hp, first, n, graph=graph)
@@ -540,10 +545,34 @@ def test_step_overlap_kernel_timing_kinds(ops, dev):
     Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
     hp = ops.StepHParams(adver=1)
     ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_stream(False)
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ta, tb = _gpu_tables(P, Q, dev), _gpu_tables(P, Q, dev)
     t = ctx.time_kernels(ta, hp)
-    assert {k: v[1] for k, v in t.items()} == {"clean": 1, "ovl": nb - 1, "adv": 1, "flush": 1}
+    assert {k: v[1] for k, v in t.items()} == {"clean": 1, "ovl": nb - 1, "adv": 1, "flush": 1, "stream": 0}
     ctx.train_planned(tb, hp)
     for x, y in zip(ta, tb):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("d", [16, 64, 256])
+def test_stream_kernel_timing_kinds(ops, dev, d):
+    """With streamed steps on, train_planned runs ONE k_stream launch plus its
+    write-back for the whole range (time_kernels reports exactly that), and the
+    result equals training."""
+    U1, I1, B, nb = 300, 200, 128, 9
+    u, i, j = _sparse_stream(5, U1, I1, B, nb, hot=16, p_hot=0.3)
+    rng = np.random.default_rng(1)
+    P = (rng.standard_normal((U1, d)) * 0.2).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
+    hp = ops.StepHParams(adver=1)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_stream(True)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ta, tb = _gpu_tables(P, Q, dev), _gpu_tables(P, Q, dev)
+    t = ctx.time_kernels(ta, hp)
+    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "ovl": 0, "adv": 0, "flush": 1, "stream": 1}
+    ctx.train_planned(tb, hp)
+    for x, y in zip(ta, tb):
+        assert torch.equal(x, y)
+    assert ctx.step_errors() == 0
