@@ -1511,6 +1511,12 @@ __global__ void __launch_bounds__(256) k_ovl(StepArgs aa, StepArgs ac, int32_t a
 // kernel after every launch, so a granule left by an earlier launch never
 // matches.
 //
+// Granule order inside a version row is component-major: element 4c + e sits at
+// granule e*(d/4) + c, so each of a lane's four 8-B accesses is one contiguous
+// run across the row-group's lanes (the element-major order put the lanes 32 B
+// apart: every store instruction wrote each 128-B line of the row partially,
+// and WRITE_SIZE read 4x the version bytes; tools/calib_fetch.hip).
+//
 // Schedule: wave w takes position p = w % P of batches t = first + w / P,
 // + D, + 2D, ... (P = slot waves + fused-triplet waves of a batch, D = waves / P).
 // A position is one unique row (clean half -> delta -> adversarial half ->
@@ -1556,15 +1562,17 @@ __device__ __forceinline__ void try_row(VSrc s, int d, int l, uint32_t tag, RowV
     return;
   }
   const u64* base = reinterpret_cast<const u64*>((uintptr_t)(s & ~1ull));
+  const int d4 = d >> 2;
   bool all = true;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int c = l + LPR * v;
     if (c * 4 < d) {
-      const u64* g = base + c * 4;
+      const u64* g = base + c;  // component-major granules
       u64 x[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = __hip_atomic_load(g + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int e = 0; e < 4; ++e)
+        x[e] = __hip_atomic_load(g + e * d4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       r.v[v] = make_float4(__uint_as_float((uint32_t)x[0]), __uint_as_float((uint32_t)x[1]),
                            __uint_as_float((uint32_t)x[2]), __uint_as_float((uint32_t)x[3]));
 #pragma unroll
@@ -1583,15 +1591,16 @@ __device__ __forceinline__ void try_row(VSrc s, int d, int l, uint32_t tag, RowV
 template <int LPR, int NV>
 __device__ __forceinline__ void store_ver(u64* dst, int d, int l, const RowV<NV>& r, uint32_t tag) {
   const u64 hi = (u64)tag << 32;
+  const int d4 = d >> 2;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int c = l + LPR * v;
     if (c * 4 < d) {
-      u64* g = dst + c * 4;
-      __hip_atomic_store(g + 0, hi | __float_as_uint(r.v[v].x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g + 1, hi | __float_as_uint(r.v[v].y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g + 2, hi | __float_as_uint(r.v[v].z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g + 3, hi | __float_as_uint(r.v[v].w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      u64* g = dst + c;  // component-major granules
+      __hip_atomic_store(g, hi | __float_as_uint(r.v[v].x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + d4, hi | __float_as_uint(r.v[v].y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 2 * d4, hi | __float_as_uint(r.v[v].z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 3 * d4, hi | __float_as_uint(r.v[v].w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1896,9 +1905,11 @@ __global__ void __launch_bounds__(256) k_stream_flush(StepArgs a, uint32_t* __re
     float* c = (item ? a.accQ : a.accP) + (int64_t)row * a.d;
     const u64* vw = vrow(a.ver_w, a, tt, kk);
     const u64* va = vrow(a.ver_a, a, tt, kk);
-    for (int e = lane; e < a.d; e += 64) {
-      w[e] = __uint_as_float((uint32_t)vw[e]);
-      c[e] = __uint_as_float((uint32_t)va[e]);
+    const int d4 = a.d >> 2;
+    for (int e = lane; e < a.d; e += 64) {  // granule e holds element 4(e % d4) + e / d4
+      const int x = 4 * (e % d4) + e / d4;
+      w[x] = __uint_as_float((uint32_t)vw[e]);
+      c[x] = __uint_as_float((uint32_t)va[e]);
     }
   }
 }

@@ -148,15 +148,19 @@ def step_kernel_name(kind: str, d: int, B: int) -> str:
     return "k_flush"
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, batches: int = 1):
     """HBM bytes per launch from the newest profiles/rNN/pmc_traffic.json (rocprofv3
-    FETCH_SIZE / WRITE_SIZE passes of this bench, tools/profile_bench.sh), or None."""
+    FETCH_SIZE / WRITE_SIZE passes of this bench, tools/profile_bench.sh), or None.
+    A k_stream record is per batch (its profiled launches span 647 batches):
+    scaled to this launch's `batches`."""
     root = os.path.join(REPO, "profiles")
     for r in sorted(os.listdir(root) if os.path.isdir(root) else [], reverse=True):
         f = os.path.join(root, r, "pmc_traffic.json")
         if os.path.isfile(f):
             with open(f) as fh:
                 rec = json.load(fh).get(kernel)
+            if rec and "traffic_bytes_per_batch" in rec:
+                return int(rec["traffic_bytes_per_batch"] * batches), f"{r}/pmc_traffic.json (per batch x {batches})"
             if rec:
                 return rec["traffic_bytes_per_launch"], f"{r}/pmc_traffic.json"
     return None
@@ -182,7 +186,7 @@ def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb, st):
     name = step_kernel_name(dom, d, B)
     if t["stream"][1]:
         per_kernel_us["stream_per_batch"] = round(1e3 * t["stream"][0] / t["stream"][1] / nb, 3)
-    tr = pmc_traffic(name)
+    tr = pmc_traffic(name, nb if kid == 4 else 1)
     return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": None if tr is None else tr[0],
