@@ -538,10 +538,15 @@ struct __align__(16) OccRec {
   int32_t pb_row;   // user slot: item j;  item slot: the other item of the triplet
   int32_t pa_src;
   int32_t pb_src;
-  int32_t pa_slot;  // local slot of pa in batch t (for its delta)
+  int32_t pa_slot;  // local slot of pa in batch t (for its delta) | SOLO_BIT if pa occurs once
   int32_t pb_slot;
   int32_t gen;
 };
+// A partner row that occurs once in the batch ("solo"): its batch-summed clean
+// gradient is this occurrence's own term, so a reader can form its delta itself
+// (k_stream, solo_delta) instead of waiting for the partner's wave to publish it.
+#define ACF_SOLO_BIT (1 << 30)
+#define ACF_SLOT_MASK (ACF_SOLO_BIT - 1)
 #define ACF_ITEM_BIT (1 << 28)
 #define ACF_SINGLE_BIT (1 << 29)   // the slot's only occurrence is a fused triplet
 #define ACF_INPLACE_BIT (1 << 30)  // the fused triplet writes this row to the table itself
@@ -587,8 +592,8 @@ __device__ __forceinline__ OccRec item_rec(const int4& own, const int4& oth, con
   r.pb_row = oth.x;
   r.pa_src = U.y;
   r.pb_src = oth.y;
-  r.pa_slot = ku;
-  r.pb_slot = k_oth;
+  r.pa_slot = ku | (info_count(U) == 1 ? ACF_SOLO_BIT : 0);
+  r.pb_slot = k_oth | (info_count(oth) == 1 ? ACF_SOLO_BIT : 0);
   r.gen = gen;
   return r;
 }
@@ -622,8 +627,8 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
   r.pb_row = J.x;
   r.pa_src = I.y;
   r.pb_src = J.y;
-  r.pa_slot = ki;
-  r.pb_slot = kj;
+  r.pa_slot = ki | (info_count(I) == 1 ? ACF_SOLO_BIT : 0);
+  r.pb_slot = kj | (info_count(J) == 1 ? ACF_SOLO_BIT : 0);
   r.gen = gen;
   const int64_t base = (int64_t)t * S;
   int32_t rr = ps.x - U.w;
@@ -825,8 +830,10 @@ struct RecV {
   __device__ int pb_row() const { return b.z; }
   __device__ int pa_src() const { return b.w; }
   __device__ int pb_src() const { return c.x; }
-  __device__ int pa_slot() const { return c.y; }
-  __device__ int pb_slot() const { return c.z; }
+  __device__ int pa_slot() const { return c.y & ACF_SLOT_MASK; }
+  __device__ int pb_slot() const { return c.z & ACF_SLOT_MASK; }
+  __device__ bool pa_solo() const { return (c.y & ACF_SOLO_BIT) != 0; }
+  __device__ bool pb_solo() const { return (c.z & ACF_SOLO_BIT) != 0; }
   __device__ int gen() const { return c.w; }
 };
 
@@ -1639,19 +1646,72 @@ __device__ __forceinline__ void stream_partners(const StepArgs& a, int is_item, 
   }
 }
 
-// Adversarial terms of one pass: partner rows (batch-start values) plus the
-// deltas their clean halves publish in this batch (wait for them).
-template <int LPR, int NV>
-__device__ __forceinline__ void stream_adv_pass(const StepArgs& a, int is_item, const RowV<NV>& ownp,
-                                                const RecV& r0, const RecV& r1, bool a0, bool a1,
-                                                RowV<NV> ra0, RowV<NV> rb0, RowV<NV> ra1, RowV<NV> rb1,
-                                                uint32_t tag, int l, RowV<NV>& GA) {
+// Delta of a SOLO partner (pb = 0: pa, 1: pb) of one occurrence, formed here
+// with the operation sequence the partner's own wave runs for a one-occurrence
+// row: its clean term from zero (occ_term), the team reduction's additions of
+// +0 (team_allreduce: member 0 holds the only term), then make_delta.  Same bits
+// as the published delta.  own / ra / rb are batch-start rows.
+template <int LPR, int NV, int TEAM>
+__device__ __forceinline__ RowV<NV> solo_delta(const StepArgs& a, int is_item, const RowV<NV>& own,
+                                               const RecV& r, const RowV<NV>& ra, const RowV<NV>& rb, int pb,
+                                               int l) {
+  float gb, loss;
+  RowV<NV> G = zero_row<NV>();
+  int p_item;
+  if (!is_item) {  // own = p_u, ra = q_i, rb = q_j: partner item i (pos) or j (neg)
+    bpr_term(dot_row<LPR, NV>(own, ra) - dot_row<LPR, NV>(own, rb), a.clip_lo, a.clip_hi, gb, loss);
+    axpy_row(G, pb ? -gb : gb, own);
+    p_item = 1;
+  } else {  // own = this item, ra = p_u, rb = the other item
+    const float dq = dot_row<LPR, NV>(ra, own), dqo = dot_row<LPR, NV>(ra, rb);
+    const int role = r.e_role() & 1;
+    bpr_term(role ? (dqo - dq) : (dq - dqo), a.clip_lo, a.clip_hi, gb, loss);
+    if (!pb) {  // the user: q_pos, q_neg terms in the user slot's order
+      axpy_row(G, gb, role ? rb : own);
+      axpy_row(G, -gb, role ? own : rb);
+      p_item = 0;
+    } else {  // the other item, in the opposite role
+      axpy_row(G, role ? gb : -gb, ra);
+      p_item = 1;
+    }
+  }
+#pragma unroll
+  for (int s = 1; s < TEAM; s <<= 1) G = add_row(G, zero_row<NV>());
+  return make_delta<LPR, NV>(a, G, p_item, pb ? r.pb_row() : r.pa_row(), l);
+}
+
+// Adversarial terms of one pass: partner rows (batch-start values) plus their
+// deltas: formed here for a solo partner, otherwise the one its clean half
+// publishes in this batch (wait for it).
+template <int LPR, int NV, int TEAM>
+__device__ __forceinline__ void stream_adv_pass(const StepArgs& a, int is_item, const RowV<NV>& own,
+                                                const RowV<NV>& ownp, const RecV& r0, const RecV& r1, bool a0,
+                                                bool a1, RowV<NV> ra0, RowV<NV> rb0, RowV<NV> ra1,
+                                                RowV<NV> rb1, uint32_t tag, int l, RowV<NV>& GA) {
   RowV<NV> da0 = zero_row<NV>(), db0 = da0, da1 = da0, db1 = da0;
-  const VSrc ta0 = a0 ? ver_at(vrow(a.ver_d, a, a.t, r0.pa_slot())) : 0;
-  const VSrc tb0 = a0 ? ver_at(vrow(a.ver_d, a, a.t, r0.pb_slot())) : 0;
-  const VSrc ta1 = a1 ? ver_at(vrow(a.ver_d, a, a.t, r1.pa_slot())) : 0;
-  const VSrc tb1 = a1 ? ver_at(vrow(a.ver_d, a, a.t, r1.pb_slot())) : 0;
-  bool pa0 = !a0, pb0 = !a0, pa1 = !a1, pb1 = !a1;
+  const bool sa0 = a0 && r0.pa_solo(), sb0 = a0 && r0.pb_solo();
+  const bool sa1 = a1 && r1.pa_solo(), sb1 = a1 && r1.pb_solo();
+  const VSrc ta0 = a0 && !sa0 ? ver_at(vrow(a.ver_d, a, a.t, r0.pa_slot())) : 0;
+  const VSrc tb0 = a0 && !sb0 ? ver_at(vrow(a.ver_d, a, a.t, r0.pb_slot())) : 0;
+  const VSrc ta1 = a1 && !sa1 ? ver_at(vrow(a.ver_d, a, a.t, r1.pa_slot())) : 0;
+  const VSrc tb1 = a1 && !sb1 ? ver_at(vrow(a.ver_d, a, a.t, r1.pb_slot())) : 0;
+  bool pa0 = !ta0, pb0 = !tb0, pa1 = !ta1, pb1 = !tb1;
+  if (__any(sa0)) {
+    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r0, ra0, rb0, 0, l);
+    if (sa0) da0 = x;
+  }
+  if (__any(sb0)) {
+    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r0, ra0, rb0, 1, l);
+    if (sb0) db0 = x;
+  }
+  if (__any(sa1)) {
+    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r1, ra1, rb1, 0, l);
+    if (sa1) da1 = x;
+  }
+  if (__any(sb1)) {
+    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r1, ra1, rb1, 1, l);
+    if (sb1) db1 = x;
+  }
   for (int it = 0;; ++it) {
     try_row<LPR, NV>(ta0, a.d, l, tag, da0, pa0);
     try_row<LPR, NV>(tb0, a.d, l, tag, db0, pb0);
@@ -1715,14 +1775,15 @@ __device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int
   auto finish_clean = [&](RowV<NV>& Gc) -> RowV<NV> {
     team_allreduce<LPR, TEAM, NV>(Gc);
     const RowV<NV> dl = make_delta<LPR, NV>(a, Gc, h.is_item, h.own_row, l);
-    if (m == 0) store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_d, a, a.t, k)), d, l, dl, tag);
+    // a one-occurrence row's delta is never read: its readers form it (solo_delta)
+    if (m == 0 && h.count > 1) store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_d, a, a.t, k)), d, l, dl, tag);
     STAMP(a.t, k, 3);
     return add_row(own, dl);
   };
   RowV<NV> GA = zero_row<NV>();
   if (h.count <= 2 * TEAM) {  // one pass (wave-uniform): partner rows kept for the adversarial half
     const RowV<NV> ownp = finish_clean(G);
-    stream_adv_pass<LPR, NV>(a, h.is_item, ownp, r0, r1, a0, a1, ra0, rb0, ra1, rb1, tag, l, GA);
+    stream_adv_pass<LPR, NV, TEAM>(a, h.is_item, own, ownp, r0, r1, a0, a1, ra0, rb0, ra1, rb1, tag, l, GA);
   } else {  // hot rows: more passes, partner rows re-read (versions never change)
     for (int base = 2 * TEAM; base < h.count; base += 2 * TEAM) {
       const int i0 = base + m, i1 = base + TEAM + m;
@@ -1744,7 +1805,7 @@ __device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int
       if (b1) q1 = occ_rec_mem(a, h, k, i1);
       RowV<NV> xa0 = zero_row<NV>(), xb0 = xa0, xa1 = xa0, xb1 = xa0;
       stream_partners<LPR, NV>(a, h.is_item, q0, q1, b0, b1, tag, l, xa0, xb0, xa1, xb1);
-      stream_adv_pass<LPR, NV>(a, h.is_item, ownp, q0, q1, b0, b1, xa0, xb0, xa1, xb1, tag, l, GA);
+      stream_adv_pass<LPR, NV, TEAM>(a, h.is_item, own, ownp, q0, q1, b0, b1, xa0, xb0, xa1, xb1, tag, l, GA);
     }
   }
   STAMP(a.t, k, 4);
