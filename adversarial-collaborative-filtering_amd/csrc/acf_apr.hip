@@ -812,6 +812,7 @@ struct StepArgs {
   const int32_t* task_list;  // [nb][task_stride] a batch's tasks (slot, or S + fused group); null: positions
   const int32_t* task_cnt;   // [nb]
   int32_t task_stride, max_depth;
+  int32_t poll_sleep;  // k_stream: s_sleep between polls of a version (0-3)
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -1622,7 +1623,12 @@ __device__ __forceinline__ bool wait_round(const StepArgs& a, bool ok, int it) {
   if ((it & 31) == 31 &&
       __any(__hip_atomic_load(a.step_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
     return true;  // another wave gave up: the launch is failing, drain it
-  __builtin_amdgcn_s_sleep(2);
+  switch (a.poll_sleep) {  // s_sleep takes an immediate
+    case 0: break;
+    case 1: __builtin_amdgcn_s_sleep(1); break;
+    case 3: __builtin_amdgcn_s_sleep(3); break;
+    default: __builtin_amdgcn_s_sleep(2); break;
+  }
   return false;
 }
 
@@ -2324,6 +2330,7 @@ struct acf_apr_ctx {
   // streamed step (k_stream): row versions of every batch of a launch
   int32_t stream = 1;        // ACF_STREAM=0 disables
   int32_t stream_depth = 2;  // ACF_STREAM_DEPTH: max waves per position (batches in flight)
+  int32_t poll_sleep = 2;    // ACF_POLL_SLEEP: s_sleep argument between version polls (0-3)
   int32_t stream_ok = -1;    // -1 unknown, 0 unavailable (allocation / occupancy), 1 ready
   int64_t stream_max_waves = 0;
   unsigned long long *ver_w = nullptr, *ver_a = nullptr, *ver_d = nullptr;
@@ -2437,6 +2444,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (const char* e = getenv("ACF_OVL_DELAY")) c->ovl_delay = std::max(0, atoi(e));
   if (const char* e = getenv("ACF_STREAM")) c->stream = atoi(e) != 0;
   if (const char* e = getenv("ACF_STREAM_DEPTH")) c->stream_depth = std::max(1, std::min(8, atoi(e)));
+  if (const char* e = getenv("ACF_POLL_SLEEP")) c->poll_sleep = std::max(0, std::min(3, atoi(e)));
   const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
   auto A = [&](auto** p, size_t n) { if (r == ACF_OK) r = dalloc(c, p, n); };
@@ -2665,6 +2673,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.ver_w = c->ver_w; a.ver_a = c->ver_a; a.ver_d = c->ver_d;
   a.epoch = c->epoch; a.nextt = c->nextt;
   a.task_list = nullptr; a.task_cnt = c->task_cnt; a.task_stride = 0; a.max_depth = 1;
+  a.poll_sleep = c->poll_sleep;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -2864,6 +2873,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     a.task_list = lists ? c->task_list : nullptr;
     a.task_stride = c->task_stride;
     a.max_depth = c->stream_depth;
+    a.poll_sleep = c->poll_sleep;
     hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
     if (kinds) kinds[li] = 4;
     ++li;
