@@ -1558,40 +1558,6 @@ __device__ __forceinline__ VSrc ver_src(const StepArgs& a, const float* table, c
 
 __device__ __forceinline__ VSrc ver_at(const u64* p) { return (VSrc)(uintptr_t)p | 1ull; }
 
-// One attempt at a row: tables are read plainly (nothing writes them in this
-// launch); a version's granules with sc1 loads, ok once every tag is this
-// launch's.  A row already ok is not re-read.
-template <int LPR, int NV>
-__device__ __forceinline__ void try_row(VSrc s, int d, int l, uint32_t tag, RowV<NV>& r, bool& ok) {
-  if (ok) return;
-  if (!(s & 1ull)) {
-    r = load_at<LPR, NV>(reinterpret_cast<const float*>((uintptr_t)s), d, l);
-    ok = true;
-    return;
-  }
-  const u64* base = reinterpret_cast<const u64*>((uintptr_t)(s & ~1ull));
-  const int d4 = d >> 2;
-  bool all = true;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int c = l + LPR * v;
-    if (c * 4 < d) {
-      const u64* g = base + c;  // component-major granules
-      u64 x[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        x[e] = __hip_atomic_load(g + e * d4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      r.v[v] = make_float4(__uint_as_float((uint32_t)x[0]), __uint_as_float((uint32_t)x[1]),
-                           __uint_as_float((uint32_t)x[2]), __uint_as_float((uint32_t)x[3]));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) all = all && (uint32_t)(x[e] >> 32) == tag;
-    } else {
-      r.v[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-  ok = all;
-}
-
 // a row as version granules: one aligned 8-B device-scope store per granule
 // (write-through, sc1), the guide's R2 form.  (A first version stored two
 // granules per inline-asm 16-B store without the trailing s_nop the guide
@@ -1632,6 +1598,82 @@ __device__ __forceinline__ bool wait_round(const StepArgs& a, bool ok, int it) {
   return false;
 }
 
+// Batched attempt over K rows: every row's loads are issued first and the tags
+// checked after, so one attempt costs one round trip however many rows wait
+// (a per-row load-then-compare made the compiler drain vmcnt between rows:
+// six serial round trips in the first wait of a slot).  Version granules are
+// read through global-address-space pointers (global_load, not flat_load,
+// which would also count in lgkmcnt).
+typedef const __attribute__((address_space(1))) u64* gu64_ptr;
+
+template <int NV>
+struct RawRow {
+  u64 x[NV][4];
+};
+
+template <int LPR, int NV>
+__device__ __forceinline__ void issue_row(VSrc s, int d, int l, bool ok, RawRow<NV>& w, RowV<NV>& r) {
+  if (ok) return;
+  if (!(s & 1ull)) {  // table row: nothing writes it in this launch
+    r = load_at<LPR, NV>(reinterpret_cast<const float*>((uintptr_t)s), d, l);
+    return;
+  }
+  const u64* base = reinterpret_cast<const u64*>((uintptr_t)(s & ~1ull));
+  const int d4 = d >> 2;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = l + LPR * v;
+    if (c * 4 < d) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        w.x[v][e] = __hip_atomic_load((gu64_ptr)(base + c + e * d4), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int LPR, int NV>
+__device__ __forceinline__ void check_row(VSrc s, int d, int l, uint32_t tag, const RawRow<NV>& w, RowV<NV>& r,
+                                          bool& ok) {
+  if (ok) return;
+  if (!(s & 1ull)) {
+    ok = true;
+    return;
+  }
+  bool all = true;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = l + LPR * v;
+    if (c * 4 < d) {
+      r.v[v] = make_float4(__uint_as_float((uint32_t)w.x[v][0]), __uint_as_float((uint32_t)w.x[v][1]),
+                           __uint_as_float((uint32_t)w.x[v][2]), __uint_as_float((uint32_t)w.x[v][3]));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) all = all && (uint32_t)(w.x[v][e] >> 32) == tag;
+    } else {
+      r.v[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  ok = all;
+}
+
+// Wait until every listed row is there (ok[k] true on entry: not needed).
+template <int LPR, int NV, int K>
+__device__ __forceinline__ void poll_rows(const StepArgs& a, const VSrc (&s)[K], RowV<NV>* const (&r)[K],
+                                          bool (&ok)[K], uint32_t tag, int l) {
+  for (int it = 0;; ++it) {
+    RawRow<NV> w[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) issue_row<LPR, NV>(s[k], a.d, l, ok[k], w[k], *r[k]);
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      check_row<LPR, NV>(s[k], a.d, l, tag, w[k], *r[k], ok[k]);
+      all = all && ok[k];
+    }
+    if (wait_round(a, all, it)) break;
+  }
+}
+
 // Partner rows of the member's two occurrences of a pass (batch-start values)
 template <int LPR, int NV>
 __device__ __forceinline__ void stream_partners(const StepArgs& a, int is_item, const RecV& r0, const RecV& r1,
@@ -1642,14 +1684,10 @@ __device__ __forceinline__ void stream_partners(const StepArgs& a, int is_item, 
   const VSrc sb0 = a0 ? ver_src(a, a.Q, a.ver_w, r0.pb_row(), r0.pb_src()) : 0;
   const VSrc sa1 = a1 ? ver_src(a, ptab, a.ver_w, r1.pa_row(), r1.pa_src()) : 0;
   const VSrc sb1 = a1 ? ver_src(a, a.Q, a.ver_w, r1.pb_row(), r1.pb_src()) : 0;
-  bool oa0 = !a0, ob0 = !a0, oa1 = !a1, ob1 = !a1;
-  for (int it = 0;; ++it) {
-    try_row<LPR, NV>(sa0, a.d, l, tag, ra0, oa0);
-    try_row<LPR, NV>(sb0, a.d, l, tag, rb0, ob0);
-    try_row<LPR, NV>(sa1, a.d, l, tag, ra1, oa1);
-    try_row<LPR, NV>(sb1, a.d, l, tag, rb1, ob1);
-    if (wait_round(a, oa0 && ob0 && oa1 && ob1, it)) break;
-  }
+  const VSrc src[4] = {sa0, sb0, sa1, sb1};
+  RowV<NV>* const dst[4] = {&ra0, &rb0, &ra1, &rb1};
+  bool ok[4] = {!a0, !a0, !a1, !a1};
+  poll_rows<LPR, NV, 4>(a, src, dst, ok, tag, l);
 }
 
 // Delta of a SOLO partner (pb = 0: pa, 1: pb) of one occurrence, formed here
@@ -1718,12 +1756,11 @@ __device__ __forceinline__ void stream_adv_pass(const StepArgs& a, int is_item, 
     const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r1, ra1, rb1, 1, l);
     if (sb1) db1 = x;
   }
-  for (int it = 0;; ++it) {
-    try_row<LPR, NV>(ta0, a.d, l, tag, da0, pa0);
-    try_row<LPR, NV>(tb0, a.d, l, tag, db0, pb0);
-    try_row<LPR, NV>(ta1, a.d, l, tag, da1, pa1);
-    try_row<LPR, NV>(tb1, a.d, l, tag, db1, pb1);
-    if (wait_round(a, pa0 && pb0 && pa1 && pb1, it)) break;
+  {
+    const VSrc src[4] = {ta0, tb0, ta1, tb1};
+    RowV<NV>* const dst[4] = {&da0, &db0, &da1, &db1};
+    bool ok[4] = {pa0, pb0, pa1, pb1};
+    poll_rows<LPR, NV, 4>(a, src, dst, ok, tag, l);
   }
   ra0 = add_row(ra0, da0);
   rb0 = add_row(rb0, db0);
@@ -1763,15 +1800,11 @@ __device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int
     const VSrc sb0 = a0 ? ver_src(a, a.Q, a.ver_w, r0.pb_row(), r0.pb_src()) : 0;
     const VSrc sa1 = a1 ? ver_src(a, ptab, a.ver_w, r1.pa_row(), r1.pa_src()) : 0;
     const VSrc sb1 = a1 ? ver_src(a, a.Q, a.ver_w, r1.pb_row(), r1.pb_src()) : 0;
-    bool oo = false, oc = m != 0, oa0 = !a0, ob0 = !a0, oa1 = !a1, ob1 = !a1;
-    for (int it = 0;; ++it) {
-      try_row<LPR, NV>(own_s, d, l, tag, own, oo);
-      try_row<LPR, NV>(acc_s, d, l, tag, acc, oc);
-      try_row<LPR, NV>(sa0, d, l, tag, ra0, oa0);
-      try_row<LPR, NV>(sb0, d, l, tag, rb0, ob0);
-      try_row<LPR, NV>(sa1, d, l, tag, ra1, oa1);
-      try_row<LPR, NV>(sb1, d, l, tag, rb1, ob1);
-      if (wait_round(a, oo && oc && oa0 && ob0 && oa1 && ob1, it)) break;
+    {
+      const VSrc src[6] = {own_s, acc_s, sa0, sb0, sa1, sb1};
+      RowV<NV>* const dst[6] = {&own, &acc, &ra0, &rb0, &ra1, &rb1};
+      bool ok[6] = {false, m != 0, !a0, !a0, !a1, !a1};
+      poll_rows<LPR, NV, 6>(a, src, dst, ok, tag, l);
     }
     STAMP(a.t, k, 2);
     occ_term<LPR, NV>(a, h.is_item, own, r0, ra0, rb0, a0, l, a.loss_clean, G);
@@ -1844,15 +1877,11 @@ __device__ __forceinline__ void stream_single(const StepArgs& a, int b, int l, u
   const VSrc ci_s = act ? ver_src(a, a.accQ, a.ver_a, i, r.b.w) : 0;
   const VSrc cj_s = act ? ver_src(a, a.accQ, a.ver_a, j, r.c.x) : 0;
   RowV<NV> p = zero_row<NV>(), qi = p, qj = p, cu = p, ci = p, cj = p;
-  bool op = !act, oi = !act, oj = !act, ou = !act, oci = !act, ocj = !act;
-  for (int it = 0;; ++it) {
-    try_row<LPR, NV>(su, d, l, tag, p, op);
-    try_row<LPR, NV>(si, d, l, tag, qi, oi);
-    try_row<LPR, NV>(sj, d, l, tag, qj, oj);
-    try_row<LPR, NV>(cu_s, d, l, tag, cu, ou);
-    try_row<LPR, NV>(ci_s, d, l, tag, ci, oci);
-    try_row<LPR, NV>(cj_s, d, l, tag, cj, ocj);
-    if (wait_round(a, op && oi && oj && ou && oci && ocj, it)) break;
+  {
+    const VSrc src[6] = {su, si, sj, cu_s, ci_s, cj_s};
+    RowV<NV>* const dst[6] = {&p, &qi, &qj, &cu, &ci, &cj};
+    bool ok[6] = {!act, !act, !act, !act, !act, !act};
+    poll_rows<LPR, NV, 6>(a, src, dst, ok, tag, l);
   }
   if (!act) return;
   float g, loss;
