@@ -6,7 +6,9 @@ medians of the per-task segments of slot tasks:
   hdr    start -> slot header loaded
   wait1  header -> own row, Adagrad slot and partner rows all there
   clean  -> delta published
-  adv    -> partner deltas there + adversarial terms
+  adv    -> partner deltas there + adversarial terms (one-pass slots split into
+           adv_solo: solo deltas formed, adv_wait: published deltas there,
+           adv_terms: adversarial terms)
   tail   -> Adagrad + versions stored
 plus the time between consecutive batches' completions (per-batch rate) and the
 start lag of a batch's tasks behind the previous batch's completion.
@@ -57,7 +59,7 @@ def main():
     assert ctx.step_errors() == 0
     st = stamps.view(nb, cap, 8).cpu().numpy().astype(np.int64)
     t0 = st[st[:, :, 0] > 0, 0].min()
-    seg = {k: [] for k in ("hdr", "wait1", "clean", "adv", "tail", "task")}
+    seg = {k: [] for k in ("hdr", "wait1", "clean", "adv", "tail", "task", "adv_solo", "adv_wait", "adv_terms")}
     done, first_start, lag = [], [], []
     for t in range(nb):
         w = st[t]
@@ -68,6 +70,10 @@ def main():
         seg["adv"] += list(full[:, 4] - full[:, 3])
         seg["tail"] += list(full[:, 5] - full[:, 4])
         seg["task"] += list(full[:, 5] - full[:, 0])
+        one = full[(full[:, 6] > 0) & (full[:, 7] > 0)]  # one-pass slots: adv split at stamps 6, 7
+        seg["adv_solo"] += list(one[:, 6] - one[:, 3])
+        seg["adv_wait"] += list(one[:, 7] - one[:, 6])
+        seg["adv_terms"] += list(one[:, 4] - one[:, 7])
         ends = w[w[:, 5] > 0, 5]
         starts = w[w[:, 0] > 0, 0]
         done.append(ends.max())
