@@ -10,7 +10,8 @@ Both counters are in KiB per dispatch.
 Usage: python tools/pmc_traffic.py gpurun_out/prof profiles/r01/pmc_traffic.json [batches_per_stream_launch]
 Writes {kernel name: {launches, fetch_kib_median, write_kib_median,
 traffic_bytes_per_launch, trace_avg_us}} for the step kernels, and for k_stream
-(one launch = many batches) also traffic_bytes_per_batch."""
+(one launch = many batches) also traffic_bytes_per_batch.  Records of kernels the
+passes did not run are kept from the existing file (from_earlier_pass)."""
 import csv
 import json
 import statistics
@@ -83,6 +84,14 @@ def main(src, dst, stream_batches=647):
             rec["traffic_bytes_per_batch"] = int(rec["traffic_bytes_per_launch"] / stream_batches)
             rec["write_factor"] = wf
         out[name] = rec
+    try:  # kernels these passes did not run (e.g. the --large list kernels) keep their earlier records
+        with open(dst) as fh:
+            prev = json.load(fh)
+        for k, v in prev.items():
+            if not k.startswith("_") and k not in out:
+                out[k] = dict(v, from_earlier_pass=True)
+    except (FileNotFoundError, ValueError):
+        pass
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
