@@ -981,13 +981,18 @@ __device__ __forceinline__ SlotRec slot_header(const StepArgs& a, int k, int m, 
   if (m + TEAM < a.R && k < a.S) s.r1 = load_rec(base + m + TEAM);
   s.r0_valid = s.r0.gen() == gen;
   s.r1_valid = s.r1.gen() == gen;
-  const int32_t meta = __shfl(s.r0_valid ? s.r0.meta() : 0, leader_lane, 64);
+  // one team per wave: the leader is lane 0, read with v_readlane (no LDS trip)
+  auto from_leader = [&](int32_t v) -> int32_t {
+    if constexpr (LPR * TEAM == 64) return __builtin_amdgcn_readlane(v, 0);
+    else return __shfl(v, leader_lane, 64);
+  };
+  const int32_t meta = from_leader(s.r0_valid ? s.r0.meta() : 0);
   // a fused triplet's slots are handled by its k_single lane-group
   s.h.count = (a.use_single && (meta & ACF_SINGLE_BIT)) ? 0 : (meta & ACF_COUNT_MASK);
   s.h.is_item = (meta & ACF_ITEM_BIT) != 0;
-  s.h.own_row = __shfl(s.r0.own_row(), leader_lane, 64);
-  s.h.own_src = __shfl(s.r0.own_src(), leader_lane, 64);
-  s.h.ovf = __shfl(s.r0.ovf(), leader_lane, 64);
+  s.h.own_row = from_leader(s.r0.own_row());
+  s.h.own_src = from_leader(s.r0.own_src());
+  s.h.ovf = from_leader(s.r0.ovf());
   return s;
 }
 
@@ -1119,6 +1124,46 @@ __device__ __forceinline__ void team_allreduce(RowV<NV>& G) {
       G.v[v].w += __shfl_xor(G.v[v].w, m, 64);
     }
   }
+}
+
+// The same butterfly for a team that spans a whole, fully active wave
+// (k_stream): the lane^16 and lane^32 exchanges use gfx950's
+// v_permlane16_swap / v_permlane32_swap (VALU) instead of ds_bpermute (an LDS
+// round trip each).  Pure data movement: the sums, and so the bits, are
+// team_allreduce's.  With vdst = src0 = x, a lane's partner value is the
+// swapped vdst in the upper half of each pair of rows, the swapped src0 below.
+template <int M>
+__device__ __forceinline__ float xor_lane_wave(float x) {
+  const uint32_t u = __float_as_uint(x);
+  if constexpr (M == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+  } else if constexpr (M == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+  } else {
+    return __shfl_xor(x, M, 64);
+  }
+}
+
+template <int M, int END, int NV>
+__device__ __forceinline__ void wave_butterfly(RowV<NV>& G) {
+  if constexpr (M < END) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      G.v[v].x += xor_lane_wave<M>(G.v[v].x);
+      G.v[v].y += xor_lane_wave<M>(G.v[v].y);
+      G.v[v].z += xor_lane_wave<M>(G.v[v].z);
+      G.v[v].w += xor_lane_wave<M>(G.v[v].w);
+    }
+    wave_butterfly<2 * M, END, NV>(G);
+  }
+}
+
+template <int LPR, int TEAM, int NV>
+__device__ __forceinline__ void team_allreduce_wave(RowV<NV>& G) {
+  static_assert(LPR * TEAM == 64, "team_allreduce_wave: one team per wave");
+  wave_butterfly<LPR, 64, NV>(G);
 }
 
 // Lane geometry of a step kernel: slot k of this team, member m, lane l in the
@@ -1833,7 +1878,7 @@ __device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int
   }
   // the clean half's end: batch-summed gradient, delta, delta published
   auto finish_clean = [&](RowV<NV>& Gc) -> RowV<NV> {
-    team_allreduce<LPR, TEAM, NV>(Gc);
+    team_allreduce_wave<LPR, TEAM, NV>(Gc);
     const RowV<NV> dl = make_delta<LPR, NV>(a, Gc, h.is_item, h.own_row, l);
     // a one-occurrence row's delta is never read: its readers form it (solo_delta)
     if (m == 0 && h.count > 1) store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_d, a, a.t, k)), d, l, dl, tag);
@@ -1869,7 +1914,7 @@ __device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int
     }
   }
   STAMP(a.t, k, 4);
-  team_allreduce<LPR, TEAM, NV>(GA);
+  team_allreduce_wave<LPR, TEAM, NV>(GA);
   if (m == 0) {
     axpy_row(G, a.reg_adv, GA);
     RowV<NV> wout;
