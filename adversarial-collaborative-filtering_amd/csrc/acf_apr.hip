@@ -812,7 +812,7 @@ struct StepArgs {
   const int32_t* task_list;  // [nb][task_stride] a batch's tasks (slot, or S + fused group); null: positions
   const int32_t* task_cnt;   // [nb]
   int32_t task_stride, max_depth;
-  int32_t poll_sleep;  // k_stream: s_sleep between polls of a version (0-3)
+  int32_t poll_sleep;  // k_stream: s_sleep between polls of a version (0-3; 4/5/6 = 8/16/32)
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -1640,6 +1640,9 @@ __device__ __forceinline__ bool wait_round(const StepArgs& a, bool ok, int it) {
     case 0: break;
     case 1: __builtin_amdgcn_s_sleep(1); break;
     case 3: __builtin_amdgcn_s_sleep(3); break;
+    case 4: __builtin_amdgcn_s_sleep(8); break;
+    case 5: __builtin_amdgcn_s_sleep(16); break;
+    case 6: __builtin_amdgcn_s_sleep(32); break;
     default: __builtin_amdgcn_s_sleep(2); break;
   }
   return false;
@@ -2429,7 +2432,7 @@ struct acf_apr_ctx {
   // streamed step (k_stream): row versions of every batch of a launch
   int32_t stream = 1;        // ACF_STREAM=0 disables
   int32_t stream_depth = 2;  // ACF_STREAM_DEPTH: max waves per position (batches in flight)
-  int32_t poll_sleep = 2;    // ACF_POLL_SLEEP: s_sleep argument between version polls (0-3)
+  int32_t poll_sleep = 2;    // ACF_POLL_SLEEP: s_sleep between version polls (0-3; 4/5/6 = 8/16/32)
   int32_t stream_ok = -1;    // -1 unknown, 0 unavailable (allocation / occupancy), 1 ready
   int64_t stream_max_waves = 0;
   unsigned long long *ver_w = nullptr, *ver_a = nullptr, *ver_d = nullptr;
@@ -2543,7 +2546,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (const char* e = getenv("ACF_OVL_DELAY")) c->ovl_delay = std::max(0, atoi(e));
   if (const char* e = getenv("ACF_STREAM")) c->stream = atoi(e) != 0;
   if (const char* e = getenv("ACF_STREAM_DEPTH")) c->stream_depth = std::max(1, std::min(8, atoi(e)));
-  if (const char* e = getenv("ACF_POLL_SLEEP")) c->poll_sleep = std::max(0, std::min(3, atoi(e)));
+  if (const char* e = getenv("ACF_POLL_SLEEP")) c->poll_sleep = std::max(0, std::min(6, atoi(e)));
   const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
   auto A = [&](auto** p, size_t n) { if (r == ACF_OK) r = dalloc(c, p, n); };
