@@ -129,10 +129,10 @@ class MF:
         """Epoch trainer: chunks of `chunk` batches, next chunk planned while one trains."""
         p = self._pipe
         if p is None or p.batch_size != batch_size or p.chunk != chunk:
-            # concurrent planning only pays at large batches (small steps are latency-bound)
+            # concurrent planning: large batches and APR (k_stream); small BPR batches plan in line
             self._pipe = p = ops.PlanPipeline(self.num_user_rows, self.num_item_rows,
                                               self.embedding_size, batch_size, chunk, self.device,
-                                              overlap=batch_size >= 4096)
+                                              overlap=None)
         return p
 
     def reset_optimizer(self):

@@ -221,14 +221,18 @@ class PlanPipeline:
     are independent calls of train_planned (each ends with its flush), so the
     result is the one of planning and training the chunks in sequence.
 
-    overlap=False plans on the caller's stream instead: at small batches the step
-    kernels are latency-bound and a concurrent plan slows them more than it saves.
+    overlap=False plans on the caller's stream instead.  overlap=None decides per
+    run: concurrent planning for large batches and for APR (the streamed step
+    k_stream leaves room beside it: 102.4M -> 113.1M triplets/s at B = 512), on
+    the caller's stream for small BPR batches, whose short per-batch kernels a
+    concurrent plan slowed more than it saved.
     """
 
     def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, batch_size: int,
-                 chunk: int, device: torch.device, overlap: bool = True):
+                 chunk: int, device: torch.device, overlap: bool | None = True):
         self.device = torch.device(device)
-        self.overlap = bool(overlap)
+        self.overlap = None if overlap is None else bool(overlap)
+        self._ov = bool(overlap)  # the current run's choice
         self.batch_size, self.chunk = int(batch_size), int(chunk)
         self.ctx = [APRContext(num_user_rows, num_item_rows, dim, batch_size, chunk, self.device)
                     for _ in range(2)]
@@ -260,7 +264,7 @@ class PlanPipeline:
     def _plan(self, k, u, i, j, b, n, check):
         B, c = self.batch_size, self.ctx[k % 2]
         s = slice(b * B, (b + n) * B)
-        if not self.overlap:
+        if not self._ov:
             c.plan(u[s], i[s], j[s], B, check=check)
             return None
         with torch.cuda.stream(self.side):
@@ -283,7 +287,8 @@ class PlanPipeline:
             raise ValueError(f"batches [{first_batch}, {first_batch + n_batches}) outside the "
                              f"{total} batches of the stream")
         main = torch.cuda.current_stream(self.device)
-        if self.overlap:
+        self._ov = self.overlap if self.overlap is not None else (B >= 4096 or bool(hp.adver))
+        if self._ov:
             ready = torch.cuda.Event()
             ready.record(main)  # triplets produced on the caller's stream
             self.side.wait_event(ready)
@@ -294,7 +299,7 @@ class PlanPipeline:
             if planned is not None:
                 main.wait_event(planned)
             self.ctx[k % 2].train_planned(tables, hp, 0, n, graph=graph)
-            if self.overlap:
+            if self._ov:
                 done = torch.cuda.Event()
                 done.record(main)
                 self._free[k % 2] = done

@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--chunk", type=int, default=647,
                    help="batches per plan / graph (the next chunk's plan overlaps this chunk's training)")
     p.add_argument("--eager", action="store_true", help="eager launches instead of hipGraph replay")
+    p.add_argument("--no-plan-overlap", action="store_true",
+                   help="plan each chunk on the timed stream instead of beside the previous chunk's training (A/B)")
     p.add_argument("--cpu-batches", type=int, default=17469, help="oracle sample size (batches, ~10-30 s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--time-batches", type=int, default=400, help="batches in the kernel-timing pass")
@@ -330,8 +332,8 @@ def main():
     tabs = init_tables(U1, I1, d, dev, seed=rank)
     P0, Q0 = tabs[0].clone(), tabs[1].clone()
     chunk = min(a.chunk, a.steps)
-    # B = 512 steps are latency-bound: planning concurrently slows them
-    pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False)
+    # chunk c+1 is planned on a side stream beside chunk c's streamed step
+    pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False if a.no_plan_overlap else None)
     pipe.set_slot_mapping(a.mapping)
     pipe.set_step_overlap(not a.no_step_overlap)
     pipe.set_stream(not a.no_stream)

@@ -450,7 +450,7 @@ def test_fused_large_batch_matches_oracle(ops, oracle, dev, adver):
         _close(la, la_w, "loss_adv")
 
 
-@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("overlap", [False, True, None])
 @pytest.mark.parametrize("chunk", [1, 3, 7])
 def test_plan_pipeline_equals_sequential(ops, dev, chunk, overlap):
     """PlanPipeline (next chunk planned on a side stream) == plan + train per
