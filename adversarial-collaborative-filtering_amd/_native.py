@@ -47,14 +47,13 @@ SIGNATURES = {
     "acf_apr_optimizer_step": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _P]),
     "acf_apr_train_planned": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _I32,
                                              _I32, _P]),
+    "acf_apr_train": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _P, _P, _P, _I32,
+                                     _I32, _I32, _I32, _P]),
     "acf_apr_time_kernels": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _I32,
-                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I32), _P]),
-    "acf_apr_time_kernels_v2": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _I32,
-                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I32), _P]),
-    "acf_apr_time_kernels_v3": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _I32,
                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I32), _P]),
     "acf_apr_set_slot_mapping": (ctypes.c_int, [_P, _I32]),
     "acf_apr_set_fusion": (ctypes.c_int, [_P, _I32]),
+    "acf_apr_set_plan_mode": (ctypes.c_int, [_P, _I32]),
     "acf_apr_set_step_overlap": (ctypes.c_int, [_P, _I32]),
     "acf_apr_set_stream": (ctypes.c_int, [_P, _I32]),
     "acf_apr_step_errors": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),

@@ -34,6 +34,10 @@
 #include <hip/hip_ext.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/block/block_radix_sort.hpp>
+#include <rocprim/block/block_scan.hpp>
+
+#include <algorithm>
 
 #include <cstdarg>
 #include <cstdio>
@@ -718,6 +722,259 @@ __global__ void k_task_list(const int32_t* __restrict__ flags, const int32_t* __
   const int32_t base = t > 0 ? incl[t * stride - 1] : 0;
   if (flags[x]) list[t * stride + incl[x] - base - 1] = y;
   if (y == stride - 1) cnt[t] = incl[x] - base;
+}
+
+// ---------------------------------------------------------------------------
+// Batch-local plan (one-wave-per-slot plans, B <= 1024): the same records,
+// task lists and next-batch table as the sort plan above, in TWO launches with
+// one workgroup per batch instead of ~30 launches of device-wide sorts/scans.
+//  - k_bplan_sort: the batch's 3B occurrences sorted by (side, row) in LDS
+//    (rocPRIM block radix sort, stable: occurrence order inside a row), its
+//    unique rows, their CSR starts, each occurrence's (slot, rank); each unique
+//    row marks batch t in its row's batch bitmap and records its local slot.
+//  - k_bplan_build: per unique row, the previous / next batch that touches the
+//    row from the bitmap (any distance: the streamed step's version source) and
+//    the previous batch's local slot; then k_records' occurrence / fused-triplet
+//    records and k_task_flags/k_task_list's task list, from LDS.
+// The occurrence order, slot order (users by row, then items by row) and CSR
+// positions (t*B + position in the sorted user part, t*2B + position in the
+// item part) are the sort plan's, so the records are bit-identical
+// (test_batch_plan_matches_sort_plan).  The bitmaps come in two buffers by
+// plan generation parity: a plan sets bits in one and clears the other, which
+// the previous plan used.
+// ---------------------------------------------------------------------------
+struct BPlanArgs {
+  const int32_t* user;
+  const int32_t* ipos;
+  const int32_t* ineg;
+  int64_t U1, I1;
+  int32_t B, S, nb, rb, kb, W, nbs;  // nbs: batch stride of slot_of (max batches)
+  int32_t R, opw, stride, gen;
+  unsigned long long* mask;        // [U1 + I1][W] batches touching each row (this plan)
+  unsigned long long* mask_clear;  // the other bitmap buffer: cleared here
+  int64_t clear_words;
+  uint16_t* slot_of;  // [U1 + I1][nbs] local slot of the row in batch t (valid where mask has t)
+  uint32_t* bkey;     // [nb][S] sorted unique keys (side << rb | row)
+  int32_t* bstart;    // [nb][S + 1] CSR start of each unique row in the sorted batch
+  int32_t* bocc;      // [nb][S] occurrence o -> slot | rank << 16
+  int2* bn;           // [nb] {unique rows, unique user rows}
+  int32_t* berr;      // [nb] range-check bits of the batch
+  int32_t* err;       // err[0] = OR of berr
+  int32_t* gen_ptr;
+  OccRec *urec, *irec, *inl, *trec;
+  int32_t* nextt;
+  int32_t* task_list;
+  int32_t* task_cnt;
+};
+
+template <int BS, int IPT>
+__global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
+  constexpr int N = BS * IPT;
+  using Sort = rocprim::block_radix_sort<uint32_t, BS, IPT, int32_t>;
+  using Scan = rocprim::block_scan<int32_t, BS>;
+  __shared__ union {
+    typename Sort::storage_type sort;
+    struct {
+      uint32_t key[N];
+      int32_t val[N];
+      int32_t start[N + 1];
+    } a;
+  } sm;
+  __shared__ typename Scan::storage_type scan_st;
+  __shared__ int32_t s_err, s_nu;
+  const int t = blockIdx.x, tid = threadIdx.x, B = p.B, S3 = 3 * B;
+  if (tid == 0) { s_err = 0; s_nu = -1; }
+  const uint32_t side_bit = 1u << p.rb;
+  uint32_t keys[IPT];
+  int32_t vals[IPT];
+  int err = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int o = tid * IPT + k;  // occurrence: users [0, B), items B + 2e + role
+    uint32_t key = ~0u;           // padding sorts after every key (stable: after equal ones too)
+    if (o < B) {
+      int32_t u = p.user[(int64_t)t * B + o];
+      if (u < 0 || u >= p.U1) { err |= 1; u = 0; }
+      key = (uint32_t)u;
+    } else if (o < S3) {
+      const int v = o - B;
+      const int64_t e = (int64_t)t * B + (v >> 1);
+      int32_t x = (v & 1) ? p.ineg[e] : p.ipos[e];
+      if (x < 0 || x >= p.I1) { err |= 2; x = 0; }
+      key = side_bit | (uint32_t)x;
+    }
+    keys[k] = key;
+    vals[k] = o;
+  }
+  __syncthreads();
+  if (err) atomicOr(&s_err, err);
+  Sort().sort(keys, vals, sm.sort, 0, p.rb + 1);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    sm.a.key[tid * IPT + k] = keys[k];
+    sm.a.val[tid * IPT + k] = vals[k];
+  }
+  __syncthreads();
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int q = tid * IPT + k;
+    cnt += (q < S3 && (q == 0 || keys[k] != sm.a.key[q - 1])) ? 1 : 0;
+  }
+  int32_t excl = 0, total = 0;
+  Scan().exclusive_scan(cnt, excl, 0, total, scan_st);
+  int32_t sl[IPT];
+  int32_t s = excl - 1;
+  const int64_t rbase = (int64_t)t * p.S;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int q = tid * IPT + k;
+    sl[k] = -1;
+    if (q >= S3) continue;
+    const uint32_t key = keys[k];
+    if (q == 0 || key != sm.a.key[q - 1]) {
+      ++s;
+      sm.a.start[s] = q;
+      const int side = (key & side_bit) ? 1 : 0;
+      const int64_t row = (int64_t)(key & (side_bit - 1));
+      const int64_t rid = side ? p.U1 + row : row;
+      p.bkey[rbase + s] = key;
+      p.bstart[(int64_t)t * (p.S + 1) + s] = q;
+      p.slot_of[rid * p.nbs + t] = (uint16_t)s;
+      atomicOr(p.mask + rid * p.W + (t >> 6), 1ull << (t & 63));
+      if (side && (q == 0 || !(sm.a.key[q - 1] & side_bit))) s_nu = s;
+    }
+    sl[k] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int q = tid * IPT + k;
+    if (q < S3) p.bocc[rbase + vals[k]] = sl[k] | ((q - sm.a.start[sl[k]]) << 16);
+  }
+  if (tid == 0) {
+    p.bstart[(int64_t)t * (p.S + 1) + total] = S3;
+    p.bn[t] = make_int2(total, s_nu < 0 ? total : s_nu);
+    p.berr[t] = s_err;
+  }
+}
+
+template <int BS, int MAXB>
+__global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
+  using Scan = rocprim::block_scan<int32_t, BS>;
+  __shared__ int4 info[3 * MAXB];
+  __shared__ uint8_t single[3 * MAXB];
+  __shared__ uint8_t gflag[MAXB];
+  __shared__ typename Scan::storage_type scan_st;
+  const int t = blockIdx.x, tid = threadIdx.x, B = p.B, S = p.S;
+  const int G = (B + p.opw - 1) / p.opw;
+  const int2 n = p.bn[t];
+  const int64_t rbase = (int64_t)t * S;
+  for (int s = tid; s < S; s += BS) {
+    single[s] = 0;
+    if (s >= n.x) {
+      p.nextt[rbase + s] = 0;  // no row: never written back
+      continue;
+    }
+    const uint32_t key = p.bkey[rbase + s];
+    const uint32_t side_bit = 1u << p.rb;
+    const int side = (key & side_bit) ? 1 : 0;
+    const int32_t row = (int32_t)(key & (side_bit - 1));
+    const int64_t rid = side ? p.U1 + row : (int64_t)row;
+    const int32_t st = p.bstart[(int64_t)t * (S + 1) + s];
+    const int32_t cnt = p.bstart[(int64_t)t * (S + 1) + s + 1] - st;
+    const int32_t ovf = side ? t * 2 * B + st - B : t * B + st;
+    const unsigned long long* m = p.mask + rid * p.W;
+    // previous batch touching the row: highest bit below t
+    int w = t >> 6;
+    unsigned long long bits = m[w] & ((1ull << (t & 63)) - 1);
+    while (!bits && w > 0) bits = m[--w];
+    int32_t src = row;
+    if (bits) {
+      const int tp = w * 64 + 63 - __clzll((long long)bits);
+      src = make_src(t - tp, p.slot_of[rid * p.nbs + tp], p.kb);
+    }
+    // next batch touching the row: lowest bit above t
+    w = t >> 6;
+    bits = (t & 63) == 63 ? 0ull : (m[w] & ~((2ull << (t & 63)) - 1));
+    const int wl = (p.nb - 1) >> 6;
+    while (!bits && w < wl) bits = m[++w];
+    const int32_t tn = bits ? w * 64 + __ffsll((long long)bits) - 1 : 0x7fffffff;
+    info[s] = make_int4(row, src, cnt | (tn == t + 1 ? ACF_INFO_NEXT : 0), ovf);
+    p.nextt[rbase + s] = tn;
+  }
+  for (int g = tid; g < G; g += BS) gflag[g] = 0;
+  __syncthreads();
+  const int gen = p.gen;
+  for (int b = tid; b < B; b += BS) {
+    const int64_t e = (int64_t)t * B + b;
+    const int32_t ou = p.bocc[rbase + b], oi = p.bocc[rbase + B + 2 * b], oj = p.bocc[rbase + B + 2 * b + 1];
+    const int32_t k = ou & 0xFFFF, ki = oi & 0xFFFF, kj = oj & 0xFFFF;
+    const int4 U = info[k], I = info[ki], J = info[kj];
+    const FuseInfo f = fuse_info(U, I, J, p.kb);
+    OccRec r;
+    r.own_row = U.x;
+    r.own_src = U.y;
+    r.meta = info_count(U) | (f.fused ? ACF_SINGLE_BIT : 0) | (f.in_u ? ACF_INPLACE_BIT : 0);
+    r.ovf = U.w;
+    r.e_role = (int32_t)e;
+    r.pa_row = I.x;
+    r.pb_row = J.x;
+    r.pa_src = I.y;
+    r.pb_src = J.y;
+    r.pa_slot = ki | (info_count(I) == 1 ? ACF_SOLO_BIT : 0);
+    r.pb_slot = kj | (info_count(J) == 1 ? ACF_SOLO_BIT : 0);
+    r.gen = gen;
+    int32_t rr = ou >> 16;
+    if (rr < p.R) p.inl[(rbase + k) * p.R + rr] = r;
+    else p.urec[U.w + rr] = r;
+    const OccRec ri = item_rec(I, J, U, (int32_t)(2 * e), k, kj, f.fused, f.in_i, gen);
+    rr = oi >> 16;
+    if (rr < p.R) p.inl[(rbase + ki) * p.R + rr] = ri;
+    else p.irec[I.w + rr] = ri;
+    const OccRec rj = item_rec(J, I, U, (int32_t)(2 * e + 1), k, ki, f.fused, f.in_j, gen);
+    rr = oj >> 16;
+    if (rr < p.R) p.inl[(rbase + kj) * p.R + rr] = rj;
+    else p.irec[J.w + rr] = rj;
+    if (f.fused) {
+      OccRec q;
+      q.own_row = U.x; q.own_src = I.x; q.meta = J.x; q.ovf = k;
+      q.e_role = ki; q.pa_row = kj; q.pb_row = U.y; q.pa_src = I.y;
+      q.pb_src = J.y;
+      q.pa_slot = 1 | (f.in_u ? 2 : 0) | (f.in_i ? 4 : 0) | (f.in_j ? 8 : 0);
+      q.pb_slot = (int32_t)e; q.gen = gen;
+      p.trec[e] = q;
+      single[k] = single[ki] = single[kj] = 1;  // the fused triplet's slots are its own
+      gflag[b / p.opw] = 1;
+    }
+  }
+  __syncthreads();
+  // task list: the non-fused slots in slot order, then the groups holding a fused triplet
+  int32_t base = 0;
+  for (int y0 = 0; y0 < S + G; y0 += BS) {
+    const int y = y0 + tid;
+    int32_t f = 0;
+    if (y < S) f = (y < n.x && !single[y]) ? 1 : 0;
+    else if (y < S + G) f = gflag[y - S];
+    int32_t excl = 0, tot = 0;
+    Scan().exclusive_scan(f, excl, 0, tot, scan_st);
+    if (f) p.task_list[(int64_t)t * p.stride + base + excl] = y;
+    base += tot;
+    __syncthreads();  // scan storage reuse
+  }
+  if (tid == 0) {
+    p.task_cnt[t] = base;
+    if (t == 0) {
+      int32_t e = 0;
+      for (int x = 0; x < p.nb; ++x) e |= p.berr[x];
+      p.err[0] = e;
+      *p.gen_ptr = gen;
+    }
+  }
+  // clear the other bitmap buffer (used by the previous plan), a stripe per batch
+  const int64_t w0 = p.clear_words * t / p.nb, w1 = p.clear_words * (t + 1) / p.nb;
+  for (int64_t x = w0 + tid; x < w1; x += BS) p.mask_clear[x] = 0ull;
 }
 
 // ---------------------------------------------------------------------------
@@ -2043,44 +2300,36 @@ __global__ void __launch_bounds__(256, 2) k_stream(StepArgs a, int32_t positions
 }
 
 // After k_stream: the last version of every row the launch updated goes to the
-// tables (weights and Adagrad slot); then the epoch moves on.  One thread per
-// slot of the range finds the rows to write back, the wave copies them.
+// tables (weights and Adagrad slot); then the epoch moves on.  One lane-group
+// per slot of the range: lane c gathers granules c, c + d/4, c + d/2, c + 3d/4
+// (elements 4c .. 4c+3 in the component-major order) of both versions and
+// stores them as one float4 each, so every slot's loads are in flight at once.
+template <int LPR>
 __global__ void __launch_bounds__(256) k_stream_flush(StepArgs a, uint32_t* __restrict__ epoch) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  constexpr int OPW = 64 / LPR;
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t x = (gid >> 6) * OPW + (int64_t)((threadIdx.x & 63) / LPR);
+  const int l = (int)(threadIdx.x & (LPR - 1));
   const int64_t n = (int64_t)(a.t_end - a.first) * a.S;
-  const int lane = threadIdx.x & 63;
-  if (x == 0) atomicAdd(epoch, 1u);  // every k_stream wave has read it (kernel boundary)
-  bool need = false;
-  int32_t t = 0, k = 0;
-  if (x < n) {
-    t = a.first + (int32_t)(x / a.S);
-    k = (int32_t)(x - (int64_t)(t - a.first) * a.S);
-    need = a.nextt[(int64_t)t * a.S + k] >= a.t_end;
-  }
-  RecV r;
-  r.a = r.b = r.c = make_int4(0, 0, 0, -1);
-  if (need) {
-    r = load_rec(a.inl + ((int64_t)t * a.S + k) * a.R);
-    need = r.gen() == *a.gen_ptr && (r.meta() & ACF_COUNT_MASK) != 0;
-  }
-  uint64_t mask = __ballot(need);
-  while (mask) {
-    const int src_lane = __ffsll((long long)mask) - 1;
-    mask &= mask - 1;
-    const int32_t tt = __shfl(t, src_lane, 64), kk = __shfl(k, src_lane, 64);
-    const int32_t row = __shfl(r.own_row(), src_lane, 64);
-    const int item = (__shfl(r.meta(), src_lane, 64) & ACF_ITEM_BIT) != 0;
-    float* w = (item ? a.Q : a.P) + (int64_t)row * a.d;
-    float* c = (item ? a.accQ : a.accP) + (int64_t)row * a.d;
-    const u64* vw = vrow(a.ver_w, a, tt, kk);
-    const u64* va = vrow(a.ver_a, a, tt, kk);
-    const int d4 = a.d >> 2;
-    for (int e = lane; e < a.d; e += 64) {  // granule e holds element 4(e % d4) + e / d4
-      const int x = 4 * (e % d4) + e / d4;
-      w[x] = __uint_as_float((uint32_t)vw[e]);
-      c[x] = __uint_as_float((uint32_t)va[e]);
-    }
-  }
+  if (gid == 0) atomicAdd(epoch, 1u);  // every k_stream wave has read it (kernel boundary)
+  if (x >= n) return;
+  const int32_t t = a.first + (int32_t)(x / a.S);
+  const int32_t k = (int32_t)(x - (int64_t)(t - a.first) * a.S);
+  if (a.nextt[(int64_t)t * a.S + k] < a.t_end) return;  // a later batch of the launch has it
+  const RecV r = load_rec(a.inl + ((int64_t)t * a.S + k) * a.R);
+  if (r.gen() != *a.gen_ptr || (r.meta() & ACF_COUNT_MASK) == 0) return;
+  const int d4 = a.d >> 2;
+  if (l >= d4) return;
+  const int item = (r.meta() & ACF_ITEM_BIT) != 0;
+  const u64* vw = vrow(a.ver_w, a, t, k);
+  const u64* va = vrow(a.ver_a, a, t, k);
+  const float4 w = make_float4(__uint_as_float((uint32_t)vw[l]), __uint_as_float((uint32_t)vw[l + d4]),
+                               __uint_as_float((uint32_t)vw[l + 2 * d4]), __uint_as_float((uint32_t)vw[l + 3 * d4]));
+  const float4 c = make_float4(__uint_as_float((uint32_t)va[l]), __uint_as_float((uint32_t)va[l + d4]),
+                               __uint_as_float((uint32_t)va[l + 2 * d4]), __uint_as_float((uint32_t)va[l + 3 * d4]));
+  const int64_t off = (int64_t)r.own_row() * a.d + 4 * l;
+  *reinterpret_cast<float4*>((item ? a.Q : a.P) + off) = w;
+  *reinterpret_cast<float4*>((item ? a.accQ : a.accP) + off) = c;
 }
 
 // Large batches with fusion (one lane-group per slot): the slot work of batch t
@@ -2439,6 +2688,16 @@ struct acf_apr_ctx {
   uint32_t* epoch = nullptr;
   int32_t *task_list = nullptr, *task_cnt = nullptr;  // streamed-step task lists of the plan
   int32_t task_lists = 0, task_stride = 0;
+  // batch-local plan (k_bplan_sort / k_bplan_build)
+  int32_t plan_mode = 0;     // 0 auto (batch-local plan where it applies), 1 always the sort plan
+  int32_t bplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
+  unsigned long long* bmask[2] = {nullptr, nullptr};
+  size_t bmask_words = 0;
+  int32_t bmask_dirty[2] = {0, 0};
+  uint16_t* slot_of = nullptr;
+  uint32_t* bkey = nullptr;
+  int32_t *bstart = nullptr, *bocc = nullptr, *berr = nullptr;
+  int2* bn = nullptr;
   hipStream_t cap_stream = nullptr;
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<void*> allocs;
@@ -2602,6 +2861,103 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   return ACF_OK;
 }
 
+// Batch-local plan buffers, allocated at first use: the two batch bitmaps, the
+// per-row local slots and the per-batch sort outputs.  Off (sort plan) when
+// the bitmaps or slot table would be large (big tables: packed plans anyway).
+static bool bplan_ready(acf_apr_ctx* c) {
+  if (c->bplan_ok >= 0) return c->bplan_ok == 1;
+  c->bplan_ok = 0;
+  const int64_t rows = c->U1 + c->I1;
+  const int32_t W = (c->maxNB + 63) / 64;
+  const size_t mask_words = (size_t)rows * W;
+  const size_t S = (size_t)3 * c->maxB;
+  if (c->maxB > 1024 || mask_words * 8 > ((size_t)64 << 20) ||
+      (size_t)rows * c->maxNB * 2 > ((size_t)256 << 20))
+    return false;
+  std::vector<void*> got;
+  auto A = [&](auto** p, size_t n) -> bool {
+    if (dalloc(c, p, n) != ACF_OK) return false;
+    got.push_back(*p);
+    return true;
+  };
+  bool ok = A(&c->bmask[0], mask_words) && A(&c->bmask[1], mask_words) &&
+            A(&c->slot_of, (size_t)rows * c->maxNB) && A(&c->bkey, (size_t)c->maxNB * S) &&
+            A(&c->bstart, (size_t)c->maxNB * (S + 1)) && A(&c->bocc, (size_t)c->maxNB * S) &&
+            A(&c->bn, (size_t)c->maxNB) && A(&c->berr, (size_t)c->maxNB);
+  ok = ok && hipMemset(c->bmask[0], 0, mask_words * 8) == hipSuccess &&
+       hipMemset(c->bmask[1], 0, mask_words * 8) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+  if (!ok) {  // give back what was allocated; the sort plan stays in use
+    (void)hipGetLastError();
+    for (void* p : got) {
+      (void)hipFree(p);
+      c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), p));
+    }
+    c->bmask[0] = c->bmask[1] = nullptr;
+    return false;
+  }
+  c->bmask_words = mask_words;
+  c->bmask_dirty[0] = c->bmask_dirty[1] = 0;
+  c->bplan_ok = 1;
+  return true;
+}
+
+static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg,
+                      int32_t B, int32_t nb, int32_t gen, int32_t kb, int32_t check, hipStream_t s) {
+  const int cur = gen & 1, oth = cur ^ 1;
+  if (c->bmask_dirty[cur])  // a plan used it and no later batch plan cleared it
+    HIP_TRY(hipMemsetAsync(c->bmask[cur], 0, c->bmask_words * 8, s));
+  BPlanArgs p;
+  p.user = user; p.ipos = ipos; p.ineg = ineg;
+  p.U1 = c->U1; p.I1 = c->I1;
+  p.B = B; p.S = 3 * B; p.nb = nb;
+  p.rb = (int32_t)bits_for((uint64_t)std::max(c->U1, c->I1));
+  p.kb = kb;
+  p.W = (c->maxNB + 63) / 64;
+  p.nbs = c->maxNB;
+  p.R = c->R;
+  p.opw = 64 / c->lpr;
+  p.stride = 3 * B + (B + p.opw - 1) / p.opw;
+  p.gen = gen;
+  p.mask = c->bmask[cur];
+  p.mask_clear = c->bmask[oth];
+  p.clear_words = c->bmask_dirty[oth] ? (int64_t)c->bmask_words : 0;
+  p.slot_of = c->slot_of;
+  p.bkey = c->bkey; p.bstart = c->bstart; p.bocc = c->bocc; p.bn = c->bn; p.berr = c->berr;
+  p.err = c->err; p.gen_ptr = c->gen_dev;
+  p.urec = c->urec; p.irec = c->irec; p.inl = c->inl; p.trec = c->trec;
+  p.nextt = c->nextt;
+  p.task_list = c->task_list; p.task_cnt = c->task_cnt;
+  // 3 occurrences per thread in the sort, one thread per slot / triplet in the
+  // build: ~24 us for a 20-batch plan against ~32 us for 6 per thread / 256-thread
+  // builds (per-thread loops serialise the build's dependent loads)
+  if (B <= 512) {
+    k_bplan_sort<512, 3><<<nb, 512, 0, s>>>(p);
+    k_bplan_build<1024, 512><<<nb, 1024, 0, s>>>(p);
+  } else {
+    k_bplan_sort<1024, 3><<<nb, 1024, 0, s>>>(p);
+    k_bplan_build<1024, 1024><<<nb, 1024, 0, s>>>(p);
+  }
+  HIP_TRY(hipGetLastError());
+  c->bmask_dirty[cur] = 1;
+  c->bmask_dirty[oth] = 0;
+  c->plan_R = c->R;
+  c->plan_kind2 = 1;
+  c->plan_kb = kb;
+  c->task_lists = 1;
+  c->task_stride = p.stride;
+  c->lists = 0;
+  if (check) {
+    int32_t herr = 0;
+    HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ACF_CHECK(herr == 0, ACF_E_RANGE, "triplet index out of range (%s%s)",
+              (herr & 1) ? "user >= num_user_rows " : "", (herr & 2) ? "item >= num_item_rows" : "");
+  }
+  c->B = B;
+  c->nb = nb;
+  return ACF_OK;
+}
+
 // sorted keys -> head flags -> one scan -> per-side compaction
 template <class KT>
 static int plan_groups(acf_apr_ctx* c, const KT& ku, const KT& ki, int64_t E, int32_t nb,
@@ -2635,6 +2991,12 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->nb = 0;
   c->last_delta_batch = -1;
   const int32_t gen = ++c->gen;
+  {
+    const int packed = c->mapping == 2 || (c->mapping == 0 && B >= ACF_PACKED_MIN_BATCH);
+    const int32_t kb = (int32_t)bits_for((uint64_t)3 * B + 1);
+    if (!packed && c->plan_mode == 0 && B <= 1024 && kb + bits_for((uint64_t)nb + 1) <= 31 && bplan_ready(c))
+      return batch_plan(c, user, ipos, ineg, B, nb, gen, kb, check, s);
+  }
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
   // 32-bit keys (segment only, occurrence as the sort value) when they fit
   const uint32_t sb = std::max(bits_for((uint64_t)nb * (uint64_t)c->U1),
@@ -2787,6 +3149,7 @@ struct Kernels {
   void *clean_apr = nullptr, *clean_bpr = nullptr, *adv = nullptr, *flush = nullptr;
   void* ovl = nullptr;  // k_ovl (one wave per slot only)
   void* stream = nullptr;  // k_stream (one wave per slot, d <= 256)
+  void* stream_flush = nullptr;  // its write-back, k_stream_flush<LPR>
   int slots_per_wave = 1;
   int lists = 0;  // list kernels: slot waves stride over the plan's per-batch lists
 };
@@ -2825,7 +3188,10 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists) {
   } else {
     kernel_ptrs_team<LPR, NV, OPW>(k, fused);
     k->ovl = reinterpret_cast<void*>(&k_ovl<LPR, NV, OPW>);
-    if constexpr (NV == 1) k->stream = reinterpret_cast<void*>(&k_stream<LPR, NV, OPW>);
+    if constexpr (NV == 1) {
+      k->stream = reinterpret_cast<void*>(&k_stream<LPR, NV, OPW>);
+      k->stream_flush = reinterpret_cast<void*>(&k_stream_flush<LPR>);
+    }
     k->slots_per_wave = 1;
   }
   k->flush = reinterpret_cast<void*>(&k_flush);
@@ -2990,11 +3356,12 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     e1 = events ? events[2 * li + 1] : nullptr;
     if (kinds) kinds[li] = 2;
     ++li;
-    const dim3 fgrid(grid_for((int64_t)n * S));
+    typedef void (*FK)(StepArgs, uint32_t*);
+    const dim3 fgrid(grid_for((int64_t)n * S * c->lpr));  // one lane-group per slot
     if (e0)
-      hipExtLaunchKernelGGL(k_stream_flush, fgrid, block, 0, s, e0, e1, 0, a, c->epoch);
+      hipExtLaunchKernelGGL(reinterpret_cast<FK>(K.stream_flush), fgrid, block, 0, s, e0, e1, 0, a, c->epoch);
     else
-      hipLaunchKernelGGL(k_stream_flush, fgrid, block, 0, s, a, c->epoch);
+      hipLaunchKernelGGL(reinterpret_cast<FK>(K.stream_flush), fgrid, block, 0, s, a, c->epoch);
     HIP_TRY(hipGetLastError());
     return ACF_OK;
   }
@@ -3090,6 +3457,11 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   c->last_delta_batch = -1;
   prepare_stream(c, hp);
   if (!graph_mode) return run_loop(c, tb, hp, first, n, s, nullptr, nullptr);
+  {  // the streamed step is two launches: a graph buys nothing
+    Kernels K;
+    if (get_kernels(c, &K, c->fusion) == ACF_OK && use_stream(c, K, hp))
+      return run_loop(c, tb, hp, first, n, s, nullptr, nullptr);
+  }
   GraphKey key;
   memset(&key, 0, sizeof(key));
   key.ptrs[0] = tb->P; key.ptrs[1] = tb->Q; key.ptrs[2] = tb->accP; key.ptrs[3] = tb->accQ;
@@ -3117,6 +3489,13 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   }
   HIP_TRY(hipGraphLaunch(it->second, s));
   return ACF_OK;
+}
+
+extern "C" int acf_apr_train(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
+                             const int32_t* user, const int32_t* ipos, const int32_t* ineg, int32_t B,
+                             int32_t nb, int32_t check, int32_t graph_mode, void* stream_) {
+  ACF_RET(acf_apr_plan(c, user, ipos, ineg, B, nb, check, stream_));
+  return acf_apr_train_planned(c, tb, hp, 0, nb, graph_mode, stream_);
 }
 
 static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp, int32_t first,
@@ -3153,21 +3532,20 @@ static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_
 extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
                                     const acf_apr_hparams* hp, int32_t first, int32_t n,
                                     double* ms_out, int32_t* launches_out, void* stream_) {
-  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 3);
-}
-
-// v2: kinds clean / adv / flush / overlapped (k_ovl = adv(t) + clean(t+1)), the
-// launch sequence acf_apr_train_planned runs
-extern "C" int acf_apr_time_kernels_v2(acf_apr_ctx* c, const acf_apr_tables* tb,
-                                       const acf_apr_hparams* hp, int32_t first, int32_t n,
-                                       double* ms_out, int32_t* launches_out, void* stream_) {
-  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 4);
+  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 5);
 }
 
 extern "C" int acf_apr_set_slot_mapping(acf_apr_ctx* c, int32_t mode) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_CHECK(mode >= 0 && mode <= 2, ACF_E_INVALID, "slot mapping must be 0 (auto), 1 or 2, got %d", mode);
   c->mapping = mode;
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_set_plan_mode(acf_apr_ctx* c, int32_t mode) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(mode == 0 || mode == 1, ACF_E_INVALID, "plan mode must be 0 (auto) or 1 (sort plan)");
+  c->plan_mode = mode;
   return ACF_OK;
 }
 
@@ -3186,12 +3564,6 @@ extern "C" int acf_apr_set_stream(acf_apr_ctx* c, int32_t on) {
 
 // v3: kinds clean / adv / flush / overlapped / streamed (k_stream), the launch
 // sequence acf_apr_train_planned runs
-extern "C" int acf_apr_time_kernels_v3(acf_apr_ctx* c, const acf_apr_tables* tb,
-                                       const acf_apr_hparams* hp, int32_t first, int32_t n,
-                                       double* ms_out, int32_t* launches_out, void* stream_) {
-  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 5);
-}
-
 extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);

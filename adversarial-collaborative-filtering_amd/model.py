@@ -129,7 +129,8 @@ class MF:
         """Epoch trainer: chunks of `chunk` batches, next chunk planned while one trains."""
         p = self._pipe
         if p is None or p.batch_size != batch_size or p.chunk != chunk:
-            # concurrent planning: large batches and APR (k_stream); small BPR batches plan in line
+            # concurrent planning for large batches only (device-wide sort plan); small
+            # batches plan in line (batch-local plan, two launches per chunk)
             self._pipe = p = ops.PlanPipeline(self.num_user_rows, self.num_item_rows,
                                               self.embedding_size, batch_size, chunk, self.device,
                                               overlap=None)
@@ -206,9 +207,8 @@ class Session:
         u, i, j = fd.get("user_input"), fd.get("item_input_pos"), fd.get("item_input_neg")
         out = {}
         if any(isinstance(n, str) and n in ("update_P", "update_Q") for n in names):
-            if not m.adver and m.adv == "grad":
-                # the BPR graph has no update ops in the reference; keep TF's error class
-                raise ValueError("update_P/update_Q exist only in the APR graph (adver=1)")
+            # build_graph always creates the adversarial ops (APR.py:197-202), so a BPR
+            # graph runs them too: delta is computed, and its optimizer never reads it
             m.delta_update(u, i, j)
             out["update_P"] = out["update_Q"] = None
         if "optimizer" in names:

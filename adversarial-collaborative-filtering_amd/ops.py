@@ -19,6 +19,22 @@ CLIP_LO = -80.0   # APR.py:148
 CLIP_HI = 1e8
 
 
+class _Null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL = _Null()
+
+
+def _on(device: torch.device):
+    """torch.cuda.device(device) unless it is already current (a few us saved per call)."""
+    return _NULL if torch.cuda.current_device() == device.index else torch.cuda.device(device)
+
+
 def _stream_ptr(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
@@ -42,12 +58,25 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype, device: torch.devic
 
 def _idx(t, name, device) -> torch.Tensor:
     """Accept [N] or [N,1] int tensors/arrays (the placeholders are [None,1])."""
+    if (isinstance(t, torch.Tensor) and t.dtype == torch.int32 and t.dim() == 1 and t.device == device
+            and t.is_contiguous()):
+        return t
     if not isinstance(t, torch.Tensor):
         t = torch.as_tensor(t)
     t = t.reshape(-1)
     if t.dtype != torch.int32:
         t = t.to(torch.int32)
     return t.to(device, non_blocking=True).contiguous()
+
+
+class StepWaitError(RuntimeError):
+    """A streamed / overlapped step gave up waiting for a row (ACF_SPIN_LIMIT
+    polls): the tables of that call hold stale rows and must not be trusted."""
+
+    def __init__(self, bits: int):
+        self.bits = int(bits)
+        super().__init__(f"step error word {bits:#x}: a step kernel gave up waiting for a row version; "
+                         "the tables of this call are not trustworthy")
 
 
 @dataclass
@@ -65,11 +94,18 @@ class StepHParams:
     clip_hi: float = CLIP_HI
 
     def to_c(self) -> HParams:
+        key = (self.lr, self.eps, self.reg, self.reg_adv, self.adver, self.adv, self.seed, self.zero_delta,
+               self.clip_lo, self.clip_hi)
+        c = self.__dict__.get("_c")
+        if c is not None and c[0] == key:
+            return c[1]
         if self.adv not in ("grad", "random"):
             raise ValueError(f"adv must be 'grad' or 'random', got {self.adv!r}")
-        return HParams(self.lr, self.eps, self.reg, self.reg_adv, self.clip_lo, self.clip_hi,
-                       int(bool(self.adver)), 0 if self.adv == "grad" else 1,
-                       int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(bool(self.zero_delta)), 0)
+        h = HParams(self.lr, self.eps, self.reg, self.reg_adv, self.clip_lo, self.clip_hi,
+                    int(bool(self.adver)), 0 if self.adv == "grad" else 1,
+                    int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(bool(self.zero_delta)), 0)
+        self.__dict__["_c"] = (key, h)
+        return h
 
 
 class APRContext:
@@ -87,6 +123,7 @@ class APRContext:
         self.batch_size = 0
         self.n_batches = 0
         self._staged = None
+        self._tb_key, self._tb = None, None
 
     def __del__(self):
         try:
@@ -120,12 +157,43 @@ class APRContext:
         return nb
 
     def _tables(self, P, Q, accP, accQ) -> Tables:
+        key = (P.data_ptr(), Q.data_ptr(), accP.data_ptr(), accQ.data_ptr(), P.shape, Q.shape, accP.shape,
+               accQ.shape, P.dtype, Q.dtype, accP.dtype, accQ.dtype, P.device, Q.device, accP.device,
+               accQ.device, P.is_contiguous(), Q.is_contiguous(), accP.is_contiguous(), accQ.is_contiguous())
+        if self._tb_key == key:  # same tensors as the last validated call
+            return self._tb
         for t, n, rows in ((P, "embedding_P", self.U1), (Q, "embedding_Q", self.I1),
                            (accP, "accumulator_P", self.U1), (accQ, "accumulator_Q", self.I1)):
             _require(t, n, torch.float32, self.device, 2)
             if tuple(t.shape) != (rows, self.d):
                 raise ValueError(f"{n} has shape {tuple(t.shape)}, expected {(rows, self.d)}")
-        return Tables(P.data_ptr(), Q.data_ptr(), accP.data_ptr(), accQ.data_ptr())
+        self._tb = Tables(P.data_ptr(), Q.data_ptr(), accP.data_ptr(), accQ.data_ptr())
+        self._tb_key = key
+        return self._tb
+
+    def train_range(self, tables, hp: StepHParams, user: torch.Tensor, item_pos: torch.Tensor,
+                    item_neg: torch.Tensor, batch_size: int, first_batch: int, n_batches: int,
+                    graph: bool = True, check: bool = False) -> None:
+        """plan + train_planned of batches [first_batch, first_batch + n_batches) of
+        device int32 triplet streams, in ONE C call (acf_apr_train); the range is
+        addressed in place (no slicing)."""
+        B, nb = int(batch_size), int(n_batches)
+        for t, n in ((user, "user"), (item_pos, "item_pos"), (item_neg, "item_neg")):
+            if t.dtype != torch.int32 or t.device != self.device or not t.is_contiguous():
+                raise ValueError(f"{n} must be a contiguous int32 tensor on {self.device}")
+            if (first_batch + nb) * B > t.numel() or first_batch < 0:
+                raise ValueError(f"batches [{first_batch}, {first_batch + nb}) outside {n}")
+        if not self.fits(B, nb):
+            raise ValueError(f"plan of {nb} x {B} exceeds context capacity {self.max_batches} x "
+                             f"{self.max_batch_size}")
+        tb, h = self._tables(*tables), hp.to_c()
+        off = first_batch * B * 4
+        with _on(self.device):
+            call("acf_apr_train", self._ptr, ctypes.byref(tb), ctypes.byref(h), user.data_ptr() + off,
+                 item_pos.data_ptr() + off, item_neg.data_ptr() + off, B, nb, int(check), int(bool(graph)),
+                 torch.cuda.current_stream(self.device).cuda_stream)
+        self._staged = (user, item_pos, item_neg)
+        self.batch_size, self.n_batches = B, nb
 
     def delta_update(self, tables, hp: StepHParams, batch: int) -> None:
         tb, h = self._tables(*tables), hp.to_c()
@@ -152,6 +220,13 @@ class APRContext:
         m = {"auto": 0, "wave": 1, "group": 2}.get(mode, mode)
         call("acf_apr_set_slot_mapping", self._ptr, int(m))
 
+    def set_plan_mode(self, mode: str | int) -> None:
+        """'auto' (batch-local plan where it applies: one-wave-per-slot plans of
+        batches <= 1,024) | 'sort' (always the device-wide sort plan).  Both
+        write identical plans; 'sort' is for A/B and the equivalence test."""
+        m = {"auto": 0, "sort": 1}.get(mode, mode)
+        call("acf_apr_set_plan_mode", self._ptr, int(m))
+
     def set_fusion(self, on: bool) -> None:
         """Fuse triplets whose three rows occur once in their batch (default on;
         identical results either way).  Applies to train_planned / time_kernels."""
@@ -169,7 +244,7 @@ class APRContext:
         ms = (ctypes.c_double * 5)()
         cnt = (ctypes.c_int32 * 5)()
         with torch.cuda.device(self.device):
-            call("acf_apr_time_kernels_v3", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
+            call("acf_apr_time_kernels", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
                  _stream_ptr(self.device))
         return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush", "ovl", "stream"))}
 
@@ -221,11 +296,13 @@ class PlanPipeline:
     are independent calls of train_planned (each ends with its flush), so the
     result is the one of planning and training the chunks in sequence.
 
-    overlap=False plans on the caller's stream instead.  overlap=None decides per
-    run: concurrent planning for large batches and for APR (the streamed step
-    k_stream leaves room beside it: 102.4M -> 113.1M triplets/s at B = 512), on
-    the caller's stream for small BPR batches, whose short per-batch kernels a
-    concurrent plan slowed more than it saved.
+    overlap=False plans on the caller's stream instead.  overlap=None (default)
+    decides per run: concurrent planning for large batches (B >= 4,096: the
+    device-wide sort plan, ~40 us per batch); in line for smaller ones, whose
+    batch-local plan (two launches per chunk) costs less than the
+    events and stream hand-offs of planning beside the step, and never shares
+    the device with the persistent k_stream.  A run of a single chunk always
+    plans in line.
     """
 
     def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, batch_size: int,
@@ -261,6 +338,10 @@ class PlanPipeline:
         for c in self.ctx:
             c.set_slot_mapping(mode)
 
+    def set_plan_mode(self, mode) -> None:
+        for c in self.ctx:
+            c.set_plan_mode(mode)
+
     def _plan(self, k, u, i, j, b, n, check):
         B, c = self.batch_size, self.ctx[k % 2]
         s = slice(b * B, (b + n) * B)
@@ -287,13 +368,18 @@ class PlanPipeline:
             raise ValueError(f"batches [{first_batch}, {first_batch + n_batches}) outside the "
                              f"{total} batches of the stream")
         main = torch.cuda.current_stream(self.device)
-        self._ov = self.overlap if self.overlap is not None else (B >= 4096 or bool(hp.adver))
+        chunks = [(b, min(self.chunk, first_batch + n_batches - b))
+                  for b in range(first_batch, first_batch + n_batches, self.chunk)]
+        self._ov = (self.overlap if self.overlap is not None else B >= 4096) and len(chunks) > 1
+        if not self._ov:  # plan + train per chunk in one C call each, on the caller's stream
+            for k, (b, n) in enumerate(chunks):
+                self.ctx[k % 2].train_range(tables, hp, u, i, j, B, b, n, graph=graph, check=check)
+            self._staged = (u, i, j)
+            return
         if self._ov:
             ready = torch.cuda.Event()
             ready.record(main)  # triplets produced on the caller's stream
             self.side.wait_event(ready)
-        chunks = [(b, min(self.chunk, first_batch + n_batches - b))
-                  for b in range(first_batch, first_batch + n_batches, self.chunk)]
         planned = self._plan(0, u, i, j, *chunks[0], check)
         for k, (b, n) in enumerate(chunks):
             if planned is not None:

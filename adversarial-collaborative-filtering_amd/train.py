@@ -60,8 +60,10 @@ def _as_epoch(model, batches) -> EpochTriplets:
 
 def training_batch(model, sess, batches, adver=False, graph=True):
     """utils.py:106-140.  dns == 1: the epoch is planned in chunks (plan_chunk),
-    each replayed as one hipGraph (delta_update + optimizer_step per batch, in
-    batch order) while the next chunk is planned on a side stream.
+    each trained by the streamed step (APR) or replayed as one hipGraph
+    (delta_update + optimizer_step per batch, in batch order).  The step error
+    word is read once per epoch: a step that gave up waiting for a row version
+    raises StepWaitError instead of leaving silently stale rows.
     dns > 1: per batch, the highest-scoring of dns negatives under the current
     weights, then the optimizer step (the reference never runs update_P/update_Q
     on this branch, so the adversarial terms see delta = 0)."""
@@ -71,6 +73,9 @@ def training_batch(model, sess, batches, adver=False, graph=True):
         hp = model.hparams(adver=int(bool(adver)))
         pipe = model.pipeline(B, min(nb, plan_chunk(B)))
         pipe.run(model.tables, hp, ep.user, ep.item_pos, ep.item_neg, graph=graph, check=True)
+        errs = pipe.step_errors()  # one stream sync per epoch
+        if errs:
+            raise ops.StepWaitError(errs)
         return ep
     user_input, item_input_pos, user_dns_list, item_dns_list = batches
     hp = model.hparams(adver=int(bool(adver)))

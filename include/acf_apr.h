@@ -117,34 +117,29 @@ int acf_apr_train_planned(acf_apr_ctx* ctx, const acf_apr_tables* tables,
                           const acf_apr_hparams* hp, int32_t first_batch,
                           int32_t n_batches, int32_t graph_mode, void* stream);
 
+/* training_batch over a triplet range in ONE call (utils.py:106-119 for
+ * n_batches consecutive batches): acf_apr_plan(user, item_pos, item_neg,
+ * batch_size, n_batches, check) followed by acf_apr_train_planned over all the
+ * planned batches.  The triplet arrays are device pointers that must stay valid
+ * until the stream has run the call. */
+int acf_apr_train(acf_apr_ctx* ctx, const acf_apr_tables* tables, const acf_apr_hparams* hp,
+                  const int32_t* user, const int32_t* item_pos, const int32_t* item_neg,
+                  int32_t batch_size, int32_t n_batches, int32_t check, int32_t graph_mode,
+                  void* stream);
+
 /* Kernel timing for roofline accounting: runs planned batches
  * [first_batch, first_batch + n_batches) exactly like acf_apr_train_planned
  * (eager, same stream, same kernels, tables updated) but brackets every kernel
  * with hipExtLaunchKernelGGL start/stop events.  Writes, per kernel kind
- * k = 0 (clean pass), 1 (adversarial pass), 2 (Adagrad apply), the summed
- * kernel time in ms to ms_out[k] and the launch count to launches_out[k].
- * Synchronous.  Not part of the reference surface. */
+ * k = 0 (clean pass, or the fused BPR step), 1 (adversarial pass + Adagrad),
+ * 2 (write-back: k_flush / k_stream_flush), 3 (overlapped step k_ovl),
+ * 4 (streamed step k_stream), the summed kernel time in ms to ms_out[k] and
+ * the launch count to launches_out[k] (arrays of 5).  Synchronous.  Not part
+ * of the reference surface. */
 int acf_apr_time_kernels(acf_apr_ctx* ctx, const acf_apr_tables* tables,
                          const acf_apr_hparams* hp, int32_t first_batch,
                          int32_t n_batches, double* ms_out, int32_t* launches_out,
                          void* stream);
-
-/* As acf_apr_time_kernels, with the launch sequence acf_apr_train_planned
- * really runs (see acf_apr_set_step_overlap): ms_out / launches_out hold 4 kinds,
- * the fourth being the overlapped step kernel (adversarial pass of batch t +
- * clean pass of batch t+1 in one launch).  Not part of the reference surface. */
-int acf_apr_time_kernels_v2(acf_apr_ctx* ctx, const acf_apr_tables* tables,
-                            const acf_apr_hparams* hp, int32_t first_batch,
-                            int32_t n_batches, double* ms_out, int32_t* launches_out,
-                            void* stream);
-
-/* As acf_apr_time_kernels_v2 with a fifth kind, the streamed step kernel
- * (see acf_apr_set_stream); its write-back kernel counts as kind 2.  Not part
- * of the reference surface. */
-int acf_apr_time_kernels_v3(acf_apr_ctx* ctx, const acf_apr_tables* tables,
-                            const acf_apr_hparams* hp, int32_t first_batch,
-                            int32_t n_batches, double* ms_out, int32_t* launches_out,
-                            void* stream);
 
 /* How step kernels map unique rows ("slots") to lanes: 0 = auto (default: one
  * wavefront per slot below 4,096 triplets per batch, where hot rows have many
@@ -161,6 +156,14 @@ int acf_apr_set_slot_mapping(acf_apr_ctx* ctx, int32_t mode);
  * kernels' own, so on and off give identical bits.  The split per-batch calls
  * (delta_update / optimizer_step) never fuse.  Not part of the reference surface. */
 int acf_apr_set_fusion(acf_apr_ctx* ctx, int32_t on);
+
+/* Which planner acf_apr_plan uses: 0 = auto (the default: the batch-local plan,
+ * one workgroup per batch in two launches, for one-wavefront-per-slot plans of
+ * batches up to 1,024 triplets on tables whose batch bitmaps fit 64 MB; the
+ * device-wide sort plan otherwise), 1 = always the device-wide sort plan.  Both
+ * write identical records, task lists and write-back tables.  Not part of the
+ * reference surface (A/B and the planner-equivalence test). */
+int acf_apr_set_plan_mode(acf_apr_ctx* ctx, int32_t mode);
 
 /* Overlapped APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
  * environment ACF_STEP_OVERLAP=0 sets the default off).  For plans with one

@@ -53,3 +53,23 @@ def oracle():
 def dev():
     import torch
     return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def fp32_parity():
+    """Multi-step fp32 parity bar: every element within 1e-5
+    absolute of the oracle (scaled by max(1, max|want|)), and at most a 1e-5
+    fraction (>= 2 elements) outside rtol 1e-5 / atol 1e-6.  Single steps are
+    held to rtol 1e-5 / atol 1e-6 outright; this bar is for results after many
+    steps, where the adversarial map amplifies summation-order rounding in rows
+    whose clean gradient nearly cancels."""
+    import numpy as np
+
+    def check(got, want, name):
+        got = got.detach().cpu().numpy() if hasattr(got, "detach") else np.asarray(got)
+        err = np.abs(got.astype(np.float64) - want)
+        scale = max(1.0, float(np.abs(want).max()))
+        assert float(err.max()) <= 1e-5 * scale, f"{name}: max abs diff {err.max():.3e}"
+        bad = int((err > 1e-6 + 1e-5 * np.abs(want)).sum())
+        assert bad <= max(2, int(1e-5 * want.size)), f"{name}: {bad} of {want.size} elements outside 1e-5"
+    return check

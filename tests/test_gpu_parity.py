@@ -316,7 +316,7 @@ def test_piecewise_calls_equal_one_call(ops, oracle, dev, adver, mapping):
 
 
 @pytest.mark.parametrize("mapping", ["wave", "group"])
-def test_hot_rows_many_occurrences(ops, oracle, dev, mapping):
+def test_hot_rows_many_occurrences(ops, oracle, dev, mapping, fp32_parity):
     """A few rows with hundreds of occurrences per batch (overflow records,
     many rounds per wave / group) still match the oracle."""
     U1, I1, d, B, nb = 12, 9, 64, 1024, 2
@@ -328,7 +328,35 @@ def test_hot_rows_many_occurrences(ops, oracle, dev, mapping):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ctx.train_planned(tabs, ops.StepHParams(adver=1))
     for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
-        np.testing.assert_allclose(g.cpu().numpy(), w, rtol=1e-4, atol=1e-5, err_msg=n)
+        fp32_parity(g, w, n)
+
+
+@pytest.mark.parametrize("mapping", ["wave", "group"])
+@pytest.mark.parametrize("shape", ["hot", "large"])
+def test_single_step_strict(ops, oracle, dev, mapping, shape):
+    """One step of the shapes the multi-step tests hold to fp32_parity (hundreds
+    of occurrences per row; B = 8,192 on 200k x 100k tables) at rtol 1e-5 /
+    atol 1e-6 outright, losses included."""
+    if shape == "hot":
+        U1, I1, d, B = 12, 9, 64, 1024
+        P, Q, u, i, j = _problem(23, U1, I1, d, B, 1)
+    else:
+        U1, I1, d, B = 200_000, 100_000, 64, 8192
+        rng = np.random.default_rng(5)
+        P = (rng.standard_normal((U1, d)) * 0.1).astype(np.float32)
+        Q = (rng.standard_normal((I1, d)) * 0.1).astype(np.float32)
+        u = rng.integers(0, U1, B).astype(np.int32)
+        i = (rng.zipf(1.3, B) % I1).astype(np.int32)
+        j = rng.integers(0, I1, B).astype(np.int32)
+    want, lc_w, la_w, _ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=1))
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, 1, dev)
+    ctx.set_slot_mapping(mapping)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ctx.train_planned(tabs, ops.StepHParams(adver=1))
+    lc, la = ctx.losses()
+    for g, w, n in zip(tabs + [lc, la], list(want) + [lc_w, la_w], ("P", "Q", "accP", "accQ", "lc", "la")):
+        _close(g, w, n)
 
 
 def test_replan_reuses_graph(ops, oracle, dev):
@@ -349,7 +377,7 @@ def test_replan_reuses_graph(ops, oracle, dev):
 
 
 @pytest.mark.parametrize("d", [64, 128])
-def test_large_batch_auto_mapping_matches_oracle(ops, oracle, dev, d):
+def test_large_batch_auto_mapping_matches_oracle(ops, oracle, dev, d, fp32_parity):
     """B = 8,192 (auto -> one lane-group per slot) on 200k x 100k tables."""
     U1, I1, B, nb = 200_000, 100_000, 8192, 2
     rng = np.random.default_rng(d)
@@ -364,7 +392,7 @@ def test_large_batch_auto_mapping_matches_oracle(ops, oracle, dev, d):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ctx.train_planned(tabs, ops.StepHParams(adver=1))
     for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
-        np.testing.assert_allclose(g.cpu().numpy(), w, rtol=1e-4, atol=1e-6, err_msg=n)
+        fp32_parity(g, w, n)
 
 
 def _sparse_stream(seed, U1, I1, B, nb, hot=64, p_hot=0.05):
@@ -429,7 +457,7 @@ def test_fused_triplets_bit_identical_to_slot_path(ops, dev, d, adver, adv, mapp
 
 
 @pytest.mark.parametrize("adver", [0, 1])
-def test_fused_large_batch_matches_oracle(ops, oracle, dev, adver):
+def test_fused_large_batch_matches_oracle(ops, oracle, dev, adver, fp32_parity):
     """B = 8,192 on 400k x 300k tables (~85% fused triplets) vs the oracle."""
     U1, I1, d, B, nb = 400_000, 300_000, 64, 8192, 3
     u, i, j = _sparse_stream(40 + adver, U1, I1, B, nb, hot=256, p_hot=0.02)
@@ -444,7 +472,7 @@ def test_fused_large_batch_matches_oracle(ops, oracle, dev, adver):
     ctx.train_planned(tabs, ops.StepHParams(adver=adver))
     lc, la = ctx.losses()
     for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
-        np.testing.assert_allclose(g.cpu().numpy(), w, rtol=1e-4, atol=1e-6, err_msg=n)
+        fp32_parity(g, w, n)
     _close(lc, lc_w, "loss_clean")
     if adver:
         _close(la, la_w, "loss_adv")
