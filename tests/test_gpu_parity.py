@@ -335,8 +335,11 @@ def test_hot_rows_many_occurrences(ops, oracle, dev, mapping, fp32_parity):
 @pytest.mark.parametrize("shape", ["hot", "large"])
 def test_single_step_strict(ops, oracle, dev, mapping, shape):
     """One step of the shapes the multi-step tests hold to fp32_parity (hundreds
-    of occurrences per row; B = 8,192 on 200k x 100k tables) at rtol 1e-5 /
-    atol 1e-6 outright, losses included."""
+    of occurrences per row; B = 8,192 on 200k x 100k tables), losses included, at
+    rtol max(1e-5, 2 n u) / atol 1e-6: n = the most terms any row sums (its
+    occurrences, x2 for a user's pos and neg branch), u = 2^-24.  Two orders of
+    an n-term fp32 sum may differ by 2 gamma_n = 2 n u relative to sum |terms|
+    (Higham); at n ~ 230 (the hot shape) that is 2.7e-5, above a flat 1e-5."""
     if shape == "hot":
         U1, I1, d, B = 12, 9, 64, 1024
         P, Q, u, i, j = _problem(23, U1, I1, d, B, 1)
@@ -355,8 +358,10 @@ def test_single_step_strict(ops, oracle, dev, mapping, shape):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ctx.train_planned(tabs, ops.StepHParams(adver=1))
     lc, la = ctx.losses()
+    n_terms = max(2 * np.bincount(u).max(), np.bincount(np.concatenate([i, j])).max())
+    rtol = max(RTOL, 2 * n_terms * 2.0 ** -24)
     for g, w, n in zip(tabs + [lc, la], list(want) + [lc_w, la_w], ("P", "Q", "accP", "accQ", "lc", "la")):
-        _close(g, w, n)
+        np.testing.assert_allclose(g.cpu().numpy(), w, rtol=rtol, atol=ATOL, err_msg=f"{n} (rtol {rtol:.1e})")
 
 
 def test_replan_reuses_graph(ops, oracle, dev):
