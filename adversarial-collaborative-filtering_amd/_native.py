@@ -66,6 +66,12 @@ SIGNATURES = {
     "acf_eval_positions_list": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P]),
     "acf_sample_epoch": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P, _U64, _I32, _I32, _P, _P,
                                         _P, _P]),
+    "acf_gather_bpr_fwd_bwd": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _P, _I64, _F, _F, _P, _P, _P,
+                                              _P, _P, _P, _P]),
+    "acf_row_segment_sum_workspace": (ctypes.c_int, [_I64, ctypes.POINTER(ctypes.c_size_t)]),
+    "acf_row_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _I64, _P, ctypes.c_size_t, _P, _P, _P, _P, _P]),
+    "acf_l2norm_perturb": (ctypes.c_int, [_P, _I64, _I32, _F, _P, _P]),
+    "acf_sparse_adagrad_apply": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _I64, _F, _P]),
     "acf_dns_select": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I64, _I32, _P, _P]),
 }
 

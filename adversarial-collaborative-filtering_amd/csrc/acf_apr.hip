@@ -64,6 +64,17 @@ static int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
+// for the other translation units of the library (acf_ops.hip)
+int acf_set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
 #define HIP_TRY(expr)                                                          \
   do {                                                                         \
     hipError_t e_ = (expr);                                                    \
@@ -77,185 +88,9 @@ static int set_error(int code, const char* fmt, ...) {
   } while (0)
 
 // ---------------------------------------------------------------------------
-// device helpers
+// device helpers (row groups, the TF-order dot product, BPR term, RNG)
 // ---------------------------------------------------------------------------
-// A table row of `d` floats is held by a row-group of LPR lanes, NV float4 per
-// lane: lane l owns float4 chunks c = l + LPR*v.  LPR is a power of two <= 64,
-// so row-groups never straddle a wavefront and reduce with __shfl_xor.
-template <int NV>
-struct RowV {
-  float4 v[NV];
-};
-
-template <int LPR, int NV>
-__device__ __forceinline__ RowV<NV> load_row(const float* __restrict__ base, int64_t row,
-                                             int d, int l) {
-  RowV<NV> r;
-  const float* p = base + row * (int64_t)d;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    int c = l + LPR * v;
-    if (c * 4 < d)
-      r.v[v] = *reinterpret_cast<const float4*>(p + c * 4);
-    else
-      r.v[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  return r;
-}
-
-template <int LPR, int NV>
-__device__ __forceinline__ void store_row(float* __restrict__ base, int64_t row, int d, int l,
-                                          const RowV<NV>& r) {
-  float* p = base + row * (int64_t)d;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    int c = l + LPR * v;
-    if (c * 4 < d) *reinterpret_cast<float4*>(p + c * 4) = r.v[v];
-  }
-}
-
-// store_row with device-scope write-through stores (sc1): once the wave's
-// vmcnt drains they are visible to every XCD, with no L2 write-back (the
-// release fence a flag would otherwise need writes back the whole L2).
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-template <int LPR, int NV>
-__device__ __forceinline__ void store_row_wt(float* __restrict__ base, int64_t row, int d, int l,
-                                             const RowV<NV>& r) {
-  float* p = base + row * (int64_t)d;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    int c = l + LPR * v;
-    if (c * 4 < d) {
-      const f32x4 x = {r.v[v].x, r.v[v].y, r.v[v].z, r.v[v].w};
-      // s_nop 1 inside the string: without it hipcc's next instruction may
-      // overwrite the data registers before the store has read them (MI355X
-      // guide, inline-asm stores)
-      asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p + c * 4), "v"(x) : "memory");
-    }
-  }
-}
-
-template <int NV>
-__device__ __forceinline__ RowV<NV> zero_row() {
-  RowV<NV> r;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) r.v[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-  return r;
-}
-
-template <int NV>
-__device__ __forceinline__ RowV<NV> add_row(const RowV<NV>& a, const RowV<NV>& b) {
-  RowV<NV> r;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    r.v[v].x = a.v[v].x + b.v[v].x;
-    r.v[v].y = a.v[v].y + b.v[v].y;
-    r.v[v].z = a.v[v].z + b.v[v].z;
-    r.v[v].w = a.v[v].w + b.v[v].w;
-  }
-  return r;
-}
-
-// acc += s * x with the product rounded first (TF's IndexedSlices sums are of
-// rounded products, so contributions that cancel, e.g. item i == j, cancel
-// exactly instead of leaving an fma residue that l2_normalize would blow up)
-template <int NV>
-__device__ __forceinline__ void axpy_row(RowV<NV>& acc, float s, const RowV<NV>& x) {
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    acc.v[v].x = acc.v[v].x + s * x.v[v].x;
-    acc.v[v].y = acc.v[v].y + s * x.v[v].y;
-    acc.v[v].z = acc.v[v].z + s * x.v[v].z;
-    acc.v[v].w = acc.v[v].w + s * x.v[v].w;
-  }
-}
-
-template <int NV>
-__device__ __forceinline__ RowV<NV> scale_row(const RowV<NV>& a, float s) {
-  RowV<NV> r;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    r.v[v].x = a.v[v].x * s;
-    r.v[v].y = a.v[v].y * s;
-    r.v[v].z = a.v[v].z * s;
-    r.v[v].w = a.v[v].w * s;
-  }
-  return r;
-}
-
-// DPP lane exchange inside a 16-lane row (v_add_f32_dpp, no LDS round trip)
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-// Sum over the LPR lanes of a row-group.  xor1 / xor2 (quad_perm), then the
-// half-row and row mirrors (lane i <-> 7-i, 15-i): after each step the lanes of
-// the merged block hold identical bits, so pairing by mirror equals pairing by
-// xor.  Beyond 16 lanes, __shfl_xor.  Every lane ends with the same bits.
-template <int LPR>
-__device__ __forceinline__ float group_sum(float s) {
-  if (LPR >= 2) s += dpp<0xB1>(s);   // quad_perm [1,0,3,2]
-  if (LPR >= 4) s += dpp<0x4E>(s);   // quad_perm [2,3,0,1]
-  if (LPR >= 8) s += dpp<0x141>(s);  // row_half_mirror
-  if (LPR >= 16) s += dpp<0x140>(s); // row_mirror
-  if (LPR >= 32) s += __shfl_xor(s, 16, 64);
-  if (LPR >= 64) s += __shfl_xor(s, 32, 64);
-  return s;
-}
-
-// Row dot product (p*q)·h of APR.py:127: per-lane partial sums of rounded
-// products, then the row-group sum.
-template <int LPR, int NV>
-__device__ __forceinline__ float dot_row(const RowV<NV>& a, const RowV<NV>& b) {
-  float s = 0.f;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {  // (p*q) rounded, then summed (APR.py:127)
-    s = s + a.v[v].x * b.v[v].x;
-    s = s + a.v[v].y * b.v[v].y;
-    s = s + a.v[v].z * b.v[v].z;
-    s = s + a.v[v].w * b.v[v].w;
-  }
-  return group_sum<LPR>(s);
-}
-
-// softplus threshold of TF's SoftplusOp: log(FLT_EPSILON) + 2.
-#define ACF_SOFTPLUS_T 13.942385f
-
-// d/dx of softplus(-clip(x)) (APR.py:148-150): TF SoftplusGrad gives
-// 1/(exp(r)+1) on features -r, negated by the Neg; clip_by_value passes the
-// gradient only where lo <= x <= hi.  Also returns the loss term.
-__device__ __forceinline__ void bpr_term(float x, float lo, float hi, float& g, float& loss) {
-  float xc = fminf(fmaxf(x, lo), hi);
-  bool pass = (x >= lo) && (x <= hi);
-  float ex = expf(xc);
-  g = pass ? -__builtin_amdgcn_rcpf(ex + 1.0f) : 0.0f;  // v_rcp_f32 (1 ulp)
-  float f = -xc;
-  loss = f > ACF_SOFTPLUS_T ? f : (f < -ACF_SOFTPLUS_T ? expf(f) : logf(expf(f) + 1.0f));
-}
-
-// counter-based RNG (splitmix64 finaliser over a mixed counter)
-__device__ __host__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ float u01(uint64_t h) {  // (0,1]
-  return ((float)(h >> 40) + 1.0f) * (1.0f / 16777216.0f);
-}
-
-// tf.truncated_normal(stddev) element: normal redrawn while |z| > 2 sigma.
-__device__ __forceinline__ float trunc_normal(uint64_t key, float stddev) {
-  for (uint32_t a = 0;; ++a) {
-    uint64_t h1 = mix64(key ^ mix64(2ull * a + 1));
-    uint64_t h2 = mix64(key ^ mix64(2ull * a + 2));
-    float r = sqrtf(-2.0f * logf(u01(h1)));
-    float z = r * cosf(6.283185307179586f * u01(h2));
-    if (fabsf(z) <= 2.0f || a > 64) return z * stddev;
-  }
-}
+#include "acf_rows.h"
 
 // ---------------------------------------------------------------------------
 // plan kernels
@@ -1445,10 +1280,10 @@ struct Geo {
 // run (APR.py:180-191, adv == "random").  Out of line: the gradient mode never
 // runs it and it would otherwise bloat every step kernel's instruction stream.
 template <int LPR, int NV>
-__device__ __noinline__ RowV<NV> random_delta(uint64_t seed, int32_t t, int32_t d, float eps, int is_item,
-                                              int32_t row, int l) {
+__device__ __noinline__ RowV<NV> random_delta(uint64_t seed, uint32_t call, int32_t t, int32_t d, float eps,
+                                              int is_item, int32_t row, int l) {
   RowV<NV> z;
-  const uint64_t rk = mix64(seed ^ mix64(((uint64_t)t << 1) | (is_item ? 1 : 0))) ^
+  const uint64_t rk = mix64(seed ^ mix64(((uint64_t)call << 33) ^ (((uint64_t)t << 1) | (is_item ? 1 : 0)))) ^
                       mix64((uint64_t)row * 0x100000001B3ull);
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
@@ -1475,7 +1310,9 @@ __device__ __forceinline__ RowV<NV> make_delta(const StepArgs& a, const RowV<NV>
     const float inv = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-12f));
     return scale_row(scale_row(G, inv), a.eps);
   }
-  return random_delta<LPR, NV>(a.seed, a.t, a.d, a.eps, is_item, row, l);
+  // keyed on the context's call counter too (advanced by every call's write-back
+  // kernel), so every run draws fresh noise, as truncated_normal does per sess.run
+  return random_delta<LPR, NV>(a.seed, *a.epoch, a.t, a.d, a.eps, is_item, row, l);
 }
 
 // A fused triplet (fuse_info): its whole step in one lane-group.  The operation
@@ -2373,6 +2210,8 @@ __global__ void __launch_bounds__(256) k_adv_list(StepArgs a) {
 // one wave per slot.
 __global__ void __launch_bounds__(256) k_flush(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  // the call counter (random delta); every kernel of this call has read it
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(const_cast<uint32_t*>(a.epoch), 1u);
   flush_slot(a, a.t, a.wnew_cur, wave, threadIdx.x & 63, 64);
 }
 
@@ -2848,11 +2687,13 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipStreamCreate failed");
   }
-  // generation 0 never matches a plan: zeroed inline / fused-triplet records read as absent
+  // generation 0 never matches a plan: zeroed inline / fused-triplet records read as absent;
+  // the epoch (version tag and call counter) starts at 1: zeroed version granules never match
+  const uint32_t kOne = 1;
   if (hipMemset(c->inl, 0, (size_t)maxNB * S * c->R * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->trec, 0, (size_t)maxE * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->gen_dev, 0, 16) != hipSuccess ||
-      hipMemset(c->epoch, 0, 16) != hipSuccess || hipMemset(c->nextt, 0, 3 * maxE * sizeof(int32_t)) != hipSuccess ||
+      hipMemcpy(c->epoch, &kOne, sizeof(kOne), hipMemcpyHostToDevice) != hipSuccess || hipMemset(c->nextt, 0, 3 * maxE * sizeof(int32_t)) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipMemset failed");
@@ -3276,12 +3117,9 @@ static int stream_ready(acf_apr_ctx* c, const Kernels& K) {
   if (dalloc(c, &c->ver_w, n) != ACF_OK || dalloc(c, &c->ver_a, n) != ACF_OK ||
       dalloc(c, &c->ver_d, n) != ACF_OK)
     return 0;
-  // tag 0 never matches: the epoch starts at 1
-  const uint32_t one = 1;
+  // tag 0 never matches: the epoch starts at 1 (acf_apr_create)
   if (hipMemset(c->ver_w, 0, n * 8) != hipSuccess || hipMemset(c->ver_a, 0, n * 8) != hipSuccess ||
-      hipMemset(c->ver_d, 0, n * 8) != hipSuccess ||
-      hipMemcpy(c->epoch, &one, sizeof(one), hipMemcpyHostToDevice) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess) {
+      hipMemset(c->ver_d, 0, n * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     (void)hipGetLastError();
     return 0;
   }

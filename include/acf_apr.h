@@ -259,6 +259,49 @@ int acf_dns_select(const float* P, const float* Q, int64_t num_user_rows,
                    const int32_t* cand, int64_t n, int32_t dns, int32_t* out_neg,
                    void* stream);
 
+/* ---- the step decomposed into TF's ops (csrc/acf_ops.hip) ----------------
+ * The fused step above is the training path; these expose its pieces one
+ * kernel each, with TF's data flow, for callers that compose the step (the
+ * PyTorch custom ops acf::gather_bpr_fwd_bwd, row_segment_sum, l2norm_perturb,
+ * sparse_adagrad_apply) and for op-level tests.  All asynchronous on `stream`. */
+
+/* The inference gathers + BPR loss of APR.py:121-150 and the gradient of the
+ * loss w.r.t. the gathered rows, as TF's IndexedSlices (APR.py:183): for each of
+ * n triplets, loss[b] = softplus(-clip(x_b)), x[b] = p.q_i - p.q_j, and
+ *   P slices: p_idx = [u ; u],  p_val = [g*q_i ; -g*q_j]   ([2n], [2n, dim])
+ *   Q slices: q_idx = [i ; j],  q_val = [g*p ; -g*p]
+ * with g = d loss / d x (zero outside the clip range): pos-branch lookups
+ * first, then neg-branch, each product rounded as TF's Mul. */
+int acf_gather_bpr_fwd_bwd(const float* P, const float* Q, int64_t num_user_rows,
+                           int64_t num_item_rows, int32_t dim, const int32_t* user,
+                           const int32_t* item_pos, const int32_t* item_neg, int64_t n,
+                           float clip_lo, float clip_hi, float* loss, float* x,
+                           int32_t* p_idx, float* p_val, int32_t* q_idx, float* q_val,
+                           void* stream);
+
+/* IndexedSlices -> unique rows (unsorted_segment_sum behind APR.py:183-187 and
+ * the optimizer's dedup, APR.py:195): the m (index, value-row) pairs become
+ * *out_k <= m unique indices in ascending order (out_uniq), each with the
+ * sequential sum of its value rows in input order (out_sum [m, dim], first
+ * *out_k rows used) and their count.  Indices must lie in [0, num_rows).
+ * out_k is a DEVICE int64.  workspace: acf_row_segment_sum_workspace(m). */
+int acf_row_segment_sum_workspace(int64_t m, size_t* bytes);
+int acf_row_segment_sum(const int32_t* idx, const float* vals, int64_t m, int32_t dim,
+                        int64_t num_rows, void* workspace, size_t workspace_bytes,
+                        int32_t* out_uniq, float* out_sum, int32_t* out_count,
+                        int64_t* out_k, void* stream);
+
+/* delta = eps * l2_normalize(g, 1) = eps * g * rsqrt(max(sum g^2, 1e-12)) for k
+ * rows (APR.py:186-191). */
+int acf_l2norm_perturb(const float* g, int64_t k, int32_t dim, float eps, float* out,
+                       void* stream);
+
+/* TF SparseApplyAdagrad on k UNIQUE rows idx of W / acc ([rows, dim]) with
+ * gradient rows g [k, dim]: acc += g^2; W -= lr * g * rsqrt(acc) (APR.py:195). */
+int acf_sparse_adagrad_apply(float* W, float* acc, int64_t rows, int32_t dim,
+                             const int32_t* idx, const float* g, int64_t k, float lr,
+                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,8 +47,49 @@ typedef struct {
   int32_t adver;      /* APR graph (1) or BPR graph (0) */
   int32_t zero_delta; /* dns>1 branch: delta tables never assigned (stay 0) */
   int32_t dense;      /* 1: reference's dense delta work (see header) */
-  int32_t reserved;
+  int32_t adv_mode;   /* 0: adv = "grad" (APR.py:180-191); 1: adv = "random" (APR.py:170-177) */
+  uint32_t call;      /* random mode: the context's call counter the HIP step read */
+  int32_t t;          /* random mode: batch index inside the planned range */
+  uint64_t seed;      /* random mode: hparams seed */
 } oracle_hparams;
+
+/* adv = "random" (APR.py:170-177): delta = eps * l2_normalize(truncated_normal(stddev
+ * 0.01)), redrawn every run.  TF's Philox stream cannot be reproduced (TF is absent,
+ * and the reference's own random branch assigns a [U, d] draw to a [U+1, d]
+ * variable and does not build), so this restates the HIP path's counter-based
+ * draw: splitmix64 keys over (seed, call counter, batch, side, row, element),
+ * Box-Muller normals redrawn beyond 2 sigma; parity is with that definition. */
+static uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static float u01(uint64_t h) { return ((float)(h >> 40) + 1.0f) * (1.0f / 16777216.0f); }
+
+static float trunc_normal(uint64_t key, float stddev) {
+  for (uint32_t a = 0;; ++a) {
+    uint64_t h1 = mix64(key ^ mix64(2ull * a + 1));
+    uint64_t h2 = mix64(key ^ mix64(2ull * a + 2));
+    float r = sqrtf(-2.0f * logf(u01(h1)));
+    float z = r * cosf(6.283185307179586f * u01(h2));
+    if (fabsf(z) <= 2.0f || a > 64) return z * stddev;
+  }
+}
+
+static void random_delta(const oracle_hparams* hp, int is_item, int32_t row, int d, float* out) {
+  const uint64_t rk = mix64(hp->seed ^ mix64(((uint64_t)hp->call << 33) ^
+                                             (((uint64_t)hp->t << 1) | (uint64_t)is_item))) ^
+                      mix64((uint64_t)row * 0x100000001B3ull);
+  float ss = 0.f;
+  for (int k = 0; k < d; ++k) {
+    out[k] = trunc_normal(rk ^ mix64((uint64_t)k), 0.01f);
+    ss = ss + out[k] * out[k];
+  }
+  float inv = 1.0f / sqrtf(ss > 1e-12f ? ss : 1e-12f);
+  for (int k = 0; k < d; ++k) out[k] = (out[k] * inv) * hp->eps;
+}
 
 #define SOFTPLUS_T 13.942385f
 
@@ -202,6 +243,10 @@ int oracle_apr_batch(float* P, float* Q, float* accP, float* accQ, int64_t U1, i
             dst[t][(size_t)s * d + k] = hp->zero_delta ? 0.f : (x[k] * inv) * hp->eps;
         }
     }
+    if (hp->adv_mode == 1 && !hp->zero_delta) {
+      for (int s = 0; s < RU.n; ++s) random_delta(hp, 0, RU.rows[s], d, dU + (size_t)s * d);
+      for (int s = 0; s < RI.n; ++s) random_delta(hp, 1, RI.rows[s], d, dI + (size_t)s * d);
+    }
     if (delta_P)
       for (int s = 0; s < RU.n; ++s)
         memcpy(delta_P + (int64_t)RU.rows[s] * d, dU + (size_t)s * d, sizeof(float) * d);
@@ -286,9 +331,11 @@ int oracle_apr_batch(float* P, float* Q, float* accP, float* accQ, int64_t U1, i
 int oracle_apr_train(float* P, float* Q, float* accP, float* accQ, int64_t U1, int64_t I1, int d,
                      const int32_t* u, const int32_t* ip, const int32_t* in, int B, int n_batches,
                      const oracle_hparams* hp) {
+  oracle_hparams h = *hp;
   for (int t = 0; t < n_batches; ++t) {
     int64_t o = (int64_t)t * B;
-    int r = oracle_apr_batch(P, Q, accP, accQ, U1, I1, d, u + o, ip + o, in + o, B, hp, NULL, NULL,
+    h.t = hp->t + t;
+    int r = oracle_apr_batch(P, Q, accP, accQ, U1, I1, d, u + o, ip + o, in + o, B, &h, NULL, NULL,
                              NULL, NULL);
     if (r) return r;
   }

@@ -37,7 +37,8 @@ class _OHP(ctypes.Structure):
         ("lr", ctypes.c_float), ("eps", ctypes.c_float), ("reg", ctypes.c_float),
         ("reg_adv", ctypes.c_float), ("clip_lo", ctypes.c_float), ("clip_hi", ctypes.c_float),
         ("adver", ctypes.c_int32), ("zero_delta", ctypes.c_int32), ("dense", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("adv_mode", ctypes.c_int32), ("call", ctypes.c_uint32), ("t", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
     ]
 
 
@@ -51,6 +52,10 @@ class HParams:
     clip_hi: float = 1e8
     adver: int = 1
     zero_delta: int = 0
+    adv: str = "grad"   # "grad" | "random" (APR.py:170-191)
+    seed: int = 0       # random mode: the HIP step's hparams seed ...
+    call: int = 1       # ... the context's call counter (1 for a fresh context's first call) ...
+    t: int = 0          # ... and the batch index inside the planned range (apr_batch)
 
 
 def _f32p(a):
@@ -99,8 +104,11 @@ class COracle:
 
     @staticmethod
     def _hp(hp: HParams, dense: bool) -> _OHP:
+        if hp.adv not in ("grad", "random"):
+            raise ValueError(f"adv must be 'grad' or 'random', got {hp.adv!r}")
         return _OHP(hp.lr, hp.eps, hp.reg, hp.reg_adv, hp.clip_lo, hp.clip_hi, int(hp.adver),
-                    int(hp.zero_delta), int(dense), 0)
+                    int(hp.zero_delta), int(dense), 0 if hp.adv == "grad" else 1, int(hp.call) & 0xFFFFFFFF,
+                    int(hp.t), int(hp.seed) & 0xFFFFFFFFFFFFFFFF)
 
     def apr_batch(self, P, Q, accP, accQ, u, i, j, hp: HParams, dense=False, want_delta=False):
         """One training_batch iteration, in place.  Returns (loss_clean, loss_adv, dP, dQ)."""

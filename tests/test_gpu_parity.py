@@ -136,6 +136,62 @@ def test_random_delta_has_norm_eps(ops, dev):
     assert float(dP[torch.tensor(untouched, device=dev)].abs().max()) == 0.0 if len(untouched) else True
 
 
+@pytest.mark.parametrize("stream", [False, True])
+@pytest.mark.parametrize("d", [16, 64])
+def test_random_delta_matches_oracle(ops, oracle, dev, stream, d):
+    """adv = "random" (APR.py:170-177) against the oracle's restatement of the
+    same counter-based draw: delta rows of the split calls, then whole calls
+    (k_stream or two kernels per step; fused triplets on) over 4 batches.  A
+    fresh context's first call reads call counter 1, its second call 2."""
+    U1, I1, B, nb = 50, 40, 64, 4
+    P, Q, u, i, j = _problem(8 + d, U1, I1, d, B, nb, dup_items=True)
+    hp = ops.StepHParams(adver=1, adv="random", seed=77)
+    # split calls, batch 0: delta tables
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    tabs = _gpu_tables(P, Q, dev)
+    ctx.delta_update(tabs, hp, 0)
+    dP, dQ = ctx.delta_tables()
+    rP, rQ = P.copy(), Q.copy()
+    aP, aQ = np.full(P.shape, 0.1, np.float32), np.full(Q.shape, 0.1, np.float32)
+    _, _, wdP, wdQ = oracle.apr_batch(rP, rQ, aP, aQ, u[:B], i[:B], j[:B],
+                                      HParams(adver=1, adv="random", seed=77, call=1, t=0), want_delta=True)
+    _close(dP, wdP, "random delta_P")
+    _close(dQ, wdQ, "random delta_Q")
+    # whole calls: a fresh context, two calls over the same 4 batches (counter 1, then 2)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_stream(stream)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    tabs = _gpu_tables(P, Q, dev)
+    rP, rQ = P.copy(), Q.copy()
+    aP, aQ = np.full(P.shape, 0.1, np.float32), np.full(Q.shape, 0.1, np.float32)
+    for call in (1, 2):
+        ctx.train_planned(tabs, hp)
+        oracle.apr_train(rP, rQ, aP, aQ, u, i, j, B, HParams(adver=1, adv="random", seed=77, call=call))
+        for g, w, n in zip(tabs, (rP, rQ, aP, aQ), ("P", "Q", "accP", "accQ")):
+            _close(g, w, f"call {call} {n}")
+    assert ctx.step_errors() == 0
+
+
+def test_random_delta_redrawn_every_call(ops, dev):
+    """The same batch stepped twice draws different noise (truncated_normal is
+    re-evaluated by every sess.run in the reference)."""
+    U1, I1, d, B = 30, 30, 32, 32
+    P, Q, u, i, j = _problem(4, U1, I1, d, B, 1)
+    ctx = ops.APRContext(U1, I1, d, B, 1, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    hp = ops.StepHParams(adver=1, adv="random", seed=9)
+    tabs = _gpu_tables(P, Q, dev)
+    draws = []
+    for _ in range(2):
+        ctx.delta_update(tabs, hp, 0)
+        draws.append(ctx.delta_tables()[0].clone())
+        ctx.optimizer_step(tabs, hp, 0)
+    rows = torch.tensor(np.unique(u), device=dev)
+    assert not torch.equal(draws[0][rows], draws[1][rows])
+    np.testing.assert_allclose(torch.linalg.vector_norm(draws[1][rows], dim=1).cpu().numpy(), 0.5, rtol=1e-5)
+
+
 def test_forward_matches_oracle(ops, oracle, dev):
     U1, I1, d, B, nb = 100, 80, 64, 50, 6
     P, Q, u, i, j = _problem(21, U1, I1, d, B, nb)
@@ -441,11 +497,15 @@ def test_fused_triplets_bit_identical_to_slot_path(ops, dev, d, adver, adv, mapp
     P = (rng.standard_normal((U1, d)) * 0.2).astype(np.float32)
     Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
     hp = ops.StepHParams(adver=adver, adv=adv, reg=0.01, seed=5)
-    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
-    ctx.set_slot_mapping(mapping)
-    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     runs = []
-    for fuse, pieces in ((False, [(0, nb)]), (True, [(0, nb)]), (True, [(0, 1), (1, 3), (4, 2)])):
+    # "random" draws fresh noise every call (the call counter is part of its key),
+    # so piecewise calls are compared only in gradient mode; a fresh context per
+    # run starts every run at the same counter
+    cases = ((False, [(0, nb)]), (True, [(0, nb)])) + ((True, [(0, 1), (1, 3), (4, 2)]),) * (adv == "grad")
+    for fuse, pieces in cases:
+        ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+        ctx.set_slot_mapping(mapping)
+        ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
         ctx.set_fusion(fuse)
         tabs = _gpu_tables(P, Q, dev)
         for first, n in pieces:

@@ -112,3 +112,22 @@ def test_product_never_imports_the_neumf_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(root, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+\S*neumf_oracle", src, re.M), f
+
+
+def test_torch_custom_ops_register():
+    """lib/libacf_torch.so registers every acf:: op of SURVEY §8(b) (loads without a GPU)."""
+    import importlib
+    tops = importlib.import_module("adversarial-collaborative-filtering_amd.torch_ops")
+    acf = tops.load()
+    for name in tops.OPS:
+        assert hasattr(acf, name), name
+    schema = str(acf.bpr_apr_step.default._schema)
+    assert "Tensor(a!) P" in schema and "-> (Tensor loss_clean, Tensor loss_adv, Tensor n_correct)" in schema
+
+
+def test_torch_custom_ops_refuse_cpu_tensors():
+    import importlib
+    import torch
+    acf = importlib.import_module("adversarial-collaborative-filtering_amd.torch_ops").load()
+    with pytest.raises(Exception):
+        acf.l2norm_perturb(torch.zeros(2, 8), 0.5)

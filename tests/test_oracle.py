@@ -208,3 +208,33 @@ def test_oracle_eval_matches_reference_sample_mode(oracle):
     np.testing.assert_array_equal(pos, _ref_positions(z, "sample"))
     hr, ndcg, auc = eval_metrics(pos, z["sample_ncand"], 10)
     np.testing.assert_allclose(np.stack([hr, ndcg, auc], 1), z["sample_raw"], rtol=1e-12)
+
+
+def test_random_delta_mode(oracle):
+    """adv = "random" (APR.py:170-177): every touched row's delta has norm eps and
+    untouched rows stay 0; the draw depends on (seed, call, batch) and not on the
+    gradient; the components look like a normalised N(0,1) sample (mean ~0,
+    variance ~eps^2/d)."""
+    rng = np.random.default_rng(0)
+    U1, I1, d, B = 300, 200, 64, 256
+    P = (rng.standard_normal((U1, d)) * 0.1).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.1).astype(np.float32)
+    u, i, j = (rng.integers(0, N, B).astype(np.int32) for N in (U1, I1, I1))
+
+    def draw(**kw):
+        hp = HParams(adver=1, adv="random", seed=5, **kw)
+        tabs = [P.copy(), Q.copy(), np.full(P.shape, 0.1, np.float32), np.full(Q.shape, 0.1, np.float32)]
+        _, _, dP, dQ = oracle.apr_batch(*tabs, u, i, j, hp, want_delta=True)
+        return dP, dQ
+
+    dP, dQ = draw(call=1, t=0)
+    touched = np.zeros(U1, bool)
+    touched[u] = True
+    np.testing.assert_allclose(np.linalg.norm(dP[touched], axis=1), 0.5, rtol=1e-5)
+    assert not dP[~touched].any()
+    np.testing.assert_allclose(np.linalg.norm(dQ[np.unique(np.concatenate([i, j]))], axis=1), 0.5, rtol=1e-5)
+    for kw in (dict(call=2, t=0), dict(call=1, t=1)):
+        assert not np.array_equal(draw(**kw)[0][touched], dP[touched])
+    np.testing.assert_array_equal(draw(call=1, t=0)[0], dP)  # deterministic
+    x = dP[touched].ravel()
+    assert abs(x.mean()) < 0.01 and abs(x.var() - 0.25 / d) < 0.1 * 0.25 / d
