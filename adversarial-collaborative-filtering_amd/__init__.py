@@ -14,8 +14,8 @@ module also registers itself as ``acf_amd``).
 import sys as _sys
 
 from . import _native  # noqa: F401
-from .data import (OriginalDataset, SyntheticDataset, get_dataset, ml1m_like, pinterest_like,
-                   synthetic_dataset, yelp_like)
+from .data import (DeviceDataset, OriginalDataset, SyntheticDataset, get_dataset, ml1m_like, pinterest_like,
+                   synthetic_dataset, synthetic_large, yelp_like)
 from .evaluate import evaluate, init_eval_model
 from .evaluation import evaluate_apr_mode, evaluate_model
 from .model import MF, Session
@@ -28,8 +28,8 @@ from .train import (output_evaluate, prediction2file, training, training_batch, 
 _sys.modules.setdefault("acf_amd", _sys.modules[__name__])
 
 __all__ = [
-    "APR", "AdversarialNeuMF", "DeviceSampler", "EpochTriplets", "MF", "NeuMF", "OriginalDataset", "Recommender", "Session",
+    "APR", "AdversarialNeuMF", "DeviceDataset", "DeviceSampler", "EpochTriplets", "MF", "NeuMF", "OriginalDataset", "Recommender", "Session",
     "SyntheticDataset", "evaluate", "evaluate_apr_mode", "evaluate_model", "get_dataset", "init_eval_model", "ml1m_like", "output_evaluate",
-    "pinterest_like", "prediction2file", "sampling", "shuffle", "synthetic_dataset", "training",
+    "pinterest_like", "prediction2file", "sampling", "shuffle", "synthetic_dataset", "synthetic_large", "training",
     "training_batch", "training_loss_acc", "write2file", "yelp_like",
 ]

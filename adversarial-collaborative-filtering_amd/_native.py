@@ -72,6 +72,9 @@ SIGNATURES = {
     "acf_row_segment_sum": (ctypes.c_int, [_P, _P, _I64, _I32, _I64, _P, ctypes.c_size_t, _P, _P, _P, _P, _P]),
     "acf_l2norm_perturb": (ctypes.c_int, [_P, _I64, _I32, _F, _P, _P]),
     "acf_sparse_adagrad_apply": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _I64, _F, _P]),
+    "acf_sample_epoch_alias": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _U64, _I32, _I32,
+                                              _P, _P, _P, _P]),
+    "acf_alias_build": (ctypes.c_int, [_P, _I64, _P, _P]),
     "acf_dns_select": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I64, _I32, _P, _P]),
 }
 

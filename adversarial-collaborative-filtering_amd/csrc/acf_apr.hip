@@ -38,6 +38,7 @@
 #include <rocprim/block/block_scan.hpp>
 
 #include <algorithm>
+#include <cmath>
 
 #include <cstdarg>
 #include <cstdio>
@@ -2413,10 +2414,15 @@ __device__ __forceinline__ bool sorted_contains(const int32_t* __restrict__ a, i
   return lo < n && a[lo] == v;
 }
 
+// One negative per triplet: a proposal from [0, num_items) — uniform
+// (APR.py:76), or from an alias table (Walker / Vose: column k kept with
+// probability prob[k], else alias[k]) — redrawn while it is in the user's
+// trainList (APR.py:77-78).
 __global__ void k_negatives(const int32_t* __restrict__ perm, const int32_t* __restrict__ pu,
                             const int32_t* __restrict__ pi, int64_t n_out, int32_t num_items,
                             int32_t num_lists, const int64_t* __restrict__ loff,
                             const int32_t* __restrict__ litems, uint64_t seed, int32_t max_tries,
+                            const float* __restrict__ prob, const int32_t* __restrict__ alias,
                             int32_t* __restrict__ ou, int32_t* __restrict__ op,
                             int32_t* __restrict__ on, int32_t* __restrict__ err) {
   int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -2435,7 +2441,8 @@ __global__ void k_negatives(const int32_t* __restrict__ perm, const int32_t* __r
   const uint64_t base = mix64(seed ^ 0xA0761D6478BD642Full) ^ mix64((uint64_t)x);
   for (int32_t a = 0; a < max_tries; ++a) {
     const uint64_t h = mix64(base + (uint64_t)a * 0x9E3779B97F4A7C15ull);
-    const int32_t j = (int32_t)(((h >> 32) * (uint64_t)num_items) >> 32);
+    int32_t j = (int32_t)(((h >> 32) * (uint64_t)num_items) >> 32);
+    if (prob && (float)(h & 0xFFFFFFull) * (1.0f / 16777216.0f) >= prob[j]) j = alias[j];
     if (!sorted_contains(lst, ln, j)) {
       on[x] = j;
       return;
@@ -3490,11 +3497,67 @@ extern "C" int acf_eval_positions_list(const float* P, const float* Q, int64_t U
   return ACF_OK;
 }
 
+static int sample_epoch(const int32_t* pu, const int32_t* pi, int64_t n_pos, int32_t B, int32_t num_items,
+                        int32_t num_lists, const int64_t* loff, const int32_t* litems, uint64_t seed,
+                        int32_t max_tries, int32_t check, const float* prob, const int32_t* alias, int32_t* ou,
+                        int32_t* op, int32_t* on, void* stream_);
+
 extern "C" int acf_sample_epoch(const int32_t* pu, const int32_t* pi, int64_t n_pos, int32_t B,
                                 int32_t num_items, int32_t num_lists, const int64_t* loff,
                                 const int32_t* litems, uint64_t seed, int32_t max_tries,
                                 int32_t check, int32_t* ou, int32_t* op, int32_t* on,
                                 void* stream_) {
+  return sample_epoch(pu, pi, n_pos, B, num_items, num_lists, loff, litems, seed, max_tries, check, nullptr,
+                      nullptr, ou, op, on, stream_);
+}
+
+extern "C" int acf_sample_epoch_alias(const int32_t* pu, const int32_t* pi, int64_t n_pos, int32_t B,
+                                      int32_t num_items, int32_t num_lists, const int64_t* loff,
+                                      const int32_t* litems, const float* prob, const int32_t* alias,
+                                      uint64_t seed, int32_t max_tries, int32_t check, int32_t* ou,
+                                      int32_t* op, int32_t* on, void* stream_) {
+  ACF_CHECK(prob && alias, ACF_E_INVALID, "NULL alias table");
+  return sample_epoch(pu, pi, n_pos, B, num_items, num_lists, loff, litems, seed, max_tries, check, prob, alias,
+                      ou, op, on, stream_);
+}
+
+// Vose's alias method, on the host in double precision (one pass, O(n)):
+// prob[k] = the chance that column k keeps k; otherwise it yields alias[k].
+extern "C" int acf_alias_build(const float* w, int64_t n, float* prob, int32_t* alias) {
+  ACF_CHECK(w && prob && alias && n > 0 && n < (1ll << 31), ACF_E_INVALID, "bad alias-table arguments");
+  double total = 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    ACF_CHECK(w[k] >= 0.f && std::isfinite(w[k]), ACF_E_INVALID, "weight %lld is negative or not finite",
+              (long long)k);
+    total += w[k];
+  }
+  ACF_CHECK(total > 0.0, ACF_E_INVALID, "weights sum to zero");
+  std::vector<double> q((size_t)n);
+  std::vector<int32_t> small, large;
+  for (int64_t k = 0; k < n; ++k) {
+    q[(size_t)k] = (double)w[k] * (double)n / total;
+    (q[(size_t)k] < 1.0 ? small : large).push_back((int32_t)k);
+  }
+  while (!small.empty() && !large.empty()) {
+    const int32_t s = small.back(), l = large.back();
+    small.pop_back();
+    prob[s] = (float)q[(size_t)s];
+    alias[s] = l;
+    q[(size_t)l] = (q[(size_t)l] + q[(size_t)s]) - 1.0;
+    if (q[(size_t)l] < 1.0) {
+      large.pop_back();
+      small.push_back(l);
+    }
+  }
+  for (int32_t k : large) { prob[k] = 1.0f; alias[k] = k; }
+  for (int32_t k : small) { prob[k] = 1.0f; alias[k] = k; }  // rounding leftovers
+  return ACF_OK;
+}
+
+static int sample_epoch(const int32_t* pu, const int32_t* pi, int64_t n_pos, int32_t B, int32_t num_items,
+                        int32_t num_lists, const int64_t* loff, const int32_t* litems, uint64_t seed,
+                        int32_t max_tries, int32_t check, const float* prob, const int32_t* alias, int32_t* ou,
+                        int32_t* op, int32_t* on, void* stream_) {
   ACF_CHECK(pu && pi && loff && ou && op && on, ACF_E_INVALID, "NULL argument");
   ACF_CHECK(B > 0 && num_items > 0 && n_pos >= 0 && n_pos < (1ll << 31), ACF_E_INVALID,
             "bad sizes");
@@ -3516,7 +3579,7 @@ extern "C" int acf_sample_epoch(const int32_t* pu, const int32_t* pi, int64_t n_
   k_perm_keys<<<grid_for(n_pos), 256, 0, s>>>(n_pos, seed, k_in, v_in);
   HIP_TRY(rocprim::radix_sort_pairs(tmp, tb, k_in, k_out, v_in, v_out, (size_t)n_pos, 0, 64, s));
   k_negatives<<<grid_for(n_out), 256, 0, s>>>(v_out, pu, pi, n_out, num_items, num_lists, loff,
-                                              litems, seed, max_tries, ou, op, on, err);
+                                              litems, seed, max_tries, prob, alias, ou, op, on, err);
   HIP_TRY(hipGetLastError());
   int32_t herr = 0;
   if (check) HIP_TRY(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s));

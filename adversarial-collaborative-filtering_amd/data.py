@@ -226,6 +226,53 @@ def synthetic_dataset(num_users: int, num_items: int, n_train: int, seed: int = 
     return SyntheticDataset(num_users, num_items, pu, pi, tests, name=name)
 
 
+class DeviceDataset:
+    """A dataset that lives only in device memory (config 5: 10M users x 5M items,
+    ~200M interactions; host copies would cost minutes): positive pairs sorted
+    by user, trainList as a sorted CSR.  Enough of the OriginalDataset surface for
+    DeviceSampler (num_users, num_items, device_arrays())."""
+
+    def __init__(self, num_users, num_items, pos_user, pos_item, list_off, list_items, name="synthetic-large"):
+        self.name = name
+        self.num_users, self.num_items = int(num_users), int(num_items)
+        self.pos_user, self.pos_item = pos_user, pos_item
+        self.list_off, self.list_items = list_off, list_items
+
+    def device_arrays(self):
+        """(pos_user int32, pos_item int32, list_off int64, list_items int32), on device."""
+        return self.pos_user, self.pos_item, self.list_off, self.list_items
+
+    def __len__(self):
+        return int(self.pos_user.numel())
+
+
+def synthetic_large(num_users: int = 10_000_000, num_items: int = 5_000_000, per_user: int = 20,
+                    zipf_s: float = 1.0, seed: int = 2019, device="cuda") -> DeviceDataset:
+    """BASELINE config 5 / SURVEY §8(d) "synthetic large": per_user interactions
+    per user (~20, 200M in all), items drawn from a Zipf(zipf_s) popularity over a
+    random permutation of the ids, generated on the device (torch, seeded).  Each
+    user's list is sorted (the sampler's rejection set); repeats are kept, as a
+    rating file may hold them."""
+    import torch
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    n = num_users * per_user
+    cdf = torch.arange(1, num_items + 1, device=dev, dtype=torch.float64).pow_(-zipf_s).cumsum_(0)
+    cdf /= cdf[-1].clone()
+    perm = torch.randperm(num_items, device=dev, generator=g).to(torch.int32)
+    items = torch.empty(n, dtype=torch.int32, device=dev)
+    step = 1 << 24
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        r = torch.rand(b - a, device=dev, dtype=torch.float64, generator=g)
+        items[a:b] = perm[torch.searchsorted(cdf, r).clamp_(max=num_items - 1)]
+    del cdf, perm
+    items = items.view(num_users, per_user).sort(dim=1).values.reshape(-1).contiguous()
+    users = torch.arange(num_users, device=dev, dtype=torch.int32).repeat_interleave(per_user)
+    off = torch.arange(0, n + 1, per_user, device=dev, dtype=torch.int64)
+    return DeviceDataset(num_users, num_items, users, items, off, items, name="synthetic-large")
+
+
 def ml1m_like(seed: int = 2019) -> SyntheticDataset:
     return synthetic_dataset(**ML1M_SHAPE, seed=seed, name="ml-1m-synthetic")
 

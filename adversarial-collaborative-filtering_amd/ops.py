@@ -467,9 +467,22 @@ def eval_positions_list(P, Q, users, test_items, cand_off, cand_items):
     return pos
 
 
+def alias_table(weights):
+    """(prob, alias) float32 / int32 numpy arrays of Vose's alias table for
+    sampling k with probability weights[k] / sum(weights) (acf_alias_build)."""
+    import numpy as np
+    w = np.ascontiguousarray(np.asarray(weights, dtype=np.float32).reshape(-1))
+    prob = np.empty(w.size, np.float32)
+    alias = np.empty(w.size, np.int32)
+    call("acf_alias_build", w.ctypes.data, w.size, prob.ctypes.data, alias.ctypes.data)
+    return prob, alias
+
+
 def sample_epoch(pos_user, pos_item, batch_size: int, num_items: int, list_off, list_items,
-                 seed: int, max_tries: int = 1 << 20, check: bool = True):
-    """Device-side shuffle + negative sampling for one epoch (APR.py:39-81)."""
+                 seed: int, max_tries: int = 1 << 20, check: bool = True, alias=None):
+    """Device-side shuffle + negative sampling for one epoch (APR.py:39-81).
+    alias: None (uniform proposals, APR.py:76) or a (prob, alias) pair of device
+    tensors from alias_table (acf_sample_epoch_alias)."""
     dev = pos_user.device
     pu = _idx(pos_user, "pos_user", dev)
     pi = _idx(pos_item, "pos_item", dev)
@@ -480,9 +493,20 @@ def sample_epoch(pos_user, pos_item, batch_size: int, num_items: int, list_off, 
     op = torch.empty(n_out, dtype=torch.int32, device=dev)
     on = torch.empty(n_out, dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
-        call("acf_sample_epoch", pu.data_ptr(), pi.data_ptr(), pu.numel(), batch_size, int(num_items),
-             off.numel() - 1, off.data_ptr(), li.data_ptr(), int(seed) & 0xFFFFFFFFFFFFFFFF,
-             int(max_tries), int(check), ou.data_ptr(), op.data_ptr(), on.data_ptr(), _stream_ptr(dev))
+        if alias is None:
+            call("acf_sample_epoch", pu.data_ptr(), pi.data_ptr(), pu.numel(), batch_size, int(num_items),
+                 off.numel() - 1, off.data_ptr(), li.data_ptr(), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                 int(max_tries), int(check), ou.data_ptr(), op.data_ptr(), on.data_ptr(), _stream_ptr(dev))
+        else:
+            prob, al = alias
+            _require(prob, "alias prob", torch.float32, dev, 1)
+            _require(al, "alias", torch.int32, dev, 1)
+            if prob.numel() != num_items or al.numel() != num_items:
+                raise ValueError(f"alias table has {prob.numel()} columns, expected num_items = {num_items}")
+            call("acf_sample_epoch_alias", pu.data_ptr(), pi.data_ptr(), pu.numel(), batch_size, int(num_items),
+                 off.numel() - 1, off.data_ptr(), li.data_ptr(), prob.data_ptr(), al.data_ptr(),
+                 int(seed) & 0xFFFFFFFFFFFFFFFF, int(max_tries), int(check), ou.data_ptr(), op.data_ptr(),
+                 on.data_ptr(), _stream_ptr(dev))
     return ou, op, on
 
 

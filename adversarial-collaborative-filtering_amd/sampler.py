@@ -97,24 +97,39 @@ class EpochTriplets:
 
 
 class DeviceSampler:
-    """GPU shuffle + negative sampler over a dataset (acf_sample_epoch)."""
+    """GPU shuffle + negative sampler over a dataset (acf_sample_epoch).
 
-    def __init__(self, dataset, batch_size: int, device, seed: int = 0):
+    ``weights`` (optional, one per item): negatives are proposed from an alias
+    table of these weights (acf_sample_epoch_alias; e.g. popularity**0.75)
+    instead of uniformly, then accepted by the same trainList rule.  Equal
+    weights give the reference's uniform sampler, draw for draw."""
+
+    def __init__(self, dataset, batch_size: int, device, seed: int = 0, weights=None):
         import torch
         self.dataset = dataset
         self.batch_size = int(batch_size)
         self.device = torch.device(device)
         self.seed = int(seed)
-        off, items = dataset.sorted_lists()
-        self.list_off = torch.as_tensor(off, dtype=torch.int64, device=self.device)
-        self.list_items = torch.as_tensor(items, dtype=torch.int32, device=self.device)
-        self.pos_user = torch.as_tensor(dataset.pair_user, dtype=torch.int32, device=self.device)
-        self.pos_item = torch.as_tensor(dataset.pair_item, dtype=torch.int32, device=self.device)
+        if hasattr(dataset, "device_arrays"):  # data.DeviceDataset: already on the device
+            self.pos_user, self.pos_item, self.list_off, self.list_items = dataset.device_arrays()
+        else:
+            off, items = dataset.sorted_lists()
+            self.list_off = torch.as_tensor(off, dtype=torch.int64, device=self.device)
+            self.list_items = torch.as_tensor(items, dtype=torch.int32, device=self.device)
+            self.pos_user = torch.as_tensor(dataset.pair_user, dtype=torch.int32, device=self.device)
+            self.pos_item = torch.as_tensor(dataset.pair_item, dtype=torch.int32, device=self.device)
         self.num_items = int(dataset.num_items)
+        self.alias = None
+        if weights is not None:
+            from . import ops
+            if len(weights) != self.num_items:
+                raise ValueError(f"{len(weights)} weights for {self.num_items} items")
+            prob, alias = ops.alias_table(weights)
+            self.alias = (torch.as_tensor(prob, device=self.device), torch.as_tensor(alias, device=self.device))
 
     def epoch(self, epoch: int, check: bool = True) -> EpochTriplets:
         from . import ops
         seed = (self.seed * 0x9E3779B1 + epoch * 0x85EBCA77 + 1) & 0xFFFFFFFFFFFFFFFF
         u, i, j = ops.sample_epoch(self.pos_user, self.pos_item, self.batch_size, self.num_items,
-                                   self.list_off, self.list_items, seed, check=check)
+                                   self.list_off, self.list_items, seed, check=check, alias=self.alias)
         return EpochTriplets(u, i, j, self.batch_size)

@@ -15,9 +15,10 @@ scaling) — the reference's experiments are independent single-process runs and
 B = 512 step has no data-parallel split worth an exchange.
 
 Extra fields: "roofline" (dominant kernel, HIP-event kernel times),
-"cpu_baseline" (oracle/apr_oracle.c in the reference's dense-delta mode, 1 core,
-bounded sample), "roofline_large_batch" (same kernels at batch 65,536 on
-10M x 5M tables, d = 128, when --large).
+"cpu_baseline" (the reference's CPU hot loop restated in torch-CPU on every
+host thread, one ml-1m epoch, APR and BPR phases), "roofline_large_batch" /
+"roofline_large_batch_d64" (BASELINE configs[4]: batch 65,536 on 10M x 5M tables,
+d = 128 / 64, alias-table negatives from the device sampler; --no-large skips).
 """
 from __future__ import annotations
 
@@ -50,10 +51,12 @@ def parse():
     p.add_argument("--eager", action="store_true", help="eager launches instead of hipGraph replay")
     p.add_argument("--no-plan-overlap", action="store_true",
                    help="plan each chunk on the timed stream instead of beside the previous chunk's training (A/B)")
-    p.add_argument("--cpu-batches", type=int, default=17469, help="oracle sample size (batches, ~10-30 s)")
+    p.add_argument("--cpu-batches", type=int, default=1941, help="CPU baseline sample (batches; 1,941 = one "
+                   "ml-1m epoch)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--time-batches", type=int, default=400, help="batches in the kernel-timing pass")
-    p.add_argument("--large", action="store_true", help="also measure batch 65536 on 10M x 5M x d128")
+    p.add_argument("--no-large", action="store_true",
+                   help="skip the synthetic-large lines (batch 65,536 on 10M x 5M, d = 128 and 64)")
     p.add_argument("--no-neumf", action="store_true", help="skip the adversarial-NeuMF line (configs[3])")
     p.add_argument("--no-step-overlap", action="store_true",
                    help="two kernels per APR step instead of the overlapped k_ovl (A/B)")
@@ -211,31 +214,59 @@ def step_bandwidth(d, B, st, triplets_per_s):
 
 
 def cpu_baseline(u, i, j, P0, Q0, B, nb):
+    """BASELINE.md §2 / SURVEY §8(d): the reference's CPU hot loop restated op for
+    op in torch-CPU fp32 with every host thread this job has (TF's CPU kernels run
+    on its intra-op pool), over ONE full ml-1m-shaped epoch (nb batches of B), for
+    the APR phase with the reference's dense delta work (value), the BPR phase,
+    and a touched-rows-only APR variant; plus the single-threaded C oracle on the
+    same epoch.  Sampling and evaluation are excluded (APR.py:261-263)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from apr_oracle import COracle, HParams
+    from apr_torch_cpu import apr_step, cpu_model, threads
+    torch.set_num_threads(threads())
+    U, I, J = (x[: nb * B].cpu().long() for x in (u, i, j))
+
+    def run(adver, dense):
+        tabs = [P0.cpu().clone(), Q0.cpu().clone(), torch.full(P0.shape, 0.1), torch.full(Q0.shape, 0.1)]
+        t0 = time.perf_counter()
+        for t in range(nb):
+            s = slice(t * B, (t + 1) * B)
+            apr_step(*tabs, U[s], I[s], J[s], adver=adver, dense=dense)
+        return nb * B / (time.perf_counter() - t0)
+
+    apr_dense, bpr, apr_sparse = run(True, True), run(False, True), run(True, False)
     o = COracle()
-    U, I, J = (x[: nb * B].cpu().numpy() for x in (u, i, j))
-    P, Q = P0.cpu().numpy().copy(), Q0.cpu().numpy().copy()
-    aP, aQ = np.full_like(P, 0.1), np.full_like(Q, 0.1)
+    Pn, Qn = P0.cpu().numpy().copy(), Q0.cpu().numpy().copy()
     t0 = time.perf_counter()
-    o.apr_train(P, Q, aP, aQ, U, I, J, B, HParams(adver=1), dense=True)
-    dt = time.perf_counter() - t0
-    return {"value": round(nb * B / dt, 1), "unit": "triplets/s", "cores": 1, "kind": "port",
-            "sample": f"{nb} batches x {B} of the same triplet stream, oracle/apr_oracle.c with the "
-                      f"reference's dense full-table delta work (APR.py:183-191), 1 thread, {dt:.1f} s",
+    o.apr_train(Pn, Qn, np.full_like(Pn, 0.1), np.full_like(Qn, 0.1), U.int().numpy(), I.int().numpy(),
+                J.int().numpy(), B, HParams(adver=1), dense=True)
+    c1 = nb * B / (time.perf_counter() - t0)
+    return {"value": round(apr_dense, 1), "unit": "triplets/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"one ml-1m-shaped epoch ({nb} batches x {B}) of the APR phase: oracle/apr_torch_cpu.py, "
+                      f"the reference's TF graph op for op in torch-CPU fp32 on {torch.get_num_threads()} threads, "
+                      f"dense delta densify/normalise/assign per batch (APR.py:183-191)",
+            "bpr_phase": round(bpr, 1),
+            "apr_touched_rows_only": round(apr_sparse, 1),
+            "c_oracle_1thread_apr_dense": round(c1, 1),
             "reference_published": {"value": round(REF_CPU_TRIPLETS_PER_S, 1),
                                     "source": "out/janEval/ml-1m-sort_apr_..._11_56_42.out:54-55 (UCL CPU, TF1)"}}
 
 
-def large_batch_roofline(acf, ops, dev, d=128):
-    """Batch 65,536 on 10M x 5M tables (d = 128: ~15 GB incl. Adagrad slots):
-    tables far beyond the 256 MB Infinity Cache, so rows come from HBM."""
-    U1, I1, B, nb, chunk = 10_000_001, 5_000_001, 65536, 64, 32
+def large_batch_roofline(acf, ops, dev, ds, d=128, nb=64, chunk=32):
+    """BASELINE configs[4] / SURVEY §8(d) "synthetic large" on one GPU: 10M users
+    x 5M items (~200M interactions, Zipf items), batch 65,536, triplets from the
+    device sampler with its alias-table negatives (equal weights: the reference's
+    uniform rule, APR.py:76-78).  Tables (d = 128: 15.4 GB with the Adagrad slots)
+    are far beyond the 256 MB Infinity Cache, so rows come from HBM."""
+    U1, I1, B = ds.num_users + 1, ds.num_items + 1, 65536
+    sampler = acf.DeviceSampler(ds, B, dev, seed=7, weights=np.ones(ds.num_items, np.float32))
+    ep = sampler.epoch(0)
+    n = nb * B
+    u, i, j = (x[:n].contiguous() for x in (ep.user, ep.item_pos, ep.item_neg))
+    del ep
     g = torch.Generator(device=dev).manual_seed(5)
-    u = torch.randint(0, U1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
-    i = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
-    j = torch.randint(0, I1 - 1, (B * nb,), device=dev, generator=g, dtype=torch.int32)
-    tabs = [torch.randn(U1, d, device=dev) * 0.01, torch.randn(I1, d, device=dev) * 0.01,
+    tabs = [torch.randn(U1, d, device=dev, generator=g) * 0.01, torch.randn(I1, d, device=dev, generator=g) * 0.01,
             torch.full((U1, d), 0.1, device=dev), torch.full((I1, d), 0.1, device=dev)]
     pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev)
     hp = ops.StepHParams(adver=1)
@@ -245,14 +276,17 @@ def large_batch_roofline(acf, ops, dev, d=128):
     pipe.run(tabs, hp, u, i, j, 0, nb)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    errors = pipe.step_errors()
     st = batch_stats(u, i, j, B, nb, U1, I1)
     rl = kernel_roofline(ops, pipe.ctx[0], tabs, hp, u, i, j, B, d, chunk, st)
     rl["triplets_per_s"] = round(nb * B / dt, 1)
     rl["step_bandwidth"] = step_bandwidth(d, B, st, nb * B / dt)
     rl["batch_stats"] = {k: round(v, 1) for k, v in st.items()}
-    rl["config"] = {"users": U1 - 1, "items": I1 - 1, "dim": d, "batch": B, "batches": nb,
-                    "chunk": chunk}
-    del tabs
+    rl["step_errors"] = errors
+    rl["config"] = {"workload": "APR, synthetic large (BASELINE configs[4], one GPU)", "users": U1 - 1,
+                    "items": I1 - 1, "interactions": len(ds), "dim": d, "batch": B, "batches": nb, "chunk": chunk,
+                    "negatives": "device sampler, alias table of equal weights (uniform, APR.py:76-78)"}
+    del tabs, pipe
     torch.cuda.empty_cache()
     return rl
 
@@ -399,12 +433,14 @@ def main():
         out["cpu_baseline"] = cpu_baseline(u, i, j, P0, Q0, B, a.cpu_batches)
     if rank == 0 and not a.no_neumf:
         out["neumf"] = neumf_bench(acf, dev)
-    if rank == 0 and a.large:
+    if rank == 0 and not a.no_large:
         del pipe, tctx
         torch.cuda.empty_cache()
-        out["roofline_large_batch"] = large_batch_roofline(acf, ops, dev, 128)
+        big = acf.synthetic_large(device=dev)
+        out["roofline_large_batch"] = large_batch_roofline(acf, ops, dev, big, 128)
+        out["roofline_large_batch_d64"] = large_batch_roofline(acf, ops, dev, big, 64)
+        del big
         torch.cuda.empty_cache()
-        out["roofline_large_batch_d64"] = large_batch_roofline(acf, ops, dev, 64)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

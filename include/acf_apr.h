@@ -251,6 +251,24 @@ int acf_sample_epoch(const int32_t* pos_user, const int32_t* pos_item, int64_t n
                      int32_t* out_user, int32_t* out_pos, int32_t* out_neg,
                      void* stream);
 
+/* acf_sample_epoch with the negatives proposed from an alias table instead of
+ * uniformly (SURVEY §8(f)1, config 5's on-GPU alias sampler): column k of the
+ * table (prob, alias: DEVICE arrays of num_items) keeps k with probability
+ * prob[k], else yields alias[k]; the proposal is then accepted or redrawn by
+ * the same trainList rule (APR.py:76-78).  A table of equal weights is the
+ * reference's uniform sampler. */
+int acf_sample_epoch_alias(const int32_t* pos_user, const int32_t* pos_item, int64_t n_pos,
+                           int32_t batch_size, int32_t num_items, int32_t num_lists,
+                           const int64_t* list_off, const int32_t* list_items,
+                           const float* prob, const int32_t* alias, uint64_t seed,
+                           int32_t max_tries, int32_t check, int32_t* out_user,
+                           int32_t* out_pos, int32_t* out_neg, void* stream);
+
+/* Builds an alias table (Vose) for sampling k with probability w[k] / sum(w).
+ * HOST arrays: w [n] (>= 0, finite, not all 0) in; prob [n], alias [n] out.
+ * Synchronous, deterministic. */
+int acf_alias_build(const float* w, int64_t n, float* prob, int32_t* alias);
+
 /* dns > 1 negative selection (utils.py:121-133): per triplet, the candidate of
  * cand[e*dns .. e*dns+dns) with the largest clean score P[user[e]].Q[c] (first
  * maximum wins, np.argmax). */

@@ -238,3 +238,26 @@ def test_random_delta_mode(oracle):
     np.testing.assert_array_equal(draw(call=1, t=0)[0], dP)  # deterministic
     x = dP[touched].ravel()
     assert abs(x.mean()) < 0.01 and abs(x.var() - 0.25 / d) < 0.1 * 0.25 / d
+
+
+@pytest.mark.parametrize("adver,dense", [(0, True), (1, True), (1, False)])
+def test_torch_cpu_baseline_matches_c_oracle(oracle, adver, dense):
+    """oracle/apr_torch_cpu.py (the multi-threaded CPU baseline) computes the same
+    steps as the C oracle, to fp32 rounding."""
+    import torch
+    from apr_torch_cpu import apr_step
+    rng = np.random.default_rng(7)
+    U1, I1, d, B, nb = 120, 90, 32, 64, 4
+    P = (rng.standard_normal((U1, d)) * 0.3).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.3).astype(np.float32)
+    u, i, j = (rng.integers(0, N, nb * B).astype(np.int32) for N in (U1, I1, I1))
+    rP, rQ = P.copy(), Q.copy()
+    aP, aQ = np.full(P.shape, 0.1, np.float32), np.full(Q.shape, 0.1, np.float32)
+    oracle.apr_train(rP, rQ, aP, aQ, u, i, j, B, HParams(adver=adver))
+    tabs = [torch.tensor(P), torch.tensor(Q), torch.full(P.shape, 0.1), torch.full(Q.shape, 0.1)]
+    for t in range(nb):
+        s = slice(t * B, (t + 1) * B)
+        apr_step(*tabs, torch.tensor(u[s]).long(), torch.tensor(i[s]).long(), torch.tensor(j[s]).long(),
+                 adver=bool(adver), dense=dense)
+    for g, w in zip(tabs, (rP, rQ, aP, aQ)):
+        np.testing.assert_allclose(g.numpy(), w, rtol=1e-4, atol=1e-5)
