@@ -493,18 +493,59 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
   }
 }
 
-// Packed mode: per slot of every batch, (non-fused << 32) | (row stays in W
-// scratch), scanned together into the per-batch slot and write-back lists.
-__global__ void k_slot_flags(const OccRec* __restrict__ inl, int64_t n, int32_t R, int32_t gen,
-                             uint64_t* __restrict__ flags) {
+// Hot slots of packed (one lane-group per slot) plans.  A large batch of
+// Zipf-popular items holds a few rows with thousands of occurrences (10M x 5M,
+// B = 65,536: the top item ~4,000), and one lane-group would sum them one pass
+// after another.  A non-fused slot with more than ACF_HOT_MIN occurrences is
+// therefore split into pieces of consecutive occurrences (at least
+// ACF_HOT_PIECE each, at most ACF_HOT_MAXP pieces); one wave sums a piece into
+// hot_part, and k_hot_combine adds a slot's pieces in piece order (fixed order:
+// deterministic bits).  Each plan appends a batch's hot slots and their pieces
+// with atomics; the order of the lists changes nothing but which wave does what.
+#define ACF_HOT_MIN 8
+#define ACF_HOT_PIECE 16
+#define ACF_HOT_MAXP 256
+
+__host__ __device__ __forceinline__ int32_t hot_pieces(int32_t count) {
+  const int32_t np = (count + ACF_HOT_PIECE - 1) / ACF_HOT_PIECE;
+  return np < ACF_HOT_MAXP ? np : ACF_HOT_MAXP;
+}
+
+// Per-batch capacity of the hot lists: slots with > ACF_HOT_MIN of a batch's
+// 3B occurrences, and sum(ceil(count / ACF_HOT_PIECE)) <= 3B / ACF_HOT_PIECE + hot slots.
+__host__ __forceinline__ int32_t hot_stride_for(int32_t B) { return 3 * B / (ACF_HOT_MIN + 1) + 1; }
+__host__ __forceinline__ int32_t piece_stride_for(int32_t B) { return 3 * B / ACF_HOT_PIECE + hot_stride_for(B); }
+
+struct HotLists {
+  int4* list;       // [nb][hot_stride]   {slot, pieces, piece base, count}
+  int4* piece;      // [nb][piece_stride] {slot, piece, pieces, piece base}
+  int32_t* cnt;     // [nb] hot slots of the batch
+  int32_t* pcnt;    // [nb] pieces of the batch
+  int32_t hot_stride, piece_stride;
+};
+
+// Packed mode: per slot of every batch, (non-fused, not hot << 32) | (row stays
+// in W scratch), scanned together into the per-batch slot and write-back lists;
+// hot slots go to the hot lists instead of the slot list.
+__global__ void k_slot_flags(const OccRec* __restrict__ inl, int64_t n, int32_t R, int32_t gen, int32_t S,
+                             uint64_t* __restrict__ flags, HotLists hl) {
   const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x >= n) return;
   const OccRec* r = inl + x * R;
-  const int32_t meta = r->meta;
-  const bool valid = r->gen == gen && (meta & ACF_COUNT_MASK) != 0;
-  const uint64_t ns = (valid && !(meta & ACF_SINGLE_BIT)) ? 1 : 0;
+  const int32_t meta = r->meta, count = meta & ACF_COUNT_MASK;
+  const bool valid = r->gen == gen && count != 0;
+  const bool hot = valid && !(meta & ACF_SINGLE_BIT) && count > ACF_HOT_MIN;
+  const uint64_t ns = (valid && !(meta & ACF_SINGLE_BIT) && !hot) ? 1 : 0;
   const uint64_t fl = (valid && !(meta & ACF_INPLACE_BIT)) ? 1 : 0;
   flags[x] = (ns << 32) | fl;
+  if (hot) {
+    const int64_t t = x / S;
+    const int32_t k = (int32_t)(x - t * S), np = hot_pieces(count);
+    const int32_t h = atomicAdd(hl.cnt + t, 1);
+    const int32_t base = atomicAdd(hl.pcnt + t, np);
+    hl.list[t * hl.hot_stride + h] = make_int4(k, np, base, count);
+    for (int32_t p = 0; p < np; ++p) hl.piece[t * hl.piece_stride + base + p] = make_int4(k, p, np, base);
+  }
 }
 
 __global__ void k_slot_lists(const uint64_t* __restrict__ flags, const uint64_t* __restrict__ incl,
@@ -906,6 +947,11 @@ struct StepArgs {
   const int32_t* task_cnt;   // [nb]
   int32_t task_stride, max_depth;
   int32_t poll_sleep;  // k_stream: s_sleep between polls of a version (0-3; 4/5/6 = 8/16/32)
+  // hot slots of list plans (k_slot_flags): piece waves [slot_waves, slot_waves +
+  // hot_waves) of a list kernel stride over the batch's pieces; partial sums in hot_part
+  HotLists hot;
+  float* hot_part;     // [piece_stride, d]
+  int32_t hot_waves;
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -2174,12 +2220,135 @@ __global__ void __launch_bounds__(256) k_stream_flush(StepArgs a, uint32_t* __re
 // is the plan's list of its NON-fused slots and the write-back the list of the
 // rows batch t-1 left in W scratch; a fixed set of slot waves strides over both
 // (most slots belong to fused triplets and would only read their record).
+// Piece p of hot slot k (pc = {k, p, pieces, piece base}): occurrences
+// [p*count/pieces, (p+1)*count/pieces), one wave whose 64/LPR lane-groups take
+// them as clean_slot's team members do (two per pass); the wave's sum goes to
+// hot_part[base + p].  ADV: adv_slot's term (own + delta, partners + their
+// deltas; the tables are current).  Losses of user occurrences as in the slot kernels.
+template <int LPR, int NV, bool ADV>
+__device__ __forceinline__ void hot_piece(const StepArgs& a, const int4 pc, int m, int l) {
+  constexpr int TEAM = 64 / LPR;
+  const int k = pc.x, d = a.d;
+  const RecV r00 = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
+  SlotHdr h;
+  h.count = r00.meta() & ACF_COUNT_MASK;
+  h.is_item = (r00.meta() & ACF_ITEM_BIT) != 0;
+  h.own_row = r00.own_row();
+  h.own_src = r00.own_src();
+  h.ovf = r00.ovf();
+  const int o0 = (int)((int64_t)pc.y * h.count / pc.z), o1 = (int)((int64_t)(pc.y + 1) * h.count / pc.z);
+  const float* own_tab = h.is_item ? a.Q : a.P;
+  const float* ptab = h.is_item ? a.P : a.Q;
+  const RowV<NV> own = ADV ? add_row(load_row<LPR, NV>(own_tab, h.own_row, d, l), load_row<LPR, NV>(a.delta, k, d, l))
+                           : load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l);
+  RowV<NV> G = zero_row<NV>();
+  for (int base = o0; base < o1; base += 2 * TEAM) {
+    const int i0 = base + m, i1 = base + TEAM + m;
+    const bool a0 = i0 < o1, a1 = i1 < o1;
+    RowV<NV> ra0 = zero_row<NV>(), rb0 = zero_row<NV>(), ra1 = zero_row<NV>(), rb1 = zero_row<NV>();
+    RecV r0, r1;
+    if (a0) r0 = occ_rec_mem(a, h, k, i0);
+    if (a1) r1 = occ_rec_mem(a, h, k, i1);
+    if (ADV) {
+      if (a0) {
+        ra0 = add_row(load_row<LPR, NV>(ptab, r0.pa_row(), d, l), load_row<LPR, NV>(a.delta, r0.pa_slot(), d, l));
+        rb0 = add_row(load_row<LPR, NV>(a.Q, r0.pb_row(), d, l), load_row<LPR, NV>(a.delta, r0.pb_slot(), d, l));
+      }
+      if (a1) {
+        ra1 = add_row(load_row<LPR, NV>(ptab, r1.pa_row(), d, l), load_row<LPR, NV>(a.delta, r1.pa_slot(), d, l));
+        rb1 = add_row(load_row<LPR, NV>(a.Q, r1.pb_row(), d, l), load_row<LPR, NV>(a.delta, r1.pb_slot(), d, l));
+      }
+    } else {
+      if (a0) {
+        ra0 = load_at<LPR, NV>(row_src(a, ptab, r0.pa_row(), r0.pa_src()), d, l);
+        rb0 = load_at<LPR, NV>(row_src(a, a.Q, r0.pb_row(), r0.pb_src()), d, l);
+      }
+      if (a1) {
+        ra1 = load_at<LPR, NV>(row_src(a, ptab, r1.pa_row(), r1.pa_src()), d, l);
+        rb1 = load_at<LPR, NV>(row_src(a, a.Q, r1.pb_row(), r1.pb_src()), d, l);
+      }
+    }
+    occ_term<LPR, NV>(a, h.is_item, own, r0, ra0, rb0, a0, l, ADV ? a.loss_adv : a.loss_clean, G);
+    if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, own, r1, ra1, rb1, a1, l, ADV ? a.loss_adv : a.loss_clean, G);
+  }
+  team_allreduce<LPR, TEAM, NV>(G);
+  if (m == 0) store_row<LPR, NV>(a.hot_part, (int64_t)pc.w + pc.y, d, l, G);
+}
+
+// piece waves of a list kernel (wave index hw in [0, hot_waves)): stride over the batch's pieces
+template <int LPR, int NV, bool ADV>
+__device__ __forceinline__ void hot_piece_waves(const StepArgs& a, int hw) {
+  const int lane = threadIdx.x & 63, m = lane / LPR, l = lane & (LPR - 1);
+  const int n = a.hot.pcnt[a.t];
+  const int4* pl = a.hot.piece + (int64_t)a.t * a.hot.piece_stride;
+  for (int x = hw; x < n; x += a.hot_waves) hot_piece<LPR, NV, ADV>(a, pl[x], m, l);
+}
+
+// Hot-slot combine: one workgroup per hot slot (strided).  Lane-group g of the
+// 256/LPR sums pieces g, g + 256/LPR, ... in turn; group 0 then adds the groups'
+// sums in group order and finishes the slot as the slot kernels' team leader does:
+// MODE 0 (APR clean): G -> g0, delta; MODE 1 (BPR): Adagrad on G;
+// MODE 2 (APR adversarial): g0 + reg_adv * G -> Adagrad.  Rows go to W scratch.
+template <int LPR, int NV, int MODE>
+__global__ void __launch_bounds__(256) k_hot_combine(StepArgs a) {
+  constexpr int NG = 256 / LPR;
+  __shared__ float4 red[NV * 256];
+  const int g = threadIdx.x / LPR, l = threadIdx.x & (LPR - 1), d = a.d;
+  const int n = a.hot.cnt[a.t];
+  const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
+  for (int hx = blockIdx.x; hx < n; hx += gridDim.x) {
+    const int4 e = hl[hx];  // {slot, pieces, piece base, count}
+    RowV<NV> G = zero_row<NV>();
+#pragma unroll 4
+    for (int p = g; p < e.y; p += NG) G = add_row(G, load_row<LPR, NV>(a.hot_part, (int64_t)e.z + p, d, l));
+#pragma unroll
+    for (int v = 0; v < NV; ++v) red[v * 256 + threadIdx.x] = G.v[v];
+    __syncthreads();
+    if (g == 0) {
+      for (int gg = 1; gg < NG; ++gg) {
+        RowV<NV> o;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) o.v[v] = red[v * 256 + gg * LPR + l];
+        G = add_row(G, o);
+      }
+      const int k = e.x;
+      const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
+      const int is_item = (r.meta() & ACF_ITEM_BIT) != 0;
+      const int32_t row = r.own_row();
+      const float* own_tab = is_item ? a.Q : a.P;
+      float* acc_tab = is_item ? a.accQ : a.accP;
+      if (MODE == 0) {
+        const RowV<NV> dl = make_delta<LPR, NV>(a, G, is_item, row, l);
+        store_row<LPR, NV>(a.g0, k, d, l, G);
+        store_row<LPR, NV>(a.delta, k, d, l, dl);
+      } else {
+        RowV<NV> acc = load_row<LPR, NV>(acc_tab, row, d, l);
+        RowV<NV> wout;
+        if (MODE == 1) {
+          const RowV<NV> own = load_at<LPR, NV>(row_src(a, own_tab, row, r.own_src()), d, l);
+          adagrad_row(a, G, own, acc, e.w, wout);
+        } else {
+          RowV<NV> G0 = load_row<LPR, NV>(a.g0, k, d, l);
+          axpy_row(G0, a.reg_adv, G);
+          const RowV<NV> own = load_row<LPR, NV>(own_tab, row, d, l);
+          adagrad_row(a, G0, own, acc, e.w, wout);
+        }
+        store_row<LPR, NV>(acc_tab, row, d, l, acc);
+        store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int LPR, int NV, bool FUSE_APPLY>
 __global__ void __launch_bounds__(256) k_clean_list(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
-  if (FUSE_APPLY && wave >= a.slot_waves) {
-    k_single<LPR, NV, false>(a, (wave - a.slot_waves) * (64 / LPR) + g, l);
+  if (wave >= a.slot_waves) {  // piece waves, then (BPR) fused-triplet waves
+    const int hw = wave - a.slot_waves;
+    if (hw < a.hot_waves) hot_piece_waves<LPR, NV, false>(a, hw);
+    else if (FUSE_APPLY) k_single<LPR, NV, false>(a, (hw - a.hot_waves) * (64 / LPR) + g, l);
     return;
   }
   const int ngroups = a.slot_waves * (64 / LPR), gid = wave * (64 / LPR) + g;
@@ -2197,8 +2366,10 @@ template <int LPR, int NV>
 __global__ void __launch_bounds__(256) k_adv_list(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
-  if (wave >= a.slot_waves) {
-    k_single<LPR, NV, true>(a, (wave - a.slot_waves) * (64 / LPR) + g, l);
+  if (wave >= a.slot_waves) {  // piece waves, then fused-triplet waves
+    const int hw = wave - a.slot_waves;
+    if (hw < a.hot_waves) hot_piece_waves<LPR, NV, true>(a, hw);
+    else k_single<LPR, NV, true>(a, (hw - a.hot_waves) * (64 / LPR) + g, l);
     return;
   }
   const int ngroups = a.slot_waves * (64 / LPR), gid = wave * (64 / LPR) + g;
@@ -2517,6 +2688,8 @@ struct acf_apr_ctx {
   int32_t lists = 0;    // the plan built slot / write-back lists (packed mode)
   int32_t touch_next = 1;  // phase 2 reads the next batch's records (ACF_TOUCH_NEXT=0 disables)
   int32_t *slot_list = nullptr, *flush_list = nullptr, *slot_cnt = nullptr, *flush_cnt = nullptr;
+  HotLists hot = {};            // hot slots of list plans (k_slot_flags)
+  float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
   int32_t overlap = 1;  // k_ovl for APR runs of one-wave-per-slot plans (ACF_STEP_OVERLAP=0 disables)
   int32_t plan_kind2 = 0;  // the plan encodes sources at every distance (k_prev_next)
@@ -2661,6 +2834,11 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->tsl, 4 * maxE); A(&c->tpos, 4 * maxE); A(&c->uinfo, maxE);
   A(&c->slot_list, 3 * maxE); A(&c->flush_list, 3 * maxE);
   A(&c->slot_cnt, maxNB); A(&c->flush_cnt, maxNB);
+  c->hot.hot_stride = hot_stride_for(maxB);
+  c->hot.piece_stride = piece_stride_for(maxB);
+  A(&c->hot.list, (size_t)maxNB * c->hot.hot_stride); A(&c->hot.piece, (size_t)maxNB * c->hot.piece_stride);
+  A(&c->hot.cnt, 2 * (size_t)maxNB);
+  A(&c->hot_part, (size_t)c->hot.piece_stride * d);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
   A(&c->iinfo, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
@@ -2673,6 +2851,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->wnew[0], S * d); A(&c->wnew[1], S * d);
   A(&c->loss_clean, maxE); A(&c->loss_adv, maxE);
   if (r != ACF_OK) { acf_apr_destroy(c); return r; }
+  c->hot.pcnt = c->hot.cnt + maxNB;
   size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
   uint32_t* k32 = reinterpret_cast<uint32_t*>(c->key_in);
   int32_t* v32 = reinterpret_cast<int32_t*>(k32 + 3 * maxE);
@@ -2935,7 +3114,8 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->lists = 0;
   if (packed) {  // per-batch lists of non-fused slots and of rows left in W scratch
     const int64_t n = (int64_t)nb * 3 * B;
-    k_slot_flags<<<grid_for(n), 256, 0, s>>>(c->inl, n, c->plan_R, gen, c->key_in);
+    HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
+    k_slot_flags<<<grid_for(n), 256, 0, s>>>(c->inl, n, c->plan_R, gen, 3 * B, c->key_in, c->hot);
     size_t tb2 = c->tmp_bytes;
     HIP_TRY(rocprim::inclusive_scan(c->tmp, tb2, c->key_in, c->key_out, (size_t)n, rocprim::plus<uint64_t>(), s));
     k_slot_lists<<<grid_for(n), 256, 0, s>>>(c->key_in, c->key_out, n, 3 * B, c->slot_list, c->flush_list,
@@ -2986,6 +3166,9 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.epoch = c->epoch; a.nextt = c->nextt;
   a.task_list = nullptr; a.task_cnt = c->task_cnt; a.task_stride = 0; a.max_depth = 1;
   a.poll_sleep = c->poll_sleep;
+  a.hot = c->hot;
+  a.hot_part = c->hot_part;
+  a.hot_waves = 0;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -2998,11 +3181,14 @@ struct Kernels {
   void* ovl = nullptr;  // k_ovl (one wave per slot only)
   void* stream = nullptr;  // k_stream (one wave per slot, d <= 256)
   void* stream_flush = nullptr;  // its write-back, k_stream_flush<LPR>
+  void *hot_clean = nullptr, *hot_bpr = nullptr, *hot_adv = nullptr;  // k_hot_combine (list kernels)
   int slots_per_wave = 1;
   int lists = 0;  // list kernels: slot waves stride over the plan's per-batch lists
 };
 
 #define ACF_LIST_WAVES 4096  // slot waves of a list kernel
+#define ACF_HOT_WAVES 2048   // piece waves of a list kernel (hot slots)
+#define ACF_HOT_BLOCKS 1024  // workgroups of k_hot_combine
 
 template <int LPR, int NV, int TEAM>
 static void kernel_ptrs_team(Kernels* k, int fused) {
@@ -3026,6 +3212,9 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists) {
     k->clean_apr = reinterpret_cast<void*>(&k_clean_list<LPR, NV, false>);
     k->clean_bpr = reinterpret_cast<void*>(&k_clean_list<LPR, NV, true>);
     k->adv = reinterpret_cast<void*>(&k_adv_list<LPR, NV>);
+    k->hot_clean = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 0>);
+    k->hot_bpr = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 1>);
+    k->hot_adv = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 2>);
     k->slots_per_wave = OPW;
     k->lists = 1;
     return;
@@ -3060,7 +3249,7 @@ static int launch(void* fn, const StepArgs& a, int waves, hipStream_t s, hipEven
                   hipEvent_t e1 = nullptr) {
   const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
   // waves past slot_waves run fused triplets: only when fusion is on
-  if (!a.use_single && a.slot_waves < waves) return set_error(ACF_E_STATE, "bad step geometry");
+  if (!a.use_single && a.slot_waves + a.hot_waves < waves) return set_error(ACF_E_STATE, "bad step geometry");
   if (e0)
     hipExtLaunchKernelGGL(reinterpret_cast<StepKernel>(fn), grid, block, 0, s, e0, e1, 0, a);
   else
@@ -3151,7 +3340,8 @@ static void prepare_stream(acf_apr_ctx* c, const acf_apr_hparams* hp) {
   if (c->stream && hp->adver && c->stream_ok < 0 && get_kernels(c, &K, c->fusion) == ACF_OK) (void)stream_ready(c, K);
 }
 
-// kinds: 0 phase 1 / fused BPR, 1 phase 2, 2 flush, 3 k_ovl with both halves, 4 k_stream
+// kinds: 0 phase 1 / fused BPR, 1 phase 2, 2 flush, 3 k_ovl with both halves, 4 k_stream,
+// 5 hot-slot combine (list kernels)
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                     int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds,
                     int allow_overlap = 2) {
@@ -3234,17 +3424,25 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
       ACF_RET(launch_ovl(K.ovl, xa, xc, SW + TW, both ? SW : 0, s, e0, e1));
     }
   } else {
+  // list kernels: piece waves of the hot slots after the slot waves, and a
+  // combine launch (kind 5) after each pass
+  const int HW = K.lists ? std::min(c->hot.piece_stride, ACF_HOT_WAVES) : 0;
+  const int HB = std::min(c->hot.hot_stride, ACF_HOT_BLOCKS);
   for (int32_t t = first; t < first + n; ++t) {
     const int pv = t > first ? 1 : 0;
     StepArgs a = make_args(c, tb, hp, t, pv);
     a.use_single = fuse;
     a.slot_waves = SW;
+    a.hot_waves = HW;
     a.touch_next = (c->touch_next && !K.lists && t + 1 < first + n) ? 1 : 0;
     if (hp->adver) {
-      ACF_RET(L(K.clean_apr, a, SW, 0));
-      ACF_RET(L(K.adv, a, SW + TW, 1));
+      ACF_RET(L(K.clean_apr, a, SW + HW, 0));
+      if (K.lists) ACF_RET(L(K.hot_clean, a, 4 * HB, 5));
+      ACF_RET(L(K.adv, a, SW + HW + TW, 1));
+      if (K.lists) ACF_RET(L(K.hot_adv, a, 4 * HB, 5));
     } else {
-      ACF_RET(L(K.clean_bpr, a, SW + TW, 0));
+      ACF_RET(L(K.clean_bpr, a, SW + HW + TW, 0));
+      if (K.lists) ACF_RET(L(K.hot_bpr, a, 4 * HB, 5));
     }
   }
   }
@@ -3351,7 +3549,7 @@ static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_
   ACF_RET(check_step(c, tb, hp, first));
   hipStream_t s = static_cast<hipStream_t>(stream_);
   prepare_stream(c, hp);
-  const int nl = 2 * n + 1;
+  const int nl = 4 * n + 2;
   std::vector<hipEvent_t> ev((size_t)2 * nl, nullptr);
   std::vector<int> kinds(nl, -1);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
@@ -3377,7 +3575,7 @@ static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_
 extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
                                     const acf_apr_hparams* hp, int32_t first, int32_t n,
                                     double* ms_out, int32_t* launches_out, void* stream_) {
-  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 5);
+  return time_kernels(c, tb, hp, first, n, ms_out, launches_out, stream_, 6);
 }
 
 extern "C" int acf_apr_set_slot_mapping(acf_apr_ctx* c, int32_t mode) {

@@ -238,15 +238,16 @@ class APRContext:
         train_planned runs (tables are trained exactly as by it).  Kinds: clean
         (phase 1, or the fused BPR step), adv (phase 2 + Adagrad), flush
         (end-of-call write-back), ovl (overlapped adv(t) + clean(t+1), k_ovl),
-        stream (the whole range in one launch, k_stream)."""
+        stream (the whole range in one launch, k_stream), hot (the hot-slot
+        combine of large-batch plans, k_hot_combine)."""
         n = self.n_batches - first if n is None else n
         tb, h = self._tables(*tables), hp.to_c()
-        ms = (ctypes.c_double * 5)()
-        cnt = (ctypes.c_int32 * 5)()
+        ms = (ctypes.c_double * 6)()
+        cnt = (ctypes.c_int32 * 6)()
         with torch.cuda.device(self.device):
             call("acf_apr_time_kernels", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
                  _stream_ptr(self.device))
-        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush", "ovl", "stream"))}
+        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush", "ovl", "stream", "hot"))}
 
     def set_stream(self, on: bool) -> None:
         """Streamed APR steps (default on; identical results either way): one

@@ -133,9 +133,10 @@ int acf_apr_train(acf_apr_ctx* ctx, const acf_apr_tables* tables, const acf_apr_
  * with hipExtLaunchKernelGGL start/stop events.  Writes, per kernel kind
  * k = 0 (clean pass, or the fused BPR step), 1 (adversarial pass + Adagrad),
  * 2 (write-back: k_flush / k_stream_flush), 3 (overlapped step k_ovl),
- * 4 (streamed step k_stream), the summed kernel time in ms to ms_out[k] and
- * the launch count to launches_out[k] (arrays of 5).  Synchronous.  Not part
- * of the reference surface. */
+ * 4 (streamed step k_stream), 5 (hot-slot combine of large-batch plans), the
+ * summed kernel time in ms to ms_out[k] and the launch count to
+ * launches_out[k] (arrays of 6).  Synchronous.  Not part of the reference
+ * surface. */
 int acf_apr_time_kernels(acf_apr_ctx* ctx, const acf_apr_tables* tables,
                          const acf_apr_hparams* hp, int32_t first_batch,
                          int32_t n_batches, double* ms_out, int32_t* launches_out,

@@ -456,6 +456,63 @@ def test_large_batch_auto_mapping_matches_oracle(ops, oracle, dev, d, fp32_parit
         fp32_parity(g, w, n)
 
 
+def _zipf_large(seed, U1, I1, d, B, nb, s=1.1):
+    """Config-5-shaped batches: uniform users and negatives, Zipf
+    positives, so a batch of 65,536 holds items with thousands of occurrences."""
+    rng = np.random.default_rng(seed)
+    P = (rng.standard_normal((U1, d)) * 0.1).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.1).astype(np.float32)
+    u = rng.integers(0, U1, nb * B).astype(np.int32)
+    i = ((rng.zipf(s, nb * B) - 1) % I1).astype(np.int32)
+    j = rng.integers(0, I1, nb * B).astype(np.int32)
+    return P, Q, u, i, j
+
+
+@pytest.mark.parametrize("d,adver", [(64, 1), (128, 1), (64, 0)])
+def test_hot_slots_large_batch_match_oracle(ops, oracle, dev, d, adver, fp32_parity):
+    """B = 65,536 with Zipf positives: slots with more than ACF_HOT_MIN (8)
+    occurrences run as pieces + k_hot_combine (the top item has ~3,000
+    occurrences per batch).  Tables and losses vs the oracle, and the hot path
+    really ran (kind 'hot' launches)."""
+    U1, I1, B, nb = 300_000, 200_000, 65536, 2
+    P, Q, u, i, j = _zipf_large(d + adver, U1, I1, d, B, nb)
+    assert np.bincount(i[:B]).max() > 1000
+    want, lc_w, la_w, _ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=adver))
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    t = ctx.time_kernels(tabs, ops.StepHParams(adver=adver))
+    assert t["hot"][1] == nb * (2 if adver else 1)
+    lc, la = ctx.losses()
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        fp32_parity(g, w, n)
+    n_terms = max(2 * np.bincount(u).max(), np.bincount(np.concatenate([i, j])).max())
+    rtol = max(RTOL, 2 * n_terms * 2.0 ** -24)  # Higham bound, as test_single_step_strict
+    np.testing.assert_allclose(lc.cpu().numpy(), lc_w, rtol=rtol, atol=ATOL)
+    if adver:
+        np.testing.assert_allclose(la.cpu().numpy(), la_w, rtol=rtol, atol=ATOL)
+    assert ctx.step_errors() == 0
+
+
+def test_hot_slots_deterministic(ops, dev):
+    """The hot lists are appended with atomics (their order varies run to run);
+    each slot's pieces are still summed in piece order, so two runs give
+    identical bits, graph or eager."""
+    U1, I1, d, B, nb = 200_000, 100_000, 64, 32768, 3
+    P, Q, u, i, j = _zipf_large(3, U1, I1, d, B, nb)
+    runs = []
+    for graph in (False, True, True):
+        tabs = _gpu_tables(P, Q, dev)
+        ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+        ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+        ctx.train_planned(tabs, ops.StepHParams(adver=1), graph=graph)
+        lc, la = ctx.losses()
+        runs.append(tabs + [lc.clone(), la.clone()])
+    for other in runs[1:]:
+        for x, y in zip(runs[0], other):
+            assert torch.equal(x, y)
+
+
 def _sparse_stream(seed, U1, I1, B, nb, hot=64, p_hot=0.05):
     """Mostly rows that occur once per batch (fused triplets), plus a small hot
     set that recurs across consecutive batches (pending / next-batch rows)."""
