@@ -441,7 +441,7 @@ __device__ __forceinline__ OccRec item_rec(const int4& own, const int4& oth, con
 // One thread per triplet: its user and two item occurrence records and, when
 // fused, its fused-triplet record.  The first R records of a slot go inline
 // only (that is the only place they are read from), later ones to the CSR.
-__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb,
+__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb, int32_t no_fuse,
                           const int4* __restrict__ tsl, const int4* __restrict__ tpos,
                           const int4* __restrict__ uinfo, const int4* __restrict__ iinfo,
                           const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
@@ -456,7 +456,8 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
   const int32_t t = (int32_t)(e / B);
   const int32_t nU = ubs[t + 1] - ubs[t];
   const int32_t k = sl.x - ubs[t], ki = nU + (sl.y - ibs[t]), kj = nU + (sl.z - ibs[t]);
-  const FuseInfo f = fuse_info(U, I, J, kb);
+  FuseInfo f = fuse_info(U, I, J, kb);
+  if (no_fuse) f.fused = f.in_u = f.in_i = f.in_j = 0;  // shard mode: item counts are rank-local
   OccRec r;
   r.own_row = U.x;
   r.own_src = U.y;
@@ -952,6 +953,11 @@ struct StepArgs {
   HotLists hot;
   float* hot_part;     // [piece_stride, d]
   int32_t hot_waves;
+  // shard mode (distributed.ShardedAPR): item rows of the batch are this rank's
+  // partial sums; an item slot's clean / adversarial sum goes to g0[k] for the
+  // exchange instead of Adagrad, and item rows are never written back
+  int32_t shard;
+  int32_t reg_B;       // batch size of reg * mean(w^2) (the global batch in shard mode)
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -1186,6 +1192,7 @@ __device__ __forceinline__ void flush_slot(const StepArgs& a, int tb, const floa
   const RecV r = load_rec(a.inl + ((int64_t)tb * a.S + k) * a.R);
   if (r.gen() != *a.gen_ptr || (r.meta() & ACF_COUNT_MASK) == 0) return;
   if (a.use_single && (r.meta() & ACF_INPLACE_BIT)) return;  // written by its fused triplet
+  if (a.shard && (r.meta() & ACF_ITEM_BIT)) return;            // owned by another rank's update
   float* dst = ((r.meta() & ACF_ITEM_BIT) ? a.Q : a.P) + (int64_t)r.own_row() * a.d;
   const float* src = wsrc + (int64_t)k * a.d;
   for (int c = tl; c * 4 < a.d; c += tn)
@@ -1230,7 +1237,7 @@ template <int NV>
 __device__ __forceinline__ void adagrad_row(const StepArgs& a, RowV<NV>& G, const RowV<NV>& w,
                                             RowV<NV>& acc, int m, RowV<NV>& wout) {
   if (a.reg != 0.f) {
-    const float coef = (2.0f * a.reg / ((float)a.B * (float)a.d)) * (float)(a.adver ? 2 * m : m);
+    const float coef = (2.0f * a.reg / ((float)a.reg_B * (float)a.d)) * (float)(a.adver ? 2 * m : m);
     axpy_row(G, coef, w);
   }
 #pragma unroll
@@ -1512,7 +1519,9 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
   team_allreduce<LPR, TEAM, NV>(G);
   if (FLUSH) flush_store(fo);
   if (FUSE_APPLY) {
-    if (m == 0) {
+    if (m == 0 && a.shard && h.is_item) {  // partial item sum for the owner
+      store_row<LPR, NV>(a.g0, k, d, l, G);
+    } else if (m == 0) {
       RowV<NV> wout;
       adagrad_row(a, G, own, acc, h.count, wout);
       store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
@@ -1604,7 +1613,9 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
   STAMP(a.diag_launch, wave, 2);
   team_allreduce<LPR, TEAM, NV>(G);
   if (OFL) flush_store(fo);
-  if (m == 0) {
+  if (m == 0 && a.shard && h.is_item) {  // partial adversarial item sum for the owner
+    store_row<LPR, NV>(a.g0, k, d, l, G);
+  } else if (m == 0) {
     axpy_row(G0, a.reg_adv, G);
     RowV<NV> wout;
     adagrad_row(a, G0, own, acc, h.count, wout);
@@ -2317,7 +2328,9 @@ __global__ void __launch_bounds__(256) k_hot_combine(StepArgs a) {
       const int32_t row = r.own_row();
       const float* own_tab = is_item ? a.Q : a.P;
       float* acc_tab = is_item ? a.accQ : a.accP;
-      if (MODE == 0) {
+      if (MODE != 0 && a.shard && is_item) {  // partial item sum for the owner
+        store_row<LPR, NV>(a.g0, k, d, l, G);
+      } else if (MODE == 0) {
         const RowV<NV> dl = make_delta<LPR, NV>(a, G, is_item, row, l);
         store_row<LPR, NV>(a.g0, k, d, l, G);
         store_row<LPR, NV>(a.delta, k, d, l, dl);
@@ -2689,6 +2702,8 @@ struct acf_apr_ctx {
   int32_t touch_next = 1;  // phase 2 reads the next batch's records (ACF_TOUCH_NEXT=0 disables)
   int32_t *slot_list = nullptr, *flush_list = nullptr, *slot_cnt = nullptr, *flush_cnt = nullptr;
   HotLists hot = {};            // hot slots of list plans (k_slot_flags)
+  int32_t shard = 0;            // shard mode (acf_apr_set_shard_mode): item rows are partial sums
+  int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
   int32_t overlap = 1;  // k_ovl for APR runs of one-wave-per-slot plans (ACF_STEP_OVERLAP=0 disables)
@@ -2721,6 +2736,11 @@ struct acf_apr_ctx {
   std::map<GraphKey, hipGraphExec_t> graphs;
   std::vector<void*> allocs;
 };
+
+// one lane-group per slot: large batches (auto), mapping 2, and always in shard mode
+static int is_packed(const acf_apr_ctx* c, int32_t B) {
+  return c->shard || c->mapping == 2 || (c->mapping == 0 && B >= ACF_PACKED_MIN_BATCH);
+}
 
 static uint32_t bits_for(uint64_t v) {  // bits to represent values in [0, v)
   uint32_t b = 0;
@@ -3019,7 +3039,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->last_delta_batch = -1;
   const int32_t gen = ++c->gen;
   {
-    const int packed = c->mapping == 2 || (c->mapping == 0 && B >= ACF_PACKED_MIN_BATCH);
+    const int packed = is_packed(c, B);
     const int32_t kb = (int32_t)bits_for((uint64_t)3 * B + 1);
     if (!packed && c->plan_mode == 0 && B <= 1024 && kb + bits_for((uint64_t)nb + 1) <= 31 && bplan_ready(c))
       return batch_plan(c, user, ipos, ineg, B, nb, gen, kb, check, s);
@@ -3054,7 +3074,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   // where each unique row's value lives at batch start, then the records; one
   // lane-group per slot (large batches) reads only a slot's first record inline
   // and never runs k_ovl, so only one-wave-per-slot plans encode t-2 sources
-  const int packed = c->mapping == 2 || (c->mapping == 0 && B >= ACF_PACKED_MIN_BATCH);
+  const int packed = is_packed(c, B);
   const int32_t kb = (int32_t)bits_for((uint64_t)3 * B + 1);
   // one-wave-per-slot plans encode every earlier batch (dt < nb must fit the src)
   const VKeys vk{(int32_t)bits_for((uint64_t)std::max(c->U1, c->I1)), (int32_t)bits_for((uint64_t)nb), 0};
@@ -3092,7 +3112,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->plan_R = packed ? 1 : c->R;
   c->plan_kind2 = all_dt;
   c->plan_kb = kb;
-  k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen, kb,
+  k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen, kb, c->shard,
                                         reinterpret_cast<const int4*>(c->tsl),
                                         reinterpret_cast<const int4*>(c->tpos), c->uinfo, c->iinfo,
                                         c->ubs, c->ibs, c->urec, c->irec, c->inl, c->trec, c->gen_dev);
@@ -3169,6 +3189,8 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.hot = c->hot;
   a.hot_part = c->hot_part;
   a.hot_waves = 0;
+  a.shard = c->shard;
+  a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -3238,8 +3260,7 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists) {
 // per slot, 2 one lane-group per slot
 
 static int get_kernels(const acf_apr_ctx* c, Kernels* k, int fused = 0) {
-  const int packed = c->mapping == 2 || (c->mapping == 0 && c->B >= ACF_PACKED_MIN_BATCH);
-  return DISPATCH_GEOM(c->d, kernel_ptrs, k, packed, fused, c->lists);
+  return DISPATCH_GEOM(c->d, kernel_ptrs, k, is_packed(c, c->B), fused || c->shard, c->lists);
 }
 
 typedef void (*StepKernel)(StepArgs);
@@ -3358,6 +3379,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     if (kinds) kinds[li] = kind;
     StepArgs b = a;
     b.diag_launch = li;
+    if (kind == 5) b.slot_waves = waves;  // k_hot_combine: workgroups stride over the hot slots
     ++li;
     return launch(fn, b, waves, s, e0, e1);
   };
@@ -3611,6 +3633,195 @@ extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);
   c->overlap = on;
+  return ACF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Shard mode (distributed.ShardedAPR).  Users live on rank u % G
+// and every triplet runs on its user's rank, so user rows are complete here;
+// an item's occurrences are spread over the ranks, so its clean / adversarial
+// sums are partial and are summed by the item's owner (rank i % G) between
+// the two passes.  One step = one plan of this rank's triplets of the batch
+// (tables: the local user shard and the fetched item working set, slots in
+// working-set order) and two passes:
+//   pass 0: clean sums.  Users: g0, delta.  Items: partial sums in g0
+//           (acf_apr_shard_items dir 0 copies them out; the owners' deltas come
+//           back through dir 1 into the delta rows).  BPR: users are updated here.
+//   pass 1: adversarial sums.  Users: Adagrad + write-back.  Items: partial
+//           sums in g0 for the owners' Adagrad (acf_shard_reduce_apply).
+// ---------------------------------------------------------------------------
+extern "C" int acf_apr_set_shard_mode(acf_apr_ctx* c, int32_t on, int32_t reg_batch) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(reg_batch >= 0, ACF_E_INVALID, "reg_batch must be >= 0");
+  c->shard = on != 0;
+  c->reg_batch = reg_batch;
+  c->nb = 0;  // re-plan: the records depend on the mode
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_shard_pass(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
+                                  int32_t pass, void* stream_) {
+  ACF_RET(check_step(c, tb, hp, 0));
+  ACF_CHECK(c->shard && c->lists && c->nb == 1, ACF_E_STATE,
+            "shard pass needs shard mode and a one-batch plan");
+  ACF_CHECK(pass == 0 || (pass == 1 && hp->adver), ACF_E_INVALID, "pass must be 0, or 1 for APR");
+  ACF_CHECK(hp->adv_mode == 0, ACF_E_INVALID, "shard mode supports adv = grad only");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  Kernels K;
+  ACF_RET(get_kernels(c, &K, 0));
+  ACF_CHECK(K.lists, ACF_E_STATE, "shard mode needs the list kernels");
+  const int S = 3 * c->B;
+  const int SW = std::min((S + K.slots_per_wave - 1) / K.slots_per_wave, ACF_LIST_WAVES);
+  const int HW = std::min(c->hot.piece_stride, ACF_HOT_WAVES);
+  const int HB = std::min(c->hot.hot_stride, ACF_HOT_BLOCKS);
+  StepArgs a = make_args(c, tb, hp, 0, 0);
+  a.use_single = 0;
+  a.slot_waves = SW;
+  a.hot_waves = HW;
+  if (pass == 0) {
+    ACF_RET(launch(hp->adver ? K.clean_apr : K.clean_bpr, a, SW + HW, s));
+  } else {
+    ACF_RET(launch(K.adv, a, SW + HW, s));
+  }
+  StepArgs ah = a;
+  ah.slot_waves = 4 * HB;  // k_hot_combine: workgroups stride over the hot slots
+  ACF_RET(launch(pass == 1 ? K.hot_adv : (hp->adver ? K.hot_clean : K.hot_bpr), ah, 4 * HB, s));
+  if (pass == 1 || !hp->adver) {  // user rows W scratch -> the user shard
+    a.slot_waves = S;
+    a.hot_waves = 0;
+    ACF_RET(launch(K.flush, a, S, s));
+  }
+  return ACF_OK;
+}
+
+// item slot rows of the current one-batch plan (slots nU .. nU + n, nU read
+// on device): dir 0 copies g0 -> buf, dir 1 copies buf -> delta
+__global__ void k_shard_items(float* __restrict__ g0, float* __restrict__ delta, const int32_t* __restrict__ ubs,
+                              float* __restrict__ buf, int64_t n4, int32_t d4, int32_t dir) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= n4) return;
+  const int64_t off = (int64_t)(ubs[1] - ubs[0]) * d4;
+  float4* b = reinterpret_cast<float4*>(buf) + x;
+  if (dir == 0) *b = reinterpret_cast<const float4*>(g0)[off + x];
+  else reinterpret_cast<float4*>(delta)[off + x] = *b;
+}
+
+extern "C" int acf_apr_shard_items(acf_apr_ctx* c, int32_t dir, float* buf, int64_t n_items, void* stream_) {
+  ACF_CHECK(c && (buf || n_items == 0), ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(c->shard && c->nb == 1, ACF_E_STATE, "shard items need shard mode and a one-batch plan");
+  ACF_CHECK(dir == 0 || dir == 1, ACF_E_INVALID, "dir must be 0 or 1");
+  ACF_CHECK(n_items >= 0 && n_items <= 2 * (int64_t)c->B, ACF_E_INVALID, "n_items %lld outside [0, 2B]",
+            (long long)n_items);
+  if (n_items == 0) return ACF_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  const int64_t n4 = n_items * (c->d / 4);
+  k_shard_items<<<grid_for(n4), 256, 0, s>>>(c->g0, c->delta, c->ubs, buf, n4, c->d / 4, dir);
+  HIP_TRY(hipGetLastError());
+  return ACF_OK;
+}
+
+// Owner side: the partial rows the requesters sent, grouped per owned row by
+// `seg` (seg[s] .. seg[s+1] index `pos`, positions into `recv` in requester
+// order: a fixed summation order).  One lane-group per owned row.
+// k_shard_delta: G = sum -> G0[s]; delta = eps * l2_normalize(G) (APR.py:186-191)
+// to every position of the row (the reply, in `recv` order).
+template <int LPR, int NV>
+__global__ void __launch_bounds__(256) k_shard_delta(StepArgs a, const float* __restrict__ recv,
+                                                     const int32_t* __restrict__ seg,
+                                                     const int32_t* __restrict__ pos, int32_t nseg,
+                                                     float* __restrict__ G0, float* __restrict__ reply) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int sx = (int)(gid / LPR), l = (int)(threadIdx.x & (LPR - 1));
+  if (sx >= nseg) return;
+  const int d = a.d;
+  RowV<NV> G = zero_row<NV>();
+  for (int p = seg[sx]; p < seg[sx + 1]; ++p) G = add_row(G, load_row<LPR, NV>(recv, pos[p], d, l));
+  store_row<LPR, NV>(G0, sx, d, l, G);
+  const RowV<NV> dl = a.zero_delta ? zero_row<NV>() : make_delta<LPR, NV>(a, G, 1, 0, l);
+  for (int p = seg[sx]; p < seg[sx + 1]; ++p) store_row<LPR, NV>(reply, pos[p], d, l, dl);
+}
+
+// k_shard_apply: G = G0[s] + reg_adv * sum (APR) or sum (BPR), then TF's sparse
+// Adagrad on the owned row (Q[rows[s]], accQ[rows[s]]), the reg term counting
+// the row's occurrences in the global batch (count[s]).
+template <int LPR, int NV>
+__global__ void __launch_bounds__(256) k_shard_apply(StepArgs a, const float* __restrict__ recv,
+                                                     const int32_t* __restrict__ seg,
+                                                     const int32_t* __restrict__ pos, int32_t nseg,
+                                                     const float* __restrict__ G0,
+                                                     const int32_t* __restrict__ rows,
+                                                     const int32_t* __restrict__ count) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int sx = (int)(gid / LPR), l = (int)(threadIdx.x & (LPR - 1));
+  if (sx >= nseg) return;
+  const int d = a.d;
+  RowV<NV> G = zero_row<NV>();
+  for (int p = seg[sx]; p < seg[sx + 1]; ++p) G = add_row(G, load_row<LPR, NV>(recv, pos[p], d, l));
+  RowV<NV> Gt = G;
+  if (a.adver) {
+    Gt = load_row<LPR, NV>(G0, sx, d, l);
+    axpy_row(Gt, a.reg_adv, G);
+  }
+  const int32_t row = rows[sx];
+  const RowV<NV> w = load_row<LPR, NV>(a.Q, row, d, l);
+  RowV<NV> acc = load_row<LPR, NV>(a.accQ, row, d, l);
+  RowV<NV> wout;
+  adagrad_row(a, Gt, w, acc, count ? count[sx] : 0, wout);
+  store_row<LPR, NV>(a.accQ, row, d, l, acc);
+  store_row<LPR, NV>(a.Q, row, d, l, wout);
+}
+
+static StepArgs owner_args(const acf_apr_hparams* hp, float* Q, float* accQ, int32_t d, int32_t reg_batch) {
+  StepArgs a;
+  memset(&a, 0, sizeof(a));
+  a.Q = Q; a.accQ = accQ; a.d = d; a.B = reg_batch; a.reg_B = reg_batch;
+  a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
+  a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
+  a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
+  return a;
+}
+
+template <int LPR, int NV>
+static void launch_shard_delta(const StepArgs& a, const float* recv, const int32_t* seg, const int32_t* pos,
+                               int32_t nseg, float* G0, float* reply, hipStream_t s) {
+  k_shard_delta<LPR, NV><<<grid_for((int64_t)nseg * LPR), 256, 0, s>>>(a, recv, seg, pos, nseg, G0, reply);
+}
+
+template <int LPR, int NV>
+static void launch_shard_apply(const StepArgs& a, const float* recv, const int32_t* seg, const int32_t* pos,
+                               int32_t nseg, const float* G0, const int32_t* rows, const int32_t* count,
+                               hipStream_t s) {
+  k_shard_apply<LPR, NV><<<grid_for((int64_t)nseg * LPR), 256, 0, s>>>(a, recv, seg, pos, nseg, G0, rows, count);
+}
+
+extern "C" int acf_shard_reduce_delta(const float* recv, const int32_t* seg, const int32_t* pos, int32_t n_rows,
+                                      int32_t d, const acf_apr_hparams* hp, float* G0, float* reply,
+                                      void* stream_) {
+  ACF_RET(check_dim(d));
+  ACF_CHECK(hp && n_rows >= 0, ACF_E_INVALID, "bad argument");
+  ACF_CHECK(hp->adv_mode == 0, ACF_E_INVALID, "shard mode supports adv = grad only");
+  if (n_rows == 0) return ACF_OK;
+  ACF_CHECK(recv && seg && pos && G0 && reply, ACF_E_INVALID, "NULL pointer");
+  const StepArgs a = owner_args(hp, nullptr, nullptr, d, 1);
+  ACF_RET(DISPATCH_GEOM(d, launch_shard_delta, a, recv, seg, pos, n_rows, G0, reply,
+                        static_cast<hipStream_t>(stream_)));
+  HIP_TRY(hipGetLastError());
+  return ACF_OK;
+}
+
+extern "C" int acf_shard_reduce_apply(float* Q, float* accQ, const float* recv, const int32_t* seg,
+                                      const int32_t* pos, int32_t n_rows, int32_t d, const acf_apr_hparams* hp,
+                                      const float* G0, const int32_t* rows, const int32_t* count,
+                                      int32_t reg_batch, void* stream_) {
+  ACF_RET(check_dim(d));
+  ACF_CHECK(hp && n_rows >= 0, ACF_E_INVALID, "bad argument");
+  if (n_rows == 0) return ACF_OK;
+  ACF_CHECK(Q && accQ && recv && seg && pos && rows && (G0 || !hp->adver), ACF_E_INVALID, "NULL pointer");
+  ACF_CHECK(hp->reg == 0.f || (count && reg_batch > 0), ACF_E_INVALID, "reg != 0 needs counts and reg_batch");
+  const StepArgs a = owner_args(hp, Q, accQ, d, reg_batch > 0 ? reg_batch : 1);
+  ACF_RET(DISPATCH_GEOM(d, launch_shard_apply, a, recv, seg, pos, n_rows, G0, rows, count,
+                        static_cast<hipStream_t>(stream_)));
+  HIP_TRY(hipGetLastError());
   return ACF_OK;
 }
 

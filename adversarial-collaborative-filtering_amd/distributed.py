@@ -1,138 +1,302 @@
-"""Row-sharded tables across the GPUs of one node (BASELINE.json configs[2]:
-"item table row-sharded across 8 x MI355X with RCCL all-gather of negative rows
-over xGMI").
+"""APR training split across the GPUs of one node (BASELINE.json
+configs[2] "item table row-sharded across 8 x MI355X" and configs[4] "8 x MI355X").
 
-Ownership: row r of P (users) and of Q (items), with its Adagrad slot, lives on
-rank r % world at local index r // world.  Nothing is replicated.
+The reference trains one process on one CPU (``training_batch``, utils.py:106-119,
+over the TF1 graph of APR.py:121-195).  Here one global batch of triplets is
+split over G ranks (one process per GPU, RCCL over xGMI) and the result is the
+single-process step up to fp32 summation order.
 
-One chunk of consecutive mini-batches (the same global triplet stream on every
-rank) runs as:
+Ownership (nothing replicated):
+  * user row u of P (and its Adagrad slot) on rank u % G at local row u // G;
+  * item row i of Q (and its Adagrad slot) on rank i % G at local row i // G.
 
-1. working set: the unique users / items the chunk touches (sorted);
-2. ONE all-gather: each rank contributes the [w | acc] rows it owns of that
-   working set (user rows and item rows — positives and sampled negatives);
-3. every rank runs the chunk's batches on the compact working-set tables with the
-   single-GPU step kernels (remapped indices) — a B = 512 step is far too small to
-   split, so it is computed redundantly rather than exchanged per phase;
-4. each owner writes its rows back.
+Routing: a triplet (u, i, j) runs on its USER's rank, so a user's batch-summed
+clean gradient, its delta and its Adagrad step are local.  An item's
+occurrences are spread over the ranks, so the batch-global item sums the graph
+needs (the delta of APR.py:183-191 and the dedup before SparseApplyAdagrad,
+APR.py:193-195) are completed by the item's owner.  One step:
 
-The per-row arithmetic and the per-row occurrence order are the ones of the
-single-GPU path, so the result is bit-identical to training the full tables on
-one device (tests/test_distributed.py checks it with gloo on CPU; on GPUs the
-collective is RCCL over xGMI).  Communication per chunk = 2 x d x 4 B x
-working-set rows; it buys capacity (tables 1/world per GPU), not speed — the
-benchmark's multi-GPU line runs independent replicas instead.
+  E1  owners send the current Q rows of each rank's item working set
+      (all_to_all; the working set is the rank's unique items of the batch);
+  P0  local clean pass (HIP, shard mode): user delta; partial item sums;
+  E2  partial item sums -> owners (all_to_all); owners sum them in requester
+      order and form delta = eps * l2_normalize(sum);
+  E3  deltas -> requesters (all_to_all);
+  P1  local adversarial pass: user Adagrad; partial adversarial item sums;
+  E4  -> owners (all_to_all); owners: G = clean + reg_adv * adversarial, Adagrad.
+
+BPR (adver = 0): E1, P0 (users updated), E2 + owner Adagrad.
+
+The working sets and the exchange plans of a whole chunk of steps are built on
+device in one go (one host sync per chunk, for the all_to_all split sizes).
+Every rank sees the same global triplet stream (the sampler is seeded
+identically) and keeps its users' triplets, in stream order.
+
+The local compute is pluggable: :class:`HipLocal` (the product path: the step
+kernels in shard mode, include/acf_apr.h) on GPUs; the CPU tests plug in the
+oracle's restatement (oracle/shard_oracle.py) to exercise the same routing and
+exchanges over gloo.
 """
 from __future__ import annotations
-
-from typing import Callable
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
-# step_fn(P, Q, accP, accQ, u, i, j, batch_size, hp) trains in place on the tables
-StepFn = Callable[..., None]
+
+class HipLocal:
+    """One rank's local passes and owner reductions on the HIP kernels."""
+
+    def __init__(self, sh: "ShardedAPR"):
+        from . import ops
+        self.ops = ops
+        self.sh = sh
+        self.ctx = ops.APRContext(sh.P.shape[0], sh.max_items, sh.d, sh.B, 1, sh.device)
+        self.ctx.set_shard_mode(True, reg_batch=sh.B)
+        # the fetched item rows are never updated locally; their Adagrad slots are unused
+        self.accQc = torch.full((sh.max_items, sh.d), 0.1, device=sh.device)
+
+    def _tables(self):
+        sh = self.sh
+        return (sh.P, sh.Qc, sh.accP, self.accQc)
+
+    def plan(self, u_rows, wi, wj):
+        self.ctx.plan(u_rows, wi, wj, u_rows.numel(), check=False)
+
+    def clean(self, hp, out):
+        self.ctx.shard_pass(self._tables(), hp, 0)
+        self.ctx.shard_items_out(out)
+
+    def set_item_delta(self, delta):
+        self.ctx.shard_items_delta(delta)
+
+    def adv(self, hp, out):
+        self.ctx.shard_pass(self._tables(), hp, 1)
+        self.ctx.shard_items_out(out)
+
+    def reduce_delta(self, hp, recv, seg, pos, G0, reply):
+        self.ops.shard_reduce_delta(recv, seg, pos, hp, G0, reply)
+
+    def reduce_apply(self, hp, recv, seg, pos, G0, rows, count):
+        self.ops.shard_reduce_apply(self.sh.Q, self.sh.accQ, recv, seg, pos, hp, G0, rows, count,
+                                    reg_batch=self.sh.B)
+
+    def step_errors(self) -> int:
+        return self.ctx.step_errors()
 
 
-def hip_step(P, Q, accP, accQ, u, i, j, batch_size, hp, _cache={}):
-    """Default step: the HIP kernels (plan + hipGraph replay) on device tensors."""
-    from . import ops
-    nb = u.numel() // batch_size
-    key = (P.shape[0], Q.shape[0], P.shape[1], batch_size, P.device)
-    ctx = _cache.get(key)
-    if ctx is None or not ctx.fits(batch_size, nb):
-        ctx = _cache[key] = ops.APRContext(P.shape[0], Q.shape[0], P.shape[1], batch_size,
-                                           max(nb, ctx.max_batches if ctx else 0), P.device)
-    ctx.plan(u, i, j, batch_size)
-    ctx.train_planned((P, Q, accP, accQ), hp, 0, nb, graph=False)
+class _Chunk:
+    """Device-side routing of one chunk of T global batches for this rank, plus
+    the host copies of the split sizes."""
 
 
-class ShardedTables:
-    """This rank's shard of embedding_P / embedding_Q and their Adagrad slots."""
+class ShardedAPR:
+    """This rank's shard of embedding_P / embedding_Q (+ Adagrad slots) and the
+    split APR step.  ``batch_size`` is the GLOBAL batch (the reference's
+    ``--batch_size``); each rank processes the triplets of its users."""
 
-    def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, device=None, group=None,
-                 init_P=None, init_Q=None, acc0: float = 0.1):
+    def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, batch_size: int, device=None,
+                 group=None, init_P=None, init_Q=None, acc0: float = 0.1, local=None):
         self.group = group
-        self.world = dist.get_world_size(group)
+        self.G = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.U1, self.I1, self.d = int(num_user_rows), int(num_item_rows), int(dim)
+        self.U1, self.I1, self.d, self.B = int(num_user_rows), int(num_item_rows), int(dim), int(batch_size)
+        if self.U1 < self.G or self.I1 < self.G:
+            raise ValueError(f"tables of {self.U1} x {self.I1} rows cannot be split over {self.G} ranks")
         self.device = torch.device(device) if device is not None else torch.device("cpu")
-        rows_u = np.arange(self.rank, self.U1, self.world)
-        rows_i = np.arange(self.rank, self.I1, self.world)
+        self._stage = self.device.type == "cuda" and dist.get_backend(group) == "gloo"
+        G, r = self.G, self.rank
         f = dict(dtype=torch.float32, device=self.device)
-        self.P = torch.empty(len(rows_u), dim, **f)
-        self.Q = torch.empty(len(rows_i), dim, **f)
+        nu, ni = len(range(r, self.U1, G)), len(range(r, self.I1, G))
+        self.P = torch.empty(nu, dim, **f)
+        self.Q = torch.empty(ni, dim, **f)
         if init_P is not None:
-            self.P.copy_(torch.as_tensor(np.asarray(init_P)[rows_u]))
-            self.Q.copy_(torch.as_tensor(np.asarray(init_Q)[rows_i]))
-        self.accP = torch.full((len(rows_u), dim), acc0, **f)
-        self.accQ = torch.full((len(rows_i), dim), acc0, **f)
+            self.P.copy_(torch.as_tensor(np.asarray(init_P, np.float32)[r::G]))
+            self.Q.copy_(torch.as_tensor(np.asarray(init_Q, np.float32)[r::G]))
+        self.accP = torch.full((nu, dim), acc0, **f)
+        self.accQ = torch.full((ni, dim), acc0, **f)
+        self.max_items = 2 * self.B  # a rank's working set of one batch: <= 2 x its triplets
+        self.Qc = torch.zeros(self.max_items, dim, **f)
+        self._send = torch.empty(self.max_items, dim, **f)
+        self._dlt = torch.empty(self.max_items, dim, **f)
+        self._recv = torch.empty(0, dim, **f)
+        self.local = local(self) if local is not None else HipLocal(self)
+        self.stats = {"steps": 0, "items_requested": 0, "rows_served": 0, "triplets": 0}
 
-    # -- helpers ---------------------------------------------------------------
-    def _gather_rows(self, table, acc, rows: np.ndarray):
-        """All-gather [w | acc] of `rows` (sorted global ids) from their owners,
-        returned in `rows` order."""
-        W, G, d = self.world, self.group, self.d
-        mine = rows[rows % W == self.rank]
-        local = torch.as_tensor(mine // W, dtype=torch.long, device=self.device)
-        payload = torch.cat([table[local], acc[local]], 1)
-        counts = np.bincount(rows % W, minlength=W)
-        cap = int(counts.max()) if len(rows) else 0
-        buf = torch.zeros(cap, 2 * d, dtype=torch.float32, device=self.device)
-        buf[: len(mine)] = payload
-        parts = [torch.empty_like(buf) for _ in range(W)]
-        dist.all_gather(parts, buf, group=G)
-        out = torch.empty(len(rows), 2 * d, dtype=torch.float32, device=self.device)
-        for r in range(W):
-            sel = np.flatnonzero(rows % W == r)
-            if len(sel):
-                out[torch.as_tensor(sel, device=self.device)] = parts[r][: len(sel)]
-        return out[:, :d].contiguous(), out[:, d:].contiguous()
+    # -- collectives ---------------------------------------------------------------
+    def _a2a(self, out, inp, out_splits, in_splits):
+        if self._stage:  # gloo with device tensors (rehearsal of several ranks on one GPU)
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def _write_back(self, table, acc, rows: np.ndarray, w, a):
-        W = self.world
-        sel = np.flatnonzero(rows % W == self.rank)
-        if not len(sel):
-            return
-        s = torch.as_tensor(sel, device=self.device)
-        local = torch.as_tensor(rows[sel] // W, dtype=torch.long, device=self.device)
-        table[local] = w[s]
-        acc[local] = a[s]
-
-    # -- training ----------------------------------------------------------------
-    def train_chunk(self, u, i, j, batch_size: int, hp, step_fn: StepFn = hip_step):
-        """Train consecutive batches of the global stream (u, i, j identical on
-        every rank).  hp: the step hyper-parameters understood by step_fn."""
-        u = np.asarray(u, dtype=np.int64).reshape(-1)
-        i = np.asarray(i, dtype=np.int64).reshape(-1)
-        j = np.asarray(j, dtype=np.int64).reshape(-1)
-        if u.size and (u.min() < 0 or u.max() >= self.U1 or min(i.min(), j.min()) < 0
-                       or max(i.max(), j.max()) >= self.I1):
+    # -- routing (one chunk of T global batches) -----------------------------------
+    def _route(self, u, i, j, T: int) -> _Chunk:
+        G, r, B, I1 = self.G, self.rank, self.B, self.I1
+        dev = self.device
+        u, i, j = (torch.as_tensor(x, device=dev).reshape(-1)[: T * B].long() for x in (u, i, j))
+        if u.numel() != T * B:
+            raise ValueError(f"{u.numel()} triplets for {T} batches of {B}")
+        if u.numel() and (int(torch.minimum(u.min(), torch.minimum(i.min(), j.min()))) < 0
+                          or int(u.max()) >= self.U1 or int(torch.maximum(i.max(), j.max())) >= I1):
             raise IndexError("triplet index outside the sharded tables")
-        ws_u = np.unique(u)
-        ws_i = np.unique(np.concatenate([i, j]))
-        Pw, aPw = self._gather_rows(self.P, self.accP, ws_u)
-        Qw, aQw = self._gather_rows(self.Q, self.accQ, ws_i)
-        to_dev = lambda x: torch.as_tensor(x.astype(np.int32), device=self.device)  # noqa: E731
-        step_fn(Pw, Qw, aPw, aQw, to_dev(np.searchsorted(ws_u, u)), to_dev(np.searchsorted(ws_i, i)),
-                to_dev(np.searchsorted(ws_i, j)), batch_size, hp)
-        self._write_back(self.P, self.accP, ws_u, Pw, aPw)
-        self._write_back(self.Q, self.accQ, ws_i, Qw, aQw)
-        return len(ws_u), len(ws_i)
+        c = _Chunk()
+        c.T = T
+        sel = torch.nonzero(u % G == r).squeeze(1)  # this rank's triplets, stream order
+        st = sel // B
+        n = sel.numel()
+        c.u_rows = (u[sel] // G).to(torch.int32)
+        items = torch.cat([i[sel], j[sel]])
+        ist = torch.cat([st, st])
+        # working set per step: unique items, ordered by (owner, id) so that each
+        # owner's rows are one contiguous block of the all_to_all buffers
+        uk, inv = torch.unique((ist * G + items % G) * I1 + items, return_inverse=True)
+        wstep, wown, wid = uk // (G * I1), (uk // I1) % G, uk % I1
+        cnt = torch.bincount(wstep * G + wown, minlength=T * G).view(T, G)
+        nloc = torch.bincount(st, minlength=T)
+        nW = cnt.sum(1)
+        wstart = torch.cumsum(nW, 0) - nW
+        widx = (inv - wstart[ist]).to(torch.int32)
+        c.wi, c.wj = widx[:n], widx[n:]
+        # the requests of the whole chunk, owner-major, in one exchange
+        order = torch.argsort((wown * T + wstep) * I1 + wid)
+        req = (wid // G)[order]
+        rc = torch.empty_like(cnt.t().contiguous())
+        self._a2a(rc.view(-1), cnt.t().contiguous().view(-1), [T] * G, [T] * G)
+        host = torch.cat([cnt.reshape(-1), rc.reshape(-1), nloc]).cpu().numpy()  # the chunk's one sync
+        c.cnt = host[: T * G].reshape(T, G)           # my requests per (step, owner)
+        c.rc = host[T * G: 2 * T * G].reshape(G, T)   # requests to me per (requester, step)
+        c.nloc = host[2 * T * G:]
+        rows = torch.empty(int(c.rc.sum()), dtype=req.dtype, device=dev)
+        self._a2a(rows, req, c.rc.sum(1).tolist(), c.cnt.sum(0).tolist())
+        # received rows in per-step all_to_all order: step, then requester, then id
+        c.R = c.rc.sum(0)                                   # rows I serve per step
+        c.Rs = np.concatenate([[0], np.cumsum(c.R)])
+        pstart = np.cumsum(c.rc, 0) - c.rc                  # [G, T] requester offset inside a step
+        blk_start = (c.Rs[:-1][None, :] + pstart).reshape(-1)  # block (requester o, step t) -> position
+        blk_len = c.rc.reshape(-1)
+        src_pos = np.concatenate([[0], np.cumsum(blk_len)])[:-1]
+        k = torch.arange(rows.numel(), device=dev) - torch.as_tensor(np.repeat(src_pos, blk_len), device=dev)
+        q = torch.as_tensor(np.repeat(blk_start, blk_len), device=dev) + k
+        served = torch.empty_like(rows)
+        served[q] = rows
+        c.served = served                                   # owner-local rows, step-major
+        # owner reduction segments: per (step, row), positions in requester order
+        step_of = torch.as_tensor(np.repeat(np.arange(T), c.R), device=dev)
+        key = step_of * (self.Q.shape[0] + 1) + served
+        skey, spos = torch.sort(key, stable=True)
+        head = torch.ones_like(skey, dtype=torch.bool)
+        if skey.numel() > 1:
+            head[1:] = skey[1:] != skey[:-1]
+        starts = torch.nonzero(head).squeeze(1)
+        c.seg = torch.cat([starts, torch.tensor([skey.numel()], device=dev)]).to(torch.int32)
+        c.pos = (spos - torch.as_tensor(c.Rs[:-1], device=dev)[step_of[spos]]).to(torch.int32)
+        c.own_rows = served[spos[starts]].to(torch.int32)
+        nseg = torch.bincount(step_of[spos[starts]], minlength=T) if starts.numel() else torch.zeros(T)
+        c.Sa = np.concatenate([[0], np.cumsum(nseg.cpu().numpy())]).astype(np.int64)
+        c.lo = np.concatenate([[0], np.cumsum(c.nloc)])
+        c.nW = c.cnt.sum(1)
+        c.count = None
+        self._chunk_items = (i, j)
+        return c
+
+    def _counts(self, c: _Chunk, i, j):
+        """Occurrences of every owned row of each step in the GLOBAL batch (the
+        reg * mean(w^2) gradient counts them, APR.py:153-154)."""
+        G, B, T = self.G, self.B, c.T
+        items = torch.cat([i, j])
+        st = torch.cat([torch.arange(T * B, device=self.device) // B] * 2)
+        mine = items % G == self.rank
+        nrow = self.Q.shape[0] + 1
+        cnt = torch.bincount(st[mine] * nrow + items[mine] // G, minlength=T * nrow)
+        seg_step = torch.as_tensor(np.repeat(np.arange(T), np.diff(c.Sa)), device=self.device)
+        return cnt[seg_step * nrow + c.own_rows.long()].to(torch.int32)
+
+    # -- one step ------------------------------------------------------------------
+    def _step(self, c: _Chunk, t: int, hp):
+        d = self.d
+        cnt, rc = c.cnt[t].tolist(), c.rc[:, t].tolist()
+        b, nw, R = int(c.nloc[t]), int(c.nW[t]), int(c.R[t])
+        if self._recv.shape[0] < R:
+            self._recv = torch.empty(max(R, 2 * self._recv.shape[0]), d, dtype=torch.float32, device=self.device)
+        lo = int(c.lo[t])
+        served = c.served[c.Rs[t]: c.Rs[t] + R]
+        seg = c.seg[c.Sa[t]: c.Sa[t + 1] + 1]
+        own_rows = c.own_rows[c.Sa[t]: c.Sa[t + 1]]
+        count = None if c.count is None else c.count[c.Sa[t]: c.Sa[t + 1]]
+        nseg = seg.numel() - 1
+        recv, reply = self._recv[:R], self._recv_reply(R)
+        part = self._send[:nw]
+        # E1: current item rows of my working set from their owners
+        self._a2a(self.Qc[:nw], self.Q.index_select(0, served.long()), cnt, rc)
+        if b:
+            self.local.plan(c.u_rows[lo: lo + b], c.wi[lo: lo + b], c.wj[lo: lo + b])
+            self.local.clean(hp, part)
+        # E2: partial clean item sums -> owners
+        self._a2a(recv, part, rc, cnt)
+        G0 = self._g0(nseg)
+        if hp.adver:
+            self.local.reduce_delta(hp, recv, seg, c.pos, G0, reply)
+            # E3: deltas -> requesters
+            self._a2a(self._dlt[:nw], reply, cnt, rc)
+            if b:
+                self.local.set_item_delta(self._dlt[:nw])
+                self.local.adv(hp, part)
+            # E4: partial adversarial item sums -> owners, who apply Adagrad
+            self._a2a(recv, part, rc, cnt)
+            self.local.reduce_apply(hp, recv, seg, c.pos, G0, own_rows, count)
+        else:
+            self.local.reduce_apply(hp, recv, seg, c.pos, None, own_rows, count)
+        st = self.stats
+        st["steps"] += 1
+        st["items_requested"] += nw
+        st["rows_served"] += R
+        st["triplets"] += b
+
+    def _recv_reply(self, R):
+        buf = getattr(self, "_reply", None)
+        if buf is None or buf.shape[0] < R:
+            self._reply = buf = torch.empty(max(R, 1), self.d, dtype=torch.float32, device=self.device)
+        return buf[:R]
+
+    def _g0(self, n):
+        buf = getattr(self, "_g0buf", None)
+        if buf is None or buf.shape[0] < n:
+            self._g0buf = buf = torch.empty(max(n, 1), self.d, dtype=torch.float32, device=self.device)
+        return buf[:n]
+
+    # -- public --------------------------------------------------------------------
+    def train(self, u, i, j, hp, chunk: int = 64) -> int:
+        """Train consecutive global batches of the stream (u, i, j), identical on
+        every rank (length a multiple of the batch size).  Returns the batches run."""
+        n = len(u) // self.B
+        for c0 in range(0, n, chunk):
+            T = min(chunk, n - c0)
+            s = slice(c0 * self.B, (c0 + T) * self.B)
+            c = self._route(u[s], i[s], j[s], T)
+            if hp.reg:
+                c.count = self._counts(c, *self._chunk_items)
+            for t in range(T):
+                self._step(c, t, hp)
+        return n
+
+    def step_errors(self) -> int:
+        return self.local.step_errors() if hasattr(self.local, "step_errors") else 0
 
     def full_tables(self):
-        """Assemble the full tables on every rank (checkpoint / evaluation)."""
+        """The full tables on every rank (checkpoints, evaluation, tests)."""
         outs = []
         for tab, n in ((self.P, self.U1), (self.Q, self.I1), (self.accP, self.U1), (self.accQ, self.I1)):
-            cap = (n + self.world - 1) // self.world
-            buf = torch.zeros(cap, self.d, dtype=torch.float32, device=self.device)
+            cap = (n + self.G - 1) // self.G
+            cdev = torch.device("cpu") if self._stage else self.device
+            buf = torch.zeros(cap, self.d, dtype=torch.float32, device=cdev)
             buf[: tab.shape[0]] = tab
-            parts = [torch.empty_like(buf) for _ in range(self.world)]
+            parts = [torch.empty_like(buf) for _ in range(self.G)]
             dist.all_gather(parts, buf, group=self.group)
-            full = torch.empty(n, self.d, dtype=torch.float32, device=self.device)
-            for r in range(self.world):
-                cnt = len(range(r, n, self.world))
-                full[r::self.world] = parts[r][:cnt]
-            outs.append(full)
+            full = torch.empty(n, self.d, dtype=torch.float32, device=cdev)
+            for r in range(self.G):
+                full[r::self.G] = parts[r][: len(range(r, n, self.G))]
+            outs.append(full.to(self.device))
         return outs

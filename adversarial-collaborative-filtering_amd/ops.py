@@ -259,6 +259,33 @@ class APRContext:
         adversarial pass of batch t and the clean pass of batch t+1 in one launch."""
         call("acf_apr_set_step_overlap", self._ptr, int(bool(on)))
 
+    # -- shard mode (distributed.ShardedAPR; include/acf_apr.h "shard mode") --------
+    def set_shard_mode(self, on: bool, reg_batch: int = 0) -> None:
+        """Item rows are this rank's partial sums (one lane-group per slot, no
+        fusion, one-batch plans); reg_batch = the global batch of the reg mean."""
+        call("acf_apr_set_shard_mode", self._ptr, int(bool(on)), int(reg_batch))
+        self.batch_size = self.n_batches = 0
+
+    def shard_pass(self, tables, hp: StepHParams, pass_: int) -> None:
+        """pass 0: clean sums (users: delta; items: partial sums); pass 1 (APR):
+        adversarial sums, user Adagrad + write-back."""
+        tb, h = self._tables(*tables), hp.to_c()
+        with torch.cuda.device(self.device):
+            call("acf_apr_shard_pass", self._ptr, ctypes.byref(tb), ctypes.byref(h), int(pass_),
+                 _stream_ptr(self.device))
+
+    def shard_items_out(self, out: torch.Tensor) -> None:
+        """The item slots' partial sums (working-set order) -> out [n_items, d]."""
+        _require(out, "out", torch.float32, self.device, 2)
+        with torch.cuda.device(self.device):
+            call("acf_apr_shard_items", self._ptr, 0, out.data_ptr(), out.shape[0], _stream_ptr(self.device))
+
+    def shard_items_delta(self, delta: torch.Tensor) -> None:
+        """The owners' deltas [n_items, d] (working-set order) -> the item slots."""
+        _require(delta, "delta", torch.float32, self.device, 2)
+        with torch.cuda.device(self.device):
+            call("acf_apr_shard_items", self._ptr, 1, delta.data_ptr(), delta.shape[0], _stream_ptr(self.device))
+
     def step_errors(self) -> int:
         """Read and clear the step error word (bit 0: an overlapped step gave up
         waiting for a row)."""
@@ -527,3 +554,38 @@ def dns_select(P, Q, user, cand, dns: int):
         call("acf_dns_select", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
              u.data_ptr(), c.data_ptr(), u.numel(), int(dns), out.data_ptr(), _stream_ptr(dev))
     return out
+
+
+def shard_reduce_delta(recv, seg, pos, hp: StepHParams, G0, reply) -> None:
+    """Owner side of the APR delta (APR.py:183-191): per owned row s, the partial
+    clean sums recv[pos[seg[s]:seg[s+1]]] in order -> G0[s]; eps * l2_normalize
+    of it -> reply[pos[...]] (include/acf_apr.h acf_shard_reduce_delta)."""
+    n = seg.numel() - 1
+    if n <= 0:
+        return
+    dev = recv.device
+    for t, nm, dt in ((recv, "recv", torch.float32), (G0, "G0", torch.float32), (reply, "reply", torch.float32),
+                      (seg, "seg", torch.int32), (pos, "pos", torch.int32)):
+        _require(t, nm, dt, dev)
+    h = hp.to_c()
+    with torch.cuda.device(dev):
+        call("acf_shard_reduce_delta", recv.data_ptr(), seg.data_ptr(), pos.data_ptr(), n, recv.shape[1],
+             ctypes.byref(h), G0.data_ptr(), reply.data_ptr(), _stream_ptr(dev))
+
+
+def shard_reduce_apply(Q, accQ, recv, seg, pos, hp: StepHParams, G0, rows, count=None, reg_batch: int = 0) -> None:
+    """Owner side of the item Adagrad (APR.py:193-195): per owned row s,
+    G0[s] + reg_adv * sum of its partial adversarial rows (BPR: the sum of its
+    partial clean rows), then sparse Adagrad on Q[rows[s]], accQ[rows[s]]."""
+    n = seg.numel() - 1
+    if n <= 0:
+        return
+    dev = recv.device
+    for t, nm, dt in ((Q, "Q", torch.float32), (accQ, "accQ", torch.float32), (recv, "recv", torch.float32),
+                      (seg, "seg", torch.int32), (pos, "pos", torch.int32), (rows, "rows", torch.int32)):
+        _require(t, nm, dt, dev)
+    h = hp.to_c()
+    with torch.cuda.device(dev):
+        call("acf_shard_reduce_apply", Q.data_ptr(), accQ.data_ptr(), recv.data_ptr(), seg.data_ptr(),
+             pos.data_ptr(), n, Q.shape[1], ctypes.byref(h), 0 if G0 is None else G0.data_ptr(),
+             rows.data_ptr(), 0 if count is None else count.data_ptr(), int(reg_batch), _stream_ptr(dev))

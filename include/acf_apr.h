@@ -186,6 +186,45 @@ int acf_apr_set_step_overlap(acf_apr_ctx* ctx, int32_t on);
  * device cannot keep the launch resident).  Not part of the reference surface. */
 int acf_apr_set_stream(acf_apr_ctx* ctx, int32_t on);
 
+/* ---- shard mode: users and items row-sharded over the ranks of one node ----
+ * SURVEY §8(e) (no reference counterpart: the reference trains on one CPU
+ * process; this splits one training_batch, utils.py:113-119, across ranks so
+ * the result is the single-process one up to fp32 summation order).  Row r of
+ * P lives on rank r % G, row r of Q on rank r % G; each rank plans the
+ * triplets of ITS users for one global batch on (its user shard, the item rows
+ * it fetched, in working-set order), and the batch-global item sums of
+ * APR.py:183-195 are completed by the item owners between the passes. */
+
+/* Shard mode on/off for the context (forces one lane-group per slot, no triplet
+ * fusion; a one-batch plan per step).  reg_batch: the global batch size the
+ * reg * mean(w^2) terms divide by (0 = the planned batch size). */
+int acf_apr_set_shard_mode(acf_apr_ctx* ctx, int32_t on, int32_t reg_batch);
+
+/* pass 0: clean sums (users complete: delta; items: partial sums in the item
+ * slots' rows; BPR also updates the users); pass 1 (APR): adversarial sums
+ * (users: Adagrad + write-back to the user shard; items: partial sums).  The
+ * item rows of `tables` are the fetched working set (never written). */
+int acf_apr_shard_pass(acf_apr_ctx* ctx, const acf_apr_tables* tables, const acf_apr_hparams* hp,
+                       int32_t pass, void* stream);
+
+/* The item slots of the current one-batch plan, in working-set order:
+ * dir 0 copies their partial sums to buf [n_items, dim]; dir 1 copies buf into
+ * their delta rows (the owners' deltas, before pass 1). */
+int acf_apr_shard_items(acf_apr_ctx* ctx, int32_t dir, float* buf, int64_t n_items, void* stream);
+
+/* Owner side, per owned row s of the step: the partial rows recv[pos[p]] for p
+ * in [seg[s], seg[s+1]) (requester order) are summed in that order.
+ * reduce_delta (APR.py:183-191): G0[s] = the sum; reply[pos[p]] = eps *
+ * l2_normalize(sum) for every p of the row (hp->zero_delta: 0).
+ * reduce_apply (APR.py:193-195): G = G0[s] + reg_adv * sum (APR; BPR: the sum),
+ * then Adagrad on Q[rows[s]] / accQ[rows[s]]; count[s] = the row's occurrences
+ * in the global batch (needed only when hp->reg != 0, with reg_batch). */
+int acf_shard_reduce_delta(const float* recv, const int32_t* seg, const int32_t* pos, int32_t n_rows,
+                           int32_t dim, const acf_apr_hparams* hp, float* G0, float* reply, void* stream);
+int acf_shard_reduce_apply(float* Q, float* accQ, const float* recv, const int32_t* seg, const int32_t* pos,
+                           int32_t n_rows, int32_t dim, const acf_apr_hparams* hp, const float* G0,
+                           const int32_t* rows, const int32_t* count, int32_t reg_batch, void* stream);
+
 /* Reads into *out and clears the step error word: bit 0 = an overlapped step
  * gave up waiting for a row (results of that call are not trustworthy).
  * Synchronous on `stream`.  Not part of the reference surface. */

@@ -1,6 +1,11 @@
-"""Row-sharded multi-process training (distributed.ShardedTables) with the gloo
-backend on CPU, world size 2: bit-identical to one process training the full
-tables.  The step function is the CPU oracle here (the HIP step on GPUs)."""
+"""The split APR step (distributed.ShardedAPR) over gloo on CPU:
+users and items row-sharded over the ranks, triplets routed by user, the
+item sums completed by their owners through all_to_all exchanges.  The local
+passes are the oracle's restatement of the HIP shard passes
+(oracle/shard_oracle.py); the routing, exchange plans and collectives are the
+product code.  Result vs one process training the full tables (the C oracle)
+at the fp32 bar (tests/conftest.py fp32_parity): the item sums are added in a
+different order (per rank, then over ranks), nothing else differs."""
 import importlib
 import os
 import socket
@@ -8,51 +13,45 @@ import sys
 
 import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import PKG, REPO
 
-U1, I1, D, B, NB, CHUNK = 53, 41, 16, 32, 6, 3
+U1, I1, D, B, NB, CHUNK = 53, 41, 16, 32, 6, 4
 
 
-def _problem():
+def _problem(hot=False):
     rng = np.random.default_rng(12)
     P = (rng.standard_normal((U1, D)) * 0.2).astype(np.float32)
     Q = (rng.standard_normal((I1, D)) * 0.2).astype(np.float32)
     u = rng.integers(0, U1, NB * B).astype(np.int32)
     i = rng.integers(0, I1, NB * B).astype(np.int32)
     j = rng.integers(0, I1, NB * B).astype(np.int32)
-    j[::13] = i[::13]
+    j[::13] = i[::13]  # the trainList quirk allows i == j
+    if hot:
+        i[::3] = 7  # one item in a third of every batch, on every rank
     return P, Q, u, i, j
 
 
-def _oracle_step(P, Q, accP, accQ, u, i, j, batch_size, hp):
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    from apr_oracle import COracle
-    arrs = [x.numpy() for x in (P, Q, accP, accQ)]
-    COracle().apr_train(*arrs, u.numpy(), i.numpy(), j.numpy(), batch_size, hp)
-    for t, a in zip((P, Q, accP, accQ), arrs):
-        t.copy_(torch.from_numpy(a))
-
-
-def _worker(rank, world, port, out_dir, adver):
+def _worker(rank, world, port, out_dir, adver, reg, hot):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from apr_oracle import HParams
+    from shard_oracle import OracleShardLocal
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     D_ = importlib.import_module(PKG + ".distributed")
-    P, Q, u, i, j = _problem()
-    sh = D_.ShardedTables(U1, I1, D, init_P=P, init_Q=Q)
+    P, Q, u, i, j = _problem(hot)
+    sh = D_.ShardedAPR(U1, I1, D, B, init_P=P, init_Q=Q, local=OracleShardLocal)
     assert sh.P.shape[0] == len(range(rank, U1, world))  # only this rank's rows
-    for c in range(0, NB, CHUNK):
-        s = slice(c * B, (c + CHUNK) * B)
-        sh.train_chunk(u[s], i[s], j[s], B, HParams(adver=adver), step_fn=_oracle_step)
+    assert sh.Q.shape[0] == len(range(rank, I1, world))
+    sh.train(u, i, j, HParams(adver=adver, reg=reg), chunk=CHUNK)
     full = sh.full_tables()
+    stats = np.array([sh.stats["triplets"], sh.stats["steps"]])
     if rank == 0:
         np.savez(os.path.join(out_dir, "sharded.npz"), *[t.numpy() for t in full])
+    np.save(os.path.join(out_dir, f"stats{rank}.npy"), stats)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -65,14 +64,19 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("adver", [0, 1])
-def test_sharded_equals_single_process(tmp_path, oracle, adver):
+@pytest.mark.parametrize("world,adver,reg,hot", [(2, 1, 0.0, False), (2, 0, 0.0, False), (3, 1, 0.01, True),
+                                                 (2, 1, 0.0, True)])
+def test_split_step_equals_single_process(tmp_path, oracle, fp32_parity, world, adver, reg, hot):
     from apr_oracle import HParams
-    world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), adver), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), adver, reg, hot), nprocs=world, join=True)
     got = np.load(os.path.join(tmp_path, "sharded.npz"))
-    P, Q, u, i, j = _problem()
+    P, Q, u, i, j = _problem(hot)
     aP, aQ = np.full_like(P, 0.1), np.full_like(Q, 0.1)
-    oracle.apr_train(P, Q, aP, aQ, u, i, j, B, HParams(adver=adver))
-    for k, want in enumerate((P, Q, aP, aQ)):
-        np.testing.assert_array_equal(got[f"arr_{k}"], want)
+    oracle.apr_train(P, Q, aP, aQ, u, i, j, B, HParams(adver=adver, reg=reg))
+    for k, (want, n) in enumerate(zip((P, Q, aP, aQ), ("P", "Q", "accP", "accQ"))):
+        fp32_parity(got[f"arr_{k}"], want, n)
+    # every triplet ran exactly once, on its user's rank
+    per_rank = [np.load(os.path.join(tmp_path, f"stats{r}.npy")) for r in range(world)]
+    assert sum(int(s[0]) for s in per_rank) == NB * B
+    for r, s in enumerate(per_rank):
+        assert int(s[0]) == int(np.sum(u % world == r)) and int(s[1]) == NB

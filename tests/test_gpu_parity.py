@@ -699,7 +699,7 @@ def test_step_overlap_kernel_timing_kinds(ops, dev):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ta, tb = _gpu_tables(P, Q, dev), _gpu_tables(P, Q, dev)
     t = ctx.time_kernels(ta, hp)
-    assert {k: v[1] for k, v in t.items()} == {"clean": 1, "ovl": nb - 1, "adv": 1, "flush": 1, "stream": 0}
+    assert {k: v[1] for k, v in t.items()} == {"clean": 1, "ovl": nb - 1, "adv": 1, "flush": 1, "stream": 0, "hot": 0}
     ctx.train_planned(tb, hp)
     for x, y in zip(ta, tb):
         assert torch.equal(x, y)
@@ -721,7 +721,7 @@ def test_stream_kernel_timing_kinds(ops, dev, d):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ta, tb = _gpu_tables(P, Q, dev), _gpu_tables(P, Q, dev)
     t = ctx.time_kernels(ta, hp)
-    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "ovl": 0, "adv": 0, "flush": 1, "stream": 1}
+    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "ovl": 0, "adv": 0, "flush": 1, "stream": 1, "hot": 0}
     ctx.train_planned(tb, hp)
     for x, y in zip(ta, tb):
         assert torch.equal(x, y)
