@@ -39,6 +39,8 @@ exchanges over gloo.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -51,7 +53,7 @@ class HipLocal:
         from . import ops
         self.ops = ops
         self.sh = sh
-        self.ctx = ops.APRContext(sh.P.shape[0], sh.max_items, sh.d, sh.B, 1, sh.device)
+        self.ctx = ops.APRContext(sh.P.shape[0], sh.max_items, sh.d, sh.b_max, 1, sh.device)
         self.ctx.set_shard_mode(True, reg_batch=sh.B)
         # the fetched item rows are never updated locally; their Adagrad slots are unused
         self.accQc = torch.full((sh.max_items, sh.d), 0.1, device=sh.device)
@@ -93,10 +95,13 @@ class _Chunk:
 class ShardedAPR:
     """This rank's shard of embedding_P / embedding_Q (+ Adagrad slots) and the
     split APR step.  ``batch_size`` is the GLOBAL batch (the reference's
-    ``--batch_size``); each rank processes the triplets of its users."""
+    ``--batch_size``); each rank processes the triplets of its users.
+    ``local_batch``: triplets are routed at sampling time (train_routed), each
+    rank holding exactly this many of every global batch (= G x local_batch)."""
 
     def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, batch_size: int, device=None,
-                 group=None, init_P=None, init_Q=None, acc0: float = 0.1, local=None):
+                 group=None, init_P=None, init_Q=None, acc0: float = 0.1, local=None,
+                 local_batch: int | None = None):
         self.group = group
         self.G = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -115,13 +120,17 @@ class ShardedAPR:
             self.Q.copy_(torch.as_tensor(np.asarray(init_Q, np.float32)[r::G]))
         self.accP = torch.full((nu, dim), acc0, **f)
         self.accQ = torch.full((ni, dim), acc0, **f)
-        self.max_items = 2 * self.B  # a rank's working set of one batch: <= 2 x its triplets
+        if local_batch is not None and local_batch * self.G != self.B:
+            raise ValueError(f"local_batch {local_batch} x {self.G} ranks != batch_size {self.B}")
+        self.b_max = int(local_batch) if local_batch is not None else self.B  # triplets of a rank per batch
+        self.routed = local_batch is not None
+        self.max_items = 2 * self.b_max  # a rank's working set of one batch: <= 2 x its triplets
         self.Qc = torch.zeros(self.max_items, dim, **f)
         self._send = torch.empty(self.max_items, dim, **f)
         self._dlt = torch.empty(self.max_items, dim, **f)
         self._recv = torch.empty(0, dim, **f)
         self.local = local(self) if local is not None else HipLocal(self)
-        self.stats = {"steps": 0, "items_requested": 0, "rows_served": 0, "triplets": 0}
+        self.stats = {"steps": 0, "items_requested": 0, "rows_served": 0, "triplets": 0, "route_s": 0.0}
 
     # -- collectives ---------------------------------------------------------------
     def _a2a(self, out, inp, out_splits, in_splits):
@@ -134,17 +143,21 @@ class ShardedAPR:
 
     # -- routing (one chunk of T global batches) -----------------------------------
     def _route(self, u, i, j, T: int) -> _Chunk:
-        G, r, B, I1 = self.G, self.rank, self.B, self.I1
+        G, r, I1 = self.G, self.rank, self.I1
+        B = self.b_max if self.routed else self.B  # triplets per batch in the stream given
         dev = self.device
         u, i, j = (torch.as_tensor(x, device=dev).reshape(-1)[: T * B].long() for x in (u, i, j))
         if u.numel() != T * B:
             raise ValueError(f"{u.numel()} triplets for {T} batches of {B}")
-        if u.numel() and (int(torch.minimum(u.min(), torch.minimum(i.min(), j.min()))) < 0
-                          or int(u.max()) >= self.U1 or int(torch.maximum(i.max(), j.max())) >= I1):
-            raise IndexError("triplet index outside the sharded tables")
+        # index checks, read with the chunk's host copy below (no extra sync):
+        # bit 0 out of range (TF Gather's InvalidArgument), bit 1 another rank's user (routed)
+        bad = ((u < 0) | (u >= self.U1) | (i < 0) | (i >= I1) | (j < 0) | (j >= I1)).any().long()
+        if self.routed:
+            bad = bad + 2 * (u % G != r).any().long()
         c = _Chunk()
         c.T = T
-        sel = torch.nonzero(u % G == r).squeeze(1)  # this rank's triplets, stream order
+        # this rank's triplets, stream order
+        sel = torch.arange(u.numel(), device=dev) if self.routed else torch.nonzero(u % G == r).squeeze(1)
         st = sel // B
         n = sel.numel()
         c.u_rows = (u[sel] // G).to(torch.int32)
@@ -165,10 +178,14 @@ class ShardedAPR:
         req = (wid // G)[order]
         rc = torch.empty_like(cnt.t().contiguous())
         self._a2a(rc.view(-1), cnt.t().contiguous().view(-1), [T] * G, [T] * G)
-        host = torch.cat([cnt.reshape(-1), rc.reshape(-1), nloc]).cpu().numpy()  # the chunk's one sync
+        host = torch.cat([cnt.reshape(-1), rc.reshape(-1), nloc, bad.reshape(1)]).cpu().numpy()  # one sync
+        if host[-1] & 1:
+            raise IndexError("triplet index outside the sharded tables")
+        if host[-1] & 2:
+            raise ValueError("train_routed: a triplet of another rank's user")
         c.cnt = host[: T * G].reshape(T, G)           # my requests per (step, owner)
         c.rc = host[T * G: 2 * T * G].reshape(G, T)   # requests to me per (requester, step)
-        c.nloc = host[2 * T * G:]
+        c.nloc = host[2 * T * G: -1]
         rows = torch.empty(int(c.rc.sum()), dtype=req.dtype, device=dev)
         self._a2a(rows, req, c.rc.sum(1).tolist(), c.cnt.sum(0).tolist())
         # received rows in per-step all_to_all order: step, then requester, then id
@@ -270,17 +287,30 @@ class ShardedAPR:
     # -- public --------------------------------------------------------------------
     def train(self, u, i, j, hp, chunk: int = 64) -> int:
         """Train consecutive global batches of the stream (u, i, j), identical on
-        every rank (length a multiple of the batch size).  Returns the batches run."""
-        n = len(u) // self.B
+        every rank (length a multiple of the batch size; train_routed: this rank's
+        triplets only, local_batch per batch).  Returns the batches run."""
+        bs = self.b_max if self.routed else self.B
+        n = len(u) // bs
         for c0 in range(0, n, chunk):
             T = min(chunk, n - c0)
-            s = slice(c0 * self.B, (c0 + T) * self.B)
+            s = slice(c0 * bs, (c0 + T) * bs)
+            t0 = time.perf_counter()
             c = self._route(u[s], i[s], j[s], T)
-            if hp.reg:
+            self.stats["route_s"] += time.perf_counter() - t0
+            if hp.reg:  # the owners count their rows in the GLOBAL batch
+                if self.routed:
+                    raise ValueError("reg != 0 needs the global stream on every rank (train, not train_routed)")
                 c.count = self._counts(c, *self._chunk_items)
             for t in range(T):
                 self._step(c, t, hp)
         return n
+
+    def train_routed(self, u, i, j, hp, chunk: int = 64) -> int:
+        """As train, for triplets routed at sampling time: this rank's users only,
+        local_batch of them per global batch (the sampler runs per rank)."""
+        if not self.routed:
+            raise ValueError("train_routed needs ShardedAPR(local_batch=...)")
+        return self.train(u, i, j, hp, chunk)
 
     def step_errors(self) -> int:
         return self.local.step_errors() if hasattr(self.local, "step_errors") else 0

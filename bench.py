@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--no-large", action="store_true",
                    help="skip the synthetic-large lines (batch 65,536 on 10M x 5M, d = 128 and 64)")
     p.add_argument("--no-neumf", action="store_true", help="skip the adversarial-NeuMF line (configs[3])")
+    p.add_argument("--no-sharded", action="store_true",
+                   help="skip the split-step lines (SURVEY 8(e): users/items sharded over the ranks)")
+    p.add_argument("--sharded-steps", type=int, default=24, help="timed steps of the config-5 split-step line")
     p.add_argument("--no-step-overlap", action="store_true",
                    help="two kernels per APR step instead of the overlapped k_ovl (A/B)")
     p.add_argument("--no-stream", action="store_true",
@@ -291,6 +294,107 @@ def large_batch_roofline(acf, ops, dev, ds, d=128, nb=64, chunk=32):
     return rl
 
 
+def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
+    """one APR step split over the ranks (distributed.ShardedAPR):
+    users and items row-sharded (row r on rank r % N), each triplet on its
+    user's rank, the batch-global item sums completed by the item owners over
+    four all_to_alls per step (RCCL over xGMI).  Two lines:
+      large: BASELINE configs[4] (10M x 5M, d = 128, Zipf items, alias-table
+             negatives), 65,536 triplets per GPU per step (weak scaling), routed at
+             sampling time (each rank samples its own users);
+      pinterest: BASELINE configs[2] (pinterest-20-shaped, d = 64), the
+             reference's global batch of 512 split over the ranks (strong scaling).
+    value = triplets of all ranks / max-over-ranks time of the timed steps."""
+    import torch.distributed as tdist
+    D_ = importlib.import_module(PKG + ".distributed")
+    own_group = False
+    if dist is None:  # one process: a world-1 group over RCCL for the collectives
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29000 + os.getpid() % 1000))
+        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        own_group = True
+    out = {}
+    try:
+        def timed(sh, run, n_trip):
+            torch.cuda.synchronize(dev)
+            tdist.barrier()
+            t0 = time.perf_counter()
+            run()
+            torch.cuda.synchronize(dev)
+            tdist.barrier()
+            el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+            tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+            tot = torch.tensor([float(n_trip)], device=dev, dtype=torch.float64)
+            tdist.all_reduce(tot)
+            return float(el.item()), float(tot.item())
+
+        # configs[4], weak scaling, routed at sampling time
+        b, d = 65536, 128
+        sel = big.pos_user % world == rank
+        sub = type(big)(big.num_users, big.num_items, big.pos_user[sel].contiguous(), big.pos_item[sel].contiguous(),
+                        big.list_off, big.list_items, name="synthetic-large-rank")
+        sampler = acf.DeviceSampler(sub, b, dev, seed=11 + rank, weights=np.ones(big.num_items, np.float32))
+        ep = sampler.epoch(0)
+        warm = 4
+        n = (warm + steps) * b
+        u, i, j = (x[:n].contiguous() for x in (ep.user, ep.item_pos, ep.item_neg))
+        del ep, sampler, sub
+        g = torch.Generator(device=dev).manual_seed(5)
+        sh = D_.ShardedAPR(big.num_users + 1, big.num_items + 1, d, b * world, device=dev, local_batch=b)
+        sh.P.normal_(0, 0.01, generator=g)
+        sh.Q.normal_(0, 0.01, generator=g)
+        hp = ops.StepHParams(adver=1)
+        sh.train_routed(u[: warm * b], i[: warm * b], j[: warm * b], hp, chunk=warm)
+        s = slice(warm * b, n)
+        st0 = dict(sh.stats)
+        el, tot = timed(sh, lambda: sh.train_routed(u[s], i[s], j[s], hp, chunk=steps), steps * b)
+        req = (sh.stats["items_requested"] - st0["items_requested"]) / steps
+        out["large"] = {
+            "metric": "APR triplets/sec, split step (users/items sharded over the ranks)",
+            "value": round(tot / el, 1), "unit": "triplets/s", "n_gpus": world, "steps": steps,
+            "ms_per_step": round(1e3 * el / steps, 4), "scaling": "weak", "dtype": "f32",
+            "data": "synthetic 10M x 5M, 200M Zipf interactions, alias-table negatives (device sampler per rank)",
+            "config": {"workload": "APR, BASELINE configs[4] split over the ranks", "users": big.num_users,
+                       "items": big.num_items, "dim": d, "per_gpu_batch": b, "global_batch": b * world,
+                       "parallelism": f"user/item row shards x{world}, all_to_all x4 per step"},
+            "exchange_bytes_per_step_rank0": int(4 * req * d * 4),
+            "items_per_rank_step": round(req, 1),
+            "route_ms_rank0": round(1e3 * (sh.stats["route_s"] - st0["route_s"]), 3),
+            "step_errors": sh.step_errors()}
+        del sh, u, i, j
+        torch.cuda.empty_cache()
+
+        # configs[2], strong scaling: the reference's global batch of 512
+        B, d = 512, 64
+        ds = acf.pinterest_like(seed=2019)
+        psamp = acf.DeviceSampler(ds, B, dev, seed=3)
+        ep = psamp.epoch(0)
+        warm, steps_p = 20, 200
+        n = (warm + steps_p) * B
+        u, i, j = (x[:n].contiguous() for x in (ep.user, ep.item_pos, ep.item_neg))
+        sh = D_.ShardedAPR(ds.num_users + 1, ds.num_items + 1, d, B, device=dev)
+        sh.P.normal_(0, 0.01, generator=g)
+        sh.Q.normal_(0, 0.01, generator=g)
+        sh.train(u[: warm * B], i[: warm * B], j[: warm * B], hp, chunk=warm)
+        s = slice(warm * B, n)
+        el, tot = timed(sh, lambda: sh.train(u[s], i[s], j[s], hp, chunk=steps_p), steps_p * B / world)
+        out["pinterest"] = {
+            "metric": "APR triplets/sec, split step (users/items sharded over the ranks)",
+            "value": round(steps_p * B / el, 1), "unit": "triplets/s", "n_gpus": world, "steps": steps_p,
+            "ms_per_step": round(1e3 * el / steps_p, 4), "scaling": "strong", "dtype": "f32",
+            "data": "synthetic pinterest-20-shaped (55,187 x 9,916), device sampler",
+            "config": {"workload": "APR, BASELINE configs[2] split over the ranks", "users": ds.num_users,
+                       "items": ds.num_items, "dim": d, "global_batch": B,
+                       "parallelism": f"user/item row shards x{world}, all_to_all x4 per step"},
+            "step_errors": sh.step_errors()}
+        del sh
+        torch.cuda.empty_cache()
+    finally:
+        if own_group:
+            tdist.destroy_process_group()
+    return out
+
+
 def neumf_bench(acf, dev):
     """BASELINE configs[3]: adversarial NeuMF (GMF + MLP towers perturbed) on
     yelp-sort-shaped synthetic data, d = 64, batch 512 (run.py --bs default), one
@@ -346,6 +450,9 @@ def neumf_bench(acf, dev):
 
 def main():
     a = parse()
+    # RCCL prints its version banner on stdout at init: keep fd 1 for the one JSON line
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -431,18 +538,22 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(u, i, j, P0, Q0, B, a.cpu_batches)
-    if rank == 0 and not a.no_neumf:
-        out["neumf"] = neumf_bench(acf, dev)
-    if rank == 0 and not a.no_large:
+    big = None
+    if not a.no_sharded or (rank == 0 and not a.no_large):
         del pipe, tctx
         torch.cuda.empty_cache()
         big = acf.synthetic_large(device=dev)
+    if not a.no_sharded:  # every rank takes part
+        out["sharded"] = sharded_lines(acf, ops, dev, dist, world, rank, big, a.sharded_steps)
+    if rank == 0 and not a.no_neumf:
+        out["neumf"] = neumf_bench(acf, dev)
+    if rank == 0 and not a.no_large:
         out["roofline_large_batch"] = large_batch_roofline(acf, ops, dev, big, 128)
         out["roofline_large_batch_d64"] = large_batch_roofline(acf, ops, dev, big, 64)
         del big
         torch.cuda.empty_cache()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
 

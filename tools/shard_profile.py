@@ -1,0 +1,20 @@
+"""The split-step bench lines alone (world 1), for rocprofv3 --kernel-trace --stats:
+   rocprofv3 --kernel-trace --stats -d gpurun_out/prof_shard -- python3 tools/shard_profile.py"""
+import importlib
+import json
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+acf = importlib.import_module(bench.PKG)
+ops = importlib.import_module(bench.PKG + ".ops")
+big = acf.synthetic_large(device=dev)
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+print(json.dumps(bench.sharded_lines(acf, ops, dev, None, 1, 0, big, steps)))
