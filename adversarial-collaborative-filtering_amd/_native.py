@@ -162,6 +162,11 @@ NEUMF_SIGNATURES = {
     "acf_neumf_predict": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P]),
     "acf_neumf_train": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I64,
                                        ctypes.POINTER(NeuMFHParams), _P, _P]),
+    "acf_kbpr_create": (ctypes.c_int, [ctypes.POINTER(_P), _I64, _I64, _I32, _I32]),
+    "acf_kbpr_destroy": (ctypes.c_int, [_P]),
+    "acf_kbpr_train": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I64,
+                                      ctypes.POINTER(NeuMFHParams), _P, _P]),
+    "acf_kbpr_predict": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P]),
 }
 
 _neumf = None

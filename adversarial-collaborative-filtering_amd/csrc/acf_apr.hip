@@ -3315,25 +3315,45 @@ static bool use_overlap(const acf_apr_ctx* c, const Kernels& K, const acf_apr_hp
 
 // Streamed step: version buffers (allocated at first use: 3 x maxNB x S x d
 // granules) and the resident-wave budget of k_stream.
+static int stream_positions(const acf_apr_ctx* c, const Kernels& K, int fuse);
+
+static void free_alloc(acf_apr_ctx* c, void* p) {
+  auto it = std::find(c->allocs.begin(), c->allocs.end(), p);
+  if (it != c->allocs.end()) {
+    (void)hipFree(p);
+    c->allocs.erase(it);
+  }
+}
+
 static int stream_ready(acf_apr_ctx* c, const Kernels& K) {
   if (c->stream_ok >= 0) return c->stream_ok;
-  c->stream_ok = 0;
   if (!K.stream) return 0;
-  int dev = 0, cus = 0, blocks = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(K.stream), 256, 0) !=
-          hipSuccess) {
-    (void)hipGetLastError();
-    return 0;
+  if (c->stream_max_waves == 0) {
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(K.stream), 256, 0) !=
+            hipSuccess) {
+      (void)hipGetLastError();
+      c->stream_ok = 0;
+      return 0;
+    }
+    // MI355X guide (residency): 256-thread blocks admitted per CU = min(API, 8,
+    // 800 / (ceil(sgpr/16)*16 + 16)); k_stream's SGPR count (< 144) caps it at 5
+    c->stream_max_waves = (int64_t)std::max(0, std::min(blocks, 5)) * cus * 4;
   }
-  // MI355X guide (residency): 256-thread blocks admitted per CU = min(API, 8,
-  // 800 / (ceil(sgpr/16)*16 + 16)); k_stream's SGPR count (< 144) caps it at 5
-  c->stream_max_waves = (int64_t)std::max(0, std::min(blocks, 5)) * cus * 4;
+  // the version buffers only for a plan the launch can keep resident (otherwise
+  // not now: a later plan with a smaller batch may fit)
+  if (stream_positions(c, K, c->fusion) > c->stream_max_waves) return 0;
+  c->stream_ok = 0;
   const size_t n = (size_t)c->maxNB * 3 * c->maxB * c->d;
   if (dalloc(c, &c->ver_w, n) != ACF_OK || dalloc(c, &c->ver_a, n) != ACF_OK ||
-      dalloc(c, &c->ver_d, n) != ACF_OK)
+      dalloc(c, &c->ver_d, n) != ACF_OK) {
+    for (void* p : {(void*)c->ver_w, (void*)c->ver_a, (void*)c->ver_d})
+      if (p) free_alloc(c, p);
+    c->ver_w = c->ver_a = c->ver_d = nullptr;
     return 0;
+  }
   // tag 0 never matches: the epoch starts at 1 (acf_apr_create)
   if (hipMemset(c->ver_w, 0, n * 8) != hipSuccess || hipMemset(c->ver_a, 0, n * 8) != hipSuccess ||
       hipMemset(c->ver_d, 0, n * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {

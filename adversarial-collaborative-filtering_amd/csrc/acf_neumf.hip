@@ -841,3 +841,248 @@ extern "C" int acf_neumf_predict(acf_neumf_ctx* c, const float* P, const int32_t
   }
   return read_err(c, s);
 }
+
+// ---------------------------------------------------------------------------
+// Keras BPR (BPR.py:23-99; run.py --model bpr, BASELINE configs[0]).
+// params = [uEmb (U1 x d) | iEmb (I1 x d)] (BPR.py:35-36), gradient and Adam
+// moments in the same layout.  Per batch of B triplets:
+//   x = u.p - u.n (Dot layers, BPR.py:42-43); loss = 1 - log(sigmoid(x))
+//   (bpr_triplet_loss, BPR.py:11-16); Keras loss = mean over the batch
+//   (identity_loss, BPR.py:19-20), so d loss / d x = SigmoidGrad(LogGrad(-1/B)).
+//   The gathered rows' gradients are summed per table row in occurrence order
+//   (users: batch order; items: the positive gathers, then the negative ones:
+//   TF's IndexedSlices densified), then Keras 2.2 Adam over the whole buffer.
+// ---------------------------------------------------------------------------
+template <int LPR>
+__device__ __forceinline__ float kb_sum(float s) {
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) s += __shfl_xor(s, m, 64);
+  return s;
+}
+
+// one lane-group of LPR lanes (one float4 each, d <= 4 LPR) per triplet
+template <int LPR>
+__global__ void __launch_bounds__(256) k_kbpr_inst(const float* __restrict__ P, const int32_t* __restrict__ u,
+                                                   const int32_t* __restrict__ ip, const int32_t* __restrict__ in,
+                                                   int32_t B, int32_t d, int64_t U1, int64_t I1,
+                                                   float* __restrict__ contrib, float* __restrict__ loss,
+                                                   int32_t* __restrict__ err) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = (int)(gid / LPR), l = (int)(threadIdx.x & (LPR - 1));
+  if (b >= B) return;
+  int32_t ru = u[b], rp = ip[b], rn = in[b];
+  if (l == 0 && (ru < 0 || ru >= U1)) atomicOr(err, 1);
+  if (l == 0 && (rp < 0 || rp >= I1 || rn < 0 || rn >= I1)) atomicOr(err, 2);
+  ru = (ru < 0 || ru >= U1) ? 0 : ru;
+  rp = (rp < 0 || rp >= I1) ? 0 : rp;
+  rn = (rn < 0 || rn >= I1) ? 0 : rn;
+  const float* Q = P + U1 * (int64_t)d;
+  const bool on = l * 4 < d;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 pu = on ? *reinterpret_cast<const float4*>(P + (int64_t)ru * d + 4 * l) : z;
+  const float4 pp = on ? *reinterpret_cast<const float4*>(Q + (int64_t)rp * d + 4 * l) : z;
+  const float4 pn = on ? *reinterpret_cast<const float4*>(Q + (int64_t)rn * d + 4 * l) : z;
+  const float dp = kb_sum<LPR>(pu.x * pp.x + pu.y * pp.y + pu.z * pp.z + pu.w * pp.w);
+  const float dn = kb_sum<LPR>(pu.x * pn.x + pu.y * pn.y + pu.z * pn.z + pu.w * pn.w);
+  const float x = dp - dn;
+  const float sg = 1.0f / (1.0f + expf(-x));           // K.sigmoid
+  if (l == 0) loss[b] = 1.0f - logf(sg);               // 1 - K.log(.)
+  const float up = -1.0f / (float)B;                   // d mean / d loss_b, through "1 - ."
+  const float g = (up * (1.0f / sg)) * sg * (1.0f - sg);  // LogGrad, then SigmoidGrad
+  if (!on) return;
+  float4 gu, gp, gn;
+  gu.x = g * pp.x + (-g) * pn.x; gu.y = g * pp.y + (-g) * pn.y;
+  gu.z = g * pp.z + (-g) * pn.z; gu.w = g * pp.w + (-g) * pn.w;
+  gp = make_float4(g * pu.x, g * pu.y, g * pu.z, g * pu.w);
+  gn = make_float4(-g * pu.x, -g * pu.y, -g * pu.z, -g * pu.w);
+  float* c = contrib + (int64_t)b * 3 * d + 4 * l;
+  *reinterpret_cast<float4*>(c) = gu;
+  *reinterpret_cast<float4*>(c + d) = gp;
+  *reinterpret_cast<float4*>(c + 2 * d) = gn;
+}
+
+// one wave per gathered row occurrence: occurrence o < B is user b = o, o >= B
+// is item slot o - B of [positives | negatives].  The first occurrence of a
+// table row owns it and adds every occurrence's contribution in order.
+__global__ void __launch_bounds__(256) k_kbpr_rows(const int32_t* __restrict__ u, const int32_t* __restrict__ ip,
+                                                   const int32_t* __restrict__ in, int32_t B, int32_t d,
+                                                   int64_t U1, int64_t I1, const float* __restrict__ contrib,
+                                                   float* __restrict__ G) {
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= 3 * (int64_t)B) return;
+  const int o = (int)wave;
+  const bool item = o >= B;
+  const int n = item ? 2 * B : B;  // occurrences of this table
+  auto row_of = [&](int k) -> int32_t {  // table row of occurrence k of this table
+    int32_t r = item ? (k < B ? ip[k] : in[k - B]) : u[k];
+    const int64_t rows = item ? I1 : U1;
+    return (r < 0 || r >= rows) ? 0 : r;
+  };
+  auto contrib_of = [&](int k) -> const float* {  // its gradient row
+    return item ? contrib + ((int64_t)(k < B ? k : k - B) * 3 + (k < B ? 1 : 2)) * d
+                : contrib + (int64_t)k * 3 * d;
+  };
+  const int me = item ? o - B : o;
+  const int32_t r = row_of(me);
+  for (int base = 0; base < me; base += 64) {  // an earlier occurrence owns the row
+    const int k = base + lane;
+    if (__any(k < me && row_of(k) == r)) return;
+  }
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};  // d <= 256: lane holds elements lane + 64 q
+  for (int base = me; base < n; base += 64) {
+    const int k = base + lane;
+    uint64_t mask = __ballot(k < n && row_of(k) == r);
+    while (mask) {
+      const int kk = base + __ffsll((unsigned long long)mask) - 1;
+      mask &= mask - 1;
+      const float* c = contrib_of(kk);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (lane + 64 * q < d) acc[q] = acc[q] + c[lane + 64 * q];
+    }
+  }
+  float* g = G + (item ? U1 * (int64_t)d : 0) + (int64_t)r * d;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (lane + 64 * q < d) g[lane + 64 * q] = g[lane + 64 * q] + acc[q];
+}
+
+struct acf_kbpr_ctx {
+  int64_t U1 = 0, I1 = 0;
+  int32_t d = 0, maxB = 0;
+  float* contrib = nullptr;
+  int32_t* err = nullptr;
+  std::vector<void*> allocs;
+};
+
+extern "C" int acf_kbpr_destroy(acf_kbpr_ctx* c) {
+  if (!c) return ACF_OK;
+  for (void* p : c->allocs) (void)hipFree(p);
+  delete c;
+  return ACF_OK;
+}
+
+extern "C" int acf_kbpr_create(acf_kbpr_ctx** out, int64_t U1, int64_t I1, int32_t d, int32_t maxB) {
+  ACF_CHECK(out != nullptr, ACF_E_INVALID, "out is NULL");
+  *out = nullptr;
+  ACF_CHECK(U1 > 0 && I1 > 0 && U1 < (1ll << 31) && I1 < (1ll << 31), ACF_E_INVALID, "bad table rows");
+  ACF_CHECK(d >= 4 && d <= 256 && d % 4 == 0, ACF_E_INVALID, "dim must be a multiple of 4 in [4, 256], got %d", d);
+  ACF_CHECK(maxB > 0 && maxB <= (1 << 24), ACF_E_INVALID, "max_batch must be in (0, 2^24], got %d", maxB);
+  acf_kbpr_ctx* c = new acf_kbpr_ctx();
+  c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB;
+  for (auto pr : {std::make_pair((void**)&c->contrib, (size_t)maxB * 3 * d * 4),
+                  std::make_pair((void**)&c->err, (size_t)16)}) {
+    if (hipMalloc(pr.first, pr.second) != hipSuccess) {
+      (void)hipGetLastError();
+      acf_kbpr_destroy(c);
+      return set_error(ACF_E_NOMEM, "hipMalloc of %zu bytes failed", pr.second);
+    }
+    c->allocs.push_back(*pr.first);
+  }
+  if (hipMemset(c->err, 0, 16) != hipSuccess) {
+    acf_kbpr_destroy(c);
+    return set_error(ACF_E_HIP, "hipMemset failed");
+  }
+  *out = c;
+  return ACF_OK;
+}
+
+template <int LPR>
+static void launch_kbpr_inst(const acf_kbpr_ctx* c, const float* P, const int32_t* u, const int32_t* ip,
+                             const int32_t* in, int32_t B, float* loss, hipStream_t s) {
+  k_kbpr_inst<LPR><<<(unsigned)(((int64_t)B * LPR + 255) / 256), 256, 0, s>>>(P, u, ip, in, B, c->d, c->U1,
+                                                                              c->I1, c->contrib, loss, c->err);
+}
+
+extern "C" int acf_kbpr_train(acf_kbpr_ctx* c, float* P, float* G, float* m, float* v, const int32_t* u,
+                              const int32_t* ip, const int32_t* in, int64_t n, int32_t batch, int64_t t_first,
+                              const acf_neumf_hparams* hp, float* losses, void* stream_) {
+  ACF_CHECK(c && P && G && m && v && u && ip && in && hp && losses, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(batch > 0 && batch <= c->maxB, ACF_E_INVALID, "batch %d outside (0, %d]", batch, c->maxB);
+  ACF_CHECK(n >= 0 && t_first >= 1, ACF_E_INVALID, "bad triplet count or Adam iteration");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  const int64_t total = (c->U1 + c->I1) * (int64_t)c->d;
+  const int64_t n4 = total / 4;
+  const unsigned ga = (unsigned)std::min<int64_t>((n4 + 255) / 256, 256 * 32);
+  int lpr = 1;
+  while (lpr * 4 < c->d) lpr <<= 1;
+  int64_t k = 0;
+  for (int64_t o = 0; o < n; o += batch, ++k) {
+    const int32_t B = (int32_t)std::min<int64_t>(batch, n - o);
+    switch (lpr) {
+      case 1: launch_kbpr_inst<1>(c, P, u + o, ip + o, in + o, B, losses + o, s); break;
+      case 2: launch_kbpr_inst<2>(c, P, u + o, ip + o, in + o, B, losses + o, s); break;
+      case 4: launch_kbpr_inst<4>(c, P, u + o, ip + o, in + o, B, losses + o, s); break;
+      case 8: launch_kbpr_inst<8>(c, P, u + o, ip + o, in + o, B, losses + o, s); break;
+      case 16: launch_kbpr_inst<16>(c, P, u + o, ip + o, in + o, B, losses + o, s); break;
+      case 32: launch_kbpr_inst<32>(c, P, u + o, ip + o, in + o, B, losses + o, s); break;
+      default: launch_kbpr_inst<64>(c, P, u + o, ip + o, in + o, B, losses + o, s); break;
+    }
+    k_kbpr_rows<<<(unsigned)((3 * (int64_t)B * 64 + 255) / 256), 256, 0, s>>>(u + o, ip + o, in + o, B, c->d,
+                                                                             c->U1, c->I1, c->contrib, G);
+    const float tt = (float)(t_first + k);
+    const float lr_t = hp->lr * (sqrtf(1.0f - powf(hp->beta2, tt)) / (1.0f - powf(hp->beta1, tt)));
+    k_nmf_adam<<<ga, 256, 0, s>>>(reinterpret_cast<float4*>(P), reinterpret_cast<float4*>(G),
+                                  reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v), n4, hp->beta1,
+                                  hp->beta2, lr_t, hp->adam_eps);
+    HIP_TRY(hipGetLastError());
+  }
+  int32_t herr = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ACF_CHECK(herr == 0, ACF_E_RANGE, "index out of range (%s%s)", (herr & 1) ? "user >= num_user_rows " : "",
+            (herr & 2) ? "item >= num_item_rows" : "");
+  return ACF_OK;
+}
+
+// predictor = Model([user, item], pDot) (BPR.py:57): u . i per pair
+template <int LPR>
+__global__ void __launch_bounds__(256) k_kbpr_predict(const float* __restrict__ P, const int32_t* __restrict__ u,
+                                                      const int32_t* __restrict__ it, int64_t n, int32_t d,
+                                                      int64_t U1, int64_t I1, float* __restrict__ out,
+                                                      int32_t* __restrict__ err) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t b = gid / LPR;
+  const int l = (int)(threadIdx.x & (LPR - 1));
+  if (b >= n) return;
+  int32_t ru = u[b], ri = it[b];
+  if (l == 0 && (ru < 0 || ru >= U1 || ri < 0 || ri >= I1)) atomicOr(err, (ru < 0 || ru >= U1) ? 1 : 2);
+  ru = (ru < 0 || ru >= U1) ? 0 : ru;
+  ri = (ri < 0 || ri >= I1) ? 0 : ri;
+  const bool on = l * 4 < d;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 a = on ? *reinterpret_cast<const float4*>(P + (int64_t)ru * d + 4 * l) : z;
+  const float4 q = on ? *reinterpret_cast<const float4*>(P + (U1 + ri) * (int64_t)d + 4 * l) : z;
+  const float s = kb_sum<LPR>(a.x * q.x + a.y * q.y + a.z * q.z + a.w * q.w);
+  if (l == 0) out[b] = s;
+}
+
+extern "C" int acf_kbpr_predict(acf_kbpr_ctx* c, const float* P, const int32_t* u, const int32_t* it, int64_t n,
+                                float* out, void* stream_) {
+  ACF_CHECK(c && P && u && it && out, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(n >= 0, ACF_E_INVALID, "negative count");
+  if (n == 0) return ACF_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  int lpr = 1;
+  while (lpr * 4 < c->d) lpr <<= 1;
+  const unsigned g = (unsigned)((n * lpr + 255) / 256);
+  switch (lpr) {
+    case 1: k_kbpr_predict<1><<<g, 256, 0, s>>>(P, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 2: k_kbpr_predict<2><<<g, 256, 0, s>>>(P, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 4: k_kbpr_predict<4><<<g, 256, 0, s>>>(P, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 8: k_kbpr_predict<8><<<g, 256, 0, s>>>(P, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 16: k_kbpr_predict<16><<<g, 256, 0, s>>>(P, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 32: k_kbpr_predict<32><<<g, 256, 0, s>>>(P, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    default: k_kbpr_predict<64><<<g, 256, 0, s>>>(P, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+  }
+  HIP_TRY(hipGetLastError());
+  int32_t herr = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ACF_CHECK(herr == 0, ACF_E_RANGE, "index out of range (%s%s)", (herr & 1) ? "user >= num_user_rows " : "",
+            (herr & 2) ? "item >= num_item_rows" : "");
+  return ACF_OK;
+}

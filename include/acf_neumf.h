@@ -78,6 +78,30 @@ int acf_neumf_train(acf_neumf_ctx* ctx, float* params, float* grad, float* m, fl
 int acf_neumf_predict(acf_neumf_ctx* ctx, const float* params, const int32_t* user,
                       const int32_t* item, int64_t n, float* scores, void* stream);
 
+/* ---- Keras BPR (BPR.py:23-99): run.py --model bpr, BASELINE configs[0] ----
+ * Parameters in one flat fp32 buffer [uEmb (num_user_rows x dim) | iEmb
+ * (num_item_rows x dim)] (BPR.py:35-36); gradient and Adam moments share the
+ * layout.  dim % 4 == 0, dim <= 256. */
+typedef struct acf_kbpr_ctx acf_kbpr_ctx;
+int acf_kbpr_create(acf_kbpr_ctx** ctx, int64_t num_user_rows, int64_t num_item_rows, int32_t dim,
+                    int32_t max_batch);
+int acf_kbpr_destroy(acf_kbpr_ctx* ctx);
+
+/* One Keras fit epoch over n already-shuffled triplets (BPR.py:70-81): per
+ * batch of `batch` (the last one partial) the gradient of
+ * mean(1 - log(sigmoid(u.p - u.n))) (BPR.py:11-20), summed per table row in
+ * occurrence order into grad, then Keras 2.2 Adam iteration t_first + k over the
+ * whole buffer (grad re-zeroed; hp: lr, beta1, beta2, adam_eps).  losses
+ * (device, [n]): each triplet's loss term.  Indices are validated at the end
+ * (ACF_E_RANGE; out-of-range rows were read as row 0).  Synchronous. */
+int acf_kbpr_train(acf_kbpr_ctx* ctx, float* params, float* grad, float* m, float* v, const int32_t* user,
+                   const int32_t* item_pos, const int32_t* item_neg, int64_t n, int32_t batch, int64_t t_first,
+                   const acf_neumf_hparams* hp, float* losses, void* stream);
+
+/* ranker.rank(users, items) (BPR.py:67-68, predictor pDot): u . i of n pairs. */
+int acf_kbpr_predict(acf_kbpr_ctx* ctx, const float* params, const int32_t* user, const int32_t* item,
+                     int64_t n, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,3 +82,41 @@ def test_checkpoint_roundtrip_format(tmp_path):
     assert train.latest_checkpoint(str(tmp_path)) == path
     z = np.load(path + ".npz")
     assert set(z.files) == {"embedding_P", "embedding_Q"}
+
+
+# --- run.py (run.py:25-280): the Keras-style Recommender driver -------------------
+def _run_cli():
+    import importlib
+    return importlib.import_module(PKG + ".run_cli")
+
+
+def test_run_py_flags_match_reference_defaults():
+    a = _run_cli().parse_args([])
+    assert (a.path, a.opath, a.model, a.data, a.d, a.verbose_eval, a.eval, a.maxlen, a.epochs, a.adv_epochs,
+            a.w, a.pp, a.bs, a.pre, a.mode, a.ckpt, a.save_model) == (
+        "", "test/", "bpr", "test", 64, 1, "all", 10, 10, 5, 0.001, 0.2, 512, "", 0, 1, 1)
+
+
+def test_run_py_dataset_semantics():
+    """1-based ids (0 = masking id), leave-one-out test item, all-mode negatives =
+    every item but 0, the user's train items and the test item; sample mode 100
+    draws outside the user's items."""
+    rc = _run_cli()
+    ds = rc.get_dataset("synthetic:60:45:1300", "", "all")
+    assert ds.testRatings[0] is None and len(ds.testRatings) == ds.num_users == 61
+    seq = ds.trainSeq
+    for u in (1, 7, 60):
+        negs = set(ds.testNegatives[u])
+        assert 0 not in negs and ds.testRatings[u] not in negs and not negs & set(seq[u])
+        assert negs | set(seq[u]) | {ds.testRatings[u], 0} == set(range(ds.num_items))
+        assert (u, seq[u][0]) in ds.trainMatrix
+    sm = rc.get_dataset("synthetic:60:45:1300", "", "sample")
+    for u in (1, 30):
+        assert len(sm.testNegatives[u]) == 100 and not set(sm.testNegatives[u]) & set(seq[u])
+
+
+def test_run_py_rejects_out_of_scope_models():
+    import pytest
+    rc = _run_cli()
+    with pytest.raises(SystemExit, match="scope"):
+        rc.make_ranker("sasrec", 10, 10, 8, rc.parse_args([]))
