@@ -441,59 +441,6 @@ __device__ __forceinline__ OccRec item_rec(const int4& own, const int4& oth, con
 // One thread per triplet: its user and two item occurrence records and, when
 // fused, its fused-triplet record.  The first R records of a slot go inline
 // only (that is the only place they are read from), later ones to the CSR.
-__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb, int32_t no_fuse,
-                          const int4* __restrict__ tsl, const int4* __restrict__ tpos,
-                          const int4* __restrict__ uinfo, const int4* __restrict__ iinfo,
-                          const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
-                          OccRec* __restrict__ urec, OccRec* __restrict__ irec,
-                          OccRec* __restrict__ inl, OccRec* __restrict__ trec,
-                          int32_t* __restrict__ gen_ptr) {
-  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (e == 0) *gen_ptr = gen;
-  if (e >= E) return;
-  const int4 sl = tsl[e], ps = tpos[e];
-  const int4 U = uinfo[sl.x], I = iinfo[sl.y], J = iinfo[sl.z];
-  const int32_t t = (int32_t)(e / B);
-  const int32_t nU = ubs[t + 1] - ubs[t];
-  const int32_t k = sl.x - ubs[t], ki = nU + (sl.y - ibs[t]), kj = nU + (sl.z - ibs[t]);
-  FuseInfo f = fuse_info(U, I, J, kb);
-  if (no_fuse) f.fused = f.in_u = f.in_i = f.in_j = 0;  // shard mode: item counts are rank-local
-  OccRec r;
-  r.own_row = U.x;
-  r.own_src = U.y;
-  r.meta = info_count(U) | (f.fused ? ACF_SINGLE_BIT : 0) | (f.in_u ? ACF_INPLACE_BIT : 0);
-  r.ovf = U.w;
-  r.e_role = (int32_t)e;
-  r.pa_row = I.x;
-  r.pb_row = J.x;
-  r.pa_src = I.y;
-  r.pb_src = J.y;
-  r.pa_slot = ki | (info_count(I) == 1 ? ACF_SOLO_BIT : 0);
-  r.pb_slot = kj | (info_count(J) == 1 ? ACF_SOLO_BIT : 0);
-  r.gen = gen;
-  const int64_t base = (int64_t)t * S;
-  int32_t rr = ps.x - U.w;
-  if (rr < R) inl[(base + k) * R + rr] = r;
-  else urec[ps.x] = r;
-  const OccRec ri = item_rec(I, J, U, (int32_t)(2 * e), k, kj, f.fused, f.in_i, gen);
-  rr = ps.y - I.w;
-  if (rr < R) inl[(base + ki) * R + rr] = ri;
-  else irec[ps.y] = ri;
-  const OccRec rj = item_rec(J, I, U, (int32_t)(2 * e + 1), k, ki, f.fused, f.in_j, gen);
-  rr = ps.z - J.w;
-  if (rr < R) inl[(base + kj) * R + rr] = rj;
-  else irec[ps.z] = rj;
-  if (f.fused) {  // other triplets' records read as absent (older generation)
-    OccRec q;
-    q.own_row = U.x; q.own_src = I.x; q.meta = J.x; q.ovf = k;
-    q.e_role = ki; q.pa_row = kj; q.pb_row = U.y; q.pa_src = I.y;
-    q.pb_src = J.y;
-    q.pa_slot = 1 | (f.in_u ? 2 : 0) | (f.in_i ? 4 : 0) | (f.in_j ? 8 : 0);
-    q.pb_slot = (int32_t)e; q.gen = gen;
-    trec[e] = q;
-  }
-}
-
 // Hot slots of packed (one lane-group per slot) plans.  A large batch of
 // Zipf-popular items holds a few rows with thousands of occurrences (10M x 5M,
 // B = 65,536: the top item ~4,000), and one lane-group would sum them one pass
@@ -525,27 +472,90 @@ struct HotLists {
   int32_t hot_stride, piece_stride;
 };
 
-// Packed mode: per slot of every batch, (non-fused, not hot << 32) | (row stays
-// in W scratch), scanned together into the per-batch slot and write-back lists;
-// hot slots go to the hot lists instead of the slot list.
-__global__ void k_slot_flags(const OccRec* __restrict__ inl, int64_t n, int32_t R, int32_t gen, int32_t S,
-                             uint64_t* __restrict__ flags, HotLists hl) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= n) return;
-  const OccRec* r = inl + x * R;
-  const int32_t meta = r->meta, count = meta & ACF_COUNT_MASK;
-  const bool valid = r->gen == gen && count != 0;
-  const bool hot = valid && !(meta & ACF_SINGLE_BIT) && count > ACF_HOT_MIN;
-  const uint64_t ns = (valid && !(meta & ACF_SINGLE_BIT) && !hot) ? 1 : 0;
-  const uint64_t fl = (valid && !(meta & ACF_INPLACE_BIT)) ? 1 : 0;
-  flags[x] = (ns << 32) | fl;
+// Per-slot flags of packed plans (non-fused and not hot << 32 | row stays in W
+// scratch), written by k_records for the slot's first occurrence (the hot
+// lists likewise); scanned into the per-batch slot and write-back lists.
+__device__ __forceinline__ void slot_flag(uint64_t* __restrict__ sflags, const HotLists& hl, int64_t t, int32_t S,
+                                          int32_t k, int32_t count, bool single, bool inplace) {
+  const bool hot = !single && count > ACF_HOT_MIN;
+  sflags[t * S + k] = ((uint64_t)(!single && !hot) << 32) | (uint64_t)(!inplace);
   if (hot) {
-    const int64_t t = x / S;
-    const int32_t k = (int32_t)(x - t * S), np = hot_pieces(count);
+    const int32_t np = hot_pieces(count);
     const int32_t h = atomicAdd(hl.cnt + t, 1);
     const int32_t base = atomicAdd(hl.pcnt + t, np);
     hl.list[t * hl.hot_stride + h] = make_int4(k, np, base, count);
     for (int32_t p = 0; p < np; ++p) hl.piece[t * hl.piece_stride + base + p] = make_int4(k, p, np, base);
+  }
+}
+
+// tri (triplet-centric list plans, see k_tri_*): every row that occurs once in
+// its batch is "single" (its triplet's lane-group steps it: SINGLE bit, and
+// INPLACE by fuse_info's rule), and every triplet gets a record in trec with
+// the single bits 16 / 32 / 64 (u / i / j) beside the fused / in-place flags.
+__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb, int32_t no_fuse,
+                          int32_t tri,
+                          const int4* __restrict__ tsl, const int4* __restrict__ tpos,
+                          const int4* __restrict__ uinfo, const int4* __restrict__ iinfo,
+                          const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
+                          OccRec* __restrict__ urec, OccRec* __restrict__ irec,
+                          OccRec* __restrict__ inl, OccRec* __restrict__ trec,
+                          int32_t* __restrict__ gen_ptr, uint64_t* __restrict__ sflags, HotLists hl) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e == 0) *gen_ptr = gen;
+  if (e >= E) return;
+  const int4 sl = tsl[e], ps = tpos[e];
+  const int4 U = uinfo[sl.x], I = iinfo[sl.y], J = iinfo[sl.z];
+  const int32_t t = (int32_t)(e / B);
+  const int32_t nU = ubs[t + 1] - ubs[t];
+  const int32_t k = sl.x - ubs[t], ki = nU + (sl.y - ibs[t]), kj = nU + (sl.z - ibs[t]);
+  FuseInfo f = fuse_info(U, I, J, kb);
+  if (no_fuse) f.fused = f.in_u = f.in_i = f.in_j = 0;  // shard mode: item counts are rank-local
+  const int su = info_count(U) == 1, si = info_count(I) == 1, sj = info_count(J) == 1;
+  if (tri) {  // single rows step in their triplet; in place by the fused rule
+    f.in_u = su && !pend1(U.y, kb) && !(U.z & ACF_INFO_NEXT);
+    f.in_i = si && !pend1(I.y, kb) && !(I.z & ACF_INFO_NEXT);
+    f.in_j = sj && !pend1(J.y, kb) && !(J.z & ACF_INFO_NEXT);
+  }
+  const int xu = tri ? su : f.fused, xi = tri ? si : f.fused, xj = tri ? sj : f.fused;
+  OccRec r;
+  r.own_row = U.x;
+  r.own_src = U.y;
+  r.meta = info_count(U) | (xu ? ACF_SINGLE_BIT : 0) | (f.in_u ? ACF_INPLACE_BIT : 0);
+  r.ovf = U.w;
+  r.e_role = (int32_t)e;
+  r.pa_row = I.x;
+  r.pb_row = J.x;
+  r.pa_src = I.y;
+  r.pb_src = J.y;
+  r.pa_slot = ki | (info_count(I) == 1 ? ACF_SOLO_BIT : 0);
+  r.pb_slot = kj | (info_count(J) == 1 ? ACF_SOLO_BIT : 0);
+  r.gen = gen;
+  const int64_t base = (int64_t)t * S;
+  int32_t rr = ps.x - U.w;
+  if (rr < R) inl[(base + k) * R + rr] = r;
+  else urec[ps.x] = r;
+  const OccRec ri = item_rec(I, J, U, (int32_t)(2 * e), k, kj, xi, f.in_i, gen);
+  rr = ps.y - I.w;
+  if (rr < R) inl[(base + ki) * R + rr] = ri;
+  else irec[ps.y] = ri;
+  const OccRec rj = item_rec(J, I, U, (int32_t)(2 * e + 1), k, ki, xj, f.in_j, gen);
+  rr = ps.z - J.w;
+  if (rr < R) inl[(base + kj) * R + rr] = rj;
+  else irec[ps.z] = rj;
+  if (sflags) {  // packed plans: the slot flags and hot lists, from each slot's first occurrence
+    if (ps.x == U.w) slot_flag(sflags, hl, t, S, k, info_count(U), xu, f.in_u);
+    if (ps.y == I.w) slot_flag(sflags, hl, t, S, ki, info_count(I), xi, f.in_i);
+    if (ps.z == J.w) slot_flag(sflags, hl, t, S, kj, info_count(J), xj, f.in_j);
+  }
+  if (f.fused || tri) {  // other triplets' records read as absent (older generation)
+    OccRec q;
+    q.own_row = U.x; q.own_src = I.x; q.meta = J.x; q.ovf = k;
+    q.e_role = ki; q.pa_row = kj; q.pb_row = U.y; q.pa_src = I.y;
+    q.pb_src = J.y;
+    q.pa_slot = (f.fused ? 1 : 0) | (f.in_u ? 2 : 0) | (f.in_i ? 4 : 0) | (f.in_j ? 8 : 0) |
+                (su ? 16 : 0) | (si ? 32 : 0) | (sj ? 64 : 0);
+    q.pb_slot = (int32_t)e; q.gen = gen;
+    trec[e] = q;
   }
 }
 
@@ -948,7 +958,7 @@ struct StepArgs {
   const int32_t* task_cnt;   // [nb]
   int32_t task_stride, max_depth;
   int32_t poll_sleep;  // k_stream: s_sleep between polls of a version (0-3; 4/5/6 = 8/16/32)
-  // hot slots of list plans (k_slot_flags): piece waves [slot_waves, slot_waves +
+  // hot slots of list plans (k_records): piece waves [slot_waves, slot_waves +
   // hot_waves) of a list kernel stride over the batch's pieces; partial sums in hot_part
   HotLists hot;
   float* hot_part;     // [piece_stride, d]
@@ -958,6 +968,9 @@ struct StepArgs {
   // exchange instead of Adagrad, and item rows are never written back
   int32_t shard;
   int32_t reg_B;       // batch size of reg * mean(w^2) (the global batch in shard mode)
+  // triplet-centric list step (k_tri_*): per-occurrence contributions of shared rows
+  const int4* tpos;    // [E] CSR positions of a triplet's three occurrences
+  float* contrib;      // users [B][2][d] (positive, negative branch), then items [2B][d]
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -2391,6 +2404,262 @@ __global__ void __launch_bounds__(256) k_adv_list(StepArgs a) {
   for (int x = gid; x < n; x += ngroups) adv_slot<LPR, NV, 1>(a, lst[x], 0, l, g * LPR, wave);
 }
 
+// ---------------------------------------------------------------------------
+// Triplet-centric list step (packed plans with fusion, not shard mode: large
+// batches).  The slot kernels above compute a triplet's BPR term once per row
+// it touches (its user slot and both item slots each re-read the partner rows
+// and deltas).  Here every triplet's lane-group computes its term ONCE:
+//  - a row that occurs once in the batch ("single") is stepped by its triplet
+//    in registers (k_single's operation sequence: delta, adversarial term,
+//    Adagrad), written in place or to W scratch by the fused rule;
+//  - a row with more occurrences ("shared") gets the triplet's rounded
+//    products as CONTRIBUTIONS (users: the positive and the negative branch,
+//    items: one vector), stored at the occurrence's CSR position; a combine
+//    sums a slot's contributions in occurrence order -- exactly the additions
+//    the one-lane-group slot path makes, so the bits are the slot path's --
+//    and finishes the row (delta, or Adagrad into W scratch).  Slots with more
+//    than ACF_HOT_MIN occurrences sum their contributions in pieces, then
+//    k_hot_combine.
+// Per batch (APR): k_tri_clean (write-back of t-1, clean contributions) ->
+// k_tri_combine<0> + k_hot_combine<0> (shared deltas) -> k_tri_adv (every
+// triplet: fused ones as k_single, the others as above) -> k_tri_combine<2> +
+// k_hot_combine<2> (shared Adagrad).  BPR: k_tri_clean<BPR> -> combine<1>.
+// ---------------------------------------------------------------------------
+#define TRI_SU 16
+#define TRI_SI 32
+#define TRI_SJ 64
+
+__device__ __forceinline__ float* tri_cu(const StepArgs& a) { return a.contrib; }
+__device__ __forceinline__ float* tri_ci(const StepArgs& a) { return a.contrib + (int64_t)2 * a.B * a.d; }
+
+// PASS 0: APR clean (shared rows: clean contributions; single rows: nothing,
+// k_tri_adv recomputes their term); 1: BPR (single rows: Adagrad; shared:
+// contributions); 2: APR adversarial.
+template <int LPR, int NV, int PASS>
+__device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
+  if (b >= a.B) return;
+  const int64_t e = (int64_t)a.t * a.B + b;
+  const RecV r = load_rec(a.trec + e);
+  if (r.c.w != *a.gen_ptr) return;
+  const int flags = r.c.y;
+  if (flags & 1) {  // fused: all three rows single
+    if (PASS == 1) k_single<LPR, NV, false>(a, b, l);
+    if (PASS == 2) k_single<LPR, NV, true>(a, b, l);
+    return;
+  }
+  const int d = a.d;
+  const int32_t u = r.a.x, i = r.a.y, j = r.a.z;
+  const int32_t ku = r.a.w, ki = r.b.x, kj = r.b.y;
+  const bool su = (flags & TRI_SU) != 0, si = (flags & TRI_SI) != 0, sj = (flags & TRI_SJ) != 0;
+  RowV<NV> p, qi, qj;
+  if (PASS == 2) {  // the tables are current (k_tri_clean wrote back batch t-1)
+    p = load_row<LPR, NV>(a.P, u, d, l);
+    qi = load_row<LPR, NV>(a.Q, i, d, l);
+    qj = load_row<LPR, NV>(a.Q, j, d, l);
+  } else {
+    p = load_at<LPR, NV>(row_src(a, a.P, u, r.b.z), d, l);
+    qi = load_at<LPR, NV>(row_src(a, a.Q, i, r.b.w), d, l);
+    qj = load_at<LPR, NV>(row_src(a, a.Q, j, r.c.x), d, l);
+  }
+  RowV<NV> cu, ci, cj;
+  if (PASS != 0) {
+    if (su) cu = load_row<LPR, NV>(a.accP, u, d, l);
+    if (si) ci = load_row<LPR, NV>(a.accQ, i, d, l);
+    if (sj) cj = load_row<LPR, NV>(a.accQ, j, d, l);
+  }
+  const int4 ps = a.tpos[e];
+  const int64_t lu = ps.x - (int64_t)a.t * a.B, li = ps.y - (int64_t)a.t * 2 * a.B,
+                lj = ps.z - (int64_t)a.t * 2 * a.B;
+  float* cuB = tri_cu(a);
+  float* ciB = tri_ci(a);
+  float g, loss;
+  bpr_term(dot_row<LPR, NV>(p, qi) - dot_row<LPR, NV>(p, qj), a.clip_lo, a.clip_hi, g, loss);
+  if (PASS != 2 && l == 0) a.loss_clean[e] = loss;
+  if (PASS != 2) {  // clean contributions of the shared rows
+    if (!su) {
+      store_row<LPR, NV>(cuB, 2 * lu, d, l, scale_row(qi, g));
+      store_row<LPR, NV>(cuB, 2 * lu + 1, d, l, scale_row(qj, -g));
+    }
+    if (!si) store_row<LPR, NV>(ciB, li, d, l, scale_row(p, g));
+    if (!sj) store_row<LPR, NV>(ciB, lj, d, l, scale_row(p, -g));
+    if (PASS == 0) return;
+  }
+  // the single rows' clean gradients (k_single's order)
+  RowV<NV> Gu = zero_row<NV>(), Gi = zero_row<NV>(), Gj = zero_row<NV>();
+  axpy_row(Gu, g, qi);
+  axpy_row(Gu, -g, qj);
+  axpy_row(Gi, g, p);
+  axpy_row(Gj, -g, p);
+  if (PASS == 2) {
+    const RowV<NV> pp = add_row(p, su ? make_delta<LPR, NV>(a, Gu, 0, u, l) : load_row<LPR, NV>(a.delta, ku, d, l));
+    const RowV<NV> qip = add_row(qi, si ? make_delta<LPR, NV>(a, Gi, 1, i, l) : load_row<LPR, NV>(a.delta, ki, d, l));
+    const RowV<NV> qjp = add_row(qj, sj ? make_delta<LPR, NV>(a, Gj, 1, j, l) : load_row<LPR, NV>(a.delta, kj, d, l));
+    float ga, la;
+    bpr_term(dot_row<LPR, NV>(pp, qip) - dot_row<LPR, NV>(pp, qjp), a.clip_lo, a.clip_hi, ga, la);
+    if (l == 0) a.loss_adv[e] = la;
+    if (!su) {
+      store_row<LPR, NV>(cuB, 2 * lu, d, l, scale_row(qip, ga));
+      store_row<LPR, NV>(cuB, 2 * lu + 1, d, l, scale_row(qjp, -ga));
+    }
+    if (!si) store_row<LPR, NV>(ciB, li, d, l, scale_row(pp, ga));
+    if (!sj) store_row<LPR, NV>(ciB, lj, d, l, scale_row(pp, -ga));
+    if (su) {
+      RowV<NV> Au = zero_row<NV>();
+      axpy_row(Au, ga, qip);
+      axpy_row(Au, -ga, qjp);
+      axpy_row(Gu, a.reg_adv, Au);
+    }
+    if (si) {
+      RowV<NV> Ai = zero_row<NV>();
+      axpy_row(Ai, ga, pp);
+      axpy_row(Gi, a.reg_adv, Ai);
+    }
+    if (sj) {
+      RowV<NV> Aj = zero_row<NV>();
+      axpy_row(Aj, -ga, pp);
+      axpy_row(Gj, a.reg_adv, Aj);
+    }
+  }
+  // Adagrad of the single rows: in place unless pending from t-1 or read by t+1
+  if (su) {
+    RowV<NV> w;
+    adagrad_row(a, Gu, p, cu, 1, w);
+    store_row<LPR, NV>(a.accP, u, d, l, cu);
+    store_row<LPR, NV>((flags & 2) ? a.P : a.wnew_cur, (flags & 2) ? u : ku, d, l, w);
+  }
+  if (si) {
+    RowV<NV> w;
+    adagrad_row(a, Gi, qi, ci, 1, w);
+    store_row<LPR, NV>(a.accQ, i, d, l, ci);
+    store_row<LPR, NV>((flags & 4) ? a.Q : a.wnew_cur, (flags & 4) ? i : ki, d, l, w);
+  }
+  if (sj) {
+    RowV<NV> w;
+    adagrad_row(a, Gj, qj, cj, 1, w);
+    store_row<LPR, NV>(a.accQ, j, d, l, cj);
+    store_row<LPR, NV>((flags & 8) ? a.Q : a.wnew_cur, (flags & 8) ? j : kj, d, l, w);
+  }
+}
+
+// header of shared slot k: count, side, own row, source, local CSR base
+struct TriSlot {
+  int32_t count, is_item, row, src;
+  int64_t base;
+};
+
+__device__ __forceinline__ TriSlot tri_slot(const StepArgs& a, int k) {
+  const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
+  TriSlot h;
+  h.count = (r.gen() == *a.gen_ptr) ? (r.meta() & ACF_COUNT_MASK) : 0;
+  h.is_item = (r.meta() & ACF_ITEM_BIT) != 0;
+  h.row = r.own_row();
+  h.src = r.own_src();
+  h.base = (int64_t)r.ovf() - (int64_t)a.t * (h.is_item ? 2 : 1) * a.B;
+  return h;
+}
+
+// contributions of occurrences [o0, o1) of a slot, added in order (a user
+// occurrence: its positive, then its negative branch, as the slot path's axpys)
+template <int LPR, int NV>
+__device__ __forceinline__ void tri_add(const StepArgs& a, const TriSlot& h, int o0, int o1, int step, int l,
+                                        RowV<NV>& G) {
+  const int d = a.d;
+  if (h.is_item) {
+    const float* c = tri_ci(a);
+    for (int o = o0; o < o1; o += step) G = add_row(G, load_row<LPR, NV>(c, h.base + o, d, l));
+  } else {
+    const float* c = tri_cu(a);
+    for (int o = o0; o < o1; o += step) {
+      G = add_row(G, load_row<LPR, NV>(c, 2 * (h.base + o), d, l));
+      G = add_row(G, load_row<LPR, NV>(c, 2 * (h.base + o) + 1, d, l));
+    }
+  }
+}
+
+// finish a shared row from its summed G (as the slot kernels' team leader and
+// k_hot_combine do): MODE 0 g0 + delta, 1 BPR Adagrad, 2 APR Adagrad
+template <int LPR, int NV, int MODE>
+__device__ __forceinline__ void tri_finish(const StepArgs& a, int k, const TriSlot& h, RowV<NV>& G, int l) {
+  const int d = a.d;
+  if (MODE == 0) {
+    const RowV<NV> dl = make_delta<LPR, NV>(a, G, h.is_item, h.row, l);
+    store_row<LPR, NV>(a.g0, k, d, l, G);
+    store_row<LPR, NV>(a.delta, k, d, l, dl);
+    return;
+  }
+  float* acc_tab = h.is_item ? a.accQ : a.accP;
+  RowV<NV> acc = load_row<LPR, NV>(acc_tab, h.row, d, l);
+  RowV<NV> wout;
+  if (MODE == 1) {
+    const RowV<NV> own = load_at<LPR, NV>(row_src(a, h.is_item ? a.Q : a.P, h.row, h.src), d, l);
+    adagrad_row(a, G, own, acc, h.count, wout);
+  } else {
+    RowV<NV> G0 = load_row<LPR, NV>(a.g0, k, d, l);
+    axpy_row(G0, a.reg_adv, G);
+    const RowV<NV> own = load_row<LPR, NV>(h.is_item ? a.Q : a.P, h.row, d, l);
+    adagrad_row(a, G0, own, acc, h.count, wout);
+  }
+  store_row<LPR, NV>(acc_tab, h.row, d, l, acc);
+  store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+}
+
+template <int LPR, int NV, bool BPR>
+__global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
+  if (wave >= a.slot_waves) {
+    tri_triplet<LPR, NV, BPR ? 1 : 0>(a, (wave - a.slot_waves) * (64 / LPR) + g, l);
+    return;
+  }
+  if (!a.prev_valid) return;  // write-back of the rows batch t-1 left in W scratch
+  const int ngroups = a.slot_waves * (64 / LPR), gid = wave * (64 / LPR) + g;
+  const int n = a.flush_cnt[a.t - 1];
+  const int32_t* lst = a.flush_list + (int64_t)(a.t - 1) * a.S;
+  for (int x = gid; x < n; x += ngroups) flush_slot(a, a.t - 1, a.wnew_prev, lst[x], l, LPR);
+}
+
+// shared slots with <= ACF_HOT_MIN occurrences: one lane-group each, in order;
+// hot slots: piece waves [slot_waves, slot_waves + hot_waves) into hot_part
+template <int LPR, int NV, int MODE>
+__global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
+  if (wave < a.slot_waves) {
+    const int ngroups = a.slot_waves * (64 / LPR), gid = wave * (64 / LPR) + g;
+    const int n = a.slot_cnt[a.t];
+    const int32_t* lst = a.slot_list + (int64_t)a.t * a.S;
+    for (int x = gid; x < n; x += ngroups) {
+      const int k = lst[x];
+      const TriSlot h = tri_slot(a, k);
+      RowV<NV> G = zero_row<NV>();
+      tri_add<LPR, NV>(a, h, 0, h.count, 1, l, G);
+      tri_finish<LPR, NV, MODE>(a, k, h, G, l);
+    }
+    return;
+  }
+  const int hw = wave - a.slot_waves;
+  if (hw >= a.hot_waves) return;
+  constexpr int TEAM = 64 / LPR;
+  const int n = a.hot.pcnt[a.t];
+  const int4* pl = a.hot.piece + (int64_t)a.t * a.hot.piece_stride;
+  for (int x = hw; x < n; x += a.hot_waves) {
+    const int4 pc = pl[x];  // {slot, piece, pieces, piece base}
+    const TriSlot h = tri_slot(a, pc.x);
+    const int o0 = (int)((int64_t)pc.y * h.count / pc.z), o1 = (int)((int64_t)(pc.y + 1) * h.count / pc.z);
+    RowV<NV> G = zero_row<NV>();
+    tri_add<LPR, NV>(a, h, o0 + g, o1, TEAM, l, G);
+    team_allreduce<LPR, TEAM, NV>(G);
+    if (g == 0) store_row<LPR, NV>(a.hot_part, (int64_t)pc.w + pc.y, a.d, l, G);
+  }
+}
+
+template <int LPR, int NV>
+__global__ void __launch_bounds__(256) k_tri_adv(StepArgs a) {
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  tri_triplet<LPR, NV, 2>(a, wave * (64 / LPR) + lane / LPR, lane & (LPR - 1));
+}
+
 // Flush the pending rows of batch t (wnew_cur) to the tables (end of a call):
 // one wave per slot.
 __global__ void __launch_bounds__(256) k_flush(StepArgs a) {
@@ -2701,8 +2970,10 @@ struct acf_apr_ctx {
   int32_t lists = 0;    // the plan built slot / write-back lists (packed mode)
   int32_t touch_next = 1;  // phase 2 reads the next batch's records (ACF_TOUCH_NEXT=0 disables)
   int32_t *slot_list = nullptr, *flush_list = nullptr, *slot_cnt = nullptr, *flush_cnt = nullptr;
-  HotLists hot = {};            // hot slots of list plans (k_slot_flags)
+  HotLists hot = {};            // hot slots of list plans (k_records)
   int32_t shard = 0;            // shard mode (acf_apr_set_shard_mode): item rows are partial sums
+  int32_t tri = 0;              // the plan is triplet-centric (packed, not shard: k_tri_*)
+  float* contrib = nullptr;     // [4 maxB, d] per-occurrence contributions of shared rows (k_tri_*)
   int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
@@ -2859,6 +3130,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->hot.list, (size_t)maxNB * c->hot.hot_stride); A(&c->hot.piece, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot.cnt, 2 * (size_t)maxNB);
   A(&c->hot_part, (size_t)c->hot.piece_stride * d);
+  A(&c->contrib, (size_t)4 * maxB * d);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
   A(&c->iinfo, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
@@ -3112,10 +3384,16 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->plan_R = packed ? 1 : c->R;
   c->plan_kind2 = all_dt;
   c->plan_kb = kb;
-  k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen, kb, c->shard,
+  c->tri = packed && !c->shard;
+  if (packed) {  // k_records writes the slot flags of the slots it finds; the rest read 0
+    HIP_TRY(hipMemsetAsync(c->key_in, 0, (size_t)3 * E * sizeof(uint64_t), s));
+    HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
+  }
+  k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen, kb, c->shard, c->tri,
                                         reinterpret_cast<const int4*>(c->tsl),
                                         reinterpret_cast<const int4*>(c->tpos), c->uinfo, c->iinfo,
-                                        c->ubs, c->ibs, c->urec, c->irec, c->inl, c->trec, c->gen_dev);
+                                        c->ubs, c->ibs, c->urec, c->irec, c->inl, c->trec, c->gen_dev,
+                                        packed ? c->key_in : nullptr, c->hot);
   HIP_TRY(hipGetLastError());
   c->task_lists = 0;
   if (all_dt) {  // streamed-step task lists
@@ -3134,8 +3412,6 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->lists = 0;
   if (packed) {  // per-batch lists of non-fused slots and of rows left in W scratch
     const int64_t n = (int64_t)nb * 3 * B;
-    HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
-    k_slot_flags<<<grid_for(n), 256, 0, s>>>(c->inl, n, c->plan_R, gen, 3 * B, c->key_in, c->hot);
     size_t tb2 = c->tmp_bytes;
     HIP_TRY(rocprim::inclusive_scan(c->tmp, tb2, c->key_in, c->key_out, (size_t)n, rocprim::plus<uint64_t>(), s));
     k_slot_lists<<<grid_for(n), 256, 0, s>>>(c->key_in, c->key_out, n, 3 * B, c->slot_list, c->flush_list,
@@ -3191,6 +3467,8 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.hot_waves = 0;
   a.shard = c->shard;
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
+  a.tpos = reinterpret_cast<const int4*>(c->tpos);
+  a.contrib = c->contrib;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -3204,6 +3482,10 @@ struct Kernels {
   void* stream = nullptr;  // k_stream (one wave per slot, d <= 256)
   void* stream_flush = nullptr;  // its write-back, k_stream_flush<LPR>
   void *hot_clean = nullptr, *hot_bpr = nullptr, *hot_adv = nullptr;  // k_hot_combine (list kernels)
+  // triplet-centric list step (tri plans with fusion): clean (APR / BPR), combine (MODE 0/1/2), adversarial
+  void *tri_clean = nullptr, *tri_clean_bpr = nullptr, *tri_adv = nullptr;
+  void* tri_comb[3] = {nullptr, nullptr, nullptr};
+  int tri = 0;
   int slots_per_wave = 1;
   int lists = 0;  // list kernels: slot waves stride over the plan's per-batch lists
 };
@@ -3227,9 +3509,24 @@ static void kernel_ptrs_team(Kernels* k, int fused) {
 // fused: the phase-2 (APR) / fused-BPR kernels also run the fused-triplet waves;
 // lists: one lane-group per slot over the plan's slot lists (packed + fused)
 template <int LPR, int NV>
-static void kernel_ptrs(Kernels* k, int packed, int fused, int lists) {
+static void kernel_ptrs(Kernels* k, int packed, int fused, int lists, int tri) {
   constexpr int OPW = 64 / LPR;
   k->flush = reinterpret_cast<void*>(&k_flush);
+  if (packed && fused && lists && tri) {
+    k->tri_clean = reinterpret_cast<void*>(&k_tri_clean<LPR, NV, false>);
+    k->tri_clean_bpr = reinterpret_cast<void*>(&k_tri_clean<LPR, NV, true>);
+    k->tri_adv = reinterpret_cast<void*>(&k_tri_adv<LPR, NV>);
+    k->tri_comb[0] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 0>);
+    k->tri_comb[1] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 1>);
+    k->tri_comb[2] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 2>);
+    k->hot_clean = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 0>);
+    k->hot_bpr = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 1>);
+    k->hot_adv = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 2>);
+    k->slots_per_wave = OPW;
+    k->lists = 1;
+    k->tri = 1;
+    return;
+  }
   if (packed && fused && lists) {
     k->clean_apr = reinterpret_cast<void*>(&k_clean_list<LPR, NV, false>);
     k->clean_bpr = reinterpret_cast<void*>(&k_clean_list<LPR, NV, true>);
@@ -3260,7 +3557,8 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists) {
 // per slot, 2 one lane-group per slot
 
 static int get_kernels(const acf_apr_ctx* c, Kernels* k, int fused = 0) {
-  return DISPATCH_GEOM(c->d, kernel_ptrs, k, is_packed(c, c->B), fused || c->shard, c->lists);
+  return DISPATCH_GEOM(c->d, kernel_ptrs, k, is_packed(c, c->B), fused || c->shard, c->lists,
+                       c->tri && fused && !c->shard);
 }
 
 typedef void (*StepKernel)(StepArgs);
@@ -3399,7 +3697,6 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     if (kinds) kinds[li] = kind;
     StepArgs b = a;
     b.diag_launch = li;
-    if (kind == 5) b.slot_waves = waves;  // k_hot_combine: workgroups stride over the hot slots
     ++li;
     return launch(fn, b, waves, s, e0, e1);
   };
@@ -3470,6 +3767,29 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   // combine launch (kind 5) after each pass
   const int HW = K.lists ? std::min(c->hot.piece_stride, ACF_HOT_WAVES) : 0;
   const int HB = std::min(c->hot.hot_stride, ACF_HOT_BLOCKS);
+  if (K.tri) {  // triplet-centric list step (see k_tri_*)
+    const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);  // one lane-group per triplet
+    for (int32_t t = first; t < first + n; ++t) {
+      StepArgs a = make_args(c, tb, hp, t, t > first ? 1 : 0);
+      a.use_single = 1;  // in-place rows are not written back
+      a.slot_waves = SW;
+      a.hot_waves = HW;
+      StepArgs ah = a;
+      ah.slot_waves = 4 * HB;
+      if (hp->adver) {
+        ACF_RET(L(K.tri_clean, a, SW + TWT, 0));
+        ACF_RET(L(K.tri_comb[0], a, SW + HW, 5));
+        ACF_RET(L(K.hot_clean, ah, 4 * HB, 5));
+        ACF_RET(L(K.tri_adv, a, TWT, 1));
+        ACF_RET(L(K.tri_comb[2], a, SW + HW, 5));
+        ACF_RET(L(K.hot_adv, ah, 4 * HB, 5));
+      } else {
+        ACF_RET(L(K.tri_clean_bpr, a, SW + TWT, 0));
+        ACF_RET(L(K.tri_comb[1], a, SW + HW, 5));
+        ACF_RET(L(K.hot_bpr, ah, 4 * HB, 5));
+      }
+    }
+  } else {
   for (int32_t t = first; t < first + n; ++t) {
     const int pv = t > first ? 1 : 0;
     StepArgs a = make_args(c, tb, hp, t, pv);
@@ -3479,13 +3799,18 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     a.touch_next = (c->touch_next && !K.lists && t + 1 < first + n) ? 1 : 0;
     if (hp->adver) {
       ACF_RET(L(K.clean_apr, a, SW + HW, 0));
-      if (K.lists) ACF_RET(L(K.hot_clean, a, 4 * HB, 5));
+      StepArgs ah = a;
+      ah.slot_waves = 4 * HB;  // k_hot_combine: workgroups stride over the hot slots
+      if (K.lists) ACF_RET(L(K.hot_clean, ah, 4 * HB, 5));
       ACF_RET(L(K.adv, a, SW + HW + TW, 1));
-      if (K.lists) ACF_RET(L(K.hot_adv, a, 4 * HB, 5));
+      if (K.lists) ACF_RET(L(K.hot_adv, ah, 4 * HB, 5));
     } else {
       ACF_RET(L(K.clean_bpr, a, SW + HW + TW, 0));
-      if (K.lists) ACF_RET(L(K.hot_bpr, a, 4 * HB, 5));
+      StepArgs ah = a;
+      ah.slot_waves = 4 * HB;
+      if (K.lists) ACF_RET(L(K.hot_bpr, ah, 4 * HB, 5));
     }
+  }
   }
   }
   StepArgs af = make_args(c, tb, hp, first + n - 1, 0);
@@ -3591,7 +3916,7 @@ static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_
   ACF_RET(check_step(c, tb, hp, first));
   hipStream_t s = static_cast<hipStream_t>(stream_);
   prepare_stream(c, hp);
-  const int nl = 4 * n + 2;
+  const int nl = 6 * n + 2;
   std::vector<hipEvent_t> ev((size_t)2 * nl, nullptr);
   std::vector<int> kinds(nl, -1);
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e));

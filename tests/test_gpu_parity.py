@@ -482,7 +482,7 @@ def test_hot_slots_large_batch_match_oracle(ops, oracle, dev, d, adver, fp32_par
     ctx = ops.APRContext(U1, I1, d, B, nb, dev)
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     t = ctx.time_kernels(tabs, ops.StepHParams(adver=adver))
-    assert t["hot"][1] == nb * (2 if adver else 1)
+    assert t["hot"][1] == nb * (4 if adver else 2)  # tri combine + hot combine per pass
     lc, la = ctx.losses()
     for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
         fp32_parity(g, w, n)
