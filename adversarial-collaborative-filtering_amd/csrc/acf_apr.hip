@@ -2442,11 +2442,10 @@ __device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
   const RecV r = load_rec(a.trec + e);
   if (r.c.w != *a.gen_ptr) return;
   const int flags = r.c.y;
-  if (flags & 1) {  // fused: all three rows single
-    if (PASS == 1) k_single<LPR, NV, false>(a, b, l);
-    if (PASS == 2) k_single<LPR, NV, true>(a, b, l);
-    return;
-  }
+  // a fused triplet (all three rows single) takes the same code as the others
+  // (k_single's operation sequence), so a wave's lane-groups do not diverge
+  // into two paths; its clean pass is empty (PASS 2 recomputes the term)
+  if (PASS == 0 && (flags & 1)) return;
   const int d = a.d;
   const int32_t u = r.a.x, i = r.a.y, j = r.a.z;
   const int32_t ku = r.a.w, ki = r.b.x, kj = r.b.y;
@@ -2461,11 +2460,16 @@ __device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
     qi = load_at<LPR, NV>(row_src(a, a.Q, i, r.b.w), d, l);
     qj = load_at<LPR, NV>(row_src(a, a.Q, j, r.c.x), d, l);
   }
-  RowV<NV> cu, ci, cj;
+  RowV<NV> cu, ci, cj, du, di, dj;  // Adagrad slots of the single rows, deltas of the shared ones
   if (PASS != 0) {
     if (su) cu = load_row<LPR, NV>(a.accP, u, d, l);
     if (si) ci = load_row<LPR, NV>(a.accQ, i, d, l);
     if (sj) cj = load_row<LPR, NV>(a.accQ, j, d, l);
+  }
+  if (PASS == 2) {  // issued with the row loads, not after the clean term
+    if (!su) du = load_row<LPR, NV>(a.delta, ku, d, l);
+    if (!si) di = load_row<LPR, NV>(a.delta, ki, d, l);
+    if (!sj) dj = load_row<LPR, NV>(a.delta, kj, d, l);
   }
   const int4 ps = a.tpos[e];
   const int64_t lu = ps.x - (int64_t)a.t * a.B, li = ps.y - (int64_t)a.t * 2 * a.B,
@@ -2474,7 +2478,7 @@ __device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
   float* ciB = tri_ci(a);
   float g, loss;
   bpr_term(dot_row<LPR, NV>(p, qi) - dot_row<LPR, NV>(p, qj), a.clip_lo, a.clip_hi, g, loss);
-  if (PASS != 2 && l == 0) a.loss_clean[e] = loss;
+  if ((PASS != 2 || (flags & 1)) && l == 0) a.loss_clean[e] = loss;
   if (PASS != 2) {  // clean contributions of the shared rows
     if (!su) {
       store_row<LPR, NV>(cuB, 2 * lu, d, l, scale_row(qi, g));
@@ -2491,9 +2495,10 @@ __device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
   axpy_row(Gi, g, p);
   axpy_row(Gj, -g, p);
   if (PASS == 2) {
-    const RowV<NV> pp = add_row(p, su ? make_delta<LPR, NV>(a, Gu, 0, u, l) : load_row<LPR, NV>(a.delta, ku, d, l));
-    const RowV<NV> qip = add_row(qi, si ? make_delta<LPR, NV>(a, Gi, 1, i, l) : load_row<LPR, NV>(a.delta, ki, d, l));
-    const RowV<NV> qjp = add_row(qj, sj ? make_delta<LPR, NV>(a, Gj, 1, j, l) : load_row<LPR, NV>(a.delta, kj, d, l));
+    if (su) du = make_delta<LPR, NV>(a, Gu, 0, u, l);
+    if (si) di = make_delta<LPR, NV>(a, Gi, 1, i, l);
+    if (sj) dj = make_delta<LPR, NV>(a, Gj, 1, j, l);
+    const RowV<NV> pp = add_row(p, du), qip = add_row(qi, di), qjp = add_row(qj, dj);
     float ga, la;
     bpr_term(dot_row<LPR, NV>(pp, qip) - dot_row<LPR, NV>(pp, qjp), a.clip_lo, a.clip_hi, ga, la);
     if (l == 0) a.loss_adv[e] = la;

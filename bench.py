@@ -136,11 +136,11 @@ def step_kernel_name(kind: str, d: int, B: int) -> str:
     while lpr < d4 and lpr < 64:
         lpr <<= 1
     nv = (d4 + lpr - 1) // lpr
-    if B >= 4096:  # packed mapping with fusion: the list kernels
+    if B >= 4096:  # packed mapping with fusion: the triplet-centric list step
         if kind == "adv":
-            return f"k_adv_list<{lpr}, {nv}>"
+            return f"k_tri_adv<{lpr}, {nv}>"
         if kind == "clean":
-            return f"k_clean_list<{lpr}, {nv}, false>"
+            return f"k_tri_clean<{lpr}, {nv}, false>"
         return "k_flush"
     team = 1 if lpr == 64 else 64 // lpr
     if kind == "stream":
