@@ -3612,8 +3612,14 @@ static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hp
 // events != nullptr: timing mode, 2 events per launch, kinds[] per launch.
 // The APR graph of a one-wave-per-slot plan runs overlapped: clean(first),
 // then k_ovl = adv(t) + clean(t+1) for t < last, k_ovl = adv(last) alone, flush.
+// Only for rows made of whole 128-B cache lines (d % 32 == 0): k_ovl's clean half reads
+// a published W(t) row with plain loads, and two rows sharing a line let the
+// first read cache the line before the second row was published (an untagged
+// stale read; seen at d = 16 in test_batch_plan_matches_sort_plan).  The
+// streamed step's version rows carry a tag in every granule, so a stale line
+// there only delays the reader.
 static bool use_overlap(const acf_apr_ctx* c, const Kernels& K, const acf_apr_hparams* hp) {
-  return c->overlap && hp->adver && K.ovl && !K.lists && K.slots_per_wave == 1 && c->plan_kind2;
+  return c->overlap && hp->adver && K.ovl && !K.lists && K.slots_per_wave == 1 && c->plan_kind2 && c->d % 32 == 0;
 }
 
 // Streamed step: version buffers (allocated at first use: 3 x maxNB x S x d
