@@ -3114,13 +3114,6 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB; c->maxNB = maxNB; c->maxE = maxE;
   geometry(d, &c->lpr, &c->nv);
   c->R = std::min(128 / c->lpr, 8);  // 2 records per team member (see slot_header)
-  if (const char* e = getenv("ACF_INLINE_R")) c->R = std::max(1, std::min(c->R, atoi(e)));  // tuning
-  if (const char* e = getenv("ACF_TOUCH_NEXT")) c->touch_next = atoi(e) != 0;
-  if (const char* e = getenv("ACF_STEP_OVERLAP")) c->overlap = atoi(e) != 0;
-  if (const char* e = getenv("ACF_OVL_DELAY")) c->ovl_delay = std::max(0, atoi(e));
-  if (const char* e = getenv("ACF_STREAM")) c->stream = atoi(e) != 0;
-  if (const char* e = getenv("ACF_STREAM_DEPTH")) c->stream_depth = std::max(1, std::min(8, atoi(e)));
-  if (const char* e = getenv("ACF_POLL_SLEEP")) c->poll_sleep = std::max(0, std::min(6, atoi(e)));
   const size_t S = (size_t)3 * maxB;
   int r = ACF_OK;
   auto A = [&](auto** p, size_t n) { if (r == ACF_OK) r = dalloc(c, p, n); };

@@ -167,7 +167,7 @@ int acf_apr_set_fusion(acf_apr_ctx* ctx, int32_t on);
 int acf_apr_set_plan_mode(acf_apr_ctx* ctx, int32_t mode);
 
 /* Overlapped APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
- * environment ACF_STEP_OVERLAP=0 sets the default off).  For plans with one
+ * the setting is per context).  For plans with one
  * wavefront per slot, the adversarial pass of batch t and the clean pass of
  * batch t+1 run in one launch: a t+1 row waits (bounded spin on a per-row flag)
  * only for the rows batch t is still updating.  Arithmetic and order of every
@@ -176,7 +176,7 @@ int acf_apr_set_plan_mode(acf_apr_ctx* ctx, int32_t mode);
 int acf_apr_set_step_overlap(acf_apr_ctx* ctx, int32_t on);
 
 /* Streamed APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
- * environment ACF_STREAM=0 sets the default off).  For plans with one wavefront
+ * the setting is per context).  For plans with one wavefront
  * per slot and dim <= 256, ONE launch runs the whole batch range: every row a
  * batch updates becomes a tagged version that later batches read (bounded spin
  * until it exists), and one write-back kernel moves the last versions to the

@@ -188,3 +188,27 @@ def test_neumf_ranker_in_evaluation_protocol(nm, acf, dev):
     assert got[0] == want[0]
     ratings = [[u, t] for u, t in enumerate(test_items)]
     assert acf.evaluate_apr_mode(R(), ratings, negs)[0] == acf.evaluate_apr_mode(O(), ratings, negs)[0]
+
+
+@pytest.mark.parametrize("adver", [0, 1])
+def test_yelp_shaped_grad_matches_oracle(nm, dev, adver):
+    """The bench's configs[3] shape (yelp-sort-shaped: 25,677 x 25,815 rows, d = 64,
+    batch 512) with Zipf-popular items (rows with many occurrences per batch):
+    one gradient of the adversarial step vs the oracle, rtol 1e-4 as above."""
+    U1, I1, d, B = 25_678, 25_816, 64, 512
+    P = N.init_params(U1, I1, d, 17)
+    rng = np.random.default_rng(4 + adver)
+    u = rng.integers(0, U1, B).astype(np.int32)
+    i = ((rng.zipf(1.2, B) - 1) % I1).astype(np.int32)
+    y = (rng.random(B) < 0.5).astype(np.float32)
+    hp_o = N.NeuMFHParams(adver=adver, eps=0.5, reg_adv=1.0)
+    want, lc, la = N.grad_step(P, u, i, y, hp_o)
+    st = _state(nm, P, dev)
+    ctx = nm.NeuMFContext(st, B)
+    loss = torch.zeros(2, device=dev)
+    ctx.grad(u, i, y, ctx.hparams(adver=adver, eps=0.5, reg_adv=1.0), loss)
+    torch.cuda.synchronize()
+    for n in N.NAMES:
+        np.testing.assert_allclose(st.view(n, st.grad).cpu().numpy(), want[n], rtol=1e-4, atol=1e-6,
+                                   err_msg=n)
+    np.testing.assert_allclose(loss.cpu().numpy(), [lc, la], rtol=1e-5)

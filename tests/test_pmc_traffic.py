@@ -65,7 +65,9 @@ def test_bench_scales_stream_record_to_its_launch():
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    rec = json.load(open(os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")))["k_stream<16, 1, 4>"]
+    newest = sorted(d for d in os.listdir(os.path.join(REPO, "profiles"))
+                    if os.path.isfile(os.path.join(REPO, "profiles", d, "pmc_traffic.json")))[-1]
+    rec = json.load(open(os.path.join(REPO, "profiles", newest, "pmc_traffic.json")))["k_stream<16, 1, 4>"]
     got, source = bench.pmc_traffic("k_stream<16, 1, 4>", 400)
     assert got == int(rec["traffic_bytes_per_batch"] * 400)
     assert "per batch x 400" in source
