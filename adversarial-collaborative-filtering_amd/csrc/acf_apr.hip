@@ -1177,11 +1177,13 @@ __device__ __forceinline__ RecV occ_rec_mem(const StepArgs& a, const SlotHdr& h,
 template <int LPR, int NV>
 __device__ __forceinline__ void occ_term(const StepArgs& a, int is_item, const RowV<NV>& own, const RecV& r,
                                          const RowV<NV>& ra, const RowV<NV>& rb, bool active, int l,
-                                         float* __restrict__ loss_out, RowV<NV>& G, float* keep = nullptr) {
+                                         float* __restrict__ loss_out, RowV<NV>& G, float* keep = nullptr,
+                                         float* gkeep = nullptr) {
   float gb, loss;
   if (!is_item) {
     const float x = dot_row<LPR, NV>(own, ra) - dot_row<LPR, NV>(own, rb);
     bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
+    if (gkeep) *gkeep = gb;
     if (active) {
       axpy_row(G, gb, ra);   // pos branch: dx+/dp = q_i
       axpy_row(G, -gb, rb);  // neg branch: dx-/dp = q_j
@@ -1193,6 +1195,7 @@ __device__ __forceinline__ void occ_term(const StepArgs& a, int is_item, const R
     const int role = active ? (r.e_role() & 1) : 0;
     const float x = role ? (dqo - dq) : (dq - dqo);
     bpr_term(x, a.clip_lo, a.clip_hi, gb, loss);
+    if (gkeep) *gkeep = gb;
     if (active) axpy_row(G, role ? -gb : gb, ra);
   }
 }
@@ -1920,24 +1923,32 @@ __device__ __forceinline__ void stream_partners(const StepArgs& a, int is_item, 
 // with the operation sequence the partner's own wave runs for a one-occurrence
 // row: its clean term from zero (occ_term), the team reduction's additions of
 // +0 (team_allreduce: member 0 holds the only term), then make_delta.  Same bits
-// as the published delta.  own / ra / rb are batch-start rows.  (Forming both
+// as the published delta.  own / ra / rb are batch-start rows; gk (if given) is
+// the occurrence's clean dloss/dx from this wave's clean term: the partner's
+// occ_term evaluates the same dot products of the same rows, so it is the
+// same bits and the dots and the loss chain need not run again.  (Forming both
 // partners' deltas in one straight-line block, with the published-delta loads
 // issued before it, measured slower: 4.56 vs 4.37 us per batch.)
 template <int LPR, int NV, int TEAM>
 __device__ __forceinline__ RowV<NV> solo_delta(const StepArgs& a, int is_item, const RowV<NV>& own,
                                                const RecV& r, const RowV<NV>& ra, const RowV<NV>& rb, int pb,
-                                               int l) {
+                                               int l, const float* gk = nullptr) {
   float gb, loss;
   RowV<NV> G = zero_row<NV>();
   int p_item;
   if (!is_item) {  // own = p_u, ra = q_i, rb = q_j: partner item i (pos) or j (neg)
-    bpr_term(dot_row<LPR, NV>(own, ra) - dot_row<LPR, NV>(own, rb), a.clip_lo, a.clip_hi, gb, loss);
+    if (gk) gb = *gk;
+    else bpr_term(dot_row<LPR, NV>(own, ra) - dot_row<LPR, NV>(own, rb), a.clip_lo, a.clip_hi, gb, loss);
     axpy_row(G, pb ? -gb : gb, own);
     p_item = 1;
   } else {  // own = this item, ra = p_u, rb = the other item
-    const float dq = dot_row<LPR, NV>(ra, own), dqo = dot_row<LPR, NV>(ra, rb);
     const int role = r.e_role() & 1;
-    bpr_term(role ? (dqo - dq) : (dq - dqo), a.clip_lo, a.clip_hi, gb, loss);
+    if (gk) {
+      gb = *gk;
+    } else {
+      const float dq = dot_row<LPR, NV>(ra, own), dqo = dot_row<LPR, NV>(ra, rb);
+      bpr_term(role ? (dqo - dq) : (dq - dqo), a.clip_lo, a.clip_hi, gb, loss);
+    }
     if (!pb) {  // the user: q_pos, q_neg terms in the user slot's order
       axpy_row(G, gb, role ? rb : own);
       axpy_row(G, -gb, role ? own : rb);
@@ -1960,7 +1971,8 @@ __device__ __forceinline__ void stream_adv_pass(const StepArgs& a, int is_item, 
                                                 const RowV<NV>& ownp, const RecV& r0, const RecV& r1, bool a0,
                                                 bool a1, RowV<NV> ra0, RowV<NV> rb0, RowV<NV> ra1,
                                                 RowV<NV> rb1, uint32_t tag, int l, RowV<NV>& GA,
-                                                int k = 0) {  // k: diagnostic stamps only
+                                                int k = 0,  // k: diagnostic stamps only
+                                                const float* g0 = nullptr, const float* g1 = nullptr) {
   RowV<NV> da0 = zero_row<NV>(), db0 = da0, da1 = da0, db1 = da0;
   const bool sa0 = a0 && r0.pa_solo(), sb0 = a0 && r0.pb_solo();
   const bool sa1 = a1 && r1.pa_solo(), sb1 = a1 && r1.pb_solo();
@@ -1970,19 +1982,19 @@ __device__ __forceinline__ void stream_adv_pass(const StepArgs& a, int is_item, 
   const VSrc tb1 = a1 && !sb1 ? ver_at(vrow(a.ver_d, a, a.t, r1.pb_slot())) : 0;
   bool pa0 = !ta0, pb0 = !tb0, pa1 = !ta1, pb1 = !tb1;
   if (__any(sa0)) {
-    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r0, ra0, rb0, 0, l);
+    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r0, ra0, rb0, 0, l, g0);
     if (sa0) da0 = x;
   }
   if (__any(sb0)) {
-    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r0, ra0, rb0, 1, l);
+    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r0, ra0, rb0, 1, l, g0);
     if (sb0) db0 = x;
   }
   if (__any(sa1)) {
-    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r1, ra1, rb1, 0, l);
+    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r1, ra1, rb1, 0, l, g1);
     if (sa1) da1 = x;
   }
   if (__any(sb1)) {
-    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r1, ra1, rb1, 1, l);
+    const RowV<NV> x = solo_delta<LPR, NV, TEAM>(a, is_item, own, r1, ra1, rb1, 1, l, g1);
     if (sb1) db1 = x;
   }
   STAMP(a.t, k, 6);
@@ -2021,7 +2033,7 @@ __device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int
   RowV<NV> ra0 = own, rb0 = own, ra1 = own, rb1 = own;
   RecV r0, r1;
   bool a0 = false, a1 = false;
-  float lc0 = 0.f, lc1 = 0.f;
+  float lc0 = 0.f, lc1 = 0.f, gc0 = 0.f, gc1 = 0.f;
   {  // first pass: own row, Adagrad slot, partners in one wait
     a0 = m < h.count;
     a1 = TEAM + m < h.count;
@@ -2041,8 +2053,8 @@ __device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int
     STAMP(a.t, k, 2);
     // clean losses are stored at the end of the task: on gfx950 vmcnt counts
     // stores too, so a store here would hold up every later wait on a load
-    occ_term<LPR, NV>(a, h.is_item, own, r0, ra0, rb0, a0, l, a.loss_clean, G, &lc0);
-    if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, own, r1, ra1, rb1, a1, l, a.loss_clean, G, &lc1);
+    occ_term<LPR, NV>(a, h.is_item, own, r0, ra0, rb0, a0, l, a.loss_clean, G, &lc0, &gc0);
+    if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, own, r1, ra1, rb1, a1, l, a.loss_clean, G, &lc1, &gc1);
   }
   // the clean half's end: batch-summed gradient, delta, delta published
   auto finish_clean = [&](RowV<NV>& Gc) -> RowV<NV> {
@@ -2056,7 +2068,8 @@ __device__ __forceinline__ void stream_slot(const StepArgs& a, int k, int m, int
   RowV<NV> GA = zero_row<NV>();
   if (h.count <= 2 * TEAM) {  // one pass (wave-uniform): partner rows kept for the adversarial half
     const RowV<NV> ownp = finish_clean(G);
-    stream_adv_pass<LPR, NV, TEAM>(a, h.is_item, own, ownp, r0, r1, a0, a1, ra0, rb0, ra1, rb1, tag, l, GA, k);
+    stream_adv_pass<LPR, NV, TEAM>(a, h.is_item, own, ownp, r0, r1, a0, a1, ra0, rb0, ra1, rb1, tag, l, GA, k, &gc0,
+                                   &gc1);
   } else {  // hot rows: more passes, partner rows re-read (versions never change)
     for (int base = 2 * TEAM; base < h.count; base += 2 * TEAM) {
       const int i0 = base + m, i1 = base + TEAM + m;

@@ -88,7 +88,55 @@ def main():
     out["span_per_batch_us"] = round(float(done[-1] - t0) / 100 / nb, 3)
     out["median_task_start_minus_prev_batch_done_us"] = round(float(np.median(lag)) / 100, 3)
     out["tasks_per_batch"] = round(float(np.mean([(st[t, :, 0] > 0).sum() for t in range(nb)])), 1)
+    out.update(critical(st, S, ep, B, nb, done))
     print(json.dumps(out, indent=1))
+
+
+def slot_counts(ep, B, t):
+    """occurrence count of every slot of batch t (slot order: users by row, then items by row)"""
+    s = slice(t * B, (t + 1) * B)
+    u = ep.user[s].cpu().numpy()
+    it = np.concatenate([ep.item_pos[s].cpu().numpy(), ep.item_neg[s].cpu().numpy()])
+    _, cu = np.unique(u, return_counts=True)
+    _, ci = np.unique(it, return_counts=True)
+    return np.concatenate([cu, ci]), len(cu)
+
+
+def critical(st, S, ep, B, nb, done):
+    """What finishes a batch last, and how task time grows with the slot's occurrence count."""
+    buckets = [(1, 1), (2, 2), (3, 4), (5, 8), (9, 16), (17, 1 << 30)]
+    dur = {b: [] for b in buckets}
+    w1 = {b: [] for b in buckets}
+    last_cnt, last_item, last_start_lag, hot_end, hot_cnt = [], [], [], [], []
+    for t in range(nb):
+        cnt, nu = slot_counts(ep, B, t)
+        w = st[t][: len(cnt)]
+        ok = (w[:, 0] > 0) & (w[:, 5] > 0)
+        for lo, hi in buckets:
+            m = ok & (cnt >= lo) & (cnt <= hi) & (w[:, 2] > 0)
+            dur[(lo, hi)] += list(w[m, 5] - w[m, 0])
+            w1[(lo, hi)] += list(w[m, 2] - w[m, 1])
+        k = int(np.argmax(np.where(ok, w[:, 5], 0)))
+        if w[k, 5] == done[t]:  # a slot task ends the batch (else a fused group)
+            last_cnt.append(int(cnt[k]))
+            last_item.append(int(k >= nu))
+            if t > 0:
+                last_start_lag.append(w[k, 0] - done[t - 1])
+        h = int(np.argmax(np.where(ok, cnt, 0)))
+        hot_end.append(w[h, 5])
+        hot_cnt.append(int(cnt[h]))
+    med = lambda v: round(float(np.median(v)) / 100, 3) if len(v) else None
+    out = {"task_us_by_count": {f"{lo}-{hi if hi < 1 << 30 else 'inf'}": [med(dur[(lo, hi)]), len(dur[(lo, hi)])]
+                                for lo, hi in buckets},
+           "wait1_us_by_count": {f"{lo}-{hi if hi < 1 << 30 else 'inf'}": med(w1[(lo, hi)]) for lo, hi in buckets},
+           "batch_ender_count_median": float(np.median(last_cnt)) if last_cnt else None,
+           "batch_ender_count_hist": np.bincount(np.minimum(last_cnt, 40)).tolist() if last_cnt else [],
+           "batch_ender_is_item_frac": float(np.mean(last_item)) if last_item else None,
+           "batches_ended_by_slot": len(last_cnt),
+           "batch_ender_start_minus_prev_done_us": med(last_start_lag),
+           "hottest_slot_count_median": float(np.median(hot_cnt)),
+           "hottest_slot_end_to_end_us": med(np.diff(np.array(hot_end, dtype=np.float64)))}
+    return out
 
 
 if __name__ == "__main__":
