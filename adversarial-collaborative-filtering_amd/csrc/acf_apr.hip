@@ -3955,7 +3955,8 @@ static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_
   return r;
 }
 
-// v1: kinds clean / adv / flush, the two-kernel step (no k_ovl)
+// per-kind launch times of the launch sequence acf_apr_train_planned runs
+// (kinds: see run_loop; include/acf_apr.h)
 extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
                                     const acf_apr_hparams* hp, int32_t first, int32_t n,
                                     double* ms_out, int32_t* launches_out, void* stream_) {
@@ -3989,8 +3990,6 @@ extern "C" int acf_apr_set_stream(acf_apr_ctx* c, int32_t on) {
   return ACF_OK;
 }
 
-// v3: kinds clean / adv / flush / overlapped / streamed (k_stream), the launch
-// sequence acf_apr_train_planned runs
 extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);
