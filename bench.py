@@ -335,7 +335,7 @@ def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
                         big.list_off, big.list_items, name="synthetic-large-rank")
         sampler = acf.DeviceSampler(sub, b, dev, seed=11 + rank, weights=np.ones(big.num_items, np.float32))
         ep = sampler.epoch(0)
-        warm = 4
+        warm = steps  # one untimed chunk of the timed size: routing buffers come from the cache
         n = (warm + steps) * b
         u, i, j = (x[:n].contiguous() for x in (ep.user, ep.item_pos, ep.item_neg))
         del ep, sampler, sub
@@ -369,7 +369,8 @@ def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
         ds = acf.pinterest_like(seed=2019)
         psamp = acf.DeviceSampler(ds, B, dev, seed=3)
         ep = psamp.epoch(0)
-        warm, steps_p = 20, 200
+        steps_p = 200
+        warm = steps_p  # as above: one untimed chunk of the timed size
         n = (warm + steps_p) * B
         u, i, j = (x[:n].contiguous() for x in (ep.user, ep.item_pos, ep.item_neg))
         sh = D_.ShardedAPR(ds.num_users + 1, ds.num_items + 1, d, B, device=dev)
