@@ -759,45 +759,82 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
   const int G = (B + p.opw - 1) / p.opw;
   const int2 n = p.bn[t];
   const int64_t rbase = (int64_t)t * S;
-  for (int s = tid; s < S; s += BS) {
-    single[s] = 0;
-    if (s >= n.x) {
+  // the triplet's occurrence slots, loaded now (k_bplan_sort wrote them): off
+  // the dependent chain of the slot pass below (B <= MAXB <= BS: one triplet per thread)
+  int32_t ou = 0, oi = 0, oj = 0;
+  if (tid < B) {
+    ou = p.bocc[rbase + tid];
+    oi = p.bocc[rbase + B + 2 * tid];
+    oj = p.bocc[rbase + B + 2 * tid + 1];
+  }
+  // per unique row: key and CSR bounds, then the row's batch bitmap word, then
+  // the previous batch's local slot.  The SPT slots of a thread go through each
+  // stage together, so their dependent loads overlap (three round trips, not 3 SPT).
+  constexpr int SPT = (3 * MAXB + BS - 1) / BS;
+  const uint32_t side_bit = 1u << p.rb;
+  uint32_t key[SPT];
+  int32_t st[SPT], en[SPT];
+  unsigned long long mw[SPT];
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int s = tid + q * BS;
+    if (s < S) single[s] = 0;
+    if (s < n.x) {
+      key[q] = p.bkey[rbase + s];
+      st[q] = p.bstart[(int64_t)t * (S + 1) + s];
+      en[q] = p.bstart[(int64_t)t * (S + 1) + s + 1];
+    } else if (s < S) {
       p.nextt[rbase + s] = 0;  // no row: never written back
-      continue;
     }
-    const uint32_t key = p.bkey[rbase + s];
-    const uint32_t side_bit = 1u << p.rb;
-    const int side = (key & side_bit) ? 1 : 0;
-    const int32_t row = (int32_t)(key & (side_bit - 1));
-    const int64_t rid = side ? p.U1 + row : (int64_t)row;
-    const int32_t st = p.bstart[(int64_t)t * (S + 1) + s];
-    const int32_t cnt = p.bstart[(int64_t)t * (S + 1) + s + 1] - st;
-    const int32_t ovf = side ? t * 2 * B + st - B : t * B + st;
-    const unsigned long long* m = p.mask + rid * p.W;
+  }
+  auto rid_of = [&](uint32_t k) -> int64_t {
+    const int32_t row = (int32_t)(k & (side_bit - 1));
+    return (k & side_bit) ? p.U1 + row : (int64_t)row;
+  };
+#pragma unroll
+  for (int q = 0; q < SPT; ++q)
+    if (tid + q * BS < n.x) mw[q] = p.mask[rid_of(key[q]) * p.W + (t >> 6)];
+  int32_t tp[SPT], prev_slot[SPT], tn[SPT];
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    tp[q] = -1;
+    tn[q] = 0x7fffffff;
+    if (tid + q * BS >= n.x) continue;
+    const unsigned long long* m = p.mask + rid_of(key[q]) * p.W;
     // previous batch touching the row: highest bit below t
     int w = t >> 6;
-    unsigned long long bits = m[w] & ((1ull << (t & 63)) - 1);
+    unsigned long long bits = mw[q] & ((1ull << (t & 63)) - 1);
     while (!bits && w > 0) bits = m[--w];
-    int32_t src = row;
-    if (bits) {
-      const int tp = w * 64 + 63 - __clzll((long long)bits);
-      src = make_src(t - tp, p.slot_of[rid * p.nbs + tp], p.kb);
-    }
+    if (bits) tp[q] = w * 64 + 63 - __clzll((long long)bits);
     // next batch touching the row: lowest bit above t
     w = t >> 6;
-    bits = (t & 63) == 63 ? 0ull : (m[w] & ~((2ull << (t & 63)) - 1));
+    bits = (t & 63) == 63 ? 0ull : (mw[q] & ~((2ull << (t & 63)) - 1));
     const int wl = (p.nb - 1) >> 6;
     while (!bits && w < wl) bits = m[++w];
-    const int32_t tn = bits ? w * 64 + __ffsll((long long)bits) - 1 : 0x7fffffff;
-    info[s] = make_int4(row, src, cnt | (tn == t + 1 ? ACF_INFO_NEXT : 0), ovf);
-    p.nextt[rbase + s] = tn;
+    if (bits) tn[q] = w * 64 + __ffsll((long long)bits) - 1;
+  }
+#pragma unroll
+  for (int q = 0; q < SPT; ++q)
+    if (tp[q] >= 0) prev_slot[q] = p.slot_of[rid_of(key[q]) * p.nbs + tp[q]];
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int s = tid + q * BS;
+    if (s >= n.x) continue;
+    const int side = (key[q] & side_bit) ? 1 : 0;
+    const int32_t row = (int32_t)(key[q] & (side_bit - 1));
+    const int32_t cnt = en[q] - st[q];
+    const int32_t ovf = side ? t * 2 * B + st[q] - B : t * B + st[q];
+    const int32_t src = tp[q] >= 0 ? make_src(t - tp[q], prev_slot[q], p.kb) : row;
+    info[s] = make_int4(row, src, cnt | (tn[q] == t + 1 ? ACF_INFO_NEXT : 0), ovf);
+    p.nextt[rbase + s] = tn[q];
   }
   for (int g = tid; g < G; g += BS) gflag[g] = 0;
   __syncthreads();
   const int gen = p.gen;
-  for (int b = tid; b < B; b += BS) {
+  static_assert(MAXB <= BS, "k_bplan_build: one triplet per thread");
+  if (tid < B) {
+    const int b = tid;
     const int64_t e = (int64_t)t * B + b;
-    const int32_t ou = p.bocc[rbase + b], oi = p.bocc[rbase + B + 2 * b], oj = p.bocc[rbase + B + 2 * b + 1];
     const int32_t k = ou & 0xFFFF, ki = oi & 0xFFFF, kj = oj & 0xFFFF;
     const int4 U = info[k], I = info[ki], J = info[kj];
     const FuseInfo f = fuse_info(U, I, J, p.kb);

@@ -157,10 +157,12 @@ class APRContext:
         return nb
 
     def _tables(self, P, Q, accP, accQ) -> Tables:
+        # the same storage, shape, strides and dtype as the last validated call (the
+        # device cannot differ at the same address)
         key = (P.data_ptr(), Q.data_ptr(), accP.data_ptr(), accQ.data_ptr(), P.shape, Q.shape, accP.shape,
-               accQ.shape, P.dtype, Q.dtype, accP.dtype, accQ.dtype, P.device, Q.device, accP.device,
-               accQ.device, P.is_contiguous(), Q.is_contiguous(), accP.is_contiguous(), accQ.is_contiguous())
-        if self._tb_key == key:  # same tensors as the last validated call
+               accQ.shape, P.stride(), Q.stride(), accP.stride(), accQ.stride(), P.dtype, Q.dtype, accP.dtype,
+               accQ.dtype)
+        if self._tb_key == key:
             return self._tb
         for t, n, rows in ((P, "embedding_P", self.U1), (Q, "embedding_Q", self.I1),
                            (accP, "accumulator_P", self.U1), (accQ, "accumulator_Q", self.I1)):
@@ -173,16 +175,18 @@ class APRContext:
 
     def train_range(self, tables, hp: StepHParams, user: torch.Tensor, item_pos: torch.Tensor,
                     item_neg: torch.Tensor, batch_size: int, first_batch: int, n_batches: int,
-                    graph: bool = True, check: bool = False) -> None:
+                    graph: bool = True, check: bool = False, _checked: bool = False) -> None:
         """plan + train_planned of batches [first_batch, first_batch + n_batches) of
         device int32 triplet streams, in ONE C call (acf_apr_train); the range is
-        addressed in place (no slicing)."""
+        addressed in place (no slicing).  (_checked: the caller, PlanPipeline.run,
+        has validated the three streams and the range.)"""
         B, nb = int(batch_size), int(n_batches)
-        for t, n in ((user, "user"), (item_pos, "item_pos"), (item_neg, "item_neg")):
-            if t.dtype != torch.int32 or t.device != self.device or not t.is_contiguous():
-                raise ValueError(f"{n} must be a contiguous int32 tensor on {self.device}")
-            if (first_batch + nb) * B > t.numel() or first_batch < 0:
-                raise ValueError(f"batches [{first_batch}, {first_batch + nb}) outside {n}")
+        if not _checked:
+            for t, n in ((user, "user"), (item_pos, "item_pos"), (item_neg, "item_neg")):
+                if t.dtype != torch.int32 or t.device != self.device or not t.is_contiguous() or t.dim() != 1:
+                    raise ValueError(f"{n} must be a contiguous 1-D int32 tensor on {self.device}")
+                if (first_batch + nb) * B > t.numel() or first_batch < 0:
+                    raise ValueError(f"batches [{first_batch}, {first_batch + nb}) outside {n}")
         if not self.fits(B, nb):
             raise ValueError(f"plan of {nb} x {B} exceeds context capacity {self.max_batches} x "
                              f"{self.max_batch_size}")
@@ -390,7 +394,7 @@ class PlanPipeline:
         B = self.batch_size
         u, i, j = (_idx(x, n, self.device) for x, n in ((user, "user"), (item_pos, "item_pos"),
                                                        (item_neg, "item_neg")))
-        total = u.numel() // B
+        total = min(u.numel(), i.numel(), j.numel()) // B
         n_batches = total - first_batch if n_batches is None else int(n_batches)
         if first_batch < 0 or n_batches <= 0 or first_batch + n_batches > total:
             raise ValueError(f"batches [{first_batch}, {first_batch + n_batches}) outside the "
@@ -401,7 +405,7 @@ class PlanPipeline:
         self._ov = (self.overlap if self.overlap is not None else B >= 4096) and len(chunks) > 1
         if not self._ov:  # plan + train per chunk in one C call each, on the caller's stream
             for k, (b, n) in enumerate(chunks):
-                self.ctx[k % 2].train_range(tables, hp, u, i, j, B, b, n, graph=graph, check=check)
+                self.ctx[k % 2].train_range(tables, hp, u, i, j, B, b, n, graph=graph, check=check, _checked=True)
             self._staged = (u, i, j)
             return
         if self._ov:
