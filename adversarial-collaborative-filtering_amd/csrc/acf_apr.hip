@@ -612,6 +612,34 @@ __global__ void k_task_list(const int32_t* __restrict__ flags, const int32_t* __
   if (y == stride - 1) cnt[t] = incl[x] - base;
 }
 
+// diagnostic build (-DACF_DIAG): s_memrealtime stamps of the plan and step kernels
+#ifdef ACF_DIAG
+__device__ uint64_t* g_stamps = nullptr;
+__device__ int g_stamp_launch = 0;
+__device__ int g_stamp_cap = 0;
+#define STAMP(launch, wave, i)                                                       \
+  do {                                                                               \
+    uint64_t t_;                                                                     \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    if (g_stamps && (threadIdx.x & 63) == 0 && (wave) < g_stamp_cap)                 \
+      g_stamps[((int64_t)(launch) * g_stamp_cap + (wave)) * 8 + (i)] = t_;          \
+  } while (0)
+#define CLOCKSTAMP(launch, wave, i)                                                  \
+  do {                                                                               \
+    uint64_t t_;                                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+    if (g_stamps && (threadIdx.x & 63) == 0 && (wave) < g_stamp_cap)                 \
+      g_stamps[((int64_t)(launch) * g_stamp_cap + (wave)) * 8 + (i)] = t_;          \
+  } while (0)
+#else
+#define CLOCKSTAMP(launch, wave, i) \
+  do {                              \
+  } while (0)
+#define STAMP(launch, wave, i) \
+  do {                         \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Batch-local plan (one-wave-per-slot plans, B <= 1024): the same records,
 // task lists and next-batch table as the sort plan above, in TWO launches with
@@ -655,6 +683,15 @@ struct BPlanArgs {
   int32_t* task_cnt;
 };
 
+// Workgroup barrier for LDS data only.  __syncthreads() also waits for every
+// outstanding global store and atomic of the wave (vmcnt(0)): after a phase of
+// scattered global writes that is a full memory round trip (≈2-4 us per barrier
+// in the plan kernels, tools/diag_plan.py) for data no other thread of the
+// workgroup reads back.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <int BS, int IPT>
 __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
   constexpr int N = BS * IPT;
@@ -671,6 +708,7 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
   __shared__ typename Scan::storage_type scan_st;
   __shared__ int32_t s_err, s_nu;
   const int t = blockIdx.x, tid = threadIdx.x, B = p.B, S3 = 3 * B;
+  STAMP(t, tid >> 6, 0);
   if (tid == 0) { s_err = 0; s_nu = -1; }
   const uint32_t side_bit = 1u << p.rb;
   uint32_t keys[IPT];
@@ -695,9 +733,11 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
     vals[k] = o;
   }
   __syncthreads();
+  STAMP(t, tid >> 6, 1);
   if (err) atomicOr(&s_err, err);
   Sort().sort(keys, vals, sm.sort, 0, p.rb + 1);
   __syncthreads();
+  STAMP(t, tid >> 6, 2);
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     sm.a.key[tid * IPT + k] = keys[k];
@@ -712,6 +752,7 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
   }
   int32_t excl = 0, total = 0;
   Scan().exclusive_scan(cnt, excl, 0, total, scan_st);
+  STAMP(t, tid >> 6, 3);
   int32_t sl[IPT];
   int32_t s = excl - 1;
   const int64_t rbase = (int64_t)t * p.S;
@@ -735,7 +776,7 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
     }
     sl[k] = s;
   }
-  __syncthreads();
+  lds_barrier();  // run starts and s_nu (LDS); the row writes above stay in flight
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     const int q = tid * IPT + k;
@@ -746,6 +787,7 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
     p.bn[t] = make_int2(total, s_nu < 0 ? total : s_nu);
     p.berr[t] = s_err;
   }
+  STAMP(t, tid >> 6, 4);
 }
 
 template <int BS, int MAXB>
@@ -757,6 +799,7 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
   __shared__ typename Scan::storage_type scan_st;
   const int t = blockIdx.x, tid = threadIdx.x, B = p.B, S = p.S;
   const int G = (B + p.opw - 1) / p.opw;
+  STAMP(t, 16 + (tid >> 6), 0);
   const int2 n = p.bn[t];
   const int64_t rbase = (int64_t)t * S;
   // the triplet's occurrence slots, loaded now (k_bplan_sort wrote them): off
@@ -791,6 +834,7 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
     const int32_t row = (int32_t)(k & (side_bit - 1));
     return (k & side_bit) ? p.U1 + row : (int64_t)row;
   };
+  STAMP(t, 16 + (tid >> 6), 1);
 #pragma unroll
   for (int q = 0; q < SPT; ++q)
     if (tid + q * BS < n.x) mw[q] = p.mask[rid_of(key[q]) * p.W + (t >> 6)];
@@ -813,6 +857,7 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
     while (!bits && w < wl) bits = m[++w];
     if (bits) tn[q] = w * 64 + __ffsll((long long)bits) - 1;
   }
+  STAMP(t, 16 + (tid >> 6), 2);
 #pragma unroll
   for (int q = 0; q < SPT; ++q)
     if (tp[q] >= 0) prev_slot[q] = p.slot_of[rid_of(key[q]) * p.nbs + tp[q]];
@@ -829,16 +874,22 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
     p.nextt[rbase + s] = tn[q];
   }
   for (int g = tid; g < G; g += BS) gflag[g] = 0;
-  __syncthreads();
+  lds_barrier();  // info (LDS); the nextt stores stay in flight
   const int gen = p.gen;
+  STAMP(t, 16 + (tid >> 6), 3);
   static_assert(MAXB <= BS, "k_bplan_build: one triplet per thread");
+  // records: formed now (the fused flags feed the task list), stored after it,
+  // so no barrier waits for them
+  OccRec r, ri, rj, q;
+  int64_t ar = 0, ai = 0, aj = 0;  // destinations: >= 0 inline index, < 0 CSR index - 1
+  bool fused = false;
+  int64_t e = 0;
   if (tid < B) {
     const int b = tid;
-    const int64_t e = (int64_t)t * B + b;
+    e = (int64_t)t * B + b;
     const int32_t k = ou & 0xFFFF, ki = oi & 0xFFFF, kj = oj & 0xFFFF;
     const int4 U = info[k], I = info[ki], J = info[kj];
     const FuseInfo f = fuse_info(U, I, J, p.kb);
-    OccRec r;
     r.own_row = U.x;
     r.own_src = U.y;
     r.meta = info_count(U) | (f.fused ? ACF_SINGLE_BIT : 0) | (f.in_u ? ACF_INPLACE_BIT : 0);
@@ -852,29 +903,26 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
     r.pb_slot = kj | (info_count(J) == 1 ? ACF_SOLO_BIT : 0);
     r.gen = gen;
     int32_t rr = ou >> 16;
-    if (rr < p.R) p.inl[(rbase + k) * p.R + rr] = r;
-    else p.urec[U.w + rr] = r;
-    const OccRec ri = item_rec(I, J, U, (int32_t)(2 * e), k, kj, f.fused, f.in_i, gen);
+    ar = rr < p.R ? (rbase + k) * p.R + rr : -1 - ((int64_t)U.w + rr);
+    ri = item_rec(I, J, U, (int32_t)(2 * e), k, kj, f.fused, f.in_i, gen);
     rr = oi >> 16;
-    if (rr < p.R) p.inl[(rbase + ki) * p.R + rr] = ri;
-    else p.irec[I.w + rr] = ri;
-    const OccRec rj = item_rec(J, I, U, (int32_t)(2 * e + 1), k, ki, f.fused, f.in_j, gen);
+    ai = rr < p.R ? (rbase + ki) * p.R + rr : -1 - ((int64_t)I.w + rr);
+    rj = item_rec(J, I, U, (int32_t)(2 * e + 1), k, ki, f.fused, f.in_j, gen);
     rr = oj >> 16;
-    if (rr < p.R) p.inl[(rbase + kj) * p.R + rr] = rj;
-    else p.irec[J.w + rr] = rj;
+    aj = rr < p.R ? (rbase + kj) * p.R + rr : -1 - ((int64_t)J.w + rr);
+    fused = f.fused;
     if (f.fused) {
-      OccRec q;
       q.own_row = U.x; q.own_src = I.x; q.meta = J.x; q.ovf = k;
       q.e_role = ki; q.pa_row = kj; q.pb_row = U.y; q.pa_src = I.y;
       q.pb_src = J.y;
       q.pa_slot = 1 | (f.in_u ? 2 : 0) | (f.in_i ? 4 : 0) | (f.in_j ? 8 : 0);
       q.pb_slot = (int32_t)e; q.gen = gen;
-      p.trec[e] = q;
       single[k] = single[ki] = single[kj] = 1;  // the fused triplet's slots are its own
       gflag[b / p.opw] = 1;
     }
   }
-  __syncthreads();
+  lds_barrier();
+  STAMP(t, 16 + (tid >> 6), 4);
   // task list: the non-fused slots in slot order, then the groups holding a fused triplet
   int32_t base = 0;
   for (int y0 = 0; y0 < S + G; y0 += BS) {
@@ -886,7 +934,14 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
     Scan().exclusive_scan(f, excl, 0, tot, scan_st);
     if (f) p.task_list[(int64_t)t * p.stride + base + excl] = y;
     base += tot;
-    __syncthreads();  // scan storage reuse
+    lds_barrier();  // scan storage reuse
+  }
+  STAMP(t, 16 + (tid >> 6), 5);
+  if (tid < B) {
+    (ar >= 0 ? p.inl[ar] : p.urec[-1 - ar]) = r;
+    (ai >= 0 ? p.inl[ai] : p.irec[-1 - ai]) = ri;
+    (aj >= 0 ? p.inl[aj] : p.irec[-1 - aj]) = rj;
+    if (fused) p.trec[e] = q;
   }
   if (tid == 0) {
     p.task_cnt[t] = base;
@@ -900,6 +955,7 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
   // clear the other bitmap buffer (used by the previous plan), a stripe per batch
   const int64_t w0 = p.clear_words * t / p.nb, w1 = p.clear_words * (t + 1) / p.nb;
   for (int64_t x = w0 + tid; x < w1; x += BS) p.mask_clear[x] = 0ull;
+  STAMP(t, 16 + (tid >> 6), 6);
 }
 
 // ---------------------------------------------------------------------------
@@ -907,32 +963,6 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
 // s_memrealtime stamps (100 MHz) to locate latency inside the step kernels.
 // The product library compiles every STAMP() to nothing.
 // ---------------------------------------------------------------------------
-#ifdef ACF_DIAG
-__device__ uint64_t* g_stamps = nullptr;
-__device__ int g_stamp_launch = 0;
-__device__ int g_stamp_cap = 0;
-#define STAMP(launch, wave, i)                                                       \
-  do {                                                                               \
-    uint64_t t_;                                                                     \
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-    if (g_stamps && (threadIdx.x & 63) == 0 && (wave) < g_stamp_cap)                 \
-      g_stamps[((int64_t)(launch) * g_stamp_cap + (wave)) * 8 + (i)] = t_;          \
-  } while (0)
-#define CLOCKSTAMP(launch, wave, i)                                                  \
-  do {                                                                               \
-    uint64_t t_;                                                                     \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
-    if (g_stamps && (threadIdx.x & 63) == 0 && (wave) < g_stamp_cap)                 \
-      g_stamps[((int64_t)(launch) * g_stamp_cap + (wave)) * 8 + (i)] = t_;          \
-  } while (0)
-#else
-#define CLOCKSTAMP(launch, wave, i) \
-  do {                              \
-  } while (0)
-#define STAMP(launch, wave, i) \
-  do {                         \
-  } while (0)
-#endif
 
 // ---------------------------------------------------------------------------
 // step kernels: one wavefront per unique row ("slot") of the batch.  The 64
