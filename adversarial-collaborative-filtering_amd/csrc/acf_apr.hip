@@ -714,18 +714,29 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
   uint32_t keys[IPT];
   int32_t vals[IPT];
   int err = 0;
+  // all loads first, the range checks after them: a check right behind its load
+  // made the compiler wait for each load in turn (IPT serial round trips)
+  int32_t raw[IPT];
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     const int o = tid * IPT + k;  // occurrence: users [0, B), items B + 2e + role
-    uint32_t key = ~0u;           // padding sorts after every key (stable: after equal ones too)
+    raw[k] = 0;
     if (o < B) {
-      int32_t u = p.user[(int64_t)t * B + o];
-      if (u < 0 || u >= p.U1) { err |= 1; u = 0; }
-      key = (uint32_t)u;
+      raw[k] = p.user[(int64_t)t * B + o];
     } else if (o < S3) {
       const int v = o - B;
-      const int64_t e = (int64_t)t * B + (v >> 1);
-      int32_t x = (v & 1) ? p.ineg[e] : p.ipos[e];
+      raw[k] = ((v & 1) ? p.ineg : p.ipos)[(int64_t)t * B + (v >> 1)];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int o = tid * IPT + k;
+    uint32_t key = ~0u;  // padding sorts after every key (stable: after equal ones too)
+    int32_t x = raw[k];
+    if (o < B) {
+      if (x < 0 || x >= p.U1) { err |= 1; x = 0; }
+      key = (uint32_t)x;
+    } else if (o < S3) {
       if (x < 0 || x >= p.I1) { err |= 2; x = 0; }
       key = side_bit | (uint32_t)x;
     }
@@ -826,8 +837,6 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
       key[q] = p.bkey[rbase + s];
       st[q] = p.bstart[(int64_t)t * (S + 1) + s];
       en[q] = p.bstart[(int64_t)t * (S + 1) + s + 1];
-    } else if (s < S) {
-      p.nextt[rbase + s] = 0;  // no row: never written back
     }
   }
   auto rid_of = [&](uint32_t k) -> int64_t {
@@ -871,7 +880,6 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
     const int32_t ovf = side ? t * 2 * B + st[q] - B : t * B + st[q];
     const int32_t src = tp[q] >= 0 ? make_src(t - tp[q], prev_slot[q], p.kb) : row;
     info[s] = make_int4(row, src, cnt | (tn[q] == t + 1 ? ACF_INFO_NEXT : 0), ovf);
-    p.nextt[rbase + s] = tn[q];
   }
   for (int g = tid; g < G; g += BS) gflag[g] = 0;
   lds_barrier();  // info (LDS); the nextt stores stay in flight
@@ -937,6 +945,13 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
     lds_barrier();  // scan storage reuse
   }
   STAMP(t, 16 + (tid >> 6), 5);
+  // every global store of the kernel from here on: on gfx950 vmcnt counts stores
+  // too, so an earlier store would have held up the loads the phases above wait for
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int s = tid + q * BS;
+    if (s < S) p.nextt[rbase + s] = s < n.x ? tn[q] : 0;  // 0: no row, never written back
+  }
   if (tid < B) {
     (ar >= 0 ? p.inl[ar] : p.urec[-1 - ar]) = r;
     (ai >= 0 ? p.inl[ai] : p.irec[-1 - ai]) = ri;

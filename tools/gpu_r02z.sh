@@ -1,12 +1,11 @@
 # LDS-only barriers in the plan kernels: plan/parity tests, plan diagnostics, short call, 20-step bench
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/r02z
+OUT=gpurun_out/${OUT_TAG:-r02z}
 mkdir -p $OUT
 timeout -k 10 500 python3 -u -m pytest -q -x --timeout 200 --timeout-method thread tests/test_gpu_plan.py tests/test_gpu_parity.py -m gpu > $OUT/pytest.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|assert|Mismatch" $OUT/pytest.log | head -30; tail -5 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
-timeout -k 10 200 python3 tools/diag_plan.py > $OUT/diag_plan.json 2> $OUT/diag_plan.err || { tail -20 $OUT/diag_plan.err; exit 1; }
-cat $OUT/diag_plan.json
+
 timeout -k 10 200 python3 tools/short_call.py --reps 30 > $OUT/sc.json 2> $OUT/sc.err
 python3 -c "
 import json,statistics as st
