@@ -358,6 +358,9 @@ def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
                        "items": big.num_items, "dim": d, "per_gpu_batch": b, "global_batch": b * world,
                        "parallelism": f"user/item row shards x{world}, all_to_all x4 per step"},
             "exchange_bytes_per_step_rank0": int(4 * req * d * 4),
+            # the share that leaves the rank (its own items stay local), averaged over
+            # the whole step: the xGMI egress rate beside the per-GPU HBM fraction (§8(e))
+            "xgmi_egress_GBs_rank0": round(4 * req * d * 4 * (world - 1) / world / (el / steps) / 1e9, 2),
             "items_per_rank_step": round(req, 1),
             "route_ms_rank0": round(1e3 * (sh.stats["route_s"] - st0["route_s"]), 3),
             "step_errors": sh.step_errors()}
