@@ -2531,10 +2531,9 @@ __device__ __forceinline__ float* tri_ci(const StepArgs& a) { return a.contrib +
 // k_tri_adv recomputes their term); 1: BPR (single rows: Adagrad; shared:
 // contributions); 2: APR adversarial.
 template <int LPR, int NV, int PASS>
-__device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
+__device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, const RecV& r, const int4 ps) {
   if (b >= a.B) return;
   const int64_t e = (int64_t)a.t * a.B + b;
-  const RecV r = load_rec(a.trec + e);
   if (r.c.w != *a.gen_ptr) return;
   const int flags = r.c.y;
   // a fused triplet (all three rows single) takes the same code as the others
@@ -2566,7 +2565,6 @@ __device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
     if (!si) di = load_row<LPR, NV>(a.delta, ki, d, l);
     if (!sj) dj = load_row<LPR, NV>(a.delta, kj, d, l);
   }
-  const int4 ps = a.tpos[e];
   const int64_t lu = ps.x - (int64_t)a.t * a.B, li = ps.y - (int64_t)a.t * 2 * a.B,
                 lj = ps.z - (int64_t)a.t * 2 * a.B;
   float* cuB = tri_cu(a);
@@ -2639,6 +2637,25 @@ __device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
     store_row<LPR, NV>(a.accQ, j, d, l, cj);
     store_row<LPR, NV>((flags & 8) ? a.Q : a.wnew_cur, (flags & 8) ? j : kj, d, l, w);
   }
+}
+
+// triplet b's record and CSR positions (loaded together, before the rows)
+__device__ __forceinline__ void tri_rec(const StepArgs& a, int b, RecV& r, int4& ps) {
+  r.a = r.b = r.c = make_int4(0, 0, 0, -1);
+  ps = make_int4(0, 0, 0, 0);
+  if (b < a.B) {
+    const int64_t e = (int64_t)a.t * a.B + b;
+    r = load_rec(a.trec + e);
+    ps = a.tpos[e];
+  }
+}
+
+template <int LPR, int NV, int PASS>
+__device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
+  RecV r;
+  int4 ps;
+  tri_rec(a, b, r, ps);
+  tri_triplet_r<LPR, NV, PASS>(a, b, l, r, ps);
 }
 
 // header of shared slot k: count, side, own row, source, local CSR base
@@ -2753,11 +2770,23 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
   }
 }
 
+// tri_gpw(NV) groups of 64/LPR consecutive triplets per wave (d <= 256: two):
+// both groups' records are loaded up front, so the second group's rows are
+// addressed without another dependent round trip, and the grid runs half as
+// many wave rounds; 4 blocks (16 waves) per CU asked of the register allocator
+__host__ __device__ constexpr int tri_gpw(int nv) { return nv == 1 ? 2 : 1; }
 template <int LPR, int NV>
-__global__ void __launch_bounds__(256) k_tri_adv(StepArgs a) {
+__global__ void __launch_bounds__(256, NV == 1 ? 4 : 1) k_tri_adv(StepArgs a) {
+  constexpr int OPW = 64 / LPR, TRI_GPW = tri_gpw(NV);
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
-  const int lane = threadIdx.x & 63;
-  tri_triplet<LPR, NV, 2>(a, wave * (64 / LPR) + lane / LPR, lane & (LPR - 1));
+  const int lane = threadIdx.x & 63, l = lane & (LPR - 1);
+  const int b0 = wave * TRI_GPW * OPW + lane / LPR;
+  RecV r[TRI_GPW];
+  int4 ps[TRI_GPW];
+#pragma unroll
+  for (int x = 0; x < TRI_GPW; ++x) tri_rec(a, b0 + x * OPW, r[x], ps[x]);
+#pragma unroll
+  for (int x = 0; x < TRI_GPW; ++x) tri_triplet_r<LPR, NV, 2>(a, b0 + x * OPW, l, r[x], ps[x]);
 }
 
 // Flush the pending rows of batch t (wnew_cur) to the tables (end of a call):
@@ -3879,7 +3908,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
         ACF_RET(L(K.tri_clean, a, SW + TWT, 0));
         ACF_RET(L(K.tri_comb[0], a, SW + HW, 5));
         ACF_RET(L(K.hot_clean, ah, 4 * HB, 5));
-        ACF_RET(L(K.tri_adv, a, TWT, 1));
+        ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
         ACF_RET(L(K.tri_comb[2], a, SW + HW, 5));
         ACF_RET(L(K.hot_adv, ah, 4 * HB, 5));
       } else {
