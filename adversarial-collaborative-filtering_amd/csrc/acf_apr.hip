@@ -2650,12 +2650,22 @@ __device__ __forceinline__ void tri_rec(const StepArgs& a, int b, RecV& r, int4&
   }
 }
 
+// tri_gpw(NV) groups of 64/LPR consecutive triplets per wave (d <= 256: two):
+// both groups' records are loaded up front, so the second group's rows are
+// addressed without another dependent round trip, and the grid runs half as
+// many wave rounds
+__host__ __device__ constexpr int tri_gpw(int nv) { return nv == 1 ? 2 : 1; }
+
 template <int LPR, int NV, int PASS>
-__device__ __forceinline__ void tri_triplet(const StepArgs& a, int b, int l) {
-  RecV r;
-  int4 ps;
-  tri_rec(a, b, r, ps);
-  tri_triplet_r<LPR, NV, PASS>(a, b, l, r, ps);
+__device__ __forceinline__ void tri_triplets(const StepArgs& a, int tw, int lane) {
+  constexpr int OPW = 64 / LPR, GPW = tri_gpw(NV);
+  const int b0 = tw * GPW * OPW + lane / LPR;
+  RecV r[GPW];
+  int4 ps[GPW];
+#pragma unroll
+  for (int x = 0; x < GPW; ++x) tri_rec(a, b0 + x * OPW, r[x], ps[x]);
+#pragma unroll
+  for (int x = 0; x < GPW; ++x) tri_triplet_r<LPR, NV, PASS>(a, b0 + x * OPW, lane & (LPR - 1), r[x], ps[x]);
 }
 
 // header of shared slot k: count, side, own row, source, local CSR base
@@ -2725,7 +2735,7 @@ __global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
   if (wave >= a.slot_waves) {
-    tri_triplet<LPR, NV, BPR ? 1 : 0>(a, (wave - a.slot_waves) * (64 / LPR) + g, l);
+    tri_triplets<LPR, NV, BPR ? 1 : 0>(a, wave - a.slot_waves, lane);
     return;
   }
   if (!a.prev_valid) return;  // write-back of the rows batch t-1 left in W scratch
@@ -2770,23 +2780,11 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
   }
 }
 
-// tri_gpw(NV) groups of 64/LPR consecutive triplets per wave (d <= 256: two):
-// both groups' records are loaded up front, so the second group's rows are
-// addressed without another dependent round trip, and the grid runs half as
-// many wave rounds; 4 blocks (16 waves) per CU asked of the register allocator
-__host__ __device__ constexpr int tri_gpw(int nv) { return nv == 1 ? 2 : 1; }
+// k_tri_adv: 4 blocks (16 waves) per CU asked of the register allocator (d <= 256)
 template <int LPR, int NV>
 __global__ void __launch_bounds__(256, NV == 1 ? 4 : 1) k_tri_adv(StepArgs a) {
-  constexpr int OPW = 64 / LPR, TRI_GPW = tri_gpw(NV);
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
-  const int lane = threadIdx.x & 63, l = lane & (LPR - 1);
-  const int b0 = wave * TRI_GPW * OPW + lane / LPR;
-  RecV r[TRI_GPW];
-  int4 ps[TRI_GPW];
-#pragma unroll
-  for (int x = 0; x < TRI_GPW; ++x) tri_rec(a, b0 + x * OPW, r[x], ps[x]);
-#pragma unroll
-  for (int x = 0; x < TRI_GPW; ++x) tri_triplet_r<LPR, NV, 2>(a, b0 + x * OPW, l, r[x], ps[x]);
+  tri_triplets<LPR, NV, 2>(a, wave, threadIdx.x & 63);
 }
 
 // Flush the pending rows of batch t (wnew_cur) to the tables (end of a call):
@@ -3905,14 +3903,14 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
       StepArgs ah = a;
       ah.slot_waves = 4 * HB;
       if (hp->adver) {
-        ACF_RET(L(K.tri_clean, a, SW + TWT, 0));
+        ACF_RET(L(K.tri_clean, a, SW + (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
         ACF_RET(L(K.tri_comb[0], a, SW + HW, 5));
         ACF_RET(L(K.hot_clean, ah, 4 * HB, 5));
         ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
         ACF_RET(L(K.tri_comb[2], a, SW + HW, 5));
         ACF_RET(L(K.hot_adv, ah, 4 * HB, 5));
       } else {
-        ACF_RET(L(K.tri_clean_bpr, a, SW + TWT, 0));
+        ACF_RET(L(K.tri_clean_bpr, a, SW + (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
         ACF_RET(L(K.tri_comb[1], a, SW + HW, 5));
         ACF_RET(L(K.hot_bpr, ah, 4 * HB, 5));
       }
