@@ -256,12 +256,15 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
                                     "source": "out/janEval/ml-1m-sort_apr_..._11_56_42.out:54-55 (UCL CPU, TF1)"}}
 
 
-def large_batch_roofline(acf, ops, dev, ds, d=128, nb=64, chunk=32):
+def large_batch_roofline(acf, ops, dev, ds, d=128, nb=256, chunk=32):
     """BASELINE configs[4] / SURVEY §8(d) "synthetic large" on one GPU: 10M users
     x 5M items (~200M interactions, Zipf items), batch 65,536, triplets from the
     device sampler with its alias-table negatives (equal weights: the reference's
     uniform rule, APR.py:76-78).  Tables (d = 128: 15.4 GB with the Adagrad slots)
-    are far beyond the 256 MB Infinity Cache, so rows come from HBM."""
+    are far beyond the 256 MB Infinity Cache, so rows come from HBM.  256 batches
+    in chunks of 32: the first chunk's plan runs in line, the others beside the
+    previous chunk's step, as in an epoch (3,052 batches) where the in-line plan
+    is amortised."""
     U1, I1, B = ds.num_users + 1, ds.num_items + 1, 65536
     sampler = acf.DeviceSampler(ds, B, dev, seed=7, weights=np.ones(ds.num_items, np.float32))
     ep = sampler.epoch(0)
