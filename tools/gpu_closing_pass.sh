@@ -1,7 +1,7 @@
-# final r02 pass 2: full GPU suite + smoke, bench lines, then rocprofv3 stats + PMC passes
+# closing pass: full GPU suite + smoke, bench lines, then rocprofv3 stats + PMC passes
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/${OUT_TAG:-r02ae}
+OUT=gpurun_out/${OUT_TAG:-closing}
 mkdir -p $OUT
 timeout -k 10 900 python3 -u -m pytest -q --timeout 200 --timeout-method thread tests -m gpu > $OUT/pytest.log 2>&1 || { echo "suite failed"; grep -E "FAILED|Error" $OUT/pytest.log | head -30; tail -5 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log

@@ -1,7 +1,7 @@
 # host enqueue cost of a 20-batch call after the lean PlanPipeline.run path
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/r02w
+OUT=gpurun_out/${OUT_TAG:-short_call}
 mkdir -p $OUT
 timeout -k 10 200 python3 tools/short_call.py --reps 30 > $OUT/sc.json 2> $OUT/sc.err
 python3 -c "
