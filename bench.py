@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--no-sharded", action="store_true",
                    help="skip the split-step lines (SURVEY 8(e): users/items sharded over the ranks)")
     p.add_argument("--sharded-steps", type=int, default=24, help="timed steps of the config-5 split-step line")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="N > 1 code path on a one-GPU box: every rank on cuda:0, gloo (host-staged) "
+                        "instead of RCCL; a rehearsal of the launch, not a measurement")
     p.add_argument("--no-step-overlap", action="store_true",
                    help="two kernels per APR step instead of the overlapped k_ovl (A/B)")
     p.add_argument("--no-stream", action="store_true",
@@ -464,10 +467,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if a.rehearse_one_gpu:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     acf = importlib.import_module(PKG)

@@ -1,0 +1,15 @@
+# bench.py's N > 1 code path (torchrun, barrier, max-over-ranks, rank-0 JSON, the
+# sharded split-step lines at world 2) rehearsed on a one-GPU box: both ranks on
+# cuda:0 over gloo (--rehearse-one-gpu).  The two-kernel step (no k_stream) so the
+# ranks' kernels never wait on waves of each other's persistent launch.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${OUT_TAG:-rehearse_n2}
+mkdir -p $OUT
+timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --rehearse-one-gpu --no-stream --no-step-overlap \
+  --no-large --no-neumf --sharded-steps 4 > $OUT/bench_n2.json 2> $OUT/bench_n2.err
+python3 -c "
+import json;d=json.loads(open('$OUT/bench_n2.json').read().strip().splitlines()[-1])
+print('n_gpus', d['n_gpus'], 'value', d['value'], 'step_errors', d['step_errors'], 'parallelism', d['config']['parallelism'])
+for k, v in d.get('sharded', {}).items(): print(k, v.get('n_gpus'), v.get('value'), v.get('config', {}).get('parallelism'))"
