@@ -22,6 +22,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 
@@ -67,7 +68,10 @@ acf_apr_hparams hparams(double lr, double eps, double reg, double reg_adv, bool 
 }
 
 // contexts (plan workspace + version buffers) by (device, tables, batch shape);
-// one MF graph owns one in the reference (APR.py:197-202)
+// one MF graph owns one in the reference (APR.py:197-202).  A context is shared
+// (reference-counted) and carries its own lock, held for a whole
+// train / copy_losses / step_errors sequence, so a concurrent call that evicts
+// it from the cache cannot destroy it under a running op.
 struct CtxKey {
   int dev;
   int64_t U1, I1;
@@ -76,22 +80,59 @@ struct CtxKey {
     return std::tie(dev, U1, I1, d, B, nb) < std::tie(o.dev, o.U1, o.I1, o.d, o.B, o.nb);
   }
 };
+struct Ctx {
+  acf_apr_ctx* c = nullptr;
+  std::mutex mu;
+  ~Ctx() {
+    if (c) acf_apr_destroy(c);
+  }
+};
+struct Entry {
+  std::shared_ptr<Ctx> ctx;
+  uint64_t last_use;
+};
 std::mutex g_mu;
-std::map<CtxKey, acf_apr_ctx*> g_ctx;
+std::map<CtxKey, Entry> g_ctx;
+uint64_t g_clock = 0;
+constexpr size_t kMaxContexts = 8;
 
-acf_apr_ctx* context(const at::Tensor& P, const at::Tensor& Q, int32_t B, int32_t nb) {
+std::shared_ptr<Ctx> context(const at::Tensor& P, const at::Tensor& Q, int32_t B, int32_t nb) {
   const CtxKey k{P.device().index(), P.size(0), Q.size(0), (int32_t)P.size(1), B, nb};
   std::lock_guard<std::mutex> lock(g_mu);
   auto it = g_ctx.find(k);
-  if (it != g_ctx.end()) return it->second;
-  if (g_ctx.size() >= 8) {  // bounded: drop the oldest key's context
-    acf_apr_destroy(g_ctx.begin()->second);
-    g_ctx.erase(g_ctx.begin());
+  if (it != g_ctx.end()) {
+    it->second.last_use = ++g_clock;
+    return it->second.ctx;
   }
-  acf_apr_ctx* c = nullptr;
-  ok(acf_apr_create(&c, k.U1, k.I1, k.d, B, nb), "acf_apr_create");
-  g_ctx.emplace(k, c);
-  return c;
+  if (g_ctx.size() >= kMaxContexts) {  // bounded: drop the least recently used context
+    auto lru = g_ctx.begin();
+    for (auto e = g_ctx.begin(); e != g_ctx.end(); ++e)
+      if (e->second.last_use < lru->second.last_use) lru = e;
+    g_ctx.erase(lru);  // destroyed when the last running op lets go of it
+  }
+  auto h = std::make_shared<Ctx>();
+  ok(acf_apr_create(&h->c, k.U1, k.I1, k.d, B, nb), "acf_apr_create");
+  g_ctx.emplace(k, Entry{h, ++g_clock});
+  return h;
+}
+
+// releases every cached context (plan workspace and k_stream version buffers,
+// linear in d and batches per call); contexts still in use by a running op are
+// destroyed when it returns.  Returns how many were dropped from the cache.
+int64_t release_contexts() {
+  std::lock_guard<std::mutex> lock(g_mu);
+  const int64_t n = (int64_t)g_ctx.size();
+  g_ctx.clear();
+  return n;
+}
+
+// an index tensor must lie in [0, rows): TF Gather's InvalidArgument, checked
+// before any kernel reads a row through it (one aminmax + one host sync)
+void check_range(const at::Tensor& idx, int64_t rows, const char* name) {
+  if (idx.numel() == 0) return;
+  auto mm = idx.aminmax();
+  const int64_t lo = std::get<0>(mm).item<int64_t>(), hi = std::get<1>(mm).item<int64_t>();
+  TORCH_CHECK_INDEX(lo >= 0 && hi < rows, name, ": index ", lo < 0 ? lo : hi, " is outside [0, ", rows, ")");
 }
 
 void check_tables(const at::Tensor& P, const at::Tensor& Q, const at::Tensor& aP, const at::Tensor& aQ) {
@@ -115,7 +156,9 @@ std::tuple<at::Tensor, at::Tensor> train(at::Tensor& P, at::Tensor& Q, at::Tenso
   TORCH_CHECK(i.numel() == n && j.numel() == n, "triplet lengths differ");
   TORCH_CHECK(B > 0 && n > 0 && n % B == 0, n, " triplets is not a positive multiple of batch_size ", B);
   const int32_t nb = (int32_t)(n / B);
-  acf_apr_ctx* c = context(P, Q, (int32_t)B, nb);
+  std::shared_ptr<Ctx> held = context(P, Q, (int32_t)B, nb);
+  std::lock_guard<std::mutex> ctx_lock(held->mu);
+  acf_apr_ctx* c = held->c;
   acf_apr_tables tb{P.data_ptr<float>(), Q.data_ptr<float>(), aP.data_ptr<float>(), aQ.data_ptr<float>()};
   const acf_apr_hparams h = hparams(lr, eps, reg, reg_adv, adver, clip_lo, clip_hi);
   void* s = stream_of(P);
@@ -143,6 +186,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bpr_apr_step(at::Tensor& P, at::T
   at::Tensor uu = idx32(u, "user", P), ii = idx32(i, "item_pos", P), jj = idx32(j, "item_neg", P);
   const int64_t B = uu.numel();
   TORCH_CHECK(B > 0 && ii.numel() == B && jj.numel() == B, "user / item_pos / item_neg must be equal, non-empty");
+  // the forward below gathers rows before train()'s device-side check runs
+  check_range(uu, P.size(0), "user");
+  check_range(ii, Q.size(0), "item_pos");
+  check_range(jj, Q.size(0), "item_neg");
   // pairwise accuracy of the batch (training_loss_acc's ACC, utils.py:159-175) before the step
   at::Tensor corr = at::empty({1}, P.options().dtype(at::kInt));
   ok(acf_bpr_forward(P.data_ptr<float>(), Q.data_ptr<float>(), P.size(0), Q.size(0), (int32_t)P.size(1),
@@ -164,6 +211,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
   at::Tensor u = idx32(u_, "user", P), i = idx32(i_, "item_pos", P), j = idx32(j_, "item_neg", P);
   const int64_t n = u.numel(), d = P.size(1);
   TORCH_CHECK(i.numel() == n && j.numel() == n, "triplet lengths differ");
+  check_range(u, P.size(0), "user");
+  check_range(i, Q.size(0), "item_pos");
+  check_range(j, Q.size(0), "item_neg");
   at::Tensor loss = at::empty({n}, P.options()), x = at::empty({n}, P.options());
   at::Tensor pi = at::empty({2 * n}, u.options()), qi = at::empty({2 * n}, u.options());
   at::Tensor pv = at::empty({2 * n, d}, P.options()), qv = at::empty({2 * n, d}, P.options());
@@ -220,6 +270,7 @@ void sparse_adagrad_apply(at::Tensor& W, at::Tensor& acc, const at::Tensor& idx_
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
   at::Tensor idx = idx32(idx_, "unique indices", W);
   TORCH_CHECK(g.size(0) == idx.numel() && g.size(1) == W.size(1), "g_rows must be [len(indices), dim]");
+  check_range(idx, W.size(0), "unique indices");
   ok(acf_sparse_adagrad_apply(W.data_ptr<float>(), acc.data_ptr<float>(), W.size(0), (int32_t)W.size(1),
                               idx.data_ptr<int32_t>(), g.data_ptr<float>(), idx.numel(), (float)lr, stream_of(W)),
      "acf_sparse_adagrad_apply");
@@ -235,6 +286,9 @@ at::Tensor score_rank(const at::Tensor& P, const at::Tensor& Q, const at::Tensor
   need(cand_off, "cand_off", at::kLong, 1);
   TORCH_CHECK(cand_off.numel() == users.numel() + 1 && tests.numel() == users.numel(),
               "cand_off must have len(users) + 1 entries and test_items len(users)");
+  check_range(users, P.size(0), "users");
+  check_range(tests, Q.size(0), "test_items");
+  check_range(cands, Q.size(0), "cand_items");
   if (cands.numel() == 0) cands = at::zeros({1}, users.options());
   at::Tensor pos = at::empty({users.numel()}, users.options());
   ok(acf_eval_positions_list(P.data_ptr<float>(), Q.data_ptr<float>(), P.size(0), Q.size(0), (int32_t)P.size(1),
@@ -257,6 +311,9 @@ at::Tensor score_rank_all(const at::Tensor& P, const at::Tensor& Q, const at::Te
   TORCH_CHECK(excl_off.numel() == users.numel() + 1 && tests.numel() == users.numel(),
               "excl_off must have len(users) + 1 entries and test_items len(users)");
   TORCH_CHECK(num_candidates >= 0 && num_candidates <= Q.size(0), "num_candidates exceeds item rows");
+  check_range(users, P.size(0), "users");
+  check_range(tests, Q.size(0), "test_items");
+  check_range(excl, Q.size(0), "excl_items");
   if (excl.numel() == 0) excl = at::zeros({1}, users.options());
   at::Tensor pos = at::empty({users.numel()}, users.options());
   ok(acf_eval_positions_all(P.data_ptr<float>(), Q.data_ptr<float>(), P.size(0), Q.size(0), (int32_t)P.size(1),
@@ -284,6 +341,7 @@ TORCH_LIBRARY(acf, m) {
   m.def("sparse_adagrad_apply(Tensor(a!) W, Tensor(b!) acc, Tensor uniq_idx, Tensor g_rows, float lr) -> ()");
   m.def("score_rank(Tensor P, Tensor Q, Tensor users, Tensor test_items, Tensor cand_off, Tensor cand_items) "
         "-> Tensor");
+  m.def("release_contexts() -> int", &release_contexts);
   m.def("score_rank_all(Tensor P, Tensor Q, Tensor users, Tensor test_items, int num_candidates, "
         "Tensor excl_off, Tensor excl_items) -> Tensor");
 }

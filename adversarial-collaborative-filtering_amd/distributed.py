@@ -150,10 +150,14 @@ class ShardedAPR:
         if u.numel() != T * B:
             raise ValueError(f"{u.numel()} triplets for {T} batches of {B}")
         # index checks, read with the chunk's host copy below (no extra sync):
-        # bit 0 out of range (TF Gather's InvalidArgument), bit 1 another rank's user (routed)
+        # bit 0 out of range (TF Gather's InvalidArgument), bit 1 another rank's user (routed).
+        # Every rank's flags travel with the first exchange, so all ranks raise together
+        # (a rank raising alone would leave its peers waiting in the next collective).
         bad = ((u < 0) | (u >= self.U1) | (i < 0) | (i >= I1) | (j < 0) | (j >= I1)).any().long()
         if self.routed:
             bad = bad + 2 * (u % G != r).any().long()
+        # clamp so that the routing below stays in range on bad input (it is discarded)
+        u, i, j = u.clamp(0, self.U1 - 1), i.clamp(0, I1 - 1), j.clamp(0, I1 - 1)
         c = _Chunk()
         c.T = T
         # this rank's triplets, stream order
@@ -176,16 +180,21 @@ class ShardedAPR:
         # the requests of the whole chunk, owner-major, in one exchange
         order = torch.argsort((wown * T + wstep) * I1 + wid)
         req = (wid // G)[order]
-        rc = torch.empty_like(cnt.t().contiguous())
-        self._a2a(rc.view(-1), cnt.t().contiguous().view(-1), [T] * G, [T] * G)
-        host = torch.cat([cnt.reshape(-1), rc.reshape(-1), nloc, bad.reshape(1)]).cpu().numpy()  # one sync
-        if host[-1] & 1:
-            raise IndexError("triplet index outside the sharded tables")
-        if host[-1] & 2:
-            raise ValueError("train_routed: a triplet of another rank's user")
+        # split sizes (T per owner) + this rank's error flags, to every rank in one exchange
+        send = torch.cat([cnt.t(), bad.reshape(1, 1).expand(G, 1)], 1).contiguous()
+        recv = torch.empty_like(send)
+        self._a2a(recv.view(-1), send.view(-1), [T + 1] * G, [T + 1] * G)
+        rc = recv[:, :T]
+        host = torch.cat([cnt.reshape(-1), rc.reshape(-1), nloc, recv[:, T]]).cpu().numpy()  # one sync
+        flags = host[-G:]
+        if flags.any():
+            who = [o for o in range(G) if flags[o]]
+            if np.bitwise_or.reduce(flags) & 1:
+                raise IndexError(f"triplet index outside the sharded tables (rank(s) {who})")
+            raise ValueError(f"train_routed: a triplet of another rank's user (rank(s) {who})")
         c.cnt = host[: T * G].reshape(T, G)           # my requests per (step, owner)
         c.rc = host[T * G: 2 * T * G].reshape(G, T)   # requests to me per (requester, step)
-        c.nloc = host[2 * T * G: -1]
+        c.nloc = host[2 * T * G: -G]
         rows = torch.empty(int(c.rc.sum()), dtype=req.dtype, device=dev)
         self._a2a(rows, req, c.rc.sum(1).tolist(), c.cnt.sum(0).tolist())
         # received rows in per-step all_to_all order: step, then requester, then id

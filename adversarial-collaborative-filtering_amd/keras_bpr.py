@@ -83,12 +83,18 @@ class BPR(Recommender):
             coo = train.tocoo()
             u, i = np.asarray(coo.row, np.int64), np.asarray(coo.col, np.int64)
         member = np.unique(u * self.iNum + i)
+        # the reference redraws until the negative is valid (BPR.py:90-92); a user whose
+        # pairs cover every item of [1, iNum) would make it loop forever: refuse instead
+        mu = member // self.iNum
+        per_user = np.bincount(mu[(member % self.iNum) >= 1], minlength=int(u.max(initial=0)) + 1)
+        if len(u) and (per_user[u] >= self.iNum - 1).any():
+            raise ValueError("get_train_instances: a user has every item of [1, iNum) as a training pair, "
+                             "so no negative exists for it")
         j = self._rng.randint(1, self.iNum, size=len(u)).astype(np.int64)
-        for _ in range(10000):
-            bad = np.isin(u * self.iNum + j, member)
-            if not bad.any():
-                break
+        bad = np.isin(u * self.iNum + j, member)
+        while bad.any():
             j[bad] = self._rng.randint(1, self.iNum, size=int(bad.sum()))
+            bad = np.isin(u * self.iNum + j, member)
         return [u.astype(np.int32), i.astype(np.int32), j.astype(np.int32)], np.ones(len(u), dtype=np.int64)
 
     def train(self, x_train, y_train, batch_size):

@@ -12,7 +12,10 @@ SURVEY.md §8(b) proposes:
 - decomposed, one TF op each: ``gather_bpr_fwd_bwd`` (APR.py:121-150,183),
   ``row_segment_sum`` (IndexedSlices dedup, APR.py:183-187,195), ``l2norm_perturb``
   (APR.py:186-191), ``sparse_adagrad_apply`` (APR.py:193-195);
-- evaluation: ``score_rank`` / ``score_rank_all`` (_eval_by_user, utils.py:211-254).
+- evaluation: ``score_rank`` / ``score_rank_all`` (_eval_by_user, utils.py:211-254);
+- ``release_contexts() -> int``: frees the cached step contexts (plan workspace and
+  the streamed step's version buffers) that ``apr_train`` / ``bpr_apr_step`` keep per
+  (device, table shape, batch shape).
 
 There is no CPU kernel: calling an op on CPU tensors raises (no fallback).
 """
@@ -25,7 +28,8 @@ import torch
 
 LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libacf_torch.so")
 OPS = ("bpr_apr_step", "apr_train", "gather_bpr_fwd_bwd", "row_segment_sum", "l2norm_perturb",
-       "sparse_adagrad_apply", "score_rank", "score_rank_all")
+       "sparse_adagrad_apply", "score_rank", "score_rank_all",
+       "release_contexts")
 _lock = threading.Lock()
 _loaded = False
 

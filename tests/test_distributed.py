@@ -80,3 +80,48 @@ def test_split_step_equals_single_process(tmp_path, oracle, fp32_parity, world, 
     assert sum(int(s[0]) for s in per_rank) == NB * B
     for r, s in enumerate(per_rank):
         assert int(s[0]) == int(np.sum(u % world == r)) and int(s[1]) == NB
+
+
+def _bad_worker(rank, world, port, out_dir, kind):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from apr_oracle import HParams
+    from shard_oracle import OracleShardLocal
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D_ = importlib.import_module(PKG + ".distributed")
+    P, Q, u, i, j = _problem()
+    if kind == "routed":  # each rank holds its own users' triplets; rank 1 slips in a foreign one
+        sel = np.nonzero(u % world == rank)[0][: B // world * NB]
+        u, i, j = u[sel].copy(), i[sel].copy(), j[sel].copy()
+        if rank == 1:
+            u[5] = 0  # user 0 lives on rank 0
+        sh = D_.ShardedAPR(U1, I1, D, B, init_P=P, init_Q=Q, local=OracleShardLocal, local_batch=B // world)
+        run = lambda: sh.train_routed(u, i, j, HParams(adver=1), chunk=CHUNK)
+    else:  # the same global stream on every rank, corrupted on rank 1 only
+        if rank == 1:
+            {"neg": u, "item": i, "neg_item": j}[kind][7] = -3 if kind != "item" else I1
+        sh = D_.ShardedAPR(U1, I1, D, B, init_P=P, init_Q=Q, local=OracleShardLocal)
+        run = lambda: sh.train(u, i, j, HParams(adver=1), chunk=CHUNK)
+    try:
+        run()
+        res = "ok"
+    except (IndexError, ValueError) as e:
+        res = type(e).__name__
+    with open(os.path.join(out_dir, f"res{rank}.txt"), "w") as f:
+        f.write(res)
+    dist.barrier()  # reached by every rank: nobody is left waiting in a collective
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("kind,want", [("neg", "IndexError"), ("item", "IndexError"), ("neg_item", "IndexError"),
+                                       ("routed", "ValueError")])
+def test_bad_triplet_on_one_rank_raises_on_every_rank(tmp_path, kind, want):
+    """a bad triplet on ONE rank must make EVERY rank raise the same
+    error before any rank enters the next collective (no hang on the peers)."""
+    world = 2
+    mp.spawn(_bad_worker, args=(world, _free_port(), str(tmp_path), kind), nprocs=world, join=True)
+    for r in range(world):
+        with open(os.path.join(tmp_path, f"res{r}.txt")) as f:
+            assert f.read() == want, f"rank {r}"

@@ -74,12 +74,43 @@ def test_apr_train_equals_pipeline(acf_ops, ops, dev):
 
 
 def test_out_of_range_raises(acf_ops, dev):
+    """Every op that gathers through an index checks it first (TF Gather's
+    InvalidArgument): IndexError, no kernel reads the row, the tables are untouched."""
     P = torch.zeros(10, 8, device=dev)
     Q = torch.zeros(10, 8, device=dev)
-    u = torch.tensor([0, 1, 2, 10], dtype=torch.int32, device=dev)
+    aP, aQ = torch.full_like(P, 0.1), torch.full_like(Q, 0.1)
     ok = torch.tensor([0, 1, 2, 3], dtype=torch.int32, device=dev)
-    with pytest.raises(RuntimeError):
-        acf_ops.bpr_apr_step(P, Q, torch.full_like(P, 0.1), torch.full_like(Q, 0.1), u, ok, ok)
+    for bad in ([0, 1, 2, 10], [0, -1, 2, 3], [0, 1, 2, 1 << 30]):
+        b = torch.tensor(bad, dtype=torch.int32, device=dev)
+        for args in ((b, ok, ok), (ok, b, ok), (ok, ok, b)):
+            with pytest.raises(IndexError):
+                acf_ops.bpr_apr_step(P, Q, aP, aQ, *args)
+            with pytest.raises(IndexError):
+                acf_ops.gather_bpr_fwd_bwd(P, Q, *args)
+        with pytest.raises(IndexError):
+            acf_ops.sparse_adagrad_apply(P, aP, b, torch.ones(4, 8, device=dev), 0.05)
+        with pytest.raises(IndexError):
+            acf_ops.score_rank(P, Q, b, ok, torch.tensor([0, 1, 2, 3, 4], device=dev), ok)
+    torch.cuda.synchronize()
+    assert not P.any() and not Q.any() and bool((aP == 0.1).all()) and bool((aQ == 0.1).all())
+
+
+def test_release_contexts(acf_ops, dev):
+    """apr_train caches a context per shape; release_contexts frees them, and the
+    next call builds a fresh one with the same results."""
+    U1, I1, d, B = 50, 40, 16, 64
+    P, Q, u, i, j = _problem(5, U1, I1, d, 2 * B)
+    tu, ti, tj = _dev(u, i, j, dev=dev)
+    outs = []
+    for _ in range(2):
+        a = _dev(P, Q, dev=dev)
+        a += [torch.full_like(a[0], 0.1), torch.full_like(a[1], 0.1)]
+        acf_ops.apr_train(*a, tu, ti, tj, B)
+        outs.append(a)
+        assert acf_ops.release_contexts() >= 1
+    assert acf_ops.release_contexts() == 0
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
 
 
 def test_row_segment_sum_is_tf_unsorted_segment_sum(acf_ops, dev):
