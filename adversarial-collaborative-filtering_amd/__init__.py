@@ -20,6 +20,7 @@ from .evaluate import evaluate, init_eval_model
 from .evaluation import evaluate_apr_mode, evaluate_model
 from .model import MF, Session
 from .neumf import AdversarialNeuMF, NeuMF
+from .fast_adversarial_mf import FastAdversarialMF
 from .recommender import APR, Recommender
 from .sampler import DeviceSampler, EpochTriplets, sampling, shuffle
 from .train import (output_evaluate, prediction2file, training, training_batch, training_loss_acc,
@@ -28,7 +29,7 @@ from .train import (output_evaluate, prediction2file, training, training_batch, 
 _sys.modules.setdefault("acf_amd", _sys.modules[__name__])
 
 __all__ = [
-    "APR", "AdversarialNeuMF", "DeviceDataset", "DeviceSampler", "EpochTriplets", "MF", "NeuMF", "OriginalDataset", "Recommender", "Session",
+    "APR", "AdversarialNeuMF", "DeviceDataset", "FastAdversarialMF", "DeviceSampler", "EpochTriplets", "MF", "NeuMF", "OriginalDataset", "Recommender", "Session",
     "SyntheticDataset", "evaluate", "evaluate_apr_mode", "evaluate_model", "get_dataset", "init_eval_model", "ml1m_like", "output_evaluate",
     "pinterest_like", "prediction2file", "sampling", "shuffle", "synthetic_dataset", "synthetic_large", "training",
     "training_batch", "training_loss_acc", "write2file", "yelp_like",

@@ -167,6 +167,13 @@ NEUMF_SIGNATURES = {
     "acf_kbpr_train": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I64,
                                       ctypes.POINTER(NeuMFHParams), _P, _P]),
     "acf_kbpr_predict": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P]),
+    "acf_amf_param_count": (_I64, [_I64, _I64, _I32]),
+    "acf_amf_create": (ctypes.c_int, [ctypes.POINTER(_P), _I64, _I64, _I32, _I32]),
+    "acf_amf_destroy": (ctypes.c_int, [_P]),
+    "acf_amf_grad": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _P]),
+    "acf_amf_train": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I64,
+                                     ctypes.POINTER(NeuMFHParams), _P, _P]),
+    "acf_amf_predict": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P]),
 }
 
 _neumf = None

@@ -1086,3 +1086,352 @@ extern "C" int acf_kbpr_predict(acf_kbpr_ctx* c, const float* P, const int32_t* 
             (herr & 2) ? "item >= num_item_rows" : "");
   return ACF_OK;
 }
+
+// ---------------------------------------------------------------------------
+// FastAdversarialMF (FastAdversarialMF.py:13-144; run.py --model amf2).
+// params = [P (U1 x d) | Q (I1 x d) | D_u | D_i], a discriminator block being
+// [W1 (d x d, Keras [in, out]) | b1 (d) | W2 (d) | b2 (1) | 3 pad]; gradient and
+// Adam moments in the same layout.  Per batch of B instances (u, i, y) with the
+// adversarial indices (ua, ia) and the players' popularity targets:
+//   pred = P[u] . Q[i]; MSE vs y                                   (:48, :74)
+//   D(e) = sigmoid(relu(e W1 + b1) . W2 + b2) on e = P[ua] / Q[ia]  (:119-127)
+//   player mf (P, Q): MSE + BCE(D_u, tu) + BCE(D_i, ti), the discriminators
+//   frozen; players disc_u / disc_i: BCE(D, du) / BCE(D, di), the embeddings
+//   frozen; all at the same pre-step parameters (AdversarialOptimizerSimultaneous),
+//   then one dense Keras Adam over the whole buffer (every player steps each batch).
+// Kernels: k_amf_inst (one lane-group per instance: gathers, MSE, both
+// discriminators forward and backward, row contributions + the per-instance
+// factors of the weight gradients), k_amf_rows (per-row sums in occurrence
+// order: P gets the u then the ua gathers, Q the i then the ia gathers),
+// k_amf_wgrad (one thread per discriminator parameter, instances in order),
+// k_nmf_adam.  Parity with the reference is unpinned (oracle/amf_oracle.py).
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ int64_t amf_disc_block(int64_t d) { return d * d + 2 * d + 4; }
+
+#define ACF_RET_NEUMF(x)         \
+  do {                           \
+    int r_ = (x);                \
+    if (r_ != ACF_OK) return r_; \
+  } while (0)
+
+struct AmfArgs {
+  const float* params;
+  float* grad;
+  const int32_t *u, *i, *ua, *ia;
+  const float *y, *tu, *ti, *du, *di;
+  int32_t B, d;
+  int64_t U1, I1;
+  float* contrib;  // [B][4][d]: MSE -> P[u], MSE -> Q[i], D_u -> P[ua], D_i -> Q[ia]
+  float* dscr;     // [2][B][3d + 4]: e, relu'(h) * dz_d * W2, relu(h), dz_d
+  float* loss;     // [B][3]: squared error, BCE(D_u, tu), BCE(D_i, ti)
+  int32_t* err;
+};
+
+__device__ __forceinline__ float4 f4_or0(const float* p, bool on) {
+  return on ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int LPR>
+__global__ void __launch_bounds__(256) k_amf_inst(AmfArgs a) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = (int)(gid / LPR), l = (int)(threadIdx.x & (LPR - 1));
+  if (b >= a.B) return;
+  const int d = a.d;
+  int32_t ru = a.u[b], ri = a.i[b], rua = a.ua[b], ria = a.ia[b];
+  if (l == 0 && (ru < 0 || ru >= a.U1 || rua < 0 || rua >= a.U1)) atomicOr(a.err, 1);
+  if (l == 0 && (ri < 0 || ri >= a.I1 || ria < 0 || ria >= a.I1)) atomicOr(a.err, 2);
+  ru = (ru < 0 || ru >= a.U1) ? 0 : ru;
+  rua = (rua < 0 || rua >= a.U1) ? 0 : rua;
+  ri = (ri < 0 || ri >= a.I1) ? 0 : ri;
+  ria = (ria < 0 || ria >= a.I1) ? 0 : ria;
+  const float* P = a.params;
+  const float* Q = P + a.U1 * (int64_t)d;
+  const bool on = l * 4 < d;
+  const float invB = 1.0f / (float)a.B;
+  // prediction and MSE (the Dot layer's gradient: dpred * the other row)
+  const float4 pu = f4_or0(P + (int64_t)ru * d + 4 * l, on), qi = f4_or0(Q + (int64_t)ri * d + 4 * l, on);
+  const float pred = kb_sum<LPR>(pu.x * qi.x + pu.y * qi.y + pu.z * qi.z + pu.w * qi.w);
+  const float diff = pred - a.y[b];
+  if (l == 0) a.loss[(int64_t)b * 3] = diff * diff;
+  const float dpred = (diff * 2.0f) * invB;  // mean's 1/B times SquareGrad's 2x
+  float* c = a.contrib + (int64_t)b * 4 * d + 4 * l;
+  if (on) {
+    *reinterpret_cast<float4*>(c) = make_float4(dpred * qi.x, dpred * qi.y, dpred * qi.z, dpred * qi.w);
+    *reinterpret_cast<float4*>(c + d) = make_float4(dpred * pu.x, dpred * pu.y, dpred * pu.z, dpred * pu.w);
+  }
+  const float* const D0 = P + (a.U1 + a.I1) * (int64_t)d;
+#pragma unroll 1
+  for (int X = 0; X < 2; ++X) {
+    const float* W1 = D0 + X * amf_disc_block(d);
+    const float* b1 = W1 + (int64_t)d * d;
+    const float* W2 = b1 + d;
+    const float b2 = W2[d];
+    const float4 e = f4_or0((X ? Q + (int64_t)ria * d : P + (int64_t)rua * d) + 4 * l, on);
+    // h = e W1 + b1: lane l holds outputs 4l..4l+3; e_k broadcast inside the lane-group
+    float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int kk = 0; kk < d / 4; ++kk) {
+      const float ek[4] = {__shfl(e.x, kk, LPR), __shfl(e.y, kk, LPR), __shfl(e.z, kk, LPR),
+                           __shfl(e.w, kk, LPR)};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 w = f4_or0(W1 + (int64_t)(4 * kk + q) * d + 4 * l, on);
+        h.x = fmaf(ek[q], w.x, h.x); h.y = fmaf(ek[q], w.y, h.y);
+        h.z = fmaf(ek[q], w.z, h.z); h.w = fmaf(ek[q], w.w, h.w);
+      }
+    }
+    const float4 bb = f4_or0(b1 + 4 * l, on), w2 = f4_or0(W2 + 4 * l, on);
+    h = make_float4(h.x + bb.x, h.y + bb.y, h.z + bb.z, h.w + bb.w);
+    const float4 act = make_float4(fmaxf(h.x, 0.f), fmaxf(h.y, 0.f), fmaxf(h.z, 0.f), fmaxf(h.w, 0.f));
+    const float z = kb_sum<LPR>(act.x * w2.x + act.y * w2.y + act.z * w2.z + act.w * w2.w) + b2;
+    const float s = 1.0f / (1.0f + expf(-z));
+    const bool inside = s >= 1e-7f && s <= 1.0f - 1e-7f;  // clip_by_value's gradient
+    const float tm = (X ? a.ti : a.tu)[b], td = (X ? a.di : a.du)[b];
+    if (l == 0) {
+      const float sc = fminf(fmaxf(s, 1e-7f), 1.0f - 1e-7f);
+      a.loss[(int64_t)b * 3 + 1 + X] = -(tm * logf(sc) + (1.0f - tm) * logf(1.0f - sc));
+    }
+    const float dzm = inside ? (s - tm) * invB : 0.f, dzd = inside ? (s - td) * invB : 0.f;
+    const float4 dhm = make_float4(h.x > 0.f ? dzm * w2.x : 0.f, h.y > 0.f ? dzm * w2.y : 0.f,
+                                   h.z > 0.f ? dzm * w2.z : 0.f, h.w > 0.f ? dzm * w2.w : 0.f);
+    // de = W1 dh_m: lane l holds rows 4l..4l+3 of W1, dh_m broadcast
+    float4 de = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int nn = 0; nn < d / 4; ++nn) {
+      const float4 g = make_float4(__shfl(dhm.x, nn, LPR), __shfl(dhm.y, nn, LPR), __shfl(dhm.z, nn, LPR),
+                                   __shfl(dhm.w, nn, LPR));
+      float* dst[4] = {&de.x, &de.y, &de.z, &de.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 w = f4_or0(W1 + (int64_t)(4 * l + q) * d + 4 * nn, on);
+        float acc = *dst[q];
+        acc = fmaf(w.x, g.x, acc); acc = fmaf(w.y, g.y, acc);
+        acc = fmaf(w.z, g.z, acc); acc = fmaf(w.w, g.w, acc);
+        *dst[q] = acc;
+      }
+    }
+    if (on) {
+      *reinterpret_cast<float4*>(c + (2 + X) * d) = de;
+      float* sc = a.dscr + ((int64_t)X * a.B + b) * (3 * d + 4);
+      *reinterpret_cast<float4*>(sc + 4 * l) = e;
+      *reinterpret_cast<float4*>(sc + d + 4 * l) =
+          make_float4(h.x > 0.f ? dzd * w2.x : 0.f, h.y > 0.f ? dzd * w2.y : 0.f, h.z > 0.f ? dzd * w2.z : 0.f,
+                      h.w > 0.f ? dzd * w2.w : 0.f);
+      *reinterpret_cast<float4*>(sc + 2 * d + 4 * l) = act;
+      if (l == 0) sc[3 * d] = dzd;
+    }
+  }
+}
+
+// one wave per gathered row occurrence, 4B of them: P's [u_0..u_{B-1}, ua_0..],
+// then Q's [i_0.., ia_0..].  The first occurrence of a row owns it and adds every
+// occurrence's contribution in that order.
+__global__ void __launch_bounds__(256) k_amf_rows(AmfArgs a) {
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int B = a.B, d = a.d;
+  if (wave >= 4 * (int64_t)B) return;
+  const bool item = wave >= 2 * B;
+  const int me = (int)(item ? wave - 2 * B : wave), n = 2 * B;
+  auto row_of = [&](int k) -> int32_t {
+    int32_t r = item ? (k < B ? a.i[k] : a.ia[k - B]) : (k < B ? a.u[k] : a.ua[k - B]);
+    const int64_t rows = item ? a.I1 : a.U1;
+    return (r < 0 || r >= rows) ? 0 : r;
+  };
+  auto contrib_of = [&](int k) -> const float* {
+    const int b = k < B ? k : k - B, slot = (k < B ? 0 : 2) + (item ? 1 : 0);
+    return a.contrib + ((int64_t)b * 4 + slot) * d;
+  };
+  const int32_t r = row_of(me);
+  for (int base = 0; base < me; base += 64) {
+    const int k = base + lane;
+    if (__any(k < me && row_of(k) == r)) return;
+  }
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int base = me; base < n; base += 64) {
+    const int k = base + lane;
+    uint64_t mask = __ballot(k < n && row_of(k) == r);
+    while (mask) {
+      const int kk = base + __ffsll((unsigned long long)mask) - 1;
+      mask &= mask - 1;
+      const float* cc = contrib_of(kk);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (lane + 64 * q < d) acc[q] = acc[q] + cc[lane + 64 * q];
+    }
+  }
+  float* g = a.grad + (item ? a.U1 * (int64_t)d : 0) + (int64_t)r * d;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (lane + 64 * q < d) g[lane + 64 * q] = g[lane + 64 * q] + acc[q];
+}
+
+// one thread per discriminator parameter: W1[k][n] = sum_b e_b[k] dh_b[n],
+// b1 = sum_b dh_b, W2 = sum_b relu(h_b) dz_b, b2 = sum_b dz_b (instances in order)
+__global__ void __launch_bounds__(256) k_amf_wgrad(AmfArgs a) {
+  const int64_t d = a.d, DB = amf_disc_block(d);
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= 2 * DB) return;
+  const int X = (int)(x / DB);
+  const int64_t j = x - X * DB;
+  const float* sc = a.dscr + (int64_t)X * a.B * (3 * d + 4);
+  const int64_t S = 3 * d + 4;
+  float acc = 0.f;
+  if (j < d * d) {
+    const int64_t k = j / d, n = j - k * d;
+    for (int b = 0; b < a.B; ++b) acc = acc + sc[b * S + k] * sc[b * S + d + n];
+  } else if (j < d * d + d) {
+    const int64_t n = j - d * d;
+    for (int b = 0; b < a.B; ++b) acc = acc + sc[b * S + d + n];
+  } else if (j < d * d + 2 * d) {
+    const int64_t n = j - d * d - d;
+    for (int b = 0; b < a.B; ++b) acc = acc + sc[b * S + 2 * d + n] * sc[b * S + 3 * d];
+  } else if (j == d * d + 2 * d) {
+    for (int b = 0; b < a.B; ++b) acc = acc + sc[b * S + 3 * d];
+  } else {
+    return;  // padding
+  }
+  float* g = a.grad + (a.U1 + a.I1) * d + x;
+  *g = *g + acc;
+}
+
+struct acf_amf_ctx {
+  int64_t U1 = 0, I1 = 0;
+  int32_t d = 0, maxB = 0;
+  float *contrib = nullptr, *dscr = nullptr;
+  int32_t* err = nullptr;
+  std::vector<void*> allocs;
+};
+
+extern "C" int64_t acf_amf_param_count(int64_t U1, int64_t I1, int32_t d) {
+  return (U1 + I1) * (int64_t)d + 2 * amf_disc_block(d);
+}
+
+extern "C" int acf_amf_destroy(acf_amf_ctx* c) {
+  if (!c) return ACF_OK;
+  for (void* p : c->allocs) (void)hipFree(p);
+  delete c;
+  return ACF_OK;
+}
+
+extern "C" int acf_amf_create(acf_amf_ctx** out, int64_t U1, int64_t I1, int32_t d, int32_t maxB) {
+  ACF_CHECK(out != nullptr, ACF_E_INVALID, "out is NULL");
+  *out = nullptr;
+  ACF_CHECK(U1 > 0 && I1 > 0 && U1 < (1ll << 31) && I1 < (1ll << 31), ACF_E_INVALID, "bad table rows");
+  ACF_CHECK(d >= 4 && d <= 256 && d % 4 == 0, ACF_E_INVALID, "dim must be a multiple of 4 in [4, 256], got %d", d);
+  ACF_CHECK(maxB > 0 && maxB <= (1 << 24), ACF_E_INVALID, "max_batch must be in (0, 2^24], got %d", maxB);
+  acf_amf_ctx* c = new acf_amf_ctx();
+  c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB;
+  for (auto pr : {std::make_pair((void**)&c->contrib, (size_t)maxB * 4 * d * 4),
+                  std::make_pair((void**)&c->dscr, (size_t)2 * maxB * (3 * d + 4) * 4),
+                  std::make_pair((void**)&c->err, (size_t)16)}) {
+    if (hipMalloc(pr.first, pr.second) != hipSuccess) {
+      (void)hipGetLastError();
+      acf_amf_destroy(c);
+      return set_error(ACF_E_NOMEM, "hipMalloc of %zu bytes failed", pr.second);
+    }
+    c->allocs.push_back(*pr.first);
+  }
+  if (hipMemset(c->err, 0, 16) != hipSuccess) {
+    acf_amf_destroy(c);
+    return set_error(ACF_E_HIP, "hipMemset failed");
+  }
+  *out = c;
+  return ACF_OK;
+}
+
+template <int LPR>
+static void launch_amf_inst(const AmfArgs& a, hipStream_t s) {
+  k_amf_inst<LPR><<<(unsigned)(((int64_t)a.B * LPR + 255) / 256), 256, 0, s>>>(a);
+}
+
+static int amf_batch(acf_amf_ctx* c, const AmfArgs& a, hipStream_t s) {
+  int lpr = 1;
+  while (lpr * 4 < c->d) lpr <<= 1;
+  switch (lpr) {
+    case 1: launch_amf_inst<1>(a, s); break;
+    case 2: launch_amf_inst<2>(a, s); break;
+    case 4: launch_amf_inst<4>(a, s); break;
+    case 8: launch_amf_inst<8>(a, s); break;
+    case 16: launch_amf_inst<16>(a, s); break;
+    case 32: launch_amf_inst<32>(a, s); break;
+    default: launch_amf_inst<64>(a, s); break;
+  }
+  k_amf_rows<<<(unsigned)((4 * (int64_t)a.B * 64 + 255) / 256), 256, 0, s>>>(a);
+  k_amf_wgrad<<<(unsigned)((2 * amf_disc_block(c->d) + 255) / 256), 256, 0, s>>>(a);
+  HIP_TRY(hipGetLastError());
+  return ACF_OK;
+}
+
+static int amf_read_err(acf_amf_ctx* c, hipStream_t s) {
+  int32_t herr = 0;
+  HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ACF_CHECK(herr == 0, ACF_E_RANGE, "index out of range (%s%s)", (herr & 1) ? "user >= num_user_rows " : "",
+            (herr & 2) ? "item >= num_item_rows" : "");
+  return ACF_OK;
+}
+
+extern "C" int acf_amf_grad(acf_amf_ctx* c, const float* params, float* grad, const int32_t* u, const int32_t* i,
+                            const float* y, const int32_t* ua, const int32_t* ia, const float* tu, const float* ti,
+                            const float* du, const float* di, int32_t B, float* loss, void* stream_) {
+  ACF_CHECK(c && params && grad && u && i && y && ua && ia && tu && ti && du && di && loss, ACF_E_INVALID,
+            "NULL argument");
+  ACF_CHECK(B > 0 && B <= c->maxB, ACF_E_INVALID, "batch %d outside (0, %d]", B, c->maxB);
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  const AmfArgs a{params, grad, u, i, ua, ia, y, tu, ti, du, di, B, c->d, c->U1, c->I1, c->contrib, c->dscr,
+                  loss, c->err};
+  ACF_RET_NEUMF(amf_batch(c, a, s));
+  return amf_read_err(c, s);
+}
+
+extern "C" int acf_amf_train(acf_amf_ctx* c, float* params, float* grad, float* m, float* v, const int32_t* u,
+                             const int32_t* i, const float* y, const int32_t* ua, const int32_t* ia, const float* tu,
+                             const float* ti, const float* du, const float* di, int64_t n, int32_t batch,
+                             int64_t t_first, const acf_neumf_hparams* hp, float* losses, void* stream_) {
+  ACF_CHECK(c && params && grad && m && v && u && i && y && ua && ia && tu && ti && du && di && hp && losses,
+            ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(batch > 0 && batch <= c->maxB, ACF_E_INVALID, "batch %d outside (0, %d]", batch, c->maxB);
+  ACF_CHECK(n >= 0 && t_first >= 1, ACF_E_INVALID, "bad instance count or Adam iteration");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  const int64_t n4 = acf_amf_param_count(c->U1, c->I1, c->d) / 4;
+  const unsigned ga = (unsigned)std::min<int64_t>((n4 + 255) / 256, 256 * 32);
+  int64_t k = 0;
+  for (int64_t o = 0; o < n; o += batch, ++k) {
+    const int32_t B = (int32_t)std::min<int64_t>(batch, n - o);
+    const AmfArgs a{params, grad, u + o, i + o, ua + o, ia + o, y + o, tu + o, ti + o, du + o, di + o,
+                    B, c->d, c->U1, c->I1, c->contrib, c->dscr, losses + 3 * o, c->err};
+    ACF_RET_NEUMF(amf_batch(c, a, s));
+    const float tt = (float)(t_first + k);
+    const float lr_t = hp->lr * (sqrtf(1.0f - powf(hp->beta2, tt)) / (1.0f - powf(hp->beta1, tt)));
+    k_nmf_adam<<<ga, 256, 0, s>>>(reinterpret_cast<float4*>(params), reinterpret_cast<float4*>(grad),
+                                  reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v), n4, hp->beta1,
+                                  hp->beta2, lr_t, hp->adam_eps);
+    HIP_TRY(hipGetLastError());
+  }
+  return amf_read_err(c, s);
+}
+
+// model = Model([user, item], pred) (FastAdversarialMF.py:51; MF.py:38-40): u . i per pair
+extern "C" int acf_amf_predict(acf_amf_ctx* c, const float* params, const int32_t* u, const int32_t* it, int64_t n,
+                               float* out, void* stream_) {
+  ACF_CHECK(c && params && u && it && out, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(n >= 0, ACF_E_INVALID, "negative count");
+  if (n == 0) return ACF_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  int lpr = 1;
+  while (lpr * 4 < c->d) lpr <<= 1;
+  const unsigned g = (unsigned)((n * lpr + 255) / 256);
+  switch (lpr) {
+    case 1: k_kbpr_predict<1><<<g, 256, 0, s>>>(params, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 2: k_kbpr_predict<2><<<g, 256, 0, s>>>(params, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 4: k_kbpr_predict<4><<<g, 256, 0, s>>>(params, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 8: k_kbpr_predict<8><<<g, 256, 0, s>>>(params, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 16: k_kbpr_predict<16><<<g, 256, 0, s>>>(params, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    case 32: k_kbpr_predict<32><<<g, 256, 0, s>>>(params, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+    default: k_kbpr_predict<64><<<g, 256, 0, s>>>(params, u, it, n, c->d, c->U1, c->I1, out, c->err); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return amf_read_err(c, s);
+}

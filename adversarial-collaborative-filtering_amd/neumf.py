@@ -164,6 +164,33 @@ class NeuMFContext:
         return out
 
 
+def mf_train_instances(train, iNum, rng):
+    """MF.py:42-56: per training pair (u, i), in the train matrix's key order, a
+    positive (label 1) and a negative j ~ U[1, iNum) redrawn while (u, j) is a
+    training pair (label 0).  The reference redraws until the negative is valid;
+    a user whose pairs cover all of [1, iNum) has none, and is refused here
+    (the reference would loop forever)."""
+    if hasattr(train, "keys"):
+        pairs = np.array(list(train.keys()), dtype=np.int64).reshape(-1, 2)
+        u, i = pairs[:, 0], pairs[:, 1]
+    else:
+        coo = train.tocoo()
+        u, i = np.asarray(coo.row, np.int64), np.asarray(coo.col, np.int64)
+    keys = np.unique(u * iNum + i)
+    per_user = np.bincount((keys // iNum)[(keys % iNum) >= 1], minlength=int(u.max(initial=0)) + 1)
+    if len(u) and (per_user[u] >= iNum - 1).any():
+        raise ValueError("get_train_instances: a user has every item of [1, iNum) as a training pair")
+    j = rng.randint(1, iNum, size=len(u)).astype(np.int64)
+    bad = np.isin(u * iNum + j, keys)
+    while bad.any():
+        j[bad] = rng.randint(1, iNum, size=int(bad.sum()))
+        bad = np.isin(u * iNum + j, keys)
+    users = np.stack([u, u], 1).reshape(-1)
+    items = np.stack([i, j], 1).reshape(-1)
+    labels = np.tile(np.array([1, 0], dtype=np.int64), len(u))
+    return [users, items], labels
+
+
 class NeuMF:
     """NeuMF.py:10-55 on the GPU, with the run.py Recommender surface."""
 
@@ -195,26 +222,8 @@ class NeuMF:
         return ""
 
     def get_train_instances(self, train):
-        """MF.py:42-56: per training pair (u, i) a positive (label 1) and a negative
-        j ~ U[1, iNum) rejected while (u, j) is a training pair (label 0), in the
-        train matrix's key order."""
-        coo = train.tocoo() if hasattr(train, "tocoo") else train
-        if hasattr(train, "keys"):
-            pairs = np.array(list(train.keys()), dtype=np.int64).reshape(-1, 2)
-            u, i = pairs[:, 0], pairs[:, 1]
-        else:
-            u, i = np.asarray(coo.row, np.int64), np.asarray(coo.col, np.int64)
-        keys = np.unique(u * self.iNum + i)
-        j = self._rng.randint(1, self.iNum, size=len(u)).astype(np.int64)
-        for _ in range(10000):
-            bad = np.isin(u * self.iNum + j, keys)
-            if not bad.any():
-                break
-            j[bad] = self._rng.randint(1, self.iNum, size=int(bad.sum()))
-        users = np.stack([u, u], 1).reshape(-1)
-        items = np.stack([i, j], 1).reshape(-1)
-        labels = np.tile(np.array([1, 0], dtype=np.int64), len(u))
-        return [users, items], labels
+        """MF.py:42-56 (see mf_train_instances)."""
+        return mf_train_instances(train, self.iNum, self._rng)
 
     def train(self, x_train, y_train, batch_size):
         """Keras fit for one epoch (MF.py:30-33): shuffled, batches of batch_size

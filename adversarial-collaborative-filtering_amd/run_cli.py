@@ -10,9 +10,10 @@ Same flags (run.py:25-75) and the same loop: ``getDataset``, the ranker,
 log lines of run.py:117-119,215-280.  Models: ``bpr`` (the Keras BPR of
 BPR.py:23-99, BASELINE configs[0]), ``apr`` / ``bpr-tf`` (the APR graph,
 switching to the adversarial model at ``--adv_epochs``, run.py:157-161,233-236),
-``neumf`` / ``aneumf`` (NeuMF.py:10-55).  The others (SASRec, Caser, GRU4Rec,
-DRCF, DREAM, APL, IRGAN, the discriminator-adversarial MF/BPR and the naive
-baselines) are out of scope and rejected.
+``neumf`` / ``aneumf`` (NeuMF.py:10-55), ``amf2`` (FastAdversarialMF.py:13-144).
+The others (SASRec, Caser, GRU4Rec, DRCF, DREAM, APL, IRGAN, the
+discriminator-adversarial MF/BPR of MF.py / BPR.py and the naive baselines) are
+out of scope and rejected.
 
 Datasets (``getDataset``, utils.py:44-78): the reference's ``Dataset`` class
 (Dataset.py:59-107) cannot run (``df = df.sort_values(..., inplace=True)`` binds
@@ -34,7 +35,7 @@ from time import time
 
 import numpy as np
 
-OUT_OF_SCOPE = {"mf", "amf", "abpr", "amf2", "apl", "irgan", "sasrec", "drcf", "gru4rec", "dream", "dream-tf",
+OUT_OF_SCOPE = {"mf", "amf", "abpr", "apl", "irgan", "sasrec", "drcf", "gru4rec", "dream", "dream-tf",
                 "caser", "pop", "mrv", "mfv", "av"}
 
 
@@ -114,7 +115,7 @@ def get_dataset(data, path, eval_mode, seed=2019):
 def make_ranker(name, uNum, iNum, dim, args, device=None):
     if name in OUT_OF_SCOPE:
         raise SystemExit(f"--model {name}: outside the MI355X build's scope (DESIGN.md §10); "
-                         "supported: bpr, apr, bpr-tf, neumf, aneumf")
+                         "supported: bpr, apr, bpr-tf, neumf, aneumf, amf2")
     if name == "bpr":
         from .keras_bpr import BPR
         return BPR(uNum, iNum, dim, seed=args.seed, device=device)
@@ -127,6 +128,9 @@ def make_ranker(name, uNum, iNum, dim, args, device=None):
     if name == "aneumf":
         from .neumf import AdversarialNeuMF
         return AdversarialNeuMF(uNum, iNum, dim, args.w, args.pp, seed=args.seed, device=device)
+    if name == "amf2":  # run.py:140-141
+        from .fast_adversarial_mf import FastAdversarialMF
+        return FastAdversarialMF(uNum, iNum, dim, args.w, args.pp, seed=args.seed, device=device)
     raise SystemExit(f"--model {name}: unknown model")
 
 

@@ -102,6 +102,47 @@ int acf_kbpr_train(acf_kbpr_ctx* ctx, float* params, float* grad, float* m, floa
 int acf_kbpr_predict(acf_kbpr_ctx* ctx, const float* params, const int32_t* user, const int32_t* item,
                      int64_t n, float* out, void* stream);
 
+/* ---- FastAdversarialMF (FastAdversarialMF.py:13-144): run.py --model amf2 ----
+ * Parameters in one flat fp32 buffer [P (num_user_rows x dim) | Q (num_item_rows x
+ * dim) | D_u | D_i] (acf_amf_param_count floats); a discriminator block (Dense(d,
+ * relu) -> Dense(1, sigmoid), FastAdversarialMF.py:119-127) is [W1 (dim x dim,
+ * Keras [in, out]) | b1 (dim) | W2 (dim) | b2 (1) | 3 pad].  Gradient and Adam
+ * moments share the layout.  A batch holds B instances: (user, item, label) of
+ * MF.py:42-56 and the adversarial indices (user_adv, item_adv) with the players'
+ * popularity targets: t_user / t_item for the mf player, d_user / d_item for the
+ * two discriminator players (FastAdversarialMF.py:89-117).  The three players'
+ * gradients are taken at the same parameters (keras_adversarial's
+ * AdversarialOptimizerSimultaneous): mf = MSE + BCE(D_u(P[ua]), t_user) +
+ * BCE(D_i(Q[ia]), t_item) w.r.t. P, Q; each discriminator its BCE w.r.t. its own
+ * weights.  dim % 4 == 0, dim <= 256.  Replaces the advModel.fit of
+ * FastAdversarialMF.py:115 (parity with the reference unpinned: it does not run). */
+typedef struct acf_amf_ctx acf_amf_ctx;
+int64_t acf_amf_param_count(int64_t num_user_rows, int64_t num_item_rows, int32_t dim);
+int acf_amf_create(acf_amf_ctx** ctx, int64_t num_user_rows, int64_t num_item_rows, int32_t dim,
+                   int32_t max_batch);
+int acf_amf_destroy(acf_amf_ctx* ctx);
+
+/* The three players' gradient of one batch ADDED to grad; loss (device, [B][3]):
+ * squared error, BCE(D_u, t_user), BCE(D_i, t_item) per instance.  Validates the
+ * indices (synchronises; ACF_E_RANGE). */
+int acf_amf_grad(acf_amf_ctx* ctx, const float* params, float* grad, const int32_t* user, const int32_t* item,
+                 const float* label, const int32_t* user_adv, const int32_t* item_adv, const float* t_user,
+                 const float* t_item, const float* d_user, const float* d_item, int32_t batch, float* loss,
+                 void* stream);
+
+/* One Keras fit epoch over n already-shuffled instances: batches of `batch` (the
+ * last one partial), each acf_amf_grad + Keras 2.2 Adam iteration t_first + k over
+ * the whole buffer (grad re-zeroed).  losses (device, [n][3]) as above.  Indices
+ * are validated at the end (ACF_E_RANGE; out-of-range rows were read as row 0). */
+int acf_amf_train(acf_amf_ctx* ctx, float* params, float* grad, float* m, float* v, const int32_t* user,
+                  const int32_t* item, const float* label, const int32_t* user_adv, const int32_t* item_adv,
+                  const float* t_user, const float* t_item, const float* d_user, const float* d_item, int64_t n,
+                  int32_t batch, int64_t t_first, const acf_neumf_hparams* hp, float* losses, void* stream);
+
+/* ranker.rank(users, items) (MF.py:38-40 on FastAdversarialMF.py:51's model): u . i. */
+int acf_amf_predict(acf_amf_ctx* ctx, const float* params, const int32_t* user, const int32_t* item, int64_t n,
+                    float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
