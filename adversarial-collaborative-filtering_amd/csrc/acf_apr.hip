@@ -2883,6 +2883,7 @@ __device__ __forceinline__ float seq_dot(const float* __restrict__ p, const floa
 }
 
 constexpr int EVAL_UB = 8;  // users per workgroup
+static int g_eval_valu = 0;  // acf_eval_set_kernel
 
 __global__ void __launch_bounds__(256) k_eval_all(const float* __restrict__ P,
                                                   const float* __restrict__ Q, int d,
@@ -2944,6 +2945,155 @@ __global__ void __launch_bounds__(256) k_eval_all(const float* __restrict__ P,
   for (int uu = 0; uu < EVAL_UB; ++uu) atomicAdd(&s_cnt[uu], cnt[uu]);
   __syncthreads();
   if (threadIdx.x < nu) positions[u0 + threadIdx.x] = s_cnt[threadIdx.x];
+}
+
+// ---- all-items ranking on MFMA (utils.py:198-267, "all" candidates) ----------
+// The U x I score sweep is a GEMM: v_mfma_f32_16x16x4_f32 tiles of 64 users x 128
+// candidates (4 waves, each 64 users x 32 candidates = 4 x 2 tiles), K staged
+// through LDS in chunks of 32.  The reference's position = #(candidates scoring
+// >= the test item) must stay EXACT for the scores the sequential round-then-add
+// dot (seq_dot, TF's product rounding) gives, including ties.  f32 MFMA is an
+// fmaf chain in k order (MI355X_MICROARCH: bitwise), so both scores are within
+// 2 gamma_d sum|p_k q_k| <= 2 gamma_d |p| |q| of the real dot product; with
+// E = 4 (d + 2) 2^-24 |p| |q| (+ a denormal floor) a candidate with
+// s_mfma - E > t is counted, one with s_mfma + E < t is not, and the rare one in
+// between is rescored with seq_dot and compared exactly.  Positions are
+// therefore bit-identical to k_eval_all's.
+__global__ void __launch_bounds__(256) k_eval_prep(const float* __restrict__ P, const float* __restrict__ Q, int d,
+                                                   const int32_t* __restrict__ users,
+                                                   const int32_t* __restrict__ tests, int n_users, int num_cand,
+                                                   float* __restrict__ tscore, float* __restrict__ pnorm,
+                                                   float* __restrict__ qnorm) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  auto norm = [&](const float* r) {
+    double ss = 0.0;
+    for (int k = 0; k < d; ++k) ss += (double)r[k] * (double)r[k];
+    return (float)(sqrt(ss) * (1.0 + 1e-6));  // rounded up
+  };
+  if (x < n_users) {
+    const float* p = P + (int64_t)users[x] * d;
+    tscore[x] = seq_dot(p, Q + (int64_t)tests[x] * d, d);
+    pnorm[x] = norm(p);
+  }
+  if (x < num_cand) qnorm[x] = norm(Q + x * d);
+}
+
+constexpr int EVM_U = 64, EVM_C = 128, EVM_KC = 32;
+
+__global__ void __launch_bounds__(256) k_eval_mfma(const float* __restrict__ P, const float* __restrict__ Q, int d,
+                                                   const int32_t* __restrict__ users, int n_users, int num_cand,
+                                                   const float* __restrict__ tscore, const float* __restrict__ pnorm,
+                                                   const float* __restrict__ qnorm, float eb, float floor_e,
+                                                   int32_t* __restrict__ positions) {
+  __shared__ float sP[EVM_U][EVM_KC + 1];
+  __shared__ float sQ[EVM_C][EVM_KC + 1];
+  __shared__ int s_cnt[EVM_U];
+  __shared__ float s_t[EVM_U], s_pn[EVM_U];
+  __shared__ int32_t s_row[EVM_U];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63;
+  const int u0 = blockIdx.y * EVM_U, c0 = blockIdx.x * EVM_C;
+  if (tid < EVM_U) {
+    const bool ok = u0 + tid < n_users;
+    s_cnt[tid] = 0;
+    s_row[tid] = ok ? users[u0 + tid] : -1;
+    s_t[tid] = ok ? tscore[u0 + tid] : 0.f;
+    s_pn[tid] = ok ? pnorm[u0 + tid] : 0.f;
+  }
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < d; k0 += EVM_KC) {
+    __syncthreads();  // s_row (first pass) / the previous chunk's reads
+    constexpr int C4 = EVM_KC / 4;
+#pragma unroll
+    for (int j = 0; j < EVM_U * C4 / 256; ++j) {
+      const int idx = tid + 256 * j, row = idx / C4, c4 = idx - row * C4, k = k0 + 4 * c4;
+      const int32_t pr = s_row[row];
+      const float4 v = (pr >= 0 && k < d) ? *reinterpret_cast<const float4*>(P + (int64_t)pr * d + k)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      sP[row][4 * c4] = v.x; sP[row][4 * c4 + 1] = v.y; sP[row][4 * c4 + 2] = v.z; sP[row][4 * c4 + 3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < EVM_C * C4 / 256; ++j) {
+      const int idx = tid + 256 * j, row = idx / C4, c4 = idx - row * C4, k = k0 + 4 * c4;
+      const int cand = c0 + row;
+      const float4 v = (cand < num_cand && k < d) ? *reinterpret_cast<const float4*>(Q + (int64_t)cand * d + k)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      sQ[row][4 * c4] = v.x; sQ[row][4 * c4 + 1] = v.y; sQ[row][4 * c4 + 2] = v.z; sQ[row][4 * c4 + 3] = v.w;
+    }
+    __syncthreads();
+    const int kend = min(EVM_KC, d - k0);
+    for (int kk = 0; kk < kend; kk += 4) {
+      float a[4], b[2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = sP[16 * r + (l & 15)][kk + (l >> 4)];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) b[c] = sQ[wave * 32 + 16 * c + (l & 15)][kk + (l >> 4)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[r], b[c], acc[r][c], 0, 0, 0);
+    }
+  }
+  // epilogue: lane l holds users 16r + 4(l >> 4) + reg, candidate 16c + (l & 15)
+  float qn[2];
+  int cand[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    cand[c] = c0 + wave * 32 + 16 * c + (l & 15);
+    qn[c] = cand[c] < num_cand ? qnorm[cand[c]] : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int ur = 16 * r + 4 * (l >> 4) + reg;
+      int cnt = 0;
+      if (u0 + ur < n_users) {
+        const float t = s_t[ur];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          if (cand[c] >= num_cand) continue;
+          const float sm = acc[r][c][reg];
+          const float e = eb * s_pn[ur] * qn[c] + floor_e;
+          if (sm - e > t) {
+            ++cnt;
+          } else if (sm + e >= t) {  // within the error band: the exact score decides
+            cnt += seq_dot(P + (int64_t)s_row[ur] * d, Q + (int64_t)cand[c] * d, d) >= t ? 1 : 0;
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) cnt += __shfl_xor(cnt, m, 64);
+      if ((l & 15) == 0 && cnt) atomicAdd(&s_cnt[ur], cnt);
+    }
+  }
+  __syncthreads();
+  if (tid < EVM_U && s_cnt[tid]) atomicAdd(positions + u0 + tid, s_cnt[tid]);
+}
+
+// the exclusion correction of k_eval_mfma's counts (trainList[u] and the test
+// item, utils.py:211-215): one wave per user, exact seq_dot scores
+__global__ void __launch_bounds__(256) k_eval_excl(const float* __restrict__ P, const float* __restrict__ Q, int d,
+                                                   const int32_t* __restrict__ users, int n_users, int num_cand,
+                                                   const float* __restrict__ tscore,
+                                                   const int64_t* __restrict__ excl_off,
+                                                   const int32_t* __restrict__ excl, int32_t* __restrict__ positions) {
+  const int64_t w = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int l = threadIdx.x & 63;
+  if (w >= n_users) return;
+  const float* p = P + (int64_t)users[w] * d;
+  const float t = tscore[w];
+  int cnt = 0;
+  for (int64_t x = excl_off[w] + l; x < excl_off[w + 1]; x += 64) {
+    const int32_t it = excl[x];
+    if (it >= 0 && it < num_cand) cnt += seq_dot(p, Q + (int64_t)it * d, d) >= t ? 1 : 0;
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) cnt += __shfl_xor(cnt, m, 64);
+  if (l == 0 && cnt) positions[w] -= cnt;
 }
 
 __global__ void __launch_bounds__(256) k_eval_list(const float* __restrict__ P,
@@ -4356,10 +4506,37 @@ extern "C" int acf_eval_positions_all(const float* P, const float* Q, int64_t U1
   ACF_CHECK(num_cand >= 0 && num_cand <= I1, ACF_E_INVALID, "num_candidates %d > item rows", num_cand);
   if (n_users <= 0) return ACF_OK;
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  const size_t lds = (size_t)EVAL_UB * d * sizeof(float);
-  k_eval_all<<<(n_users + EVAL_UB - 1) / EVAL_UB, 256, lds, s>>>(P, Q, d, users, tests, n_users,
-                                                                  num_cand, excl_off, excl, positions);
+  if (g_eval_valu) {  // the VALU sweep (acf_eval_set_kernel(0): A/B only)
+    const size_t lds = (size_t)EVAL_UB * d * sizeof(float);
+    k_eval_all<<<(n_users + EVAL_UB - 1) / EVAL_UB, 256, lds, s>>>(P, Q, d, users, tests, n_users,
+                                                                    num_cand, excl_off, excl, positions);
+    HIP_TRY(hipGetLastError());
+    return ACF_OK;
+  }
+  float* scr = nullptr;
+  const size_t nf = 2 * (size_t)n_users + (size_t)std::max(num_cand, 1);
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scr), nf * sizeof(float), s));
+  float *tscore = scr, *pnorm = scr + n_users, *qnorm = scr + 2 * (size_t)n_users;
+  HIP_TRY(hipMemsetAsync(positions, 0, (size_t)n_users * sizeof(int32_t), s));
+  k_eval_prep<<<grid_for(std::max<int64_t>(n_users, num_cand)), 256, 0, s>>>(P, Q, d, users, tests, n_users,
+                                                                            num_cand, tscore, pnorm, qnorm);
+  if (num_cand > 0) {
+    const float eb = 4.0f * (float)(d + 2) * 5.9604645e-8f;  // 4 (d + 2) 2^-24
+    const float floor_e = (float)d * 1.1754944e-38f * 4.0f;   // denormal products flushed by MFMA
+    const dim3 grid((unsigned)((num_cand + EVM_C - 1) / EVM_C), (unsigned)((n_users + EVM_U - 1) / EVM_U));
+    k_eval_mfma<<<grid, 256, 0, s>>>(P, Q, d, users, n_users, num_cand, tscore, pnorm, qnorm, eb, floor_e,
+                                     positions);
+  }
+  k_eval_excl<<<grid_for((int64_t)n_users * 64), 256, 0, s>>>(P, Q, d, users, n_users, num_cand, tscore, excl_off,
+                                                               excl, positions);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipFreeAsync(scr, s));
+  return ACF_OK;
+}
+
+// test / A-B only: 1 (default) the MFMA sweep, 0 the VALU sweep k_eval_all
+extern "C" int acf_eval_set_kernel(int32_t mfma) {
+  g_eval_valu = mfma ? 0 : 1;
   return ACF_OK;
 }
 

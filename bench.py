@@ -58,6 +58,7 @@ def parse():
     p.add_argument("--no-large", action="store_true",
                    help="skip the synthetic-large lines (batch 65,536 on 10M x 5M, d = 128 and 64)")
     p.add_argument("--no-neumf", action="store_true", help="skip the adversarial-NeuMF line (configs[3])")
+    p.add_argument("--no-eval", action="store_true", help="skip the all-items evaluation line (SURVEY 8(f)2)")
     p.add_argument("--no-sharded", action="store_true",
                    help="skip the split-step lines (SURVEY 8(e): users/items sharded over the ranks)")
     p.add_argument("--sharded-steps", type=int, default=24, help="timed steps of the config-5 split-step line")
@@ -468,6 +469,56 @@ def neumf_bench(acf, dev):
                          "traffic": (pmc_traffic("k_nmf_adam") or (None,))[0]}}
 
 
+def eval_bench(acf, dev, reps=5):
+    """the all-items ranking of utils.py:178-267 ("all" mode, K =
+    100: every item but the user's trainList and test item) at the ml-1m and
+    pinterest-20 shapes, d = 64, on random tables of the trained magnitude.  The
+    U x I score sweep runs on v_mfma_f32_16x16x4_f32 (k_eval_mfma, with exact
+    rescoring inside the f32 error band), timed per whole positions call (prep +
+    sweep + exclusion correction) with HIP events; the VALU sweep (k_eval_all)
+    beside it, and both must give the same positions.  Roofline: the sweep's
+    2 U I d flops against the f32 MFMA peak (157.3 TFLOP/s)."""
+    from argparse import Namespace
+    ev = importlib.import_module(PKG + ".evaluate")
+    lib = importlib.import_module(PKG + "._native").load()
+    out = {}
+    for name, ds, ref_s in (("ml-1m", acf.ml1m_like(seed=2019), 5.3), ("pinterest-20", acf.pinterest_like(seed=2019),
+                                                                        None)):
+        d = 64
+        g = torch.Generator(device=dev).manual_seed(3)
+        P = torch.randn(ds.num_users + 1, d, device=dev, generator=g) * 0.3
+        Q = torch.randn(ds.num_items + 1, d, device=dev, generator=g) * 0.3
+        plan = ev.init_eval_model(ds, Namespace(eval_mode="all"))
+        nu, nc = len(plan.users), plan.num_candidates
+
+        def timed(mfma):
+            lib.acf_eval_set_kernel(1 if mfma else 0)
+            try:
+                pos = ev.positions(P, Q, plan)  # warm
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize(dev)
+                e0.record()
+                for _ in range(reps):
+                    pos = ev.positions(P, Q, plan)
+                e1.record()
+                torch.cuda.synchronize(dev)
+                return e0.elapsed_time(e1) / reps, pos.cpu().numpy()
+            finally:
+                lib.acf_eval_set_kernel(1)
+
+        ms, pos = timed(True)
+        ms_valu, pos_valu = timed(False)
+        tf = 2.0 * nu * nc * d / (ms * 1e-3) / 1e12
+        out[name] = {"users": nu, "candidates": nc, "dim": d, "ms_per_eval": round(ms, 3),
+                     "users_per_s": round(nu / (ms * 1e-3), 1), "valu_ms_per_eval": round(ms_valu, 3),
+                     "positions_equal_valu": bool((pos == pos_valu).all()),
+                     "roofline": {"bound": "mfma", "kernel": "k_eval_mfma", "achieved": round(tf, 2),
+                                  "peak": 157.3, "unit": "TFLOP/s", "frac": round(tf / 157.3, 4)},
+                     "reference_published_s": ref_s}
+        del P, Q, plan
+    return out
+
+
 def main():
     a = parse()
     # RCCL prints its version banner on stdout at init: keep fd 1 for the one JSON line
@@ -576,6 +627,8 @@ def main():
         out["sharded"] = sharded_lines(acf, ops, dev, dist, world, rank, big, a.sharded_steps)
     if rank == 0 and not a.no_neumf:
         out["neumf"] = neumf_bench(acf, dev)
+    if rank == 0 and not a.no_eval:
+        out["eval_all_items"] = eval_bench(acf, dev)
     if rank == 0 and not a.no_large:
         out["roofline_large_batch"] = large_batch_roofline(acf, ops, dev, big, 128)
         out["roofline_large_batch_d64"] = large_batch_roofline(acf, ops, dev, big, 64)

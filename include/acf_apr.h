@@ -274,6 +274,12 @@ int acf_eval_positions_list(const float* P, const float* Q, int64_t num_user_row
                             const int64_t* cand_off, const int32_t* cand_items,
                             int32_t* positions, void* stream);
 
+/* Test / A-B only: 1 (default) acf_eval_positions_all sweeps the scores on MFMA
+ * (v_mfma_f32_16x16x4_f32 tiles, exact rescoring of candidates within the f32
+ * error band of the test score: positions identical to the VALU sweep); 0 the
+ * VALU sweep.  Process-wide. */
+int acf_eval_set_kernel(int32_t mfma);
+
 /* ---- sampler: shuffle/_get_train_batch (APR.py:39-81) --------------------
  * Shuffles the n_pos positive pairs with a counter-based permutation of
  * `seed`, keeps floor(n_pos / batch_size) * batch_size of them (drop-last,

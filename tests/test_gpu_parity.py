@@ -4,11 +4,14 @@ Tolerance: fp32, rtol 1e-5 / atol 1e-6 on tables of magnitude O(0.1-1) — the
 bar north_star sets ("within 1e-5 fp32").  Differences come only from the order
 of the per-row dot-product sums (wavefront butterfly vs sequential).
 """
+import importlib
+
 import numpy as np
 import pytest
 import torch
 
 from apr_oracle import HParams
+from conftest import PKG
 
 pytestmark = pytest.mark.gpu
 RTOL, ATOL = 1e-5, 1e-6
@@ -253,6 +256,40 @@ def test_eval_positions_random_tables(ops, oracle, dev):
                                  torch.tensor(users, device=dev), torch.tensor(tests, device=dev), I1 - 1,
                                  off, excl).cpu().numpy()
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("d", [16, 64, 100, 256])
+def test_eval_mfma_exact_near_ties(ops, oracle, dev, d):
+    """The MFMA sweep (k_eval_mfma) gives the oracle's positions exactly, also where
+    candidates score within the f32 error band of the test item (rescored with the
+    sequential dot): near-copies of each user's test row, exact copies (real ties),
+    and ragged tile edges (users and candidates not multiples of 64 / 128)."""
+    rng = np.random.default_rng(d)
+    U1, I1 = 150, 700
+    P = rng.standard_normal((U1, d)).astype(np.float32)
+    Q = rng.standard_normal((I1, d)).astype(np.float32)
+    users = rng.permutation(U1)[:133].astype(np.int32)
+    tests = rng.integers(0, 600, len(users)).astype(np.int32)
+    for k, t in enumerate(tests[:60]):  # near-ties and exact ties of the test row
+        row = 600 + k
+        Q[row] = Q[t] * np.float32(1 + (k % 5 - 2) * 1e-7) if k % 3 else Q[t]
+    num_cand = 677
+    lists = [np.unique(np.append(rng.integers(0, num_cand, 20), t)).astype(np.int32) for t in tests]
+    off = np.zeros(len(users) + 1, np.int64)
+    np.cumsum([len(x) for x in lists], out=off[1:])
+    excl = np.concatenate(lists)
+    want = oracle.eval_positions_all(P, Q, users, tests, num_cand, off, excl)
+    args = (torch.tensor(P, device=dev), torch.tensor(Q, device=dev), torch.tensor(users, device=dev),
+            torch.tensor(tests, device=dev), num_cand, off, excl)
+    got = ops.eval_positions_all(*args).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    lib = importlib.import_module(PKG + "._native").load()
+    lib.acf_eval_set_kernel(0)
+    try:
+        valu = ops.eval_positions_all(*args).cpu().numpy()
+    finally:
+        lib.acf_eval_set_kernel(1)
+    np.testing.assert_array_equal(valu, want)
 
 
 def test_sampler_properties(ops, acf, dev):
