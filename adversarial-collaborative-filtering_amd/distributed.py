@@ -27,6 +27,12 @@ APR.py:193-195) are completed by the item's owner.  One step:
 
 BPR (adver = 0): E1, P0 (users updated), E2 + owner Adagrad.
 
+E1 has two forms (``item_exchange``): "all_to_all" (default) sends each rank just
+the rows of its working set; "allgather" is the form BASELINE.json's north_star
+and configs[2] name -- an RCCL all_gather of every rank's Q shard (the small
+pinterest item table replicated for the step), from which each rank takes the
+rows its negatives and positives need.  E2-E4 are the same in both.
+
 The working sets and the exchange plans of a whole chunk of steps are built on
 device in one go (one host sync per chunk, for the all_to_all split sizes).
 Every rank sees the same global triplet stream (the sampler is seeded
@@ -101,7 +107,10 @@ class ShardedAPR:
 
     def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, batch_size: int, device=None,
                  group=None, init_P=None, init_Q=None, acc0: float = 0.1, local=None,
-                 local_batch: int | None = None):
+                 local_batch: int | None = None, item_exchange: str = "all_to_all"):
+        if item_exchange not in ("all_to_all", "allgather"):
+            raise ValueError(f"item_exchange must be 'all_to_all' or 'allgather', got {item_exchange!r}")
+        self.item_exchange = item_exchange
         self.group = group
         self.G = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -129,6 +138,9 @@ class ShardedAPR:
         self._send = torch.empty(self.max_items, dim, **f)
         self._dlt = torch.empty(self.max_items, dim, **f)
         self._recv = torch.empty(0, dim, **f)
+        self._qcap = (self.I1 + G - 1) // G  # rows of the largest Q shard (all_gather slots)
+        self._qpad = torch.zeros(self._qcap, dim, **f) if item_exchange == "allgather" else None
+        self._qall = torch.empty(G * self._qcap, dim, **f) if item_exchange == "allgather" else None
         self.local = local(self) if local is not None else HipLocal(self)
         self.stats = {"steps": 0, "items_requested": 0, "rows_served": 0, "triplets": 0, "route_s": 0.0}
 
@@ -140,6 +152,18 @@ class ShardedAPR:
             out.copy_(o)
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def _gather_q(self):
+        """E1, "allgather" form: every rank's Q shard to every rank (RCCL all_gather);
+        row i is then at _qall[(i % G) * cap + i // G]."""
+        n = self.Q.shape[0]
+        self._qpad[:n] = self.Q
+        if self._stage:
+            parts = [torch.empty(self._qcap, self.d) for _ in range(self.G)]
+            dist.all_gather(parts, self._qpad.cpu(), group=self.group)
+            self._qall.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(self._qall, self._qpad, group=self.group)
 
     # -- routing (one chunk of T global batches) -----------------------------------
     def _route(self, u, i, j, T: int) -> _Chunk:
@@ -177,6 +201,8 @@ class ShardedAPR:
         wstart = torch.cumsum(nW, 0) - nW
         widx = (inv - wstart[ist]).to(torch.int32)
         c.wi, c.wj = widx[:n], widx[n:]
+        if self.item_exchange == "allgather":  # where each working-set row sits in the gathered table
+            c.wslot = ((wid % G) * self._qcap + wid // G).long()
         # the requests of the whole chunk, owner-major, in one exchange
         order = torch.argsort((wown * T + wstep) * I1 + wid)
         req = (wid // G)[order]
@@ -224,6 +250,7 @@ class ShardedAPR:
         c.Sa = np.concatenate([[0], np.cumsum(nseg.cpu().numpy())]).astype(np.int64)
         c.lo = np.concatenate([[0], np.cumsum(c.nloc)])
         c.nW = c.cnt.sum(1)
+        c.w0 = np.concatenate([[0], np.cumsum(c.nW)])  # working-set start of each step (host)
         c.count = None
         self._chunk_items = (i, j)
         return c
@@ -256,7 +283,12 @@ class ShardedAPR:
         recv, reply = self._recv[:R], self._recv_reply(R)
         part = self._send[:nw]
         # E1: current item rows of my working set from their owners
-        self._a2a(self.Qc[:nw], self.Q.index_select(0, served.long()), cnt, rc)
+        if self.item_exchange == "allgather":
+            self._gather_q()
+            w0 = int(c.w0[t])
+            torch.index_select(self._qall, 0, c.wslot[w0: w0 + nw], out=self.Qc[:nw])
+        else:
+            self._a2a(self.Qc[:nw], self.Q.index_select(0, served.long()), cnt, rc)
         if b:
             self.local.plan(c.u_rows[lo: lo + b], c.wi[lo: lo + b], c.wj[lo: lo + b])
             self.local.clean(hp, part)

@@ -393,23 +393,24 @@ def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
         warm = steps_p  # as above: one untimed chunk of the timed size
         n = (warm + steps_p) * B
         u, i, j = (x[:n].contiguous() for x in (ep.user, ep.item_pos, ep.item_neg))
-        sh = D_.ShardedAPR(ds.num_users + 1, ds.num_items + 1, d, B, device=dev)
-        sh.P.normal_(0, 0.01, generator=g)
-        sh.Q.normal_(0, 0.01, generator=g)
-        sh.train(u[: warm * B], i[: warm * B], j[: warm * B], hp, chunk=warm)
-        s = slice(warm * B, n)
-        el, tot = timed(sh, lambda: sh.train(u[s], i[s], j[s], hp, chunk=steps_p), steps_p * B / world)
-        out["pinterest"] = {
-            "metric": "APR triplets/sec, split step (users/items sharded over the ranks)",
-            "value": round(steps_p * B / el, 1), "unit": "triplets/s", "n_gpus": world, "steps": steps_p,
-            "ms_per_step": round(1e3 * el / steps_p, 4), "scaling": "strong", "dtype": "f32",
-            "data": "synthetic pinterest-20-shaped (55,187 x 9,916), device sampler",
-            "config": {"workload": "APR, BASELINE configs[2] split over the ranks", "users": ds.num_users,
-                       "items": ds.num_items, "dim": d, "global_batch": B,
-                       "parallelism": f"user/item row shards x{world}, all_to_all x4 per step"},
-            "step_errors": sh.step_errors()}
-        del sh
-        torch.cuda.empty_cache()
+        for key, exchange in (("pinterest", "all_to_all"), ("pinterest_allgather", "allgather")):
+            sh = D_.ShardedAPR(ds.num_users + 1, ds.num_items + 1, d, B, device=dev, item_exchange=exchange)
+            sh.P.normal_(0, 0.01, generator=g)
+            sh.Q.normal_(0, 0.01, generator=g)
+            sh.train(u[: warm * B], i[: warm * B], j[: warm * B], hp, chunk=warm)
+            s = slice(warm * B, n)
+            el, tot = timed(sh, lambda: sh.train(u[s], i[s], j[s], hp, chunk=steps_p), steps_p * B / world)
+            out[key] = {
+                "metric": "APR triplets/sec, split step (users/items sharded over the ranks)",
+                "value": round(steps_p * B / el, 1), "unit": "triplets/s", "n_gpus": world, "steps": steps_p,
+                "ms_per_step": round(1e3 * el / steps_p, 4), "scaling": "strong", "dtype": "f32",
+                "data": "synthetic pinterest-20-shaped (55,187 x 9,916), device sampler",
+                "config": {"workload": "APR, BASELINE configs[2] split over the ranks", "users": ds.num_users,
+                           "items": ds.num_items, "dim": d, "global_batch": B,
+                           "parallelism": f"user/item row shards x{world}, E1 by {exchange}, all_to_all x3"},
+                "step_errors": sh.step_errors()}
+            del sh
+            torch.cuda.empty_cache()
     finally:
         if own_group:
             tdist.destroy_process_group()

@@ -34,7 +34,7 @@ def _problem(hot=False):
     return P, Q, u, i, j
 
 
-def _worker(rank, world, port, out_dir, adver, reg, hot):
+def _worker(rank, world, port, out_dir, adver, reg, hot, exchange="all_to_all"):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from apr_oracle import HParams
@@ -43,7 +43,7 @@ def _worker(rank, world, port, out_dir, adver, reg, hot):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     D_ = importlib.import_module(PKG + ".distributed")
     P, Q, u, i, j = _problem(hot)
-    sh = D_.ShardedAPR(U1, I1, D, B, init_P=P, init_Q=Q, local=OracleShardLocal)
+    sh = D_.ShardedAPR(U1, I1, D, B, init_P=P, init_Q=Q, local=OracleShardLocal, item_exchange=exchange)
     assert sh.P.shape[0] == len(range(rank, U1, world))  # only this rank's rows
     assert sh.Q.shape[0] == len(range(rank, I1, world))
     sh.train(u, i, j, HParams(adver=adver, reg=reg), chunk=CHUNK)
@@ -64,11 +64,17 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,adver,reg,hot", [(2, 1, 0.0, False), (2, 0, 0.0, False), (3, 1, 0.01, True),
-                                                 (2, 1, 0.0, True)])
-def test_split_step_equals_single_process(tmp_path, oracle, fp32_parity, world, adver, reg, hot):
+@pytest.mark.parametrize("world,adver,reg,hot,exchange", [(2, 1, 0.0, False, "all_to_all"),
+                                                          (2, 0, 0.0, False, "all_to_all"),
+                                                          (3, 1, 0.01, True, "all_to_all"),
+                                                          (2, 1, 0.0, True, "all_to_all"),
+                                                          (2, 1, 0.0, False, "allgather"),
+                                                          (3, 1, 0.01, True, "allgather")])
+def test_split_step_equals_single_process(tmp_path, oracle, fp32_parity, world, adver, reg, hot, exchange):
+    """exchange "allgather": E1 as the all_gather of every Q shard (north_star's
+    form for configs[2]) instead of the working-set all_to_all."""
     from apr_oracle import HParams
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), adver, reg, hot), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), adver, reg, hot, exchange), nprocs=world, join=True)
     got = np.load(os.path.join(tmp_path, "sharded.npz"))
     P, Q, u, i, j = _problem(hot)
     aP, aQ = np.full_like(P, 0.1), np.full_like(Q, 0.1)

@@ -54,9 +54,14 @@ def _want(oracle, P, Q, u, i, j, B, adver, reg=0.0):
     return P, Q, aP, aQ
 
 
-@pytest.mark.parametrize("shape,adver,reg", [("pinterest", 1, 0.0), ("pinterest", 0, 0.0),
-                                             ("pinterest", 1, 0.01), ("zipf_large", 1, 0.0)])
-def test_sharded_rccl_world1_matches_oracle(ops, oracle, dev, fp32_parity, shape, adver, reg):
+@pytest.mark.parametrize("shape,adver,reg,exchange", [("pinterest", 1, 0.0, "all_to_all"),
+                                                      ("pinterest", 0, 0.0, "all_to_all"),
+                                                      ("pinterest", 1, 0.01, "all_to_all"),
+                                                      ("zipf_large", 1, 0.0, "all_to_all"),
+                                                      ("pinterest", 1, 0.0, "allgather"),
+                                                      ("pinterest", 0, 0.01, "allgather")])
+def test_sharded_rccl_world1_matches_oracle(ops, oracle, dev, fp32_parity, shape, adver, reg, exchange):
+    """exchange "allgather": E1 as the RCCL all_gather of the Q shards (configs[2]'s form)."""
     D_ = importlib.import_module(PKG + ".distributed")
     if shape == "pinterest":
         U1, I1, d, B, nb, z = 55_188, 9_917, 64, 512, 12, None
@@ -67,7 +72,7 @@ def test_sharded_rccl_world1_matches_oracle(ops, oracle, dev, fp32_parity, shape
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:
-        sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q)
+        sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, item_exchange=exchange)
         uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
         sh.train(uu, ii, jj, ops.StepHParams(adver=adver, reg=reg), chunk=5)
         got = sh.full_tables()
@@ -79,7 +84,7 @@ def test_sharded_rccl_world1_matches_oracle(ops, oracle, dev, fp32_parity, shape
         fp32_parity(g, w, n)
 
 
-def _worker(rank, world, port, out_dir, adver):
+def _worker(rank, world, port, out_dir, adver, exchange="all_to_all"):
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda", 0)
@@ -88,7 +93,7 @@ def _worker(rank, world, port, out_dir, adver):
     D_ = importlib.import_module(PKG + ".distributed")
     ops = importlib.import_module(PKG + ".ops")
     P, Q, u, i, j = _problem(7 + adver, 20_000, 9_000, 64, 4096, 4, 1.2)
-    sh = D_.ShardedAPR(20_000, 9_000, 64, 4096, device=dev, init_P=P, init_Q=Q)
+    sh = D_.ShardedAPR(20_000, 9_000, 64, 4096, device=dev, init_P=P, init_Q=Q, item_exchange=exchange)
     uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
     sh.train(uu, ii, jj, ops.StepHParams(adver=adver), chunk=3)
     full = sh.full_tables()
@@ -99,10 +104,10 @@ def _worker(rank, world, port, out_dir, adver):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("adver", [1, 0])
-def test_sharded_two_ranks_one_gpu_matches_oracle(oracle, fp32_parity, tmp_path, adver):
+@pytest.mark.parametrize("adver,exchange", [(1, "all_to_all"), (0, "all_to_all"), (1, "allgather")])
+def test_sharded_two_ranks_one_gpu_matches_oracle(oracle, fp32_parity, tmp_path, adver, exchange):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), adver), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), adver, exchange), nprocs=world, join=True)
     got = np.load(os.path.join(tmp_path, "w2.npz"))
     P, Q, u, i, j = _problem(7 + adver, 20_000, 9_000, 64, 4096, 4, 1.2)
     want = _want(oracle, P, Q, u, i, j, 4096, adver)
