@@ -232,12 +232,19 @@ __device__ __forceinline__ int find_local(const int32_t* __restrict__ uniq, cons
   return -1;
 }
 
+// inplace (triplet-centric plans, every row updated in its table): every row is
+// read from its table and nothing depends on the next batch, so no search.
 __global__ void k_slot_info(const int32_t* __restrict__ uniq, const int32_t* __restrict__ off,
                             const int32_t* __restrict__ ubs, const int32_t* __restrict__ bstart,
                             int32_t n_uniq, int32_t nb, int32_t item_side, int32_t kb,
-                            int4* __restrict__ info) {
+                            int4* __restrict__ info, int32_t inplace) {
   int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (g >= n_uniq || g >= bstart[nb]) return;  // bstart[nb] = unique rows of the plan
+  if (inplace) {
+    const int32_t row = uniq[g], o = off[g];
+    info[g] = make_int4(row, row, off[g + 1] - o, o);
+    return;
+  }
   // batch of g: last t with bstart[t] <= g
   int lo = 0, hi = nb;  // answer in [0, nb)
   while (hi - lo > 1) {
@@ -530,18 +537,20 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
   r.pa_slot = ki | (info_count(I) == 1 ? ACF_SOLO_BIT : 0);
   r.pb_slot = kj | (info_count(J) == 1 ? ACF_SOLO_BIT : 0);
   r.gen = gen;
+  // the CSR records (occurrences past the first R) are read by the slot kernels
+  // only: the triplet-centric step reads a slot's first record and trec
   const int64_t base = (int64_t)t * S;
   int32_t rr = ps.x - U.w;
   if (rr < R) inl[(base + k) * R + rr] = r;
-  else urec[ps.x] = r;
+  else if (!tri) urec[ps.x] = r;
   const OccRec ri = item_rec(I, J, U, (int32_t)(2 * e), k, kj, xi, f.in_i, gen);
   rr = ps.y - I.w;
   if (rr < R) inl[(base + ki) * R + rr] = ri;
-  else irec[ps.y] = ri;
+  else if (!tri) irec[ps.y] = ri;
   const OccRec rj = item_rec(J, I, U, (int32_t)(2 * e + 1), k, ki, xj, f.in_j, gen);
   rr = ps.z - J.w;
   if (rr < R) inl[(base + kj) * R + rr] = rj;
-  else irec[ps.z] = rj;
+  else if (!tri) irec[ps.z] = rj;
   if (sflags) {  // packed plans: the slot flags and hot lists, from each slot's first occurrence
     if (ps.x == U.w) slot_flag(sflags, hl, t, S, k, info_count(U), xu, f.in_u);
     if (ps.y == I.w) slot_flag(sflags, hl, t, S, ki, info_count(I), xi, f.in_i);
@@ -1053,6 +1062,7 @@ struct StepArgs {
   // triplet-centric list step (k_tri_*): per-occurrence contributions of shared rows
   const int4* tpos;    // [E] CSR positions of a triplet's three occurrences
   float* contrib;      // users [B][2][d] (positive, negative branch), then items [2B][d]
+  int32_t inplace;     // triplet-centric plans: every row is updated in its table (no W scratch)
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -2455,7 +2465,8 @@ __global__ void __launch_bounds__(256) k_hot_combine(StepArgs a) {
           adagrad_row(a, G0, own, acc, e.w, wout);
         }
         store_row<LPR, NV>(acc_tab, row, d, l, acc);
-        store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+        if (a.inplace) store_row<LPR, NV>(is_item ? a.Q : a.P, row, d, l, wout);
+        else store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
       }
     }
     __syncthreads();
@@ -2727,7 +2738,8 @@ __device__ __forceinline__ void tri_finish(const StepArgs& a, int k, const TriSl
     adagrad_row(a, G0, own, acc, h.count, wout);
   }
   store_row<LPR, NV>(acc_tab, h.row, d, l, acc);
-  store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+  if (a.inplace) store_row<LPR, NV>(h.is_item ? a.Q : a.P, h.row, d, l, wout);
+  else store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
 }
 
 template <int LPR, int NV, bool BPR>
@@ -2793,6 +2805,7 @@ __global__ void __launch_bounds__(256) k_flush(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   // the call counter (random delta); every kernel of this call has read it
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(const_cast<uint32_t*>(a.epoch), 1u);
+  if (a.inplace) return;  // nothing left in W scratch
   flush_slot(a, a.t, a.wnew_cur, wave, threadIdx.x & 63, 64);
 }
 
@@ -3645,16 +3658,19 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
                                              c->uoff, c->ioff, c->ubs, c->ibs, 3 * B, kb, c->uinfo, c->iinfo,
                                              c->nextt);
   } else {
+    // triplet-centric plans (packed, fusion on, not shard mode) update every row in
+    // its table: no source / next-batch search (k_slot_info inplace)
+    const int32_t tri_plan = packed && !c->shard && c->fusion;
     k_slot_info<<<grid_for(E), 256, 0, s>>>(c->uuniq, c->uoff, c->ubs, c->ubs, (int32_t)E, nb, 0, kb,
-                                            c->uinfo);
+                                            c->uinfo, tri_plan);
     k_slot_info<<<grid_for(2 * E), 256, 0, s>>>(c->iuniq, c->ioff, c->ubs, c->ibs, (int32_t)(2 * E), nb, 1,
-                                                kb, c->iinfo);
+                                                kb, c->iinfo, tri_plan);
   }
   HIP_TRY(hipGetLastError());
   c->plan_R = packed ? 1 : c->R;
   c->plan_kind2 = all_dt;
   c->plan_kb = kb;
-  c->tri = packed && !c->shard;
+  c->tri = packed && !c->shard && c->fusion;
   if (packed) {  // k_records writes the slot flags of the slots it finds; the rest read 0
     HIP_TRY(hipMemsetAsync(c->key_in, 0, (size_t)3 * E * sizeof(uint64_t), s));
     HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
@@ -3739,6 +3755,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
   a.contrib = c->contrib;
+  a.inplace = c->tri;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -3957,9 +3974,14 @@ static void prepare_stream(acf_apr_ctx* c, const acf_apr_hparams* hp) {
 
 // kinds: 0 phase 1 / fused BPR, 1 phase 2, 2 flush, 3 k_ovl with both halves, 4 k_stream,
 // 5 hot-slot combine (list kernels)
+// tri_phases (triplet-centric plans, one batch through the two-phase API): bit 0
+// the clean phase (delta_update), bit 1 the adversarial / BPR phase + the
+// call-counter bump (optimizer_step); train_planned runs both.
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                     int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds,
-                    int allow_overlap = 2) {
+                    int allow_overlap = 2, int tri_phases = 3) {
+  ACF_CHECK(!(c->tri && !c->fusion), ACF_E_STATE,
+            "fusion was switched off after a triplet-centric plan (rows are updated in place): plan again");
   Kernels K;
   ACF_RET(get_kernels(c, &K, c->fusion));
   const int S = 3 * c->B;
@@ -4046,25 +4068,33 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   if (K.tri) {  // triplet-centric list step (see k_tri_*)
     const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);  // one lane-group per triplet
     for (int32_t t = first; t < first + n; ++t) {
-      StepArgs a = make_args(c, tb, hp, t, t > first ? 1 : 0);
-      a.use_single = 1;  // in-place rows are not written back
+      // every row is updated in its table (StepArgs.inplace): nothing pending from t-1
+      StepArgs a = make_args(c, tb, hp, t, 0);
+      a.use_single = 1;
       a.slot_waves = SW;
       a.hot_waves = HW;
       StepArgs ah = a;
       ah.slot_waves = 4 * HB;
+      StepArgs at = a;
+      at.slot_waves = 0;  // k_tri_clean: triplet waves only (no write-back of t-1)
       if (hp->adver) {
-        ACF_RET(L(K.tri_clean, a, SW + (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
-        ACF_RET(L(K.tri_comb[0], a, SW + HW, 5));
-        ACF_RET(L(K.hot_clean, ah, 4 * HB, 5));
-        ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
-        ACF_RET(L(K.tri_comb[2], a, SW + HW, 5));
-        ACF_RET(L(K.hot_adv, ah, 4 * HB, 5));
-      } else {
-        ACF_RET(L(K.tri_clean_bpr, a, SW + (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
+        if (tri_phases & 1) {
+          ACF_RET(L(K.tri_clean, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
+          ACF_RET(L(K.tri_comb[0], a, SW + HW, 5));
+          ACF_RET(L(K.hot_clean, ah, 4 * HB, 5));
+        }
+        if (tri_phases & 2) {
+          ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
+          ACF_RET(L(K.tri_comb[2], a, SW + HW, 5));
+          ACF_RET(L(K.hot_adv, ah, 4 * HB, 5));
+        }
+      } else if (tri_phases & 2) {
+        ACF_RET(L(K.tri_clean_bpr, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
         ACF_RET(L(K.tri_comb[1], a, SW + HW, 5));
         ACF_RET(L(K.hot_bpr, ah, 4 * HB, 5));
       }
     }
+    if (!(tri_phases & 2)) return ACF_OK;  // delta_update: no call-counter bump
   } else {
   for (int32_t t = first; t < first + n; ++t) {
     const int pv = t > first ? 1 : 0;
@@ -4092,7 +4122,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   StepArgs af = make_args(c, tb, hp, first + n - 1, 0);
   af.use_single = fuse;
   af.slot_waves = S;
-  ACF_RET(L(K.flush, af, S, 2));
+  ACF_RET(L(K.flush, af, K.tri ? 4 : S, 2));  // in place (tri): the call-counter bump only
   return ACF_OK;
 }
 
@@ -4101,6 +4131,11 @@ extern "C" int acf_apr_delta_update(acf_apr_ctx* c, const acf_apr_tables* tb,
   ACF_RET(check_step(c, tb, hp, t));
   ACF_CHECK(hp->adver, ACF_E_INVALID, "delta_update needs hparams.adver = 1 (APR graph)");
   hipStream_t s = static_cast<hipStream_t>(stream_);
+  if (c->tri) {  // triplet-centric plan: its clean phase
+    ACF_RET(run_loop(c, tb, hp, t, 1, s, nullptr, nullptr, 0, 1));
+    c->last_delta_batch = t;
+    return ACF_OK;
+  }
   Kernels K;
   ACF_RET(get_kernels(c, &K));
   const int SW = (3 * c->B + K.slots_per_wave - 1) / K.slots_per_wave;
@@ -4115,6 +4150,11 @@ extern "C" int acf_apr_optimizer_step(acf_apr_ctx* c, const acf_apr_tables* tb,
                                       const acf_apr_hparams* hp, int32_t t, void* stream_) {
   ACF_RET(check_step(c, tb, hp, t));
   hipStream_t s = static_cast<hipStream_t>(stream_);
+  if (c->tri) {  // triplet-centric plan: its adversarial (or BPR) phase, rows in place
+    ACF_CHECK(!hp->adver || c->last_delta_batch == t, ACF_E_STATE,
+              "APR optimizer step on batch %d needs acf_apr_delta_update on the same batch first", t);
+    return run_loop(c, tb, hp, t, 1, s, nullptr, nullptr, 0, 2);
+  }
   Kernels K;
   ACF_RET(get_kernels(c, &K));
   const int SW = (3 * c->B + K.slots_per_wave - 1) / K.slots_per_wave;

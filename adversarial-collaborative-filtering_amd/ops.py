@@ -233,7 +233,10 @@ class APRContext:
 
     def set_fusion(self, on: bool) -> None:
         """Fuse triplets whose three rows occur once in their batch (default on;
-        identical results either way).  Applies to train_planned / time_kernels."""
+        identical results either way).  Applies to train_planned / time_kernels;
+        for large batches (one lane-group per slot) set it before plan(): a plan
+        made with fusion on is triplet-centric and updates every row in place, and
+        training it with fusion off raises."""
         call("acf_apr_set_fusion", self._ptr, int(bool(on)))
 
     def time_kernels(self, tables, hp: StepHParams, first: int = 0, n: int | None = None):
@@ -345,6 +348,8 @@ class PlanPipeline:
         self.batch_size, self.chunk = int(batch_size), int(chunk)
         self.ctx = [APRContext(num_user_rows, num_item_rows, dim, batch_size, chunk, self.device)
                     for _ in range(2)]
+        # default priority: a high-priority plan stream halved the configs[4] rate
+        # (608M -> 313M triplets/s at d = 64, tools/large_prio.py, r03)
         self.side = torch.cuda.Stream(self.device)
         self._free = [None, None]  # event: the last training on ctx[k] has been issued before it
 

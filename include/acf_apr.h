@@ -154,8 +154,13 @@ int acf_apr_set_slot_mapping(acf_apr_ctx* ctx, int32_t mode);
  * default; 0 = off).  A triplet whose user, positive and negative item each
  * occur once in its batch is stepped start to finish by one lane-group (no
  * batch-wide aggregation is needed for it); the arithmetic per row is the slot
- * kernels' own, so on and off give identical bits.  The split per-batch calls
- * (delta_update / optimizer_step) never fuse.  Not part of the reference surface. */
+ * kernels' own, so on and off give identical bits.  For one-lane-group-per-slot
+ * plans (batches >= 4,096) the setting at acf_apr_plan time decides the plan: on
+ * gives a triplet-centric plan whose steps (train_planned and the split per-batch
+ * calls alike) update every row in its table; training such a plan with fusion
+ * switched off returns ACF_E_STATE (plan again).  Otherwise the split per-batch
+ * calls (delta_update / optimizer_step) never fuse.  Not part of the reference
+ * surface. */
 int acf_apr_set_fusion(acf_apr_ctx* ctx, int32_t on);
 
 /* Which planner acf_apr_plan uses: 0 = auto (the default: the batch-local plan,

@@ -599,8 +599,8 @@ def test_fused_triplets_bit_identical_to_slot_path(ops, dev, d, adver, adv, mapp
     for fuse, pieces in cases:
         ctx = ops.APRContext(U1, I1, d, B, nb, dev)
         ctx.set_slot_mapping(mapping)
+        ctx.set_fusion(fuse)  # before the plan: a triplet-centric plan updates rows in place
         ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
-        ctx.set_fusion(fuse)
         tabs = _gpu_tables(P, Q, dev)
         for first, n in pieces:
             ctx.train_planned(tabs, hp, first, n, graph=first == 0)
