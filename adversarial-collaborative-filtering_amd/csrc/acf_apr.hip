@@ -476,6 +476,8 @@ struct HotLists {
   int4* piece;      // [nb][piece_stride] {slot, piece, pieces, piece base}
   int32_t* cnt;     // [nb] hot slots of the batch
   int32_t* pcnt;    // [nb] pieces of the batch
+  int32_t* arrive;  // [nb][piece_stride] at a hot slot's piece base: its pieces stored so far
+                    // (triplet-centric combine: the slot's combine waits for all of them)
   int32_t hot_stride, piece_stride;
 };
 
@@ -1054,6 +1056,7 @@ struct StepArgs {
   HotLists hot;
   float* hot_part;     // [piece_stride, d]
   int32_t hot_waves;
+  int32_t hot_blocks;  // k_tri_combine: hot-slot combining workgroups after the piece waves (0: k_hot_combine)
   // shard mode (distributed.ShardedAPR): item rows of the batch are this rank's
   // partial sums; an item slot's clean / adversarial sum goes to g0[k] for the
   // exchange instead of Adagrad, and item rows are never written back
@@ -2418,59 +2421,96 @@ __device__ __forceinline__ void hot_piece_waves(const StepArgs& a, int hw) {
 // sums in group order and finishes the slot as the slot kernels' team leader does:
 // MODE 0 (APR clean): G -> g0, delta; MODE 1 (BPR): Adagrad on G;
 // MODE 2 (APR adversarial): g0 + reg_adv * G -> Adagrad.  Rows go to W scratch.
-template <int LPR, int NV, int MODE>
-__global__ void __launch_bounds__(256) k_hot_combine(StepArgs a) {
-  constexpr int NG = 256 / LPR;
-  __shared__ float4 red[NV * 256];
-  const int g = threadIdx.x / LPR, l = threadIdx.x & (LPR - 1), d = a.d;
-  const int n = a.hot.cnt[a.t];
-  const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
-  for (int hx = blockIdx.x; hx < n; hx += gridDim.x) {
-    const int4 e = hl[hx];  // {slot, pieces, piece base, count}
-    RowV<NV> G = zero_row<NV>();
-#pragma unroll 4
-    for (int p = g; p < e.y; p += NG) G = add_row(G, load_row<LPR, NV>(a.hot_part, (int64_t)e.z + p, d, l));
+// a piece sum read back: plain loads, or (SC1) device-scope loads of the 8-B
+// halves of each float4 (the pieces were stored write-through in this launch by
+// other workgroups: MI355X guide, Guideline 16)
+template <int LPR, int NV, bool SC1>
+__device__ __forceinline__ RowV<NV> load_piece(const float* __restrict__ base, int64_t row, int d, int l) {
+  if constexpr (!SC1) {
+    return load_row<LPR, NV>(base, row, d, l);
+  } else {
+    RowV<NV> r;
+    const float* p = base + row * (int64_t)d;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) red[v * 256 + threadIdx.x] = G.v[v];
-    __syncthreads();
-    if (g == 0) {
-      for (int gg = 1; gg < NG; ++gg) {
-        RowV<NV> o;
-#pragma unroll
-        for (int v = 0; v < NV; ++v) o.v[v] = red[v * 256 + gg * LPR + l];
-        G = add_row(G, o);
-      }
-      const int k = e.x;
-      const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
-      const int is_item = (r.meta() & ACF_ITEM_BIT) != 0;
-      const int32_t row = r.own_row();
-      const float* own_tab = is_item ? a.Q : a.P;
-      float* acc_tab = is_item ? a.accQ : a.accP;
-      if (MODE != 0 && a.shard && is_item) {  // partial item sum for the owner
-        store_row<LPR, NV>(a.g0, k, d, l, G);
-      } else if (MODE == 0) {
-        const RowV<NV> dl = make_delta<LPR, NV>(a, G, is_item, row, l);
-        store_row<LPR, NV>(a.g0, k, d, l, G);
-        store_row<LPR, NV>(a.delta, k, d, l, dl);
+    for (int v = 0; v < NV; ++v) {
+      const int c = l + LPR * v;
+      if (c * 4 < d) {
+        const u64 lo = __hip_atomic_load((const __attribute__((address_space(1))) u64*)(p + c * 4),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 hi = __hip_atomic_load((const __attribute__((address_space(1))) u64*)(p + c * 4 + 2),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.v[v] = make_float4(__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
+                             __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32)));
       } else {
-        RowV<NV> acc = load_row<LPR, NV>(acc_tab, row, d, l);
-        RowV<NV> wout;
-        if (MODE == 1) {
-          const RowV<NV> own = load_at<LPR, NV>(row_src(a, own_tab, row, r.own_src()), d, l);
-          adagrad_row(a, G, own, acc, e.w, wout);
-        } else {
-          RowV<NV> G0 = load_row<LPR, NV>(a.g0, k, d, l);
-          axpy_row(G0, a.reg_adv, G);
-          const RowV<NV> own = load_row<LPR, NV>(own_tab, row, d, l);
-          adagrad_row(a, G0, own, acc, e.w, wout);
-        }
-        store_row<LPR, NV>(acc_tab, row, d, l, acc);
-        if (a.inplace) store_row<LPR, NV>(is_item ? a.Q : a.P, row, d, l, wout);
-        else store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+        r.v[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-    __syncthreads();
+    return r;
   }
+}
+
+// One hot slot e = {slot, pieces, piece base, count} by a 256-thread workgroup:
+// lane-group g of the 256/LPR sums pieces g, g + 256/LPR, ... in turn; group 0
+// then adds the groups' sums in group order and finishes the slot as the slot
+// kernels' team leader does: MODE 0 (APR clean): G -> g0, delta; MODE 1 (BPR):
+// Adagrad on G; MODE 2 (APR adversarial): g0 + reg_adv * G -> Adagrad.  Rows go
+// to W scratch, or to their table in place (a.inplace).  Ends with a barrier.
+template <int LPR, int NV, int MODE, bool SC1>
+__device__ __forceinline__ void hot_combine_slot(const StepArgs& a, const int4 e, float4* __restrict__ red) {
+  constexpr int NG = 256 / LPR;
+  const int g = threadIdx.x / LPR, l = threadIdx.x & (LPR - 1), d = a.d;
+  RowV<NV> G = zero_row<NV>();
+#pragma unroll 4
+  for (int p = g; p < e.y; p += NG) G = add_row(G, load_piece<LPR, NV, SC1>(a.hot_part, (int64_t)e.z + p, d, l));
+#pragma unroll
+  for (int v = 0; v < NV; ++v) red[v * 256 + threadIdx.x] = G.v[v];
+  __syncthreads();
+  if (g == 0) {
+    for (int gg = 1; gg < NG; ++gg) {
+      RowV<NV> o;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) o.v[v] = red[v * 256 + gg * LPR + l];
+      G = add_row(G, o);
+    }
+    const int k = e.x;
+    const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
+    const int is_item = (r.meta() & ACF_ITEM_BIT) != 0;
+    const int32_t row = r.own_row();
+    const float* own_tab = is_item ? a.Q : a.P;
+    float* acc_tab = is_item ? a.accQ : a.accP;
+    if (MODE != 0 && a.shard && is_item) {  // partial item sum for the owner
+      store_row<LPR, NV>(a.g0, k, d, l, G);
+    } else if (MODE == 0) {
+      const RowV<NV> dl = make_delta<LPR, NV>(a, G, is_item, row, l);
+      store_row<LPR, NV>(a.g0, k, d, l, G);
+      store_row<LPR, NV>(a.delta, k, d, l, dl);
+    } else {
+      RowV<NV> acc = load_row<LPR, NV>(acc_tab, row, d, l);
+      RowV<NV> wout;
+      if (MODE == 1) {
+        const RowV<NV> own = load_at<LPR, NV>(row_src(a, own_tab, row, r.own_src()), d, l);
+        adagrad_row(a, G, own, acc, e.w, wout);
+      } else {
+        RowV<NV> G0 = load_row<LPR, NV>(a.g0, k, d, l);
+        axpy_row(G0, a.reg_adv, G);
+        const RowV<NV> own = load_row<LPR, NV>(own_tab, row, d, l);
+        adagrad_row(a, G0, own, acc, e.w, wout);
+      }
+      store_row<LPR, NV>(acc_tab, row, d, l, acc);
+      if (a.inplace) store_row<LPR, NV>(is_item ? a.Q : a.P, row, d, l, wout);
+      else store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
+    }
+  }
+  __syncthreads();
+}
+
+// Hot-slot combine: one workgroup per hot slot (strided); see hot_combine_slot.
+template <int LPR, int NV, int MODE>
+__global__ void __launch_bounds__(256) k_hot_combine(StepArgs a) {
+  __shared__ float4 red[NV * 256];
+  const int n = a.hot.cnt[a.t];
+  const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
+  for (int hx = blockIdx.x; hx < n; hx += gridDim.x) hot_combine_slot<LPR, NV, MODE, false>(a, hl[hx], red);
 }
 
 template <int LPR, int NV, bool FUSE_APPLY>
@@ -2758,9 +2798,17 @@ __global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
 }
 
 // shared slots with <= ACF_HOT_MIN occurrences: one lane-group each, in order;
-// hot slots: piece waves [slot_waves, slot_waves + hot_waves) into hot_part
+// hot slots: piece waves [slot_waves, slot_waves + hot_waves) into hot_part, then
+// hot_blocks workgroups (waves from slot_waves + hot_waves on) that each combine
+// hot slots as k_hot_combine does once all their pieces are stored.  A piece is
+// stored write-through, the wave drains its stores, and one lane adds 1 to the
+// slot's arrival count; a combining workgroup polls that count (device scope),
+// and every load of the pieces is a device-scope load (Guideline 16, row 1).
+// The combining workgroups come after every piece wave in dispatch order, so
+// the pieces they wait for are already running: the launch always drains.
 template <int LPR, int NV, int MODE>
 __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
+  __shared__ float4 red[NV * 256];
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
   if (wave < a.slot_waves) {
@@ -2776,19 +2824,50 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
     }
     return;
   }
+  int32_t* arrive = a.hot.arrive + (int64_t)a.t * a.hot.piece_stride;
   const int hw = wave - a.slot_waves;
-  if (hw >= a.hot_waves) return;
-  constexpr int TEAM = 64 / LPR;
-  const int n = a.hot.pcnt[a.t];
-  const int4* pl = a.hot.piece + (int64_t)a.t * a.hot.piece_stride;
-  for (int x = hw; x < n; x += a.hot_waves) {
-    const int4 pc = pl[x];  // {slot, piece, pieces, piece base}
-    const TriSlot h = tri_slot(a, pc.x);
-    const int o0 = (int)((int64_t)pc.y * h.count / pc.z), o1 = (int)((int64_t)(pc.y + 1) * h.count / pc.z);
-    RowV<NV> G = zero_row<NV>();
-    tri_add<LPR, NV>(a, h, o0 + g, o1, TEAM, l, G);
-    team_allreduce<LPR, TEAM, NV>(G);
-    if (g == 0) store_row<LPR, NV>(a.hot_part, (int64_t)pc.w + pc.y, a.d, l, G);
+  if (hw < a.hot_waves) {
+    constexpr int TEAM = 64 / LPR;
+    const int n = a.hot.pcnt[a.t];
+    const int4* pl = a.hot.piece + (int64_t)a.t * a.hot.piece_stride;
+    for (int x = hw; x < n; x += a.hot_waves) {
+      const int4 pc = pl[x];  // {slot, piece, pieces, piece base}
+      const TriSlot h = tri_slot(a, pc.x);
+      const int o0 = (int)((int64_t)pc.y * h.count / pc.z), o1 = (int)((int64_t)(pc.y + 1) * h.count / pc.z);
+      RowV<NV> G = zero_row<NV>();
+      tri_add<LPR, NV>(a, h, o0 + g, o1, TEAM, l, G);
+      team_allreduce<LPR, TEAM, NV>(G);
+      if (a.hot_blocks == 0) {  // combined by k_hot_combine (the next launch)
+        if (g == 0) store_row<LPR, NV>(a.hot_part, (int64_t)pc.w + pc.y, a.d, l, G);
+        continue;
+      }
+      if (g == 0) store_row_wt<LPR, NV>(a.hot_part, (int64_t)pc.w + pc.y, a.d, l, G);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(arrive + pc.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  // hot-slot combining workgroups (whole workgroups: slot_waves + hot_waves is a multiple of 4)
+  const int hb = (wave - a.slot_waves - a.hot_waves) >> 2;
+  if (hb >= a.hot_blocks) return;
+  const int n = a.hot.cnt[a.t];
+  const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
+  for (int hx = hb; hx < n; hx += a.hot_blocks) {
+    const int4 e = hl[hx];  // {slot, pieces, piece base, count}
+    if (threadIdx.x == 0) {
+      int it = 0;
+      while (__hip_atomic_load(arrive + e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.y) {
+        if (++it > ACF_SPIN_LIMIT) {
+          atomicOr(a.step_err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      // every piece of this pass is in: ready for the next pass over the batch
+      __hip_atomic_store(arrive + e.z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    hot_combine_slot<LPR, NV, MODE, true>(a, e, red);
   }
 }
 
@@ -3412,6 +3491,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   c->hot.piece_stride = piece_stride_for(maxB);
   A(&c->hot.list, (size_t)maxNB * c->hot.hot_stride); A(&c->hot.piece, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot.cnt, 2 * (size_t)maxNB);
+  A(&c->hot.arrive, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot_part, (size_t)c->hot.piece_stride * d);
   A(&c->contrib, (size_t)4 * maxB * d);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
@@ -3674,6 +3754,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   if (packed) {  // k_records writes the slot flags of the slots it finds; the rest read 0
     HIP_TRY(hipMemsetAsync(c->key_in, 0, (size_t)3 * E * sizeof(uint64_t), s));
     HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
+    HIP_TRY(hipMemsetAsync(c->hot.arrive, 0, (size_t)nb * c->hot.piece_stride * sizeof(int32_t), s));
   }
   k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen, kb, c->shard, c->tri,
                                         reinterpret_cast<const int4*>(c->tsl),
@@ -3751,6 +3832,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.hot = c->hot;
   a.hot_part = c->hot_part;
   a.hot_waves = 0;
+  a.hot_blocks = 0;
   a.shard = c->shard;
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
@@ -3780,6 +3862,7 @@ struct Kernels {
 #define ACF_LIST_WAVES 4096  // slot waves of a list kernel
 #define ACF_HOT_WAVES 2048   // piece waves of a list kernel (hot slots)
 #define ACF_HOT_BLOCKS 1024  // workgroups of k_hot_combine
+#define ACF_TRI_HOT_BLOCKS 512  // hot-slot combining workgroups of k_tri_combine
 
 template <int LPR, int NV, int TEAM>
 static void kernel_ptrs_team(Kernels* k, int fused) {
@@ -4066,6 +4149,9 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   const int HW = K.lists ? std::min(c->hot.piece_stride, ACF_HOT_WAVES) : 0;
   const int HB = std::min(c->hot.hot_stride, ACF_HOT_BLOCKS);
   if (K.tri) {  // triplet-centric list step (see k_tri_*)
+    // k_tri_combine with its hot-slot combining workgroups after the piece waves
+    // (whole workgroups: the two wave ranges rounded up to multiples of 4)
+    const int SW4 = (SW + 3) & ~3, HW4 = (HW + 3) & ~3, HBT = std::min(HB, ACF_TRI_HOT_BLOCKS);
     const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);  // one lane-group per triplet
     for (int32_t t = first; t < first + n; ++t) {
       // every row is updated in its table (StepArgs.inplace): nothing pending from t-1
@@ -4077,21 +4163,24 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
       ah.slot_waves = 4 * HB;
       StepArgs at = a;
       at.slot_waves = 0;  // k_tri_clean: triplet waves only (no write-back of t-1)
+      StepArgs ac = a;
+      ac.slot_waves = SW4;
+      ac.hot_waves = HW4;
+      ac.hot_blocks = HBT;
+      const int CW = SW4 + HW4 + 4 * HBT;
+      (void)ah;
       if (hp->adver) {
         if (tri_phases & 1) {
           ACF_RET(L(K.tri_clean, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
-          ACF_RET(L(K.tri_comb[0], a, SW + HW, 5));
-          ACF_RET(L(K.hot_clean, ah, 4 * HB, 5));
+          ACF_RET(L(K.tri_comb[0], ac, CW, 5));
         }
         if (tri_phases & 2) {
           ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
-          ACF_RET(L(K.tri_comb[2], a, SW + HW, 5));
-          ACF_RET(L(K.hot_adv, ah, 4 * HB, 5));
+          ACF_RET(L(K.tri_comb[2], ac, CW, 5));
         }
       } else if (tri_phases & 2) {
         ACF_RET(L(K.tri_clean_bpr, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
-        ACF_RET(L(K.tri_comb[1], a, SW + HW, 5));
-        ACF_RET(L(K.hot_bpr, ah, 4 * HB, 5));
+        ACF_RET(L(K.tri_comb[1], ac, CW, 5));
       }
     }
     if (!(tri_phases & 2)) return ACF_OK;  // delta_update: no call-counter bump
