@@ -497,18 +497,6 @@ __device__ __forceinline__ void slot_flag(uint64_t* __restrict__ sflags, const H
   }
 }
 
-// Arrival counter of occurrence o (rank in its slot) of a slot with `count`
-// occurrences whose first one sits at local CSR position `base` (merged
-// triplet passes): the counter of the piece holding it -- the CSR position of
-// that piece's first occurrence; a slot of <= ACF_HOT_MIN occurrences is one
-// piece.  Pieces as in hot_piece: [p count / np, (p + 1) count / np).
-__device__ __forceinline__ int32_t tri_counter(int32_t o, int32_t count, int32_t base) {
-  if (count <= ACF_HOT_MIN) return base;
-  const int32_t np = hot_pieces(count);
-  const int32_t p = (int32_t)(((int64_t)(o + 1) * np - 1) / count);
-  return base + (int32_t)((int64_t)p * count / np);
-}
-
 // tri (triplet-centric list plans, see k_tri_*): every row that occurs once in
 // its batch is "single" (its triplet's lane-group steps it: SINGLE bit, and
 // INPLACE by fuse_info's rule), and every triplet gets a record in trec with
@@ -575,11 +563,6 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
     q.own_row = U.x; q.own_src = I.x; q.meta = J.x; q.ovf = k;
     q.e_role = ki; q.pa_row = kj; q.pb_row = U.y; q.pa_src = I.y;
     q.pb_src = J.y;
-    if (tri) {  // every row is read from its table: the source fields carry arrival counters
-      q.pb_row = tri_counter(ps.x - U.w, info_count(U), U.w - t * B);
-      q.pa_src = B + tri_counter(ps.y - I.w, info_count(I), I.w - t * 2 * B);
-      q.pb_src = B + tri_counter(ps.z - J.w, info_count(J), J.w - t * 2 * B);
-    }
     q.pa_slot = (f.fused ? 1 : 0) | (f.in_u ? 2 : 0) | (f.in_i ? 4 : 0) | (f.in_j ? 8 : 0) |
                 (su ? 16 : 0) | (si ? 32 : 0) | (sj ? 64 : 0);
     q.pb_slot = (int32_t)e; q.gen = gen;
@@ -1079,8 +1062,7 @@ struct StepArgs {
   // follows with comb_slot_waves slot waves, hot_waves piece waves, hot_blocks
   // workgroups; slot_arrive counts the stored contributions of each shared slot
   int32_t tri_waves, comb_slot_waves;
-  int32_t* slot_arrive;  // [nb][3B] stored contributions per piece, at the piece's first CSR
-                         // position (users [0, B), items B + [0, 2B); see tri_counter)
+  int32_t* slot_arrive;  // [nb][S]
   // shard mode (distributed.ShardedAPR): item rows of the batch are this rank's
   // partial sums; an item slot's clean / adversarial sum goes to g0[k] for the
   // exchange instead of Adagrad, and item rows are never written back
@@ -2759,11 +2741,10 @@ __device__ __forceinline__ void tri_triplets(const StepArgs& a, int tw, int lane
 #pragma unroll
   for (int x = 0; x < GPW; ++x) {
     if (b0 + x * OPW >= a.B || r[x].c.w != gen) continue;
-    // the plan put each shared row's arrival counter (its piece's) in the source fields
     const int flags = r[x].c.y;
-    if (!(flags & TRI_SU)) __hip_atomic_fetch_add(arr + r[x].b.z, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!(flags & TRI_SI)) __hip_atomic_fetch_add(arr + r[x].b.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!(flags & TRI_SJ)) __hip_atomic_fetch_add(arr + r[x].c.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!(flags & TRI_SU)) __hip_atomic_fetch_add(arr + r[x].a.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!(flags & TRI_SI)) __hip_atomic_fetch_add(arr + r[x].b.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!(flags & TRI_SJ)) __hip_atomic_fetch_add(arr + r[x].b.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2887,10 +2868,9 @@ __device__ __forceinline__ void tri_combine_region(const StepArgs& a, int cw, in
     for (int x = gid; x < n; x += ngroups) {
       const int k = lst[x];
       const TriSlot h = tri_slot(a, k);
-      if (MERGED) {  // one piece: the counter at the slot's first CSR position
-        int32_t* cnt = sarr + (h.is_item ? a.B : 0) + h.base;
-        wait_count(a, cnt, h.count);
-        if (l == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next pass
+      if (MERGED) {
+        wait_count(a, sarr + k, h.count);
+        if (l == 0) __hip_atomic_store(sarr + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next pass
       }
       RowV<NV> G = zero_row<NV>();
       tri_add<LPR, NV, MERGED>(a, h, 0, h.count, 1, l, G);
@@ -2907,12 +2887,8 @@ __device__ __forceinline__ void tri_combine_region(const StepArgs& a, int cw, in
     for (int x = hw; x < n; x += a.hot_waves) {
       const int4 pc = pl[x];  // {slot, piece, pieces, piece base}
       const TriSlot h = tri_slot(a, pc.x);
+      if (MERGED) wait_count(a, sarr + pc.x, h.count);  // the slot's combining workgroup resets it
       const int o0 = (int)((int64_t)pc.y * h.count / pc.z), o1 = (int)((int64_t)(pc.y + 1) * h.count / pc.z);
-      if (MERGED) {  // the piece's counter: at its first occurrence's CSR position
-        int32_t* cnt = sarr + (h.is_item ? a.B : 0) + h.base + o0;
-        wait_count(a, cnt, o1 - o0);
-        if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next pass
-      }
       RowV<NV> G = zero_row<NV>();
       tri_add<LPR, NV, MERGED>(a, h, o0 + g, o1, TEAM, l, G);
       team_allreduce<LPR, TEAM, NV>(G);
@@ -2938,6 +2914,7 @@ __device__ __forceinline__ void tri_combine_region(const StepArgs& a, int cw, in
       wait_count(a, arrive + e.z, e.y);
       // every piece of this pass is in: ready for the next pass over the batch
       __hip_atomic_store(arrive + e.z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (MERGED) __hip_atomic_store(sarr + e.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     hot_combine_slot<LPR, NV, MODE, true>(a, e, red);
