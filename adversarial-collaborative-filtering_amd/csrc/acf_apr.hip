@@ -1057,12 +1057,6 @@ struct StepArgs {
   float* hot_part;     // [piece_stride, d]
   int32_t hot_waves;
   int32_t hot_blocks;  // k_tri_combine: hot-slot combining workgroups after the piece waves (0: k_hot_combine)
-  // merged triplet pass (k_tri_clean / k_tri_adv with the combine appended): the
-  // first tri_waves waves are triplet waves (0: not merged), the combine section
-  // follows with comb_slot_waves slot waves, hot_waves piece waves, hot_blocks
-  // workgroups; slot_arrive counts the stored contributions of each shared slot
-  int32_t tri_waves, comb_slot_waves;
-  int32_t* slot_arrive;  // [nb][S]
   // shard mode (distributed.ShardedAPR): item rows of the batch are this rank's
   // partial sums; an item slot's clean / adversarial sum goes to g0[k] for the
   // exchange instead of Adagrad, and item rows are never written back
@@ -2584,14 +2578,6 @@ __global__ void __launch_bounds__(256) k_adv_list(StepArgs a) {
 __device__ __forceinline__ float* tri_cu(const StepArgs& a) { return a.contrib; }
 __device__ __forceinline__ float* tri_ci(const StepArgs& a) { return a.contrib + (int64_t)2 * a.B * a.d; }
 
-// a shared row's contribution: write-through when the combine runs in the same
-// launch (merged pass; its reader polls the slot's arrival count)
-template <int LPR, int NV>
-__device__ __forceinline__ void store_contrib(const StepArgs& a, float* base, int64_t row, int l, const RowV<NV>& v) {
-  if (a.tri_waves) store_row_wt<LPR, NV>(base, row, a.d, l, v);
-  else store_row<LPR, NV>(base, row, a.d, l, v);
-}
-
 // PASS 0: APR clean (shared rows: clean contributions; single rows: nothing,
 // k_tri_adv recomputes their term); 1: BPR (single rows: Adagrad; shared:
 // contributions); 2: APR adversarial.
@@ -2639,11 +2625,11 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
   if ((PASS != 2 || (flags & 1)) && l == 0) a.loss_clean[e] = loss;
   if (PASS != 2) {  // clean contributions of the shared rows
     if (!su) {
-      store_contrib<LPR, NV>(a, cuB, 2 * lu, l, scale_row(qi, g));
-      store_contrib<LPR, NV>(a, cuB, 2 * lu + 1, l, scale_row(qj, -g));
+      store_row<LPR, NV>(cuB, 2 * lu, d, l, scale_row(qi, g));
+      store_row<LPR, NV>(cuB, 2 * lu + 1, d, l, scale_row(qj, -g));
     }
-    if (!si) store_contrib<LPR, NV>(a, ciB, li, l, scale_row(p, g));
-    if (!sj) store_contrib<LPR, NV>(a, ciB, lj, l, scale_row(p, -g));
+    if (!si) store_row<LPR, NV>(ciB, li, d, l, scale_row(p, g));
+    if (!sj) store_row<LPR, NV>(ciB, lj, d, l, scale_row(p, -g));
     if (PASS == 0) return;
   }
   // the single rows' clean gradients (k_single's order)
@@ -2661,11 +2647,11 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
     bpr_term(dot_row<LPR, NV>(pp, qip) - dot_row<LPR, NV>(pp, qjp), a.clip_lo, a.clip_hi, ga, la);
     if (l == 0) a.loss_adv[e] = la;
     if (!su) {
-      store_contrib<LPR, NV>(a, cuB, 2 * lu, l, scale_row(qip, ga));
-      store_contrib<LPR, NV>(a, cuB, 2 * lu + 1, l, scale_row(qjp, -ga));
+      store_row<LPR, NV>(cuB, 2 * lu, d, l, scale_row(qip, ga));
+      store_row<LPR, NV>(cuB, 2 * lu + 1, d, l, scale_row(qjp, -ga));
     }
-    if (!si) store_contrib<LPR, NV>(a, ciB, li, l, scale_row(pp, ga));
-    if (!sj) store_contrib<LPR, NV>(a, ciB, lj, l, scale_row(pp, -ga));
+    if (!si) store_row<LPR, NV>(ciB, li, d, l, scale_row(pp, ga));
+    if (!sj) store_row<LPR, NV>(ciB, lj, d, l, scale_row(pp, -ga));
     if (su) {
       RowV<NV> Au = zero_row<NV>();
       axpy_row(Au, ga, qip);
@@ -2731,21 +2717,6 @@ __device__ __forceinline__ void tri_triplets(const StepArgs& a, int tw, int lane
   for (int x = 0; x < GPW; ++x) tri_rec(a, b0 + x * OPW, r[x], ps[x]);
 #pragma unroll
   for (int x = 0; x < GPW; ++x) tri_triplet_r<LPR, NV, PASS>(a, b0 + x * OPW, lane & (LPR - 1), r[x], ps[x]);
-  if (!a.tri_waves) return;
-  // merged pass: once the wave's write-through stores have drained, count every
-  // shared-row contribution at its slot (one lane per lane-group)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if ((lane & (LPR - 1)) != 0) return;
-  const int32_t gen = *a.gen_ptr;
-  int32_t* arr = a.slot_arrive + (int64_t)a.t * a.S;
-#pragma unroll
-  for (int x = 0; x < GPW; ++x) {
-    if (b0 + x * OPW >= a.B || r[x].c.w != gen) continue;
-    const int flags = r[x].c.y;
-    if (!(flags & TRI_SU)) __hip_atomic_fetch_add(arr + r[x].a.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!(flags & TRI_SI)) __hip_atomic_fetch_add(arr + r[x].b.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!(flags & TRI_SJ)) __hip_atomic_fetch_add(arr + r[x].b.y, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // header of shared slot k: count, side, own row, source, local CSR base
@@ -2767,31 +2738,19 @@ __device__ __forceinline__ TriSlot tri_slot(const StepArgs& a, int k) {
 
 // contributions of occurrences [o0, o1) of a slot, added in order (a user
 // occurrence: its positive, then its negative branch, as the slot path's axpys)
-template <int LPR, int NV, bool SC1 = false>
+template <int LPR, int NV>
 __device__ __forceinline__ void tri_add(const StepArgs& a, const TriSlot& h, int o0, int o1, int step, int l,
                                         RowV<NV>& G) {
   const int d = a.d;
   if (h.is_item) {
     const float* c = tri_ci(a);
-    for (int o = o0; o < o1; o += step) G = add_row(G, load_piece<LPR, NV, SC1>(c, h.base + o, d, l));
+    for (int o = o0; o < o1; o += step) G = add_row(G, load_row<LPR, NV>(c, h.base + o, d, l));
   } else {
     const float* c = tri_cu(a);
     for (int o = o0; o < o1; o += step) {
-      G = add_row(G, load_piece<LPR, NV, SC1>(c, 2 * (h.base + o), d, l));
-      G = add_row(G, load_piece<LPR, NV, SC1>(c, 2 * (h.base + o) + 1, d, l));
+      G = add_row(G, load_row<LPR, NV>(c, 2 * (h.base + o), d, l));
+      G = add_row(G, load_row<LPR, NV>(c, 2 * (h.base + o) + 1, d, l));
     }
-  }
-}
-
-// spin (device-scope loads) until *p >= target; bounded: a give-up sets the step error bit
-__device__ __forceinline__ void wait_count(const StepArgs& a, const int32_t* p, int32_t target) {
-  int it = 0;
-  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (++it > ACF_SPIN_LIMIT) {
-      atomicOr(a.step_err, 1);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(2);
   }
 }
 
@@ -2823,18 +2782,12 @@ __device__ __forceinline__ void tri_finish(const StepArgs& a, int k, const TriSl
   else store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
 }
 
-template <int LPR, int NV, int MODE, bool MERGED>
-__device__ __forceinline__ void tri_combine_region(const StepArgs& a, int cw, int sw, float4* __restrict__ red);
-
 template <int LPR, int NV, bool BPR>
 __global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
-  __shared__ float4 red[NV * 256];
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
   if (wave >= a.slot_waves) {
-    const int tw = wave - a.slot_waves;
-    if (!a.tri_waves || tw < a.tri_waves) tri_triplets<LPR, NV, BPR ? 1 : 0>(a, tw, lane);
-    else tri_combine_region<LPR, NV, BPR ? 1 : 0, true>(a, tw - a.tri_waves, a.comb_slot_waves, red);
+    tri_triplets<LPR, NV, BPR ? 1 : 0>(a, wave - a.slot_waves, lane);
     return;
   }
   if (!a.prev_valid) return;  // write-back of the rows batch t-1 left in W scratch
@@ -2844,42 +2797,35 @@ __global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
   for (int x = gid; x < n; x += ngroups) flush_slot(a, a.t - 1, a.wnew_prev, lst[x], l, LPR);
 }
 
-// The combine of a pass (wave cw of the section): shared slots with <=
-// ACF_HOT_MIN occurrences, one lane-group each, their contributions in order;
-// hot slots: piece waves [sw, sw + hot_waves) into hot_part, then hot_blocks
-// workgroups that each combine hot slots as k_hot_combine does once all their
-// pieces are stored.  A piece is stored write-through, the wave drains its
-// stores, and one lane adds 1 to the slot's arrival count; a combining workgroup
-// polls that count (device scope), and every load of the pieces is a
-// device-scope load (Guideline 16, row 1).  MERGED (the section follows the
-// pass's own triplet waves in one launch): slot lane-groups and piece waves
-// first wait for all of their slot's contributions the same way (slot_arrive),
-// which the triplet waves stored write-through.  Every wait is on waves that
-// come earlier in dispatch order and never wait themselves on later ones, so
-// the launch always drains.
-template <int LPR, int NV, int MODE, bool MERGED>
-__device__ __forceinline__ void tri_combine_region(const StepArgs& a, int cw, int sw, float4* __restrict__ red) {
+// shared slots with <= ACF_HOT_MIN occurrences: one lane-group each, in order;
+// hot slots: piece waves [slot_waves, slot_waves + hot_waves) into hot_part, then
+// hot_blocks workgroups (waves from slot_waves + hot_waves on) that each combine
+// hot slots as k_hot_combine does once all their pieces are stored.  A piece is
+// stored write-through, the wave drains its stores, and one lane adds 1 to the
+// slot's arrival count; a combining workgroup polls that count (device scope),
+// and every load of the pieces is a device-scope load (Guideline 16, row 1).
+// The combining workgroups come after every piece wave in dispatch order, so
+// the pieces they wait for are already running: the launch always drains.
+template <int LPR, int NV, int MODE>
+__global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
+  __shared__ float4 red[NV * 256];
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
-  int32_t* sarr = a.slot_arrive + (int64_t)a.t * a.S;
-  if (cw < sw) {
-    const int ngroups = sw * (64 / LPR), gid = cw * (64 / LPR) + g;
+  if (wave < a.slot_waves) {
+    const int ngroups = a.slot_waves * (64 / LPR), gid = wave * (64 / LPR) + g;
     const int n = a.slot_cnt[a.t];
     const int32_t* lst = a.slot_list + (int64_t)a.t * a.S;
     for (int x = gid; x < n; x += ngroups) {
       const int k = lst[x];
       const TriSlot h = tri_slot(a, k);
-      if (MERGED) {
-        wait_count(a, sarr + k, h.count);
-        if (l == 0) __hip_atomic_store(sarr + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next pass
-      }
       RowV<NV> G = zero_row<NV>();
-      tri_add<LPR, NV, MERGED>(a, h, 0, h.count, 1, l, G);
+      tri_add<LPR, NV>(a, h, 0, h.count, 1, l, G);
       tri_finish<LPR, NV, MODE>(a, k, h, G, l);
     }
     return;
   }
   int32_t* arrive = a.hot.arrive + (int64_t)a.t * a.hot.piece_stride;
-  const int hw = cw - sw;
+  const int hw = wave - a.slot_waves;
   if (hw < a.hot_waves) {
     constexpr int TEAM = 64 / LPR;
     const int n = a.hot.pcnt[a.t];
@@ -2887,10 +2833,9 @@ __device__ __forceinline__ void tri_combine_region(const StepArgs& a, int cw, in
     for (int x = hw; x < n; x += a.hot_waves) {
       const int4 pc = pl[x];  // {slot, piece, pieces, piece base}
       const TriSlot h = tri_slot(a, pc.x);
-      if (MERGED) wait_count(a, sarr + pc.x, h.count);  // the slot's combining workgroup resets it
       const int o0 = (int)((int64_t)pc.y * h.count / pc.z), o1 = (int)((int64_t)(pc.y + 1) * h.count / pc.z);
       RowV<NV> G = zero_row<NV>();
-      tri_add<LPR, NV, MERGED>(a, h, o0 + g, o1, TEAM, l, G);
+      tri_add<LPR, NV>(a, h, o0 + g, o1, TEAM, l, G);
       team_allreduce<LPR, TEAM, NV>(G);
       if (a.hot_blocks == 0) {  // combined by k_hot_combine (the next launch)
         if (g == 0) store_row<LPR, NV>(a.hot_part, (int64_t)pc.w + pc.y, a.d, l, G);
@@ -2902,40 +2847,35 @@ __device__ __forceinline__ void tri_combine_region(const StepArgs& a, int cw, in
     }
     return;
   }
-  // hot-slot combining workgroups (whole workgroups: the section's start and sw +
-  // hot_waves are multiples of 4 waves)
-  const int hb = (hw - a.hot_waves) >> 2;
+  // hot-slot combining workgroups (whole workgroups: slot_waves + hot_waves is a multiple of 4)
+  const int hb = (wave - a.slot_waves - a.hot_waves) >> 2;
   if (hb >= a.hot_blocks) return;
   const int n = a.hot.cnt[a.t];
   const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
   for (int hx = hb; hx < n; hx += a.hot_blocks) {
     const int4 e = hl[hx];  // {slot, pieces, piece base, count}
     if (threadIdx.x == 0) {
-      wait_count(a, arrive + e.z, e.y);
+      int it = 0;
+      while (__hip_atomic_load(arrive + e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.y) {
+        if (++it > ACF_SPIN_LIMIT) {
+          atomicOr(a.step_err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
       // every piece of this pass is in: ready for the next pass over the batch
       __hip_atomic_store(arrive + e.z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (MERGED) __hip_atomic_store(sarr + e.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     hot_combine_slot<LPR, NV, MODE, true>(a, e, red);
   }
 }
 
-// the combine of a pass as its own launch (after the triplet kernel)
-template <int LPR, int NV, int MODE>
-__global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
-  __shared__ float4 red[NV * 256];
-  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
-  tri_combine_region<LPR, NV, MODE, false>(a, wave, a.slot_waves, red);
-}
-
 // k_tri_adv: 4 blocks (16 waves) per CU asked of the register allocator (d <= 256)
 template <int LPR, int NV>
 __global__ void __launch_bounds__(256, NV == 1 ? 4 : 1) k_tri_adv(StepArgs a) {
-  __shared__ float4 red[NV * 256];
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
-  if (!a.tri_waves || wave < a.tri_waves) tri_triplets<LPR, NV, 2>(a, wave, threadIdx.x & 63);
-  else tri_combine_region<LPR, NV, 2, true>(a, wave - a.tri_waves, a.comb_slot_waves, red);
+  tri_triplets<LPR, NV, 2>(a, wave, threadIdx.x & 63);
 }
 
 // Flush the pending rows of batch t (wnew_cur) to the tables (end of a call):
@@ -3403,7 +3343,6 @@ struct acf_apr_ctx {
   int32_t shard = 0;            // shard mode (acf_apr_set_shard_mode): item rows are partial sums
   int32_t tri = 0;              // the plan is triplet-centric (packed, not shard: k_tri_*)
   float* contrib = nullptr;     // [4 maxB, d] per-occurrence contributions of shared rows (k_tri_*)
-  int32_t* slot_arrive = nullptr;  // [maxNB][3 maxB] stored contributions per shared slot (merged k_tri_*)
   int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
@@ -3553,7 +3492,6 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->hot.list, (size_t)maxNB * c->hot.hot_stride); A(&c->hot.piece, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot.cnt, 2 * (size_t)maxNB);
   A(&c->hot.arrive, (size_t)maxNB * c->hot.piece_stride);
-  A(&c->slot_arrive, 3 * maxE);
   A(&c->hot_part, (size_t)c->hot.piece_stride * d);
   A(&c->contrib, (size_t)4 * maxB * d);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
@@ -3817,7 +3755,6 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
     HIP_TRY(hipMemsetAsync(c->key_in, 0, (size_t)3 * E * sizeof(uint64_t), s));
     HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
     HIP_TRY(hipMemsetAsync(c->hot.arrive, 0, (size_t)nb * c->hot.piece_stride * sizeof(int32_t), s));
-    HIP_TRY(hipMemsetAsync(c->slot_arrive, 0, (size_t)nb * 3 * B * sizeof(int32_t), s));
   }
   k_records<<<grid_for(E), 256, 0, s>>>(E, B, 3 * B, c->plan_R, gen, kb, c->shard, c->tri,
                                         reinterpret_cast<const int4*>(c->tsl),
@@ -3896,9 +3833,6 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.hot_part = c->hot_part;
   a.hot_waves = 0;
   a.hot_blocks = 0;
-  a.tri_waves = 0;
-  a.comb_slot_waves = 0;
-  a.slot_arrive = c->slot_arrive;
   a.shard = c->shard;
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
@@ -4229,21 +4163,24 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
       ah.slot_waves = 4 * HB;
       StepArgs at = a;
       at.slot_waves = 0;  // k_tri_clean: triplet waves only (no write-back of t-1)
-      // one launch per pass: the triplet waves, then the pass's combine (slot
-      // lane-groups, hot pieces, hot-slot workgroups) waiting on arrival counts
-      const int TW4 = ((TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv) + 3) & ~3;
-      StepArgs am = at;
-      am.tri_waves = TW4;
-      am.comb_slot_waves = SW4;
-      am.hot_waves = HW4;
-      am.hot_blocks = HBT;
-      const int MW = TW4 + SW4 + HW4 + 4 * HBT;
+      StepArgs ac = a;
+      ac.slot_waves = SW4;
+      ac.hot_waves = HW4;
+      ac.hot_blocks = HBT;
+      const int CW = SW4 + HW4 + 4 * HBT;
       (void)ah;
       if (hp->adver) {
-        if (tri_phases & 1) ACF_RET(L(K.tri_clean, am, MW, 0));
-        if (tri_phases & 2) ACF_RET(L(K.tri_adv, am, MW, 1));
+        if (tri_phases & 1) {
+          ACF_RET(L(K.tri_clean, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
+          ACF_RET(L(K.tri_comb[0], ac, CW, 5));
+        }
+        if (tri_phases & 2) {
+          ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
+          ACF_RET(L(K.tri_comb[2], ac, CW, 5));
+        }
       } else if (tri_phases & 2) {
-        ACF_RET(L(K.tri_clean_bpr, am, MW, 0));
+        ACF_RET(L(K.tri_clean_bpr, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
+        ACF_RET(L(K.tri_comb[1], ac, CW, 5));
       }
     }
     if (!(tri_phases & 2)) return ACF_OK;  // delta_update: no call-counter bump
