@@ -5,21 +5,20 @@
 // binary cross-entropy + Adam) and scored by MF.py:38-40.  One training step
 // (Keras train_on_batch) here:
 //
-//   k_nmf_inst<CLEAN>   one workgroup per 16 instances: gather MF_U[u], MF_I[i],
-//                       MLP_U[u], MLP_I[i]; MLP [2d -> 2d -> d] relu on f32 MFMA
-//                       (16x16x4, exact f32 products); head; BCE
-//                       (prediction clipped to [1e-7, 1-1e-7]); backward through
-//                       head and MLP; per-instance row contributions + the
-//                       activations the weight gradients need (scratch)
-//   k_nmf_wpart/wsum    weight gradients as split-K outer-product sums: LDS
-//                       tiles of 32x32 outputs x 64 instances, then the chunks
-//                       summed in a fixed order (deterministic, no atomics)
+//   k_nmf_inst<CLEAN>   workgroups looping over blocks of 16 instances: gather
+//                       MF_U[u], MF_I[i], MLP_U[u], MLP_I[i]; MLP [2d -> 2d -> d]
+//                       relu on f32 MFMA (16x16x4, exact f32 products); head;
+//                       BCE (prediction clipped to [1e-7, 1-1e-7]); backward
+//                       through head and MLP; per-instance row contributions;
+//                       the weight gradients of the block (outer products over
+//                       its 16 instances on MFMA) into the workgroup's slot
 //   k_nmf_rows          one wave per (instance, side): the row's first
 //                       occurrence owns it and sums every occurrence's
 //                       contribution in instance order into the gradient row;
-//                       with adver also delta = eps * g / |g| of that row
-//   (adver) k_nmf_inst<ADV>, k_nmf_wgrad, k_nmf_rows on the perturbed rows,
-//                       scaled by reg_adv
+//                       with adver also delta = eps * g / |g| of that row.  The
+//                       step's last k_nmf_rows launch also sums the weight-
+//                       gradient slots in slot order (deterministic, no atomics)
+//   (adver) k_nmf_inst<ADV>, k_nmf_rows on the perturbed rows, scaled by reg_adv
 //   k_nmf_adam          Keras 2.2 Adam over the WHOLE flat parameter buffer
 //                       (Keras densifies the embedding IndexedSlices, so every
 //                       row's moments decay and every row moves): one HBM
@@ -98,9 +97,9 @@ struct NArgs {
   const float* y;
   int64_t U1, I1;
   int32_t B, d;
-  float scale_over_B;  // 1/B (clean) or reg_adv/B (adversarial)
-  // scratch [B, ...]
-  float *h0, *a1, *f, *dz1, *dz2, *dlogit, *loss, *contrib;  // contrib [B][4][d]
+  float scale_over_B;    // 1/B (clean) or reg_adv/B (adversarial)
+  float* contrib;        // [B][4][d] per-instance row contributions
+  float* wpart;          // [gridDim.x][nout] this pass's weight-gradient partials (one slot per workgroup)
   const float* delta;    // [B][4][d], rows written at their owner instance
   const int32_t* owner;  // [B][2] first occurrence of the instance's user / item
   float* pred;
@@ -111,7 +110,30 @@ __device__ __forceinline__ int32_t clamp_idx(int32_t r, int64_t n) { return (r <
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int MR = 16;  // instances per workgroup = the MFMA tile height
+constexpr int MR = 16;        // instances per block = the MFMA tile height
+constexpr int NSLOT = 256;    // workgroups (= weight-gradient partial slots) per training pass, at most
+constexpr int DFAST = 64;     // the dimension with a compile-time specialisation of k_nmf_inst
+
+// Weight-gradient partial vector of one workgroup: the parameter buffer's tail from
+// S_W1 on, element for element -- W1 [2d][2d] | b1 [2d] | W2 [2d][d] | b2 [d] |
+// Wo [2d] | bo | (pad: the loss sum, 2 spare) -- so slot element x is the gradient
+// of parameter off[S_W1] + x, and the slot sum can ride on the Adam stream.
+struct WOut {
+  int64_t w1, b1, w2, b2, wo, bo, loss, n;
+};
+
+__host__ __device__ __forceinline__ WOut wout(int64_t d) {
+  WOut o;
+  o.w1 = 0;
+  o.b1 = 4 * d * d;
+  o.w2 = o.b1 + 2 * d;
+  o.b2 = o.w2 + 2 * d * d;
+  o.wo = o.b2 + d;
+  o.bo = o.wo + 2 * d;
+  o.loss = o.bo + 1;
+  o.n = o.bo + 4;  // = Layout total - off[S_W1], a multiple of 4
+  return o;
+}
 
 // W1 and W2 are staged in LDS (row stride +1 float: the transposed reads of the
 // backward products are then conflict-free) when they fit beside the activations
@@ -122,7 +144,8 @@ __host__ __device__ __forceinline__ bool weights_in_lds(int d) { return d <= 64;
 // the 16 lanes reading one k hit different banks); w(k, n) = W[k*ldw + n], or
 // W[n*ldw + k] with TRANS (the backward products with W^T).  The 4 waves take
 // 32-column panels (two 16x16 tiles, two independent accumulators) round-robin;
-// epi(row, col, value) consumes every output element.
+// epi(row, col, value) consumes every output element.  With a compile-time d
+// every bound and offset folds to an immediate.
 // Lane maps (cdna_hip_programming.md §3): A[l&15][k0 + (l>>4)], B[k0 + (l>>4)][l&15],
 // C/D: col = l&15, row = 4*(l>>4) + reg.
 template <bool TRANS>
@@ -190,8 +213,78 @@ __device__ __forceinline__ void mfma_panel(const float* sA, int lda, const float
   }
 }
 
+// Weight gradients of a block over its MR instances, 16x16 output tiles:
+// W1 += h0^T dz1 [2d][2d], then W2 += a1^T dz2 [2d][d];
+// out[k][n] (+)= sum_t A[t][k] * Bm[t][n] with A / Bm in LDS (row t), a t-ordered
+// chain of 4 MFMAs per tile; each wave takes OG tiles at a time (independent
+// chains).  The slot is accumulated across the workgroup's blocks (ACC: add to what
+// this lane stored for the previous block -- the same lane, the same address).
+constexpr int OG = 4;
+
+// one weight gradient [K][N] (A rows with leading dimension lda, Bm rows ldb);
+// EXACT: K and N multiples of 16 (no bounds); tiles tt = wave + 4 * (OG*i + g)
+template <bool ACC, bool EXACT>
+__device__ __forceinline__ void outer_mat(const float* A, int lda, const float* Bm, int ldb, int K, int N,
+                                          float* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, h = lane >> 4;
+  const int tn = (N + 15) / 16, T = ((K + 15) / 16) * tn;
+  const float* Ar = A + h * lda + r;   // lane's element of row t = h, column r
+  const float* Br = Bm + h * ldb + r;
+  for (int tb = wave; tb < T; tb += 4 * OG) {
+    float av[OG][MR / 4], bv[OG][MR / 4];
+    int k0[OG], n0[OG];
+#pragma unroll
+    for (int g = 0; g < OG; ++g) {
+      const int tt = tb + 4 * g;  // wave-uniform
+      k0[g] = (tt / tn) * 16;
+      n0[g] = (tt % tn) * 16;
+#pragma unroll
+      for (int j = 0; j < MR / 4; ++j) {
+        const bool okA = tt < T && (EXACT || k0[g] + r < K), okB = tt < T && (EXACT || n0[g] + r < N);
+        av[g][j] = okA ? Ar[4 * j * lda + k0[g]] : 0.f;
+        bv[g][j] = okB ? Br[4 * j * ldb + n0[g]] : 0.f;
+      }
+    }
+    f32x4 c[OG];
+#pragma unroll
+    for (int g = 0; g < OG; ++g) c[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < MR / 4; ++j)
+#pragma unroll
+      for (int g = 0; g < OG; ++g) c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][j], bv[g][j], c[g], 0, 0, 0);
+#pragma unroll
+    for (int g = 0; g < OG; ++g) {
+      if (tb + 4 * g >= T) break;
+      float* o = out + (int64_t)(k0[g] + 4 * h) * N + n0[g] + r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (EXACT || (k0[g] + 4 * h + q < K && n0[g] + r < N)) {
+          float* p = o + (int64_t)q * N;
+          *p = ACC ? *p + c[g][q] : c[g][q];  // (ACC a template: no speculative load of the slot)
+        }
+      }
+    }
+  }
+}
+
+template <bool ACC, bool EXACT>
+__device__ __forceinline__ void outer_tiles(const float* s_h0, const float* s_dz1, const float* s_a1,
+                                            const float* s_dz2, int d, float* __restrict__ w1,
+                                            float* __restrict__ w2) {
+  const int d2 = 2 * d;
+  outer_mat<ACC, EXACT>(s_h0, d2 + 1, s_dz1, d2 + 1, d2, d2, w1);
+  outer_mat<ACC, EXACT>(s_a1, d2 + 1, s_dz2, d + 1, d2, d, w2);
+}
+
 #ifdef NMF_DIAG  // diagnostic build only: phase stamps (100 MHz) of workgroup 0, clean pass
 __device__ uint64_t g_nmf_stamps[16];
+__device__ uint64_t g_nmf_rstamps[8];  // k_nmf_rows, workgroup 0 wave 0 (owner of u[0]), clean pass
+#define RSTAMP(i)                                                                          \
+  do {                                                                                     \
+    uint64_t t_;                                                                           \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    if (with_delta && blockIdx.x == 0 && threadIdx.x == 0) g_nmf_rstamps[i] = t_;          \
+  } while (0)
 #define NSTAMP(i)                                                                          \
   do {                                                                                     \
     uint64_t t_;                                                                           \
@@ -202,57 +295,98 @@ __device__ uint64_t g_nmf_stamps[16];
 #define NSTAMP(i) \
   do {            \
   } while (0)
+#define RSTAMP(i) \
+  do {            \
+  } while (0)
 #endif
 
-template <int MODE>
+// One workgroup per slot, looping over blocks of MR instances (blk = blockIdx.x,
+// + gridDim.x, ...): the MLP forward (and, MODE 0 / 1, the backward) of a block on
+// MFMA with every operand in LDS, the row contributions to global scratch, and the
+// block's weight gradients accumulated into the workgroup's slot of a.wpart
+// (outer products on MFMA; bias / head / loss sums per owning thread).  MODE 2 is
+// prediction only.  DC = compile-time d (0: a.d at run time).
+template <int MODE, int DC>
 __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a) {
   extern __shared__ float sm[];
   NSTAMP(0);
-  const int d = a.d, d2 = 2 * d, tid = threadIdx.x;
+  const int d = DC ? DC : a.d, d2 = 2 * d, tid = threadIdx.x;
   const int L2 = d2 + 1, L1 = d + 1;  // padded leading dimensions
-  const int64_t b0 = (int64_t)blockIdx.x * MR;
-  const int nt = (int)min((int64_t)MR, (int64_t)a.B - b0);
-  float* s_x = sm;                 // [MR][L2]  h0 = MLP_U[u] | MLP_I[i]; later dz1
+  const int64_t nblk = ((int64_t)a.B + MR - 1) / MR;
+  float* s_x = sm;                 // [MR][L2]  h0 = MLP_U[u] | MLP_I[i]
   float* s_a1 = s_x + MR * L2;     // [MR][L2]
-  float* s_f = s_a1 + MR * L2;     // [MR][L2]  MF_U*MF_I | a2
+  float* s_f = s_a1 + MR * L2;     // [MR][L2]  MF_U*MF_I | a2; later dz1
   float* s_mu = s_f + MR * L2;     // [MR][L1]
   float* s_mi = s_mu + MR * L1;    // [MR][L1]
   float* s_dz2 = s_mi + MR * L1;   // [MR][L1]
-  float* s_dl = s_dz2 + MR * L1;   // [MR]
-  float* s_vec = s_dl + MR;        // b1 [2d] | b2 [d] | Wo [2d] | bo (+3)
+  float* s_dl = s_dz2 + MR * L1;   // [MR] d loss / d logit
+  float* s_ls = s_dl + MR;         // [MR] per-instance loss
+  float* s_vec = s_ls + MR;        // b1 [2d] | b2 [d] | Wo [2d] | bo (+3)
   float* s_b1 = s_vec, *s_b2 = s_vec + d2, *s_wo = s_b2 + d, *s_bo = s_wo + d2;
   float* s_w1 = s_bo + 4;          // [2d][2d+1] (weights_in_lds)
   float* s_w2 = s_w1 + d2 * L2;    // [2d][d+1]
   const bool wl = weights_in_lds(d);
-  // One round trip for everything the workgroup needs: each thread issues its
-  // index -> row gathers, its share of W1 / W2 and of the bias / head vectors,
-  // and only then stores them to LDS.
+  // Prologue, in issue order: the first block's indices (and owners), its row
+  // gathers, the weights, biases and head (once per workgroup), and only then the
+  // LDS stores -- the weights stream in behind the row gathers.
+  // Row gathers of a block: one round trip for the indices (and owners), one for
+  // every row element; no branch on the data (a bad index is clamped to row 0 and
+  // flagged once at the end).
   constexpr int QG = MR * 128 / 256;  // gather elements per thread (d <= 128)
+  // element x = tid + 256 q of the block's MR x d; with a compile-time d that is a
+  // multiple of 16 the live q are known and the gathers need no branch
+  auto live = [&](int q) { return (MR * d) % 256 == 0 ? q < MR * d / 256 : tid + 256 * q < MR * d; };
   float g[QG][4];
+  int bad = 0;
+  int32_t uu[QG], ii[QG], ou[QG], oi[QG];
+  auto gather_idx = [&](int64_t blk) {
+    const int64_t b0 = blk * MR;
+    const int nt = (int)min((int64_t)MR, (int64_t)a.B - b0);
 #pragma unroll
-  for (int q = 0; q < QG; ++q) {
-    const int x = tid + 256 * q;
-    const int t = x / d, k = x - t * d;
-    g[q][0] = g[q][1] = g[q][2] = g[q][3] = 0.f;
-    if (x < MR * d && t < nt) {
-      int32_t uu = a.u[b0 + t], ii = a.i[b0 + t];
-      if (uu < 0 || uu >= a.U1) { if (k == 0) atomicOr(a.err, 1); uu = 0; }
-      if (ii < 0 || ii >= a.I1) { if (k == 0) atomicOr(a.err, 2); ii = 0; }
-      const int64_t ru = (int64_t)uu * d + k, ri = (int64_t)ii * d + k;
-      g[q][0] = a.P[a.off[S_MF_U] + ru];
-      g[q][1] = a.P[a.off[S_MF_I] + ri];
-      g[q][2] = a.P[a.off[S_MLP_U] + ru];
-      g[q][3] = a.P[a.off[S_MLP_I] + ri];
+    for (int q = 0; q < QG; ++q) {
+      const int x = tid + 256 * q, t = x / d;
+      const int64_t b = b0 + ((x < MR * d && t < nt) ? t : 0);
+      uu[q] = a.u[b];
+      ii[q] = a.i[b];
       if (MODE == 1) {
-        const int64_t b = b0 + t;
-        const float* du = a.delta + (int64_t)a.owner[2 * b] * 4 * d;
-        const float* di = a.delta + (int64_t)a.owner[2 * b + 1] * 4 * d;
-        g[q][0] = g[q][0] + du[0 * d + k];
-        g[q][1] = g[q][1] + di[1 * d + k];
-        g[q][2] = g[q][2] + du[2 * d + k];
-        g[q][3] = g[q][3] + di[3 * d + k];
+        ou[q] = a.owner[2 * b];
+        oi[q] = a.owner[2 * b + 1];
       }
     }
+  };
+  auto gather_rows = [&](int64_t blk) {
+    const int64_t b0 = blk * MR;
+    const int nt = (int)min((int64_t)MR, (int64_t)a.B - b0);
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+      const int x = tid + 256 * q;
+      if (live(q)) {
+        const int t = x / d, k = x - t * d;
+        const bool ok = t < nt;
+        const bool ub = uu[q] < 0 || uu[q] >= a.U1, ib = ii[q] < 0 || ii[q] >= a.I1;
+        bad |= (ok && ub ? 1 : 0) | (ok && ib ? 2 : 0);
+        const int64_t ru = (int64_t)(ub ? 0 : uu[q]) * d + k, ri = (int64_t)(ib ? 0 : ii[q]) * d + k;
+        float v0 = a.P[a.off[S_MF_U] + ru], v1_ = a.P[a.off[S_MF_I] + ri];
+        float v2_ = a.P[a.off[S_MLP_U] + ru], v3 = a.P[a.off[S_MLP_I] + ri];
+        if (MODE == 1) {
+          const float* du = a.delta + (int64_t)ou[q] * 4 * d;
+          const float* di = a.delta + (int64_t)oi[q] * 4 * d;
+          v0 = v0 + du[0 * d + k];
+          v1_ = v1_ + di[1 * d + k];
+          v2_ = v2_ + du[2 * d + k];
+          v3 = v3 + di[3 * d + k];
+        }
+        g[q][0] = ok ? v0 : 0.f;
+        g[q][1] = ok ? v1_ : 0.f;
+        g[q][2] = ok ? v2_ : 0.f;
+        g[q][3] = ok ? v3 : 0.f;
+      }
+    }
+  };
+  int64_t blk = blockIdx.x;
+  if (blk < nblk) {
+    gather_idx(blk);
+    gather_rows(blk);
   }
   constexpr int Q1 = 64 * 64 * 4 / 4 / 256, Q2 = 64 * 64 * 2 / 4 / 256;  // weights_in_lds: d <= 64
   const int n1 = wl ? d2 * d2 / 4 : 0, n2 = wl ? d2 * d / 4 : 0;
@@ -279,7 +413,6 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a) {
       vv[q] = a.P[src];
     }
   }
-  // stores
 #pragma unroll
   for (int q = 0; q < QV; ++q)
     if (tid + 256 * q < nvec) s_vec[tid + 256 * q] = vv[q];
@@ -301,273 +434,330 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a) {
       dst[0] = v2[q].x; dst[1] = v2[q].y; dst[2] = v2[q].z; dst[3] = v2[q].w;
     }
   }
-#pragma unroll
-  for (int q = 0; q < QG; ++q) {
-    const int x = tid + 256 * q;
-    if (x < MR * d) {
-      const int t = x / d, k = x - t * d;
-      const float mu = g[q][0], mi = g[q][1], lu = g[q][2], li = g[q][3];
-      if (MODE != 2 && t < nt) {
-        a.h0[(b0 + t) * d2 + k] = lu;
-        a.h0[(b0 + t) * d2 + d + k] = li;
-      }
-      s_mu[t * L1 + k] = mu;
-      s_mi[t * L1 + k] = mi;
-      s_x[t * L2 + k] = lu;
-      s_x[t * L2 + d + k] = li;
-      s_f[t * L2 + k] = mu * mi;  // GMF tower
-    }
-  }
-  __syncthreads();
   NSTAMP(1);
-  NSTAMP(2);
   const float* W1 = wl ? s_w1 : a.P + a.off[S_W1];
   const float* W2 = wl ? s_w2 : a.P + a.off[S_W2];
   const int ld1 = wl ? L2 : d2, ld2 = wl ? L1 : d;
   const float* Wo = s_wo;
   const float* b1 = s_b1;
   const float* b2 = s_b2;
-  // layer 1: a1 = relu(h0 W1 + b1)
-  mfma_panel<false>(s_x, L2, W1, ld1, d2, d2, [&](int row, int col, float v) {
-    const float z = v + b1[col];
-    s_a1[row * L2 + col] = z > 0.f ? z : 0.f;
-  });
-  __syncthreads();
-  NSTAMP(3);
-  // layer 2: a2 = relu(a1 W2 + b2) -> f[d:2d]
-  mfma_panel<false>(s_a1, L2, W2, ld2, d2, d, [&](int row, int col, float v) {
-    const float z = v + b2[col];
-    s_f[row * L2 + d + col] = z > 0.f ? z : 0.f;
-  });
-  __syncthreads();
-  NSTAMP(4);
-  // head: 16 lanes per instance, p = sigmoid(f Wo + bo); Keras BCE on clip(p)
-  {
-    const int row = tid >> 4, part = tid & 15;
-    float sacc = 0.f;
-    for (int k = part; k < d2; k += 16) sacc = sacc + s_f[row * L2 + k] * Wo[k];
+  const WOut wo_ = wout(d);
+  float* slot = MODE == 2 ? nullptr : a.wpart + (int64_t)blockIdx.x * wo_.n;
+  // vector partials owned by threads across the workgroup's blocks
+  float acc_wo = 0.f, acc_b1 = 0.f, acc_b2 = 0.f, acc_bo = 0.f, acc_ls = 0.f;
+  for (int it = 0; blk < nblk; ++it, blk += gridDim.x) {
+    const int64_t b0 = blk * MR;
+    const int nt = (int)min((int64_t)MR, (int64_t)a.B - b0);
 #pragma unroll
-    for (int m = 1; m < 16; m <<= 1) sacc += __shfl_xor(sacc, m, 64);
-    if (part == 0) {
-      const float logit = sacc + s_bo[0];
-      const float p = 1.0f / (1.0f + expf(-logit));
-      if (MODE == 2) {
-        if (row < nt) a.pred[b0 + row] = p;
-      } else {
-        const float y = row < nt ? a.y[b0 + row] : 0.f;
-        const bool inside = p >= 1e-7f && p <= 1.0f - 1e-7f;  // clip_by_value's gradient
-        const float dl = (row < nt && inside) ? (p - y) * a.scale_over_B : 0.f;
-        const float pc = fminf(fmaxf(p, 1e-7f), 1.0f - 1e-7f);
-        s_dl[row] = dl;
-        if (row < nt) {
-          a.dlogit[b0 + row] = dl;
-          a.loss[b0 + row] = -(y * logf(pc) + (1.0f - y) * logf(1.0f - pc));
+    for (int q = 0; q < QG; ++q) {
+      const int x = tid + 256 * q;
+      if (live(q)) {
+        const int t = x / d, k = x - t * d;
+        const float mu = g[q][0], mi = g[q][1], lu = g[q][2], li = g[q][3];
+        s_mu[t * L1 + k] = mu;
+        s_mi[t * L1 + k] = mi;
+        s_x[t * L2 + k] = lu;
+        s_x[t * L2 + d + k] = li;
+        s_f[t * L2 + k] = mu * mi;  // GMF tower
+      }
+    }
+    __syncthreads();
+    // the next block's rows fly while this one computes
+    if (blk + gridDim.x < nblk) {
+      gather_idx(blk + gridDim.x);
+      gather_rows(blk + gridDim.x);
+    }
+    NSTAMP(2);
+    // layer 1: a1 = relu(h0 W1 + b1)
+    mfma_panel<false>(s_x, L2, W1, ld1, d2, d2, [&](int row, int col, float v) {
+      const float z = v + b1[col];
+      s_a1[row * L2 + col] = z > 0.f ? z : 0.f;
+    });
+    __syncthreads();
+    NSTAMP(3);
+    // layer 2: a2 = relu(a1 W2 + b2) -> f[d:2d]
+    mfma_panel<false>(s_a1, L2, W2, ld2, d2, d, [&](int row, int col, float v) {
+      const float z = v + b2[col];
+      s_f[row * L2 + d + col] = z > 0.f ? z : 0.f;
+    });
+    __syncthreads();
+    NSTAMP(4);
+    // head: 16 lanes per instance, p = sigmoid(f Wo + bo); Keras BCE on clip(p)
+    {
+      const int row = tid >> 4, part = tid & 15;
+      float sacc = 0.f;
+      for (int k = part; k < d2; k += 16) sacc = sacc + s_f[row * L2 + k] * Wo[k];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) sacc += __shfl_xor(sacc, m, 64);
+      if (part == 0) {
+        const float logit = sacc + s_bo[0];
+        const float p = 1.0f / (1.0f + expf(-logit));
+        if (MODE == 2) {
+          if (row < nt) a.pred[b0 + row] = p;
+        } else {
+          const float y = row < nt ? a.y[b0 + row] : 0.f;
+          const bool inside = p >= 1e-7f && p <= 1.0f - 1e-7f;  // clip_by_value's gradient
+          const float pc = fminf(fmaxf(p, 1e-7f), 1.0f - 1e-7f);
+          s_dl[row] = (row < nt && inside) ? (p - y) * a.scale_over_B : 0.f;
+          s_ls[row] = row < nt ? -(y * logf(pc) + (1.0f - y) * logf(1.0f - pc)) : 0.f;
         }
       }
     }
+    __syncthreads();
+    if (MODE == 2) continue;
+    NSTAMP(5);
+    // dz2 = (dl * Wo[d:2d]) * (a2 > 0); GMF row contributions dmf * MF_I / dmf * MF_U;
+    // the head's weight gradients (f^T dl, sum dl) and the loss sum
+    for (int x = tid; x < MR * d; x += 256) {
+      const int t = x / d, k = x - t * d;
+      const float dl = s_dl[t];
+      const float dz = s_f[t * L2 + d + k] > 0.f ? dl * Wo[d + k] : 0.f;
+      s_dz2[t * L1 + k] = dz;
+      if (t < nt) {
+        const float dmf = dl * Wo[k];
+        a.contrib[((b0 + t) * 4 + S_MF_U) * d + k] = dmf * s_mi[t * L1 + k];
+        a.contrib[((b0 + t) * 4 + S_MF_I) * d + k] = dmf * s_mu[t * L1 + k];
+      }
+    }
+    if (tid < d2)
+      for (int t = 0; t < nt; ++t) acc_wo = acc_wo + s_f[t * L2 + tid] * s_dl[t];
+    if (tid == 0)
+      for (int t = 0; t < nt; ++t) {
+        acc_bo = acc_bo + s_dl[t];
+        acc_ls = acc_ls + s_ls[t];
+      }
+    __syncthreads();
+    NSTAMP(6);
+    // dz1 = (dz2 W2^T) * (a1 > 0) -> s_f (f is spent)
+    mfma_panel<true>(s_dz2, L1, W2, ld2, d, d2, [&](int row, int col, float v) {
+      s_f[row * L2 + col] = s_a1[row * L2 + col] > 0.f ? v : 0.f;
+    });
+    __syncthreads();
+    NSTAMP(7);
+    // dh0 = dz1 W1^T -> MLP_U / MLP_I row contributions
+    mfma_panel<true>(s_f, L2, W1, ld1, d2, d2, [&](int row, int col, float v) {
+      if (row < nt) {
+        const int tab = col < d ? S_MLP_U : S_MLP_I, kk = col < d ? col : col - d;
+        a.contrib[((b0 + row) * 4 + tab) * d + kk] = v;
+      }
+    });
+    NSTAMP(8);
+    // weight gradients: W1 += h0^T dz1 [2d][2d], W2 += a1^T dz2 [2d][d] (16x16 tiles
+    // round-robin over the waves), b1 += sum dz1, b2 += sum dz2
+    {
+      constexpr bool EX = DC != 0 && DC % 16 == 0;
+      if (it == 0)
+        outer_tiles<false, EX>(s_x, s_f, s_a1, s_dz2, d, slot + wo_.w1, slot + wo_.w2);
+      else
+        outer_tiles<true, EX>(s_x, s_f, s_a1, s_dz2, d, slot + wo_.w1, slot + wo_.w2);
+      NSTAMP(9);
+      if (tid < d2)
+        for (int t = 0; t < nt; ++t) acc_b1 = acc_b1 + s_f[t * L2 + tid];
+      if (tid < d)
+        for (int t = 0; t < nt; ++t) acc_b2 = acc_b2 + s_dz2[t * L1 + tid];
+    }
+    __syncthreads();
+    NSTAMP(10);
   }
-  if (MODE == 2) return;
-  __syncthreads();
-  NSTAMP(5);
-  // dz2 = (dl * Wo[d:2d]) * (a2 > 0); GMF row contributions dmf * MF_I / dmf * MF_U
-  for (int x = tid; x < MR * d; x += 256) {
-    const int t = x / d, k = x - t * d;
-    const float dl = s_dl[t];
-    const float dz = s_f[t * L2 + d + k] > 0.f ? dl * Wo[d + k] : 0.f;
-    s_dz2[t * L1 + k] = dz;
-    if (t < nt) {
-      const float dmf = dl * Wo[k];
-      a.contrib[((b0 + t) * 4 + S_MF_U) * d + k] = dmf * s_mi[t * L1 + k];
-      a.contrib[((b0 + t) * 4 + S_MF_I) * d + k] = dmf * s_mu[t * L1 + k];
-      a.dz2[(b0 + t) * d + k] = dz;
+  if (MODE != 2) {
+    if (tid < d2) {
+      slot[wo_.wo + tid] = acc_wo;
+      slot[wo_.b1 + tid] = acc_b1;
+    }
+    if (tid < d) slot[wo_.b2 + tid] = acc_b2;
+    if (tid == 0) {
+      slot[wo_.bo] = acc_bo;
+      slot[wo_.loss] = acc_ls;
     }
   }
-  __syncthreads();
-  NSTAMP(6);
-  // dz1 = (dz2 W2^T) * (a1 > 0) -> s_x (h0 is already in the scratch)
-  mfma_panel<true>(s_dz2, L1, W2, ld2, d, d2, [&](int row, int col, float v) {
-    s_x[row * L2 + col] = s_a1[row * L2 + col] > 0.f ? v : 0.f;
-  });
-  __syncthreads();
-  NSTAMP(7);
-  // dh0 = dz1 W1^T -> MLP_U / MLP_I row contributions
-  mfma_panel<true>(s_x, L2, W1, ld1, d2, d2, [&](int row, int col, float v) {
-    if (row < nt) {
-      const int tab = col < d ? S_MLP_U : S_MLP_I, kk = col < d ? col : col - d;
-      a.contrib[((b0 + row) * 4 + tab) * d + kk] = v;
-    }
-  });
-  // activations for the weight gradients
-  for (int x = tid; x < MR * d2; x += 256) {
-    const int t = x / d2, k = x - t * d2;
-    if (t < nt) {
-      const int64_t g = (b0 + t) * d2 + k;
-      a.a1[g] = s_a1[t * L2 + k];
-      a.f[g] = s_f[t * L2 + k];
-      a.dz1[g] = s_x[t * L2 + k];
-    }
-  }
-  NSTAMP(8);
+  if (bad) atomicOr(a.err, bad);
 }
 
-// Weight gradients: every one is a sum over the batch of an outer product,
-// out[k][n] = sum_b A[b][k] * Bm[b][n] (A = 1 for biases and the loss):
-//   0 W1 = h0^T dz1 [2d,2d]   1 W2 = a1^T dz2 [2d,d]   2 Wo = f^T dlogit [2d,1]
-//   3 b1 = 1^T dz1 [1,2d]     4 b2 = 1^T dz2 [1,d]     5 bo = 1^T dlogit   6 loss sum
-// k_nmf_wpart: one workgroup per (32x32 output tile, chunk of 64 instances),
-// operands staged in LDS, 4 outputs per thread, summed in instance order;
-// k_nmf_wsum: one thread per output, the chunks summed in order (deterministic).
-constexpr int WT = 32, WCH = 64, NMAT = 7;
+// Weight gradients of the step: slot element x summed over the passes' slots in
+// slot order (deterministic, no atomics); G += clean sum, then += adversarial sum;
+// the loss element gives the passes' mean losses.  k_nmf_adam does the same sums
+// in-line when it is handed the slots (acf_neumf_train).
+// (loads issued SB at a time, added in slot order)
+constexpr int SB = 8;
 
-struct WMat {
-  const float* A;  // [B][lda] or nullptr (ones)
-  const float* Bm; // [B][ldb]
-  int K, N, lda, ldb;
-  int64_t out_off;  // offset in the partial / output vector
-  int tiles_n, tile0;
-};
-
-struct WJobs {
-  WMat m[NMAT];
-  int ntiles;
-  int64_t nout;
-};
-
-static WJobs make_jobs(const NArgs& a) {
-  const int d = a.d, d2 = 2 * d;
-  WJobs J;
-  const float* ones = nullptr;
-  const WMat base[NMAT] = {{a.h0, a.dz1, d2, d2, d2, d2, 0, 0, 0},  {a.a1, a.dz2, d2, d, d2, d, 0, 0, 0},
-                           {a.f, a.dlogit, d2, 1, d2, 1, 0, 0, 0},  {ones, a.dz1, 1, d2, 0, d2, 0, 0, 0},
-                           {ones, a.dz2, 1, d, 0, d, 0, 0, 0},      {ones, a.dlogit, 1, 1, 0, 1, 0, 0, 0},
-                           {ones, a.loss, 1, 1, 0, 1, 0, 0, 0}};
-  int64_t off = 0;
-  int tiles = 0;
-  for (int q = 0; q < NMAT; ++q) {
-    J.m[q] = base[q];
-    J.m[q].out_off = off;
-    J.m[q].tiles_n = (base[q].N + WT - 1) / WT;
-    J.m[q].tile0 = tiles;
-    off += (int64_t)base[q].K * base[q].N;
-    tiles += ((base[q].K + WT - 1) / WT) * J.m[q].tiles_n;
-  }
-  J.ntiles = tiles;
-  J.nout = off;
-  return J;
-}
-
-__global__ void __launch_bounds__(256) k_nmf_wpart(WJobs J, int B, float* __restrict__ part) {
-  __shared__ float sA[WCH][WT + 1], sB[WCH][WT + 1];
-  const int tile = blockIdx.x, chunk = blockIdx.y, tid = threadIdx.x;
-  int q = 0;
-  while (q + 1 < NMAT && tile >= J.m[q + 1].tile0) ++q;
-  const WMat& M = J.m[q];
-  const int lt = tile - M.tile0, kt = lt / M.tiles_n, ntl = lt - kt * M.tiles_n;
-  const int k0 = kt * WT, n0 = ntl * WT, b0 = chunk * WCH;
-  for (int x = tid; x < WCH * WT; x += 256) {
-    const int r = x / WT, c = x - r * WT, b = b0 + r;
-    const bool inb = b < B;
-    sA[r][c] = (inb && k0 + c < M.K) ? (M.A ? M.A[(int64_t)b * M.lda + k0 + c] : 1.0f) : 0.f;
-    sB[r][c] = (inb && n0 + c < M.N) ? M.Bm[(int64_t)b * M.ldb + n0 + c] : 0.f;
-  }
-  __syncthreads();
-  const int kl = tid >> 3, nl = (tid & 7) * 4;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  const int nb = min(WCH, B - b0);
-  for (int r = 0; r < nb; ++r) {
-    const float av = sA[r][kl];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = acc[j] + av * sB[r][nl + j];
-  }
-  const int k = k0 + kl;
-  if (k < M.K) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (n0 + nl + j < M.N) part[(int64_t)chunk * J.nout + M.out_off + (int64_t)k * M.N + n0 + nl + j] = acc[j];
-  }
-}
-
-__global__ void __launch_bounds__(256) k_nmf_wsum(NArgs a, WJobs J, int nchunks, const float* __restrict__ part,
-                                                  float* loss_out, int which) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= J.nout) return;
+__device__ __forceinline__ float slot_sum(const float* part, int p, int nslot, int64_t nout, int64_t x) {
   float acc = 0.f;
-  for (int c = 0; c < nchunks; ++c) acc = acc + part[(int64_t)c * J.nout + x];
-  const int64_t loss_at = J.m[6].out_off;
-  if (x == loss_at) {
-    if (loss_out) loss_out[which] = acc / (float)a.B;
+  const float* q = part + (int64_t)p * nslot * nout + x;
+  for (int s0 = 0; s0 < nslot; s0 += SB) {
+    float v[SB];
+#pragma unroll
+    for (int j = 0; j < SB; ++j) v[j] = s0 + j < nslot ? q[(int64_t)(s0 + j) * nout] : 0.f;
+#pragma unroll
+    for (int j = 0; j < SB; ++j)
+      if (s0 + j < nslot) acc = acc + v[j];
+  }
+  return acc;
+}
+
+// four consecutive elements (x a multiple of 4, nout a multiple of 4)
+__device__ __forceinline__ float4 slot_sum4(const float* part, int p, int nslot, int64_t nout, int64_t x) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4* q = reinterpret_cast<const float4*>(part + (int64_t)p * nslot * nout + x);
+  const int64_t st = nout / 4;
+  for (int s0 = 0; s0 < nslot; s0 += SB) {
+    float4 v[SB];
+#pragma unroll
+    for (int j = 0; j < SB; ++j) v[j] = s0 + j < nslot ? q[(s0 + j) * st] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < SB; ++j)
+      if (s0 + j < nslot) {
+        acc.x = acc.x + v[j].x;
+        acc.y = acc.y + v[j].y;
+        acc.z = acc.z + v[j].z;
+        acc.w = acc.w + v[j].w;
+      }
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void wsum_one(const NArgs& a, int64_t x, int nslot, int npass, const float* part,
+                                         float* loss_out) {
+  const WOut o = wout(a.d);
+  if (x > o.loss) return;
+  const float acc0 = slot_sum(part, 0, nslot, o.n, x);
+  const float acc1 = npass > 1 ? slot_sum(part, 1, nslot, o.n, x) : 0.f;
+  if (x == o.loss) {
+    if (loss_out) {
+      loss_out[0] = acc0 / (float)a.B;
+      loss_out[1] = npass > 1 ? acc1 / (float)a.B : 0.f;
+    }
     return;
   }
-  // output segment -> parameter segment
-  static constexpr int seg_of[NMAT - 1] = {S_W1, S_W2, S_WO, S_B1, S_B2, S_BO};
-  int q = 0;
-  while (q + 1 < NMAT - 1 && x >= J.m[q + 1].out_off) ++q;
-  float* dst = a.G + a.off[seg_of[q]] + (x - J.m[q].out_off);
-  *dst = *dst + acc;
+  float* dst = a.G + a.off[S_W1] + x;
+  float v = *dst + acc0;
+  if (npass > 1) v = v + acc1;
+  *dst = v;
 }
 
-constexpr int MAX_Q = 2;  // d <= 128: each lane holds up to 2 of a row's elements
+constexpr int MAX_Q = 2;   // d <= 128: each lane holds up to 2 of a row's elements
+constexpr int RCH = 2048;  // batch indices staged in LDS per round
+constexpr int RBATCH = 8;  // occurrences whose contributions are loaded together
 
 // One wave per (instance b, side s): s = 0 the user's MF_U / MLP_U rows, s = 1
 // the item's MF_I / MLP_I rows.  The first occurrence of the row in the batch
 // owns it: sums all its occurrences' contributions in instance order, adds the
 // sum to the gradient rows and (with_delta) writes delta = eps*g/|g| per table.
+// The workgroup stages the batch's indices in LDS (rounds of RCH); an owner's
+// occurrences are loaded RBATCH at a time and added in order.  Workgroups past
+// the rows' (blockIdx.x >= rows_blocks) sum the weight gradients (k_nmf_wsum's
+// work, fused into this launch).
 __global__ void __launch_bounds__(256) k_nmf_rows(NArgs a, int32_t* __restrict__ owner,
-                                                  float* __restrict__ delta, int with_delta,
-                                                  float eps) {
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  const int B = a.B, d = a.d;
-  if (wave >= 2 * (int64_t)B) return;
-  const int b = (int)(wave >> 1), s = (int)(wave & 1);
-  const int32_t* idx = s ? a.i : a.u;
-  const int64_t nrows = s ? a.I1 : a.U1;
-  const int32_t r = clamp_idx(idx[b], nrows);
-  int first = b;
-  for (int base = 0; base < b; base += 64) {
-    const int j = base + lane;
-    const bool m = j < b && clamp_idx(idx[j], nrows) == r;
-    const uint64_t mask = __ballot(m);
-    if (mask) {
-      first = base + __ffsll((unsigned long long)mask) - 1;
-      break;
-    }
+                                                  float* __restrict__ delta, int with_delta, float eps,
+                                                  unsigned rows_blocks, int nslot, int npass,
+                                                  const float* __restrict__ part, float* loss_out) {
+  if (blockIdx.x >= rows_blocks) {
+    wsum_one(a, (int64_t)(blockIdx.x - rows_blocks) * 256 + threadIdx.x, nslot, npass, part, loss_out);
+    return;
   }
-  if (lane == 0) owner[2 * b + s] = first;
-  if (first != b) return;
+  __shared__ int32_t s_idx[2][RCH];
+  RSTAMP(0);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int B = a.B, d = a.d;
+  const int64_t item = (int64_t)blockIdx.x * 4 + wave;
+  const bool live = item < 2 * (int64_t)B;
+  const int b = live ? (int)(item >> 1) : 0, s = (int)(item & 1);
+  const int64_t nrows = s ? a.I1 : a.U1;
+  const int32_t r = clamp_idx((s ? a.i : a.u)[b], nrows);
   const int tA = s ? S_MF_I : S_MF_U, tB = s ? S_MLP_I : S_MLP_U;
-  float gA[MAX_Q], gB[MAX_Q];
+  int first = -1;
+  float gA[MAX_Q], gB[MAX_Q], oA[MAX_Q], oB[MAX_Q];
+  // the row's gradient, fetched now (used if this wave owns the row)
 #pragma unroll
-  for (int q = 0; q < MAX_Q; ++q) gA[q] = gB[q] = 0.f;
-  for (int base = b; base < B; base += 64) {
-    const int j = base + lane;
-    uint64_t mask = __ballot(j < B && clamp_idx(idx[j], nrows) == r);
-    while (mask) {
-      const int jj = base + __ffsll((unsigned long long)mask) - 1;
-      mask &= mask - 1;
+  for (int q = 0; q < MAX_Q; ++q) {
+    const int k = lane + 64 * q;
+    gA[q] = gB[q] = 0.f;
+    oA[q] = live && k < d ? a.G[a.off[tA] + (int64_t)r * d + k] : 0.f;
+    oB[q] = live && k < d ? a.G[a.off[tB] + (int64_t)r * d + k] : 0.f;
+  }
+  for (int c0 = 0; c0 < B; c0 += RCH) {
+    const int n = min(RCH, B - c0);
+    if (c0 > 0) __syncthreads();
+    int32_t su[RCH / 256], si[RCH / 256];
 #pragma unroll
-      for (int q = 0; q < MAX_Q; ++q) {
-        const int k = lane + 64 * q;
-        if (k < d) {
-          gA[q] = gA[q] + a.contrib[((int64_t)jj * 4 + tA) * d + k];
-          gB[q] = gB[q] + a.contrib[((int64_t)jj * 4 + tB) * d + k];
+    for (int q = 0; q < RCH / 256; ++q) {
+      const int x = threadIdx.x + 256 * q;
+      su[q] = x < n ? a.u[c0 + x] : 0;
+      si[q] = x < n ? a.i[c0 + x] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < RCH / 256; ++q) {
+      const int x = threadIdx.x + 256 * q;
+      if (x < n) {
+        s_idx[0][x] = clamp_idx(su[q], a.U1);
+        s_idx[1][x] = clamp_idx(si[q], a.I1);
+      }
+    }
+    __syncthreads();
+    RSTAMP(1);
+    if (!live) continue;
+    const int32_t* L = s_idx[s];
+    if (first < 0) {  // the first occurrence (b itself at the latest)
+      for (int base = 0; base < n && c0 + base <= b; base += 64) {
+        const int j = base + lane;
+        const uint64_t mask = __ballot(j < n && c0 + j <= b && L[j] == r);
+        if (mask) {
+          first = c0 + base + __ffsll((unsigned long long)mask) - 1;
+          break;
         }
       }
     }
+    RSTAMP(2);
+    if (first != b) continue;
+    for (int base = max(b - c0, 0) & ~63; base < n; base += 64) {
+      const int j = base + lane;
+      uint64_t mask = __ballot(j < n && c0 + j >= b && L[j] == r);
+      while (mask) {
+        int js[RBATCH];
+#pragma unroll
+        for (int e = 0; e < RBATCH; ++e) {
+          js[e] = -1;
+          if (mask) {
+            js[e] = c0 + base + __ffsll((unsigned long long)mask) - 1;
+            mask &= mask - 1;
+          }
+        }
+        float va[RBATCH][MAX_Q], vb[RBATCH][MAX_Q];
+#pragma unroll
+        for (int e = 0; e < RBATCH; ++e)
+#pragma unroll
+          for (int q = 0; q < MAX_Q; ++q) {
+            const int k = lane + 64 * q;
+            const bool ok = js[e] >= 0 && k < d;
+            va[e][q] = ok ? a.contrib[((int64_t)js[e] * 4 + tA) * d + k] : 0.f;
+            vb[e][q] = ok ? a.contrib[((int64_t)js[e] * 4 + tB) * d + k] : 0.f;
+          }
+#pragma unroll
+        for (int e = 0; e < RBATCH; ++e)
+          if (js[e] >= 0)
+#pragma unroll
+            for (int q = 0; q < MAX_Q; ++q) {
+              gA[q] = gA[q] + va[e][q];
+              gB[q] = gB[q] + vb[e][q];
+            }
+      }
+    }
   }
+  RSTAMP(3);
+  if (!live) return;
+  if (lane == 0) owner[2 * b + s] = first;
+  if (first != b) return;
   float ssA = 0.f, ssB = 0.f;
 #pragma unroll
   for (int q = 0; q < MAX_Q; ++q) {
     const int k = lane + 64 * q;
     if (k < d) {
-      float* ga = a.G + a.off[tA] + (int64_t)r * d + k;
-      float* gb = a.G + a.off[tB] + (int64_t)r * d + k;
-      *ga = *ga + gA[q];
-      *gb = *gb + gB[q];
+      a.G[a.off[tA] + (int64_t)r * d + k] = oA[q] + gA[q];
+      a.G[a.off[tB] + (int64_t)r * d + k] = oB[q] + gB[q];
       ssA = ssA + gA[q] * gA[q];
       ssB = ssB + gB[q] * gB[q];
     }
   }
+  RSTAMP(4);
   if (!with_delta) return;
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) {
@@ -583,18 +773,53 @@ __global__ void __launch_bounds__(256) k_nmf_rows(NArgs a, int32_t* __restrict__
       delta[((int64_t)b * 4 + tB) * d + k] = gB[q] * invB * eps;
     }
   }
+  RSTAMP(5);
 }
+
+// NeuMF's weight-gradient slots handed to k_nmf_adam (acf_neumf_train): the
+// float4s from base4 on get the slot sums of k_nmf_inst (wsum_one's arithmetic)
+// added to their gradient first; the loss element goes to loss_out.
+struct AdamSlots {
+  const float* part = nullptr;  // nullptr: plain Adam
+  int nslot = 0, npass = 0;
+  int64_t base4 = 0, nout = 0;  // first float4 of the slot range; slot length (floats)
+  float* loss_out = nullptr;
+  float B = 1.f;  // the batch, for the mean losses
+};
 
 // Keras 2.2 Adam (keras/optimizers.py Adam.get_updates), dense, float4 stream:
 // m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g^2; p -= lr_t*m / (sqrt(v) + eps); g = 0.
 __global__ void __launch_bounds__(256) k_nmf_adam(float4* __restrict__ p, float4* __restrict__ g,
                                                   float4* __restrict__ m, float4* __restrict__ v,
                                                   int64_t n4, float b1, float b2, float lr_t,
-                                                  float eps) {
+                                                  float eps, AdamSlots ws = AdamSlots()) {
   const float c1 = 1.0f - b1, c2 = 1.0f - b2;
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4;
-       x += (int64_t)gridDim.x * blockDim.x) {
-    const float4 gg = g[x];
+  // with slots the stream runs from the top down: the slot range (the buffer's
+  // tail) is summed in the first sweep, under the rest of the stream
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = ws.part ? n4 - 1 - i : i;
+    float4 gg = g[x];
+    if (ws.part && x >= ws.base4) {
+      const int64_t e0 = 4 * (x - ws.base4);
+      const int64_t loss_x = ws.nout - 3;
+      float4 s4[2];
+      s4[0] = slot_sum4(ws.part, 0, ws.nslot, ws.nout, e0);
+      s4[1] = ws.npass > 1 ? slot_sum4(ws.part, 1, ws.nslot, ws.nout, e0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float sum[2][4] = {{s4[0].x, s4[0].y, s4[0].z, s4[0].w}, {s4[1].x, s4[1].y, s4[1].z, s4[1].w}};
+      float* gc = &gg.x;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (e0 + c < loss_x) {
+          float t = gc[c] + sum[0][c];
+          if (ws.npass > 1) t = t + sum[1][c];
+          gc[c] = t;
+        } else if (e0 + c == loss_x && ws.loss_out) {
+          ws.loss_out[0] = sum[0][c] / ws.B;
+          ws.loss_out[1] = ws.npass > 1 ? sum[1][c] / ws.B : 0.f;
+        }
+      }
+    }
     float4 mm = m[x], vv = v[x], pp = p[x];
 #define ACF_ADAM(c)                                        \
   mm.c = b1 * mm.c + c1 * gg.c;                            \
@@ -616,9 +841,9 @@ struct acf_neumf_ctx {
   int64_t U1 = 0, I1 = 0;
   int32_t d = 0, maxB = 0;
   Layout L;
-  float *h0 = nullptr, *a1 = nullptr, *f = nullptr, *dz1 = nullptr, *dz2 = nullptr;
-  float *dlogit = nullptr, *loss = nullptr, *contrib = nullptr, *delta = nullptr;
-  float* wpart = nullptr;  // [B/64 chunks][weight-gradient outputs]
+  float *contrib = nullptr, *delta = nullptr;
+  float* wpart = nullptr;  // [2 passes][slots][weight-gradient outputs]
+  int32_t nslot = 0;       // workgroups (slots) of a training pass at max_batch
   int32_t *owner = nullptr, *err = nullptr;
   std::vector<void*> allocs;
 };
@@ -678,11 +903,9 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
     c->allocs.push_back(q);
     *p = static_cast<std::remove_reference_t<decltype(*p)>>(q);
   };
-  A(&c->h0, B * 2 * dd); A(&c->a1, B * 2 * dd); A(&c->f, B * 2 * dd); A(&c->dz1, B * 2 * dd);
-  A(&c->dz2, B * dd); A(&c->dlogit, B); A(&c->loss, B); A(&c->contrib, B * 4 * dd);
-  A(&c->delta, B * 4 * dd); A(&c->owner, 2 * B); A(&c->err, 4);
-  const size_t nout = 4 * dd * dd + 2 * dd + 2 * dd * dd + dd + 2 * dd + 2 + 4;
-  A(&c->wpart, ((B + WCH - 1) / WCH) * nout);
+  A(&c->contrib, B * 4 * dd); A(&c->delta, B * 4 * dd); A(&c->owner, 2 * B); A(&c->err, 4);
+  c->nslot = (int32_t)std::min<int64_t>(((int64_t)maxB + MR - 1) / MR, NSLOT);
+  A(&c->wpart, 2 * (size_t)c->nslot * (size_t)wout(d).n);
   if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
     r = set_error(ACF_E_HIP, "hipMemset failed");
   if (r == ACF_OK) r = set_inst_smem_limit();
@@ -699,14 +922,13 @@ static NArgs make_args(acf_neumf_ctx* c, const float* P, float* G, const int32_t
   a.u = u; a.i = i; a.y = y;
   a.U1 = c->U1; a.I1 = c->I1; a.B = B; a.d = c->d;
   a.scale_over_B = (float)((double)scale / (double)B);
-  a.h0 = c->h0; a.a1 = c->a1; a.f = c->f; a.dz1 = c->dz1; a.dz2 = c->dz2;
-  a.dlogit = c->dlogit; a.loss = c->loss; a.contrib = c->contrib;
+  a.contrib = c->contrib; a.wpart = c->wpart;
   a.delta = c->delta; a.owner = c->owner; a.pred = nullptr; a.err = c->err;
   return a;
 }
 
 static size_t inst_smem(int d) {
-  size_t f = (size_t)3 * MR * (2 * d + 1) + 3 * MR * (d + 1) + MR + 5 * d + 4;
+  size_t f = (size_t)3 * MR * (2 * d + 1) + 3 * MR * (d + 1) + 2 * MR + 5 * d + 4;
   if (weights_in_lds(d)) f += (size_t)2 * d * (2 * d + 1) + (size_t)2 * d * (d + 1);
   return f * sizeof(float);
 }
@@ -716,12 +938,13 @@ static int set_inst_smem_limit() {
   static int done = 0;
   if (done) return ACF_OK;
   const int bytes = 150 * 1024;
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_inst<0>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_inst<1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_inst<2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  const void* fns[] = {reinterpret_cast<const void*>(&k_nmf_inst<0, 0>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<1, 0>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<2, 0>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<0, DFAST>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<1, DFAST>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<2, DFAST>)};
+  for (const void* f : fns) HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   done = 1;
   return ACF_OK;
 }
@@ -735,31 +958,37 @@ static int read_err(acf_neumf_ctx* c, hipStream_t s) {
   return ACF_OK;
 }
 
+template <int MODE>
+static void launch_inst(const NArgs& a, unsigned grid, hipStream_t s) {
+  if (a.d == DFAST)
+    k_nmf_inst<MODE, DFAST><<<grid, 256, inst_smem(a.d), s>>>(a);
+  else
+    k_nmf_inst<MODE, 0><<<grid, 256, inst_smem(a.d), s>>>(a);
+}
+
+// clean pass: k_nmf_inst<0> -> k_nmf_rows (owners, rows, delta); adversarial
+// pass: k_nmf_inst<1> -> k_nmf_rows; the last k_nmf_rows launch also sums the
+// passes' weight-gradient slots into G (wsum), unless the caller leaves that to
+// k_nmf_adam (acf_neumf_train)
 static int launch_grad(acf_neumf_ctx* c, const float* P, float* G, const int32_t* u, const int32_t* i,
                        const float* y, int32_t B, const acf_neumf_hparams* hp, float* loss_out,
-                       hipStream_t s) {
-  const int d = c->d;
-  const unsigned gi = (unsigned)((B + MR - 1) / MR);
-  const unsigned gr = (unsigned)((2 * (int64_t)B * 64 + 255) / 256);
+                       hipStream_t s, bool wsum = true) {
+  const unsigned gi = (unsigned)std::min<int64_t>(((int64_t)B + MR - 1) / MR, NSLOT);
+  const unsigned gr = (unsigned)((2 * (int64_t)B + 3) / 4);
+  const WOut o = wout(c->d);
+  const unsigned gs = wsum ? (unsigned)((o.n + 255) / 256) : 0u;
+  const int npass = hp->adver ? 2 : 1;
   NArgs a = make_args(c, P, G, u, i, y, B, 1.0f);
-  const WJobs J = make_jobs(a);
-  const int nch = (B + WCH - 1) / WCH;
-  const dim3 gp((unsigned)J.ntiles, (unsigned)nch);
-  const unsigned gs = (unsigned)((J.nout + 255) / 256);
-  k_nmf_inst<0><<<gi, 256, inst_smem(d), s>>>(a);
-  k_nmf_wpart<<<gp, 256, 0, s>>>(J, B, c->wpart);
-  k_nmf_wsum<<<gs, 256, 0, s>>>(a, J, nch, c->wpart, loss_out, 0);
-  k_nmf_rows<<<gr, 256, 0, s>>>(a, c->owner, c->delta, hp->adver ? 1 : 0, hp->eps);
+  launch_inst<0>(a, gi, s);
+  k_nmf_rows<<<gr + (npass == 1 ? gs : 0), 256, 0, s>>>(a, c->owner, c->delta, hp->adver ? 1 : 0, hp->eps, gr,
+                                                       (int)gi, npass, c->wpart, loss_out);
   HIP_TRY(hipGetLastError());
   if (hp->adver) {
     NArgs b = make_args(c, P, G, u, i, y, B, hp->reg_adv);
-    k_nmf_inst<1><<<gi, 256, inst_smem(d), s>>>(b);
-    k_nmf_wpart<<<gp, 256, 0, s>>>(J, B, c->wpart);
-    k_nmf_wsum<<<gs, 256, 0, s>>>(b, J, nch, c->wpart, loss_out, 1);
-    k_nmf_rows<<<gr, 256, 0, s>>>(b, c->owner, c->delta, 0, 0.f);
+    b.wpart = c->wpart + (int64_t)gi * o.n;
+    launch_inst<1>(b, gi, s);
+    k_nmf_rows<<<gr + gs, 256, 0, s>>>(b, c->owner, c->delta, 0, 0.f, gr, (int)gi, npass, c->wpart, loss_out);
     HIP_TRY(hipGetLastError());
-  } else if (loss_out) {
-    HIP_TRY(hipMemsetAsync(loss_out + 1, 0, sizeof(float), s));
   }
   return ACF_OK;
 }
@@ -778,7 +1007,7 @@ extern "C" int acf_neumf_grad(acf_neumf_ctx* c, const float* P, float* G, const 
 }
 
 static int launch_adam(acf_neumf_ctx* c, float* P, float* G, float* m, float* v, int64_t t,
-                       const acf_neumf_hparams* hp, hipStream_t s) {
+                       const acf_neumf_hparams* hp, hipStream_t s, const AdamSlots& ws = AdamSlots()) {
   // lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t), evaluated in float32 as Keras does
   const float tt = (float)t;
   const float lr_t = hp->lr * (sqrtf(1.0f - powf(hp->beta2, tt)) / (1.0f - powf(hp->beta1, tt)));
@@ -786,7 +1015,7 @@ static int launch_adam(acf_neumf_ctx* c, float* P, float* G, float* m, float* v,
   const unsigned grid = (unsigned)std::min<int64_t>((n4 + 255) / 256, 256 * 32);
   k_nmf_adam<<<grid, 256, 0, s>>>(reinterpret_cast<float4*>(P), reinterpret_cast<float4*>(G),
                                   reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v), n4,
-                                  hp->beta1, hp->beta2, lr_t, hp->adam_eps);
+                                  hp->beta1, hp->beta2, lr_t, hp->adam_eps, ws);
   HIP_TRY(hipGetLastError());
   return ACF_OK;
 }
@@ -810,8 +1039,18 @@ extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, f
   int64_t k = 0;
   for (int64_t o = 0; o < n; o += batch, ++k) {
     const int32_t B = (int32_t)std::min<int64_t>(batch, n - o);
-    int r = launch_grad(c, P, G, u + o, i + o, y + o, B, hp, losses ? losses + 2 * k : nullptr, s);
-    if (r == ACF_OK) r = launch_adam(c, P, G, m, v, t_first + k, hp, s);
+    // the weight-gradient slot sums ride on the Adam stream (same arithmetic as
+    // acf_neumf_grad's wsum, so train == grad + adam bit for bit)
+    int r = launch_grad(c, P, G, u + o, i + o, y + o, B, hp, nullptr, s, false);
+    AdamSlots ws;
+    ws.part = c->wpart;
+    ws.nslot = (int)std::min<int64_t>(((int64_t)B + MR - 1) / MR, NSLOT);
+    ws.npass = hp->adver ? 2 : 1;
+    ws.base4 = c->L.off[S_W1] / 4;
+    ws.nout = wout(c->d).n;
+    ws.loss_out = losses ? losses + 2 * k : nullptr;
+    ws.B = (float)B;
+    if (r == ACF_OK) r = launch_adam(c, P, G, m, v, t_first + k, hp, s, ws);
     if (r != ACF_OK) return r;
   }
   return read_err(c, s);
@@ -821,6 +1060,7 @@ extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, f
 extern "C" int acf_neumf_diag_stamps(uint64_t* out) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nmf_stamps), 16 * sizeof(uint64_t)));
+  HIP_TRY(hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_nmf_rstamps), 8 * sizeof(uint64_t)));
   return ACF_OK;
 }
 #endif
@@ -836,7 +1076,7 @@ extern "C" int acf_neumf_predict(acf_neumf_ctx* c, const float* P, const int32_t
     const int32_t m = (int32_t)std::min(chunk, n - o);
     NArgs a = make_args(c, P, nullptr, u + o, i + o, nullptr, m, 1.0f);
     a.pred = out + o;
-    k_nmf_inst<2><<<(unsigned)((m + MR - 1) / MR), 256, inst_smem(c->d), s>>>(a);
+    launch_inst<2>(a, (unsigned)std::min<int64_t>(((int64_t)m + MR - 1) / MR, 512), s);
     HIP_TRY(hipGetLastError());
   }
   return read_err(c, s);

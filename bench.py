@@ -446,16 +446,29 @@ def neumf_bench(acf, dev):
     dt = time.perf_counter() - t0
     nb = losses.shape[0]
     st = r.state
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 50
-    e0.record()
-    for _ in range(reps):
-        ctx.adam(hp)
-    e1.record()
-    torch.cuda.synchronize(dev)
-    adam_us = e0.elapsed_time(e1) * 1e3 / reps
+
+    def adam_time(c, reps=50):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c.adam(hp)
+        e0.record()
+        for _ in range(reps):
+            c.adam(hp)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) * 1e3 / reps
+
+    # the yelp-shaped buffer (212 MB of p, g, m, v) stays in the 256 MB Infinity
+    # Cache between steps: its Adam rate is not an HBM rate.  The roofline is
+    # taken on the same kernel over a 1.2 GB buffer (262,144 user rows), which
+    # streams from HBM; the yelp-shaped rate is reported beside it.
+    adam_us_mall = adam_time(ctx)
     nparam = st.params.numel()
-    achieved = 8 * 4 * nparam / (adam_us * 1e-6) / 1e9
+    big = nm.NeuMFState(262_144, ds.num_items + 1, d, dev)
+    bctx = nm.NeuMFContext(big, B)
+    adam_us = adam_time(bctx)
+    nbig = big.params.numel()
+    achieved = 8 * 4 * nbig / (adam_us * 1e-6) / 1e9
+    del bctx, big
     return {"metric": "adversarial NeuMF training instances/sec (yelp-sort-shaped, d=64)",
             "value": round(n / dt, 1), "unit": "instances/s", "ms_per_step": round(1e3 * dt / nb, 4),
             "dtype": "f32", "data": "synthetic yelp-sort-shaped (25,677 users x 25,815 items, 705k "
@@ -466,8 +479,13 @@ def neumf_bench(acf, dev):
             "final_loss": round(float(losses[-1, 0]), 5),
             "roofline": {"bound": "hbm", "kernel": "k_nmf_adam", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "bytes_per_launch": 8 * 4 * nparam, "avg_launch_us": round(adam_us, 3),
-                         "traffic": (pmc_traffic("k_nmf_adam") or (None,))[0]}}
+                         "bytes_per_launch": 8 * 4 * nbig, "avg_launch_us": round(adam_us, 3),
+                         "buffer": "1.2 GB (262,144 user rows: beyond the 256 MB Infinity Cache)",
+                         "traffic": None},
+            "adam_yelp_shape": {"bytes_per_launch": 8 * 4 * nparam, "avg_launch_us": round(adam_us_mall, 3),
+                                "achieved_GBs": round(8 * 4 * nparam / (adam_us_mall * 1e-6) / 1e9, 2),
+                                "note": "212 MB buffer resident in the Infinity Cache between steps",
+                                "traffic": (pmc_traffic("k_nmf_adam") or (None,))[0]}}
 
 
 def eval_bench(acf, dev, reps=5):

@@ -19,15 +19,19 @@ st = nm.NeuMFState(U, I, d, "cuda")
 st.keras_init(0)
 ctx = nm.NeuMFContext(st, B)
 rng = np.random.default_rng(0)
-names = ["indices+weights", "gather", "fwd1", "fwd2", "head", "dz2", "bwd2", "bwd1+scratch"]
+names = ["prologue", "stash", "fwd1", "fwd2", "head", "dz2", "bwd2", "bwd1", "wgrad_tiles", "bias+sync"]
 for rep in range(5):
     u = rng.integers(0, U, B).astype(np.int32)
     i = rng.integers(0, I, B).astype(np.int32)
     y = (rng.random(B) < 0.5).astype(np.float32)
     ctx.grad(u, i, y, ctx.hparams(adver=1))
     torch.cuda.synchronize()
-    buf = (ctypes.c_uint64 * 16)()
+    buf = (ctypes.c_uint64 * 24)()
     lib.acf_neumf_diag_stamps(buf)
-    t = np.array(buf[:9], dtype=np.int64)
+    t = np.array(buf[:11], dtype=np.int64)
     dt = np.diff(t) * 10 / 1000.0  # us
     print("rep", rep, " ".join(f"{n}={x:.2f}" for n, x in zip(names, dt)), f"total={dt.sum():.2f}us")
+    rt = np.array(buf[16:22], dtype=np.int64)
+    rd = np.diff(rt) * 10 / 1000.0
+    print("    rows", " ".join(f"{n}={x:.2f}" for n, x in zip(["stage", "first", "accum", "g_store", "delta"], rd)),
+          f"total={rd.sum():.2f}us", f"(starts {(rt[0] - t[-1]) * 10 / 1000.0:.2f}us after inst wg0 end)")
