@@ -57,6 +57,9 @@ SIGNATURES = {
     "acf_apr_set_step_overlap": (ctypes.c_int, [_P, _I32]),
     "acf_apr_set_stream": (ctypes.c_int, [_P, _I32]),
     "acf_apr_step_errors": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
+    "acf_apr_set_failsafe": (ctypes.c_int, [_P, _I32]),
+    "acf_apr_set_spin_limit": (ctypes.c_int, [_P, _I32]),
+    "acf_apr_stream_recoveries": (ctypes.c_int, [_P, ctypes.POINTER(_I64)]),
     "acf_apr_copy_losses": (ctypes.c_int, [_P, _P, _P, _P]),
     "acf_apr_delta_scatter": (ctypes.c_int, [_P, _P, _P, _P]),
     "acf_bpr_forward": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _P, _I32, _I32, _F, _F, _P, _P,

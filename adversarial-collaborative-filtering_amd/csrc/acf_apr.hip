@@ -1051,6 +1051,12 @@ struct StepArgs {
   const int32_t* task_cnt;   // [nb]
   int32_t task_stride, max_depth;
   int32_t poll_sleep;  // k_stream: s_sleep between polls of a version (0-3; 4/5/6 = 8/16/32)
+  // k_stream's give-ups: the call's failure word (bit 0: a version wait gave up
+  // after spin_limit polls) -- k_stream_flush writes nothing when it is set, so a
+  // failed call leaves the tables as they were and can be replayed exactly
+  int32_t* fail;
+  int32_t spin_limit;
+  int32_t* fail_host;  // host-mapped copy of the failure word (written by the flush)
   // hot slots of list plans (k_records): piece waves [slot_waves, slot_waves +
   // hot_waves) of a list kernel stride over the batch's pieces; partial sums in hot_part
   HotLists hot;
@@ -1892,12 +1898,12 @@ __device__ __forceinline__ void store_ver(u64* dst, int d, int l, const RowV<NV>
 // wave-uniform end of a wait round: true = stop (all there, or give up)
 __device__ __forceinline__ bool wait_round(const StepArgs& a, bool ok, int it) {
   if (__all(ok)) return true;
-  if (it >= ACF_SPIN_LIMIT) {
-    if ((threadIdx.x & 63) == 0) atomicOr(a.step_err, 1);
+  if (it >= a.spin_limit) {
+    if ((threadIdx.x & 63) == 0) atomicOr(a.fail, 1);
     return true;
   }
   if ((it & 31) == 31 &&
-      __any(__hip_atomic_load(a.step_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
+      __any(__hip_atomic_load(a.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
     return true;  // another wave gave up: the launch is failing, drain it
   switch (a.poll_sleep) {  // s_sleep takes an immediate
     case 0: break;
@@ -2320,6 +2326,12 @@ __global__ void __launch_bounds__(256, 2) k_stream(StepArgs a, int32_t positions
 // per slot of the range: lane c gathers granules c, c + d/4, c + d/2, c + 3d/4
 // (elements 4c .. 4c+3 in the component-major order) of both versions and
 // stores them as one float4 each, so every slot's loads are in flight at once.
+// A failed launch (a.fail set: some wait gave up) writes nothing: the tables are
+// as before the call.  A verified call (fail_host set) leaves the epoch alone too:
+// the host replays the chunk on the two-kernel schedule, which reads the same
+// call counter and bumps the epoch as this flush would have (stale granules of
+// the failed launch carry the old tag and never match again).  An unverified
+// one bumps it, so the next launch cannot match the failed launch's granules.
 template <int LPR>
 __global__ void __launch_bounds__(256) k_stream_flush(StepArgs a, uint32_t* __restrict__ epoch) {
   constexpr int OPW = 64 / LPR;
@@ -2327,8 +2339,12 @@ __global__ void __launch_bounds__(256) k_stream_flush(StepArgs a, uint32_t* __re
   const int64_t x = (gid >> 6) * OPW + (int64_t)((threadIdx.x & 63) / LPR);
   const int l = (int)(threadIdx.x & (LPR - 1));
   const int64_t n = (int64_t)(a.t_end - a.first) * a.S;
-  if (gid == 0) atomicAdd(epoch, 1u);  // every k_stream wave has read it (kernel boundary)
-  if (x >= n) return;
+  const int32_t failed = *a.fail;  // k_stream has ended (kernel boundary)
+  if (gid == 0) {
+    if (!failed || !a.fail_host) atomicAdd(epoch, 1u);  // every k_stream wave has read it
+    if (a.fail_host) *a.fail_host = failed;
+  }
+  if (failed || x >= n) return;
   const int32_t t = a.first + (int32_t)(x / a.S);
   const int32_t k = (int32_t)(x - (int64_t)(t - a.first) * a.S);
   if (a.nextt[(int64_t)t * a.S + k] < a.t_end) return;  // a later batch of the launch has it
@@ -3356,6 +3372,11 @@ struct acf_apr_ctx {
   int32_t stream = 1;        // ACF_STREAM=0 disables
   int32_t stream_depth = 2;  // ACF_STREAM_DEPTH: max waves per position (batches in flight)
   int32_t poll_sleep = 2;    // ACF_POLL_SLEEP: s_sleep between version polls (0-3; 4/5/6 = 8/16/32)
+  int32_t spin_limit = ACF_SPIN_LIMIT;  // k_stream version polls before a give-up (acf_apr_set_spin_limit)
+  int32_t failsafe = 1;      // verify every streamed call, replay a failed one (acf_apr_set_failsafe)
+  int32_t* fail_host = nullptr;      // host-mapped failure word of the last streamed call
+  int32_t* fail_host_dev = nullptr;  // its device address
+  int64_t recoveries = 0;    // streamed calls replayed on the two-kernel schedule
   int32_t stream_ok = -1;    // -1 unknown, 0 unavailable (allocation / occupancy), 1 ready
   int64_t stream_max_waves = 0;
   unsigned long long *ver_w = nullptr, *ver_a = nullptr, *ver_d = nullptr;
@@ -3455,6 +3476,7 @@ extern "C" int acf_apr_destroy(acf_apr_ctx* c) {
   c->graphs.clear();
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
+  if (c->fail_host) (void)hipHostFree(c->fail_host);
   delete c;
   return ACF_OK;
 }
@@ -3829,6 +3851,9 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.epoch = c->epoch; a.nextt = c->nextt;
   a.task_list = nullptr; a.task_cnt = c->task_cnt; a.task_stride = 0; a.max_depth = 1;
   a.poll_sleep = c->poll_sleep;
+  a.fail = c->err + 1;  // k_stream launches: the call's own word (err + 2)
+  a.spin_limit = c->spin_limit;
+  a.fail_host = nullptr;
   a.hot = c->hot;
   a.hot_part = c->hot_part;
   a.hot_waves = 0;
@@ -4034,6 +4059,19 @@ static int stream_ready(acf_apr_ctx* c, const Kernels& K) {
     (void)hipGetLastError();
     return 0;
   }
+  // the host-mapped failure word the flush reports to (verified calls)
+  if (!c->fail_host) {
+    void* h = nullptr;
+    void* dptr = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess || hipHostGetDevicePointer(&dptr, h, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      if (h) (void)hipHostFree(h);
+      return 0;
+    }
+    c->fail_host = static_cast<int32_t*>(h);
+    c->fail_host_dev = static_cast<int32_t*>(dptr);
+    *c->fail_host = 0;
+  }
   c->stream_ok = 1;
   return 1;
 }
@@ -4041,6 +4079,15 @@ static int stream_ready(acf_apr_ctx* c, const Kernels& K) {
 static int stream_positions(const acf_apr_ctx* c, const Kernels& K, int fuse) {
   const int TW = fuse ? (c->B + 64 / c->lpr - 1) / (64 / c->lpr) : 0;
   return 3 * c->B + TW;
+}
+
+static int capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return st != hipStreamCaptureStatusNone;
 }
 
 // (stream_ready allocates: call prepare_stream before any capture)
@@ -4097,6 +4144,9 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     a.task_stride = c->task_stride;
     a.max_depth = c->stream_depth;
     a.poll_sleep = c->poll_sleep;
+    a.fail = c->err + 2;  // this call's failure word (zero: reset after every failure)
+    const bool verify = c->failsafe && !events && capturing(s) == 0;
+    a.fail_host = verify ? c->fail_host_dev : nullptr;
     hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
     if (kinds) kinds[li] = 4;
     ++li;
@@ -4118,7 +4168,17 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     else
       hipLaunchKernelGGL(reinterpret_cast<FK>(K.stream_flush), fgrid, block, 0, s, a, c->epoch);
     HIP_TRY(hipGetLastError());
-    return ACF_OK;
+    if (!verify) return ACF_OK;  // a give-up stays in err + 2: acf_apr_step_errors reports it
+    // Verified call: k_stream needs all of its waves resident (another process or
+    // a concurrent persistent kernel on the device can starve its hand-offs).  A
+    // give-up left the tables untouched (gated flush): replay the chunk on the
+    // two-kernel schedule, which waits on nothing.
+    HIP_TRY(hipStreamSynchronize(s));
+    if (*(volatile int32_t*)c->fail_host == 0) return ACF_OK;
+    *(volatile int32_t*)c->fail_host = 0;
+    HIP_TRY(hipMemsetAsync(c->err + 2, 0, sizeof(int32_t), s));
+    ++c->recoveries;
+    return run_loop(c, tb, hp, first, n, s, nullptr, nullptr, 0, tri_phases);
   }
   if (allow_overlap && use_overlap(c, K, hp)) {
     HIP_TRY(hipMemsetAsync(c->flags + (size_t)first * S, 0, (size_t)n * S * sizeof(int32_t), s));
@@ -4577,9 +4637,31 @@ extern "C" int acf_shard_reduce_apply(float* Q, float* accQ, const float* recv, 
 extern "C" int acf_apr_step_errors(acf_apr_ctx* c, int32_t* out, void* stream_) {
   ACF_CHECK(c && out, ACF_E_INVALID, "NULL argument");
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  HIP_TRY(hipMemcpyAsync(out, c->err + 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemsetAsync(c->err + 1, 0, sizeof(int32_t), s));
+  int32_t w[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(w, c->err + 1, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemsetAsync(c->err + 1, 0, 2 * sizeof(int32_t), s));
   HIP_TRY(hipStreamSynchronize(s));
+  *out = w[0] | w[1];  // step waits, and unverified streamed calls that gave up
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_set_failsafe(acf_apr_ctx* c, int32_t on) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "failsafe must be 0 or 1, got %d", on);
+  c->failsafe = on;
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_set_spin_limit(acf_apr_ctx* c, int32_t polls) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(polls >= 0, ACF_E_INVALID, "spin limit must be >= 0, got %d", polls);
+  c->spin_limit = polls;
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_stream_recoveries(acf_apr_ctx* c, int64_t* out) {
+  ACF_CHECK(c && out, ACF_E_INVALID, "NULL argument");
+  *out = c->recoveries;
   return ACF_OK;
 }
 

@@ -266,6 +266,25 @@ class APRContext:
         adversarial pass of batch t and the clean pass of batch t+1 in one launch."""
         call("acf_apr_set_step_overlap", self._ptr, int(bool(on)))
 
+    def set_failsafe(self, on: bool) -> None:
+        """Verified streamed steps (default on): each streamed call syncs its stream
+        once and, when a hand-off wait gave up (k_stream needs all its waves
+        resident), replays the chunk on the two-kernel schedule -- exact, the
+        tables are untouched by a failed launch.  Off: calls stay asynchronous and
+        a give-up is reported by step_errors() (the chunk is then not applied)."""
+        call("acf_apr_set_failsafe", self._ptr, int(bool(on)))
+
+    def set_spin_limit(self, polls: int) -> None:
+        """Version polls before a k_stream wait gives up (default 65,536; tests use
+        0 to force the replay)."""
+        call("acf_apr_set_spin_limit", self._ptr, int(polls))
+
+    def stream_recoveries(self) -> int:
+        """Streamed calls replayed on the two-kernel schedule so far."""
+        out = ctypes.c_int64(0)
+        call("acf_apr_stream_recoveries", self._ptr, ctypes.byref(out))
+        return int(out.value)
+
     # -- shard mode (distributed.ShardedAPR; include/acf_apr.h "shard mode") --------
     def set_shard_mode(self, on: bool, reg_batch: int = 0) -> None:
         """Item rows are this rank's partial sums (one lane-group per slot, no
@@ -294,8 +313,8 @@ class APRContext:
             call("acf_apr_shard_items", self._ptr, 1, delta.data_ptr(), delta.shape[0], _stream_ptr(self.device))
 
     def step_errors(self) -> int:
-        """Read and clear the step error word (bit 0: an overlapped step gave up
-        waiting for a row)."""
+        """Read and clear the step error words (bit 0: an overlapped step gave up
+        waiting for a row, or an unverified streamed call gave up -- set_failsafe)."""
         out = ctypes.c_int32(0)
         with torch.cuda.device(self.device):
             call("acf_apr_step_errors", self._ptr, ctypes.byref(out), _stream_ptr(self.device))
@@ -370,6 +389,17 @@ class PlanPipeline:
         for c in self.ctx:
             e |= c.step_errors()
         return e
+
+    def set_failsafe(self, on: bool) -> None:
+        for c in self.ctx:
+            c.set_failsafe(on)
+
+    def set_spin_limit(self, polls: int) -> None:
+        for c in self.ctx:
+            c.set_spin_limit(polls)
+
+    def stream_recoveries(self) -> int:
+        return sum(c.stream_recoveries() for c in self.ctx)
 
     def set_slot_mapping(self, mode) -> None:
         for c in self.ctx:

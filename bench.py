@@ -600,6 +600,7 @@ def main():
     value = world * a.steps * B / elapsed
     finite = bool(torch.isfinite(tabs[0]).all() and torch.isfinite(tabs[1]).all())
     step_errors = pipe.step_errors()
+    recoveries = pipe.stream_recoveries()  # streamed calls replayed (a hand-off wait gave up)
     # roofline of the dominant kernel (separate eager pass with per-launch events)
     tctx = ops.APRContext(U1, I1, d, B, a.time_batches, dev)
     tctx.set_slot_mapping(a.mapping)
@@ -631,6 +632,7 @@ def main():
         "batch_stats": {k: round(v, 1) for k, v in st.items()},
         "tables_finite": finite,
         "step_errors": step_errors,
+        "stream_recoveries": recoveries,
         "step_overlap": not a.no_step_overlap,
         "step_stream": roof["kernel"].startswith("k_stream"),
     }

@@ -191,6 +191,21 @@ int acf_apr_set_step_overlap(acf_apr_ctx* ctx, int32_t on);
  * device cannot keep the launch resident).  Not part of the reference surface. */
 int acf_apr_set_stream(acf_apr_ctx* ctx, int32_t on);
 
+/* Failure safety of the streamed step (k_stream).  k_stream needs every one of
+ * its waves resident; when a hand-off wait gives up (another process or a
+ * concurrent persistent kernel on the device), its flush writes nothing, so the
+ * tables are as before the call.  failsafe = 1 (default): every streamed call
+ * synchronises its stream once at its end and, after a give-up, replays the
+ * chunk on the two-kernel schedule (exact: same result as acf_apr_set_stream 0).
+ * failsafe = 0: calls stay asynchronous; a give-up is reported by
+ * acf_apr_step_errors (bit 0) and the chunk's rows are not applied.
+ * acf_apr_set_spin_limit: version polls before a give-up (default 65,536; 0
+ * gives up at the first unready poll -- tests force the replay with it).
+ * acf_apr_stream_recoveries: streamed calls replayed so far. */
+int acf_apr_set_failsafe(acf_apr_ctx* ctx, int32_t on);
+int acf_apr_set_spin_limit(acf_apr_ctx* ctx, int32_t polls);
+int acf_apr_stream_recoveries(acf_apr_ctx* ctx, int64_t* out);
+
 /* ---- shard mode: users and items row-sharded over the ranks of one node ----
  * SURVEY §8(e) (no reference counterpart: the reference trains on one CPU
  * process; this splits one training_batch, utils.py:113-119, across ranks so

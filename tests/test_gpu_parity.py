@@ -763,3 +763,55 @@ def test_stream_kernel_timing_kinds(ops, dev, d):
     for x, y in zip(ta, tb):
         assert torch.equal(x, y)
     assert ctx.step_errors() == 0
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+def test_stream_give_up_replays_exactly(ops, acf, dev, fuse):
+    """k_stream failure safety (it needs all of its waves resident): with a spin
+    limit of 0 every hand-off wait gives up at once, the gated flush writes
+    nothing, and the verified call replays the chunk on the two-kernel schedule --
+    the same bits as set_stream(False), no step error, the replay counted.  With
+    failsafe off the give-up is reported by step_errors and the tables are left
+    exactly as they were."""
+    B, nb, d = 512, 24, 64
+    U1, I1, u, i, j = _overlap_stream("ml1m", acf, dev, B, nb, seed=11)
+    rng = np.random.default_rng(3)
+    P = (rng.standard_normal((U1, d)) * 0.2).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
+    hp = ops.StepHParams(adver=1, reg=0.01, seed=5)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_fusion(fuse)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ctx.set_stream(False)
+    ref = _gpu_tables(P, Q, dev)
+    ctx.train_planned(ref, hp)
+    ref_l = [x.clone() for x in ctx.losses()]
+    ctx.set_stream(True)
+    ctx.set_spin_limit(0)
+    for pieces in ([(0, nb)], [(0, 5), (5, nb - 5)]):
+        before = ctx.stream_recoveries()
+        got = _gpu_tables(P, Q, dev)
+        for first, n in pieces:
+            ctx.train_planned(got, hp, first, n)
+        torch.cuda.synchronize()
+        assert ctx.stream_recoveries() - before >= 1
+        assert ctx.step_errors() == 0
+        for x, y in zip(ref + ref_l, got + list(ctx.losses())):
+            assert torch.equal(x, y)
+    ctx.set_failsafe(False)
+    got = _gpu_tables(P, Q, dev)
+    ctx.train_planned(got, hp)
+    torch.cuda.synchronize()
+    assert ctx.step_errors() & 1
+    for x, y in zip(_gpu_tables(P, Q, dev), got):
+        assert torch.equal(x, y)
+    # and a normal limit again: the streamed call goes through without a replay
+    ctx.set_failsafe(True)
+    ctx.set_spin_limit(1 << 16)
+    before = ctx.stream_recoveries()
+    got = _gpu_tables(P, Q, dev)
+    ctx.train_planned(got, hp)
+    torch.cuda.synchronize()
+    assert ctx.step_errors() == 0 and ctx.stream_recoveries() == before
+    for x, y in zip(ref, got):
+        assert torch.equal(x, y)
