@@ -206,7 +206,12 @@ def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb, st):
             "bytes_per_launch": int(alg_bytes), "avg_launch_us": round(avg_ms * 1e3, 3),
             "batches_per_launch": nb if kid == 4 else 1,
             "per_kernel_avg_us": per_kernel_us,
-            "achieved_unique_rw_GBs": None if rw is None else round(rw, 2)}
+            "achieved_unique_rw_GBs": None if rw is None else round(rw, 2),
+            # the dominant kernel's measured HBM traffic (PMC, reads + writes) per
+            # second: how close the kernel runs to the memory system, which the
+            # read-only algorithmic frac above does not show for write-heavy steps
+            "traffic_GBs": None if tr is None else round(tr[0] / (avg_ms * 1e-3) / 1e9, 2),
+            "traffic_frac_of_copy_ceiling": None if tr is None else round(tr[0] / (avg_ms * 1e-3) / 1e9 / 6290.0, 4)}
 
 
 def step_bandwidth(d, B, st, triplets_per_s):
