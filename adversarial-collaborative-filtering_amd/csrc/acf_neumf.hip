@@ -99,6 +99,8 @@ struct NArgs {
   int32_t B, d;
   float scale_over_B;    // 1/B (clean) or reg_adv/B (adversarial)
   float* contrib;        // [B][4][d] per-instance row contributions
+  // the activations the weight gradients need (k_nmf_inst -> k_nmf_rows' gradient workgroups)
+  float *h0, *a1, *dz1, *dz2;  // [B][2d], [B][2d], [B][2d], [B][d]
   float* wpart;          // [gridDim.x][nout] this pass's weight-gradient partials (one slot per workgroup)
   const float* delta;    // [B][4][d], rows written at their owner instance
   const int32_t* owner;  // [B][2] first occurrence of the instance's user / item
@@ -221,16 +223,17 @@ __device__ __forceinline__ void mfma_panel(const float* sA, int lda, const float
 // this lane stored for the previous block -- the same lane, the same address).
 constexpr int OG = 4;
 
-// one weight gradient [K][N] (A rows with leading dimension lda, Bm rows ldb);
-// EXACT: K and N multiples of 16 (no bounds); tiles tt = wave + 4 * (OG*i + g)
+// one weight gradient [K][N] (A rows with leading dimension lda, Bm rows ldb),
+// its tiles [tlo, thi) (row-major over 16x16 tiles); EXACT: K and N multiples of
+// 16 (no bounds); tiles tt = tlo + wave + 4 * (OG*i + g)
 template <bool ACC, bool EXACT>
 __device__ __forceinline__ void outer_mat(const float* A, int lda, const float* Bm, int ldb, int K, int N,
-                                          float* __restrict__ out) {
+                                          float* __restrict__ out, int tlo, int thi) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, h = lane >> 4;
-  const int tn = (N + 15) / 16, T = ((K + 15) / 16) * tn;
+  const int tn = (N + 15) / 16, T = thi;
   const float* Ar = A + h * lda + r;   // lane's element of row t = h, column r
   const float* Br = Bm + h * ldb + r;
-  for (int tb = wave; tb < T; tb += 4 * OG) {
+  for (int tb = tlo + wave; tb < T; tb += 4 * OG) {
     float av[OG][MR / 4], bv[OG][MR / 4];
     int k0[OG], n0[OG];
 #pragma unroll
@@ -267,14 +270,104 @@ __device__ __forceinline__ void outer_mat(const float* A, int lda, const float* 
   }
 }
 
+// tiles [lo, hi) of the two gradients' tile space (W1's T1 tiles, then W2's)
+__host__ __device__ __forceinline__ int wtiles1(int d) { return ((2 * d + 15) / 16) * ((2 * d + 15) / 16); }
+__host__ __device__ __forceinline__ int wtiles(int d) { return wtiles1(d) + ((2 * d + 15) / 16) * ((d + 15) / 16); }
+
 template <bool ACC, bool EXACT>
 __device__ __forceinline__ void outer_tiles(const float* s_h0, const float* s_dz1, const float* s_a1,
                                             const float* s_dz2, int d, float* __restrict__ w1,
-                                            float* __restrict__ w2) {
-  const int d2 = 2 * d;
-  outer_mat<ACC, EXACT>(s_h0, d2 + 1, s_dz1, d2 + 1, d2, d2, w1);
-  outer_mat<ACC, EXACT>(s_a1, d2 + 1, s_dz2, d + 1, d2, d, w2);
+                                            float* __restrict__ w2, int lo, int hi) {
+  const int d2 = 2 * d, T1 = wtiles1(d);
+  if (lo < T1) outer_mat<ACC, EXACT>(s_h0, d2 + 1, s_dz1, d2 + 1, d2, d2, w1, lo, min(hi, T1));
+  if (hi > T1) outer_mat<ACC, EXACT>(s_a1, d2 + 1, s_dz2, d + 1, d2, d, w2, max(lo, T1) - T1, hi - T1);
 }
+
+// k_nmf_rows' weight-gradient workgroups take the tiles in groups of one wave round
+constexpr int WG_TILES = 4 * OG;
+
+// Weight-gradient workgroup (slot w, tile group g) -- extra workgroups of the NEXT
+// launch after k_nmf_inst (the adversarial k_nmf_inst for the clean pass, the last
+// k_nmf_rows for the adversarial pass), which leave most CUs idle: for the blocks
+// w, w + nslot, ... of k_nmf_inst's 16 instances, stage h0, dz1, a1, dz2 in LDS
+// (padded rows; instances past the batch are zero) and add tiles
+// [g WG_TILES, (g+1) WG_TILES) of W1 += h0^T dz1, W2 += a1^T dz2 to slot w (the
+// slot k_nmf_inst's workgroup w writes the vector partials of).
+#ifdef NMF_DIAG
+__device__ uint64_t g_nmf_wstamps[8];  // weight-gradient workgroup (0, 0) of the last launch that ran one
+#define WSTAMP(i)                                                                          \
+  do {                                                                                     \
+    uint64_t t_;                                                                           \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    if (w == 0 && g == 0 && threadIdx.x == 0) g_nmf_wstamps[i] = t_;                      \
+  } while (0)
+#else
+#define WSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
+template <bool EXACT>
+__device__ __forceinline__ void wgrad_group(const NArgs& a, int w, int g, int nslot, float* sm) {
+  WSTAMP(0);
+  const int d = a.d, d2 = 2 * d, L2 = d2 + 1, L1 = d + 1, tid = threadIdx.x;
+  float* s_h0 = sm;
+  float* s_dz1 = s_h0 + MR * L2;
+  float* s_a1 = s_dz1 + MR * L2;
+  float* s_dz2 = s_a1 + MR * L2;
+  const WOut o = wout(d);
+  float* slot = a.wpart + (int64_t)w * o.n;
+  const int64_t nblk = ((int64_t)a.B + MR - 1) / MR;
+  const int lo = g * WG_TILES, hi = min(lo + WG_TILES, wtiles(d));
+  for (int64_t blk = w; blk < nblk; blk += nslot) {
+    const int64_t b0 = blk * MR;
+    const int nt = (int)min((int64_t)MR, (int64_t)a.B - b0);
+    if (blk != w) __syncthreads();  // the previous block's tiles are done with LDS
+    // every load first (one round trip), the LDS stores after them
+    constexpr int QA = MR * 256 / 256, QB = MR * 128 / 256;  // d <= 128
+    float v0[QA], v1[QA], v2[QA], v3[QB];
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int x = tid + 256 * q, t = x / d2, k = x - t * d2;
+      if (256 * q < MR * d2) {  // uniform (MR d2 is a multiple of 64)
+        const int64_t gi = (b0 + (x < MR * d2 && t < nt ? t : 0)) * d2 + (x < MR * d2 ? k : 0);
+        v0[q] = a.h0[gi];
+        v1[q] = a.dz1[gi];
+        v2[q] = a.a1[gi];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int x = tid + 256 * q, t = x / d, k = x - t * d;
+      if (256 * q < MR * d) v3[q] = a.dz2[(b0 + (x < MR * d && t < nt ? t : 0)) * d + (x < MR * d ? k : 0)];
+    }
+    WSTAMP(1);
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int x = tid + 256 * q, t = x / d2, k = x - t * d2;
+      if (x < MR * d2) {
+        const bool ok = t < nt;
+        s_h0[t * L2 + k] = ok ? v0[q] : 0.f;
+        s_dz1[t * L2 + k] = ok ? v1[q] : 0.f;
+        s_a1[t * L2 + k] = ok ? v2[q] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int x = tid + 256 * q, t = x / d, k = x - t * d;
+      if (x < MR * d) s_dz2[t * L1 + k] = t < nt ? v3[q] : 0.f;
+    }
+    __syncthreads();
+    WSTAMP(2);
+    if (blk == w)
+      outer_tiles<false, EXACT>(s_h0, s_dz1, s_a1, s_dz2, d, slot + o.w1, slot + o.w2, lo, hi);
+    else
+      outer_tiles<true, EXACT>(s_h0, s_dz1, s_a1, s_dz2, d, slot + o.w1, slot + o.w2, lo, hi);
+    WSTAMP(3);
+  }
+}
+
+static size_t wgrad_smem(int d) { return (size_t)MR * (3 * (2 * d + 1) + (d + 1)) * sizeof(float); }
 
 #ifdef NMF_DIAG  // diagnostic build only: phase stamps (100 MHz) of workgroup 0, clean pass
 __device__ uint64_t g_nmf_stamps[16];
@@ -307,8 +400,14 @@ __device__ uint64_t g_nmf_rstamps[8];  // k_nmf_rows, workgroup 0 wave 0 (owner 
 // (outer products on MFMA; bias / head / loss sums per owning thread).  MODE 2 is
 // prediction only.  DC = compile-time d (0: a.d at run time).
 template <int MODE, int DC>
-__global__ void __launch_bounds__(256) k_nmf_inst(NArgs a) {
+__global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned inst_blocks) {
   extern __shared__ float sm[];
+  if (blockIdx.x >= inst_blocks) {  // the previous pass's weight-gradient workgroups
+    const int x = (int)(blockIdx.x - inst_blocks), ns = (int)inst_blocks;
+    if (wg.d % 16 == 0) wgrad_group<true>(wg, x % ns, x / ns, ns, sm);
+    else wgrad_group<false>(wg, x % ns, x / ns, ns, sm);
+    return;
+  }
   NSTAMP(0);
   const int d = DC ? DC : a.d, d2 = 2 * d, tid = threadIdx.x;
   const int L2 = d2 + 1, L1 = d + 1;  // padded leading dimensions
@@ -445,7 +544,7 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a) {
   float* slot = MODE == 2 ? nullptr : a.wpart + (int64_t)blockIdx.x * wo_.n;
   // vector partials owned by threads across the workgroup's blocks
   float acc_wo = 0.f, acc_b1 = 0.f, acc_b2 = 0.f, acc_bo = 0.f, acc_ls = 0.f;
-  for (int it = 0; blk < nblk; ++it, blk += gridDim.x) {
+  for (; blk < nblk; blk += inst_blocks) {
     const int64_t b0 = blk * MR;
     const int nt = (int)min((int64_t)MR, (int64_t)a.B - b0);
 #pragma unroll
@@ -463,9 +562,9 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a) {
     }
     __syncthreads();
     // the next block's rows fly while this one computes
-    if (blk + gridDim.x < nblk) {
-      gather_idx(blk + gridDim.x);
-      gather_rows(blk + gridDim.x);
+    if (blk + inst_blocks < nblk) {
+      gather_idx(blk + inst_blocks);
+      gather_rows(blk + inst_blocks);
     }
     NSTAMP(2);
     // layer 1: a1 = relu(h0 W1 + b1)
@@ -542,20 +641,26 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a) {
       }
     });
     NSTAMP(8);
-    // weight gradients: W1 += h0^T dz1 [2d][2d], W2 += a1^T dz2 [2d][d] (16x16 tiles
-    // round-robin over the waves), b1 += sum dz1, b2 += sum dz2
-    {
-      constexpr bool EX = DC != 0 && DC % 16 == 0;
-      if (it == 0)
-        outer_tiles<false, EX>(s_x, s_f, s_a1, s_dz2, d, slot + wo_.w1, slot + wo_.w2);
-      else
-        outer_tiles<true, EX>(s_x, s_f, s_a1, s_dz2, d, slot + wo_.w1, slot + wo_.w2);
-      NSTAMP(9);
-      if (tid < d2)
-        for (int t = 0; t < nt; ++t) acc_b1 = acc_b1 + s_f[t * L2 + tid];
-      if (tid < d)
-        for (int t = 0; t < nt; ++t) acc_b2 = acc_b2 + s_dz2[t * L1 + tid];
+    // the weight gradients' operands -> k_nmf_rows' gradient workgroups (W1 += h0^T dz1,
+    // W2 += a1^T dz2 on MFMA there, beside the row sums); b1 += sum dz1, b2 += sum dz2 here
+    for (int x = tid; x < MR * d2; x += 256) {
+      const int t = x / d2, k = x - t * d2;
+      if (t < nt) {
+        const int64_t g = (b0 + t) * d2 + k;
+        a.h0[g] = s_x[t * L2 + k];
+        a.a1[g] = s_a1[t * L2 + k];
+        a.dz1[g] = s_f[t * L2 + k];
+      }
     }
+    for (int x = tid; x < MR * d; x += 256) {
+      const int t = x / d, k = x - t * d;
+      if (t < nt) a.dz2[(b0 + t) * d + k] = s_dz2[t * L1 + k];
+    }
+    if (tid < d2)
+      for (int t = 0; t < nt; ++t) acc_b1 = acc_b1 + s_f[t * L2 + tid];
+    if (tid < d)
+      for (int t = 0; t < nt; ++t) acc_b2 = acc_b2 + s_dz2[t * L1 + tid];
+    NSTAMP(9);
     __syncthreads();
     NSTAMP(10);
   }
@@ -634,6 +739,12 @@ __device__ __forceinline__ void wsum_one(const NArgs& a, int64_t x, int nslot, i
   *dst = v;
 }
 
+// acf_neumf_grad: the passes' slots summed into G (acf_neumf_train does it on the Adam stream)
+__global__ void __launch_bounds__(256) k_nmf_wsum(NArgs a, int nslot, int npass, const float* __restrict__ part,
+                                                  float* loss_out) {
+  wsum_one(a, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, nslot, npass, part, loss_out);
+}
+
 constexpr int MAX_Q = 2;   // d <= 128: each lane holds up to 2 of a row's elements
 constexpr int RCH = 2048;  // batch indices staged in LDS per round
 constexpr int RBATCH = 8;  // occurrences whose contributions are loaded together
@@ -644,14 +755,17 @@ constexpr int RBATCH = 8;  // occurrences whose contributions are loaded togethe
 // sum to the gradient rows and (with_delta) writes delta = eps*g/|g| per table.
 // The workgroup stages the batch's indices in LDS (rounds of RCH); an owner's
 // occurrences are loaded RBATCH at a time and added in order.  Workgroups past
-// the rows' (blockIdx.x >= rows_blocks) sum the weight gradients (k_nmf_wsum's
-// work, fused into this launch).
+// the rows' (blockIdx.x >= rows_blocks) are the pass's weight-gradient
+// workgroups (wgrad_group; nslot slots x tile groups): latency-bound row sums
+// leave the CUs free for their MFMA tiles.
 __global__ void __launch_bounds__(256) k_nmf_rows(NArgs a, int32_t* __restrict__ owner,
                                                   float* __restrict__ delta, int with_delta, float eps,
-                                                  unsigned rows_blocks, int nslot, int npass,
-                                                  const float* __restrict__ part, float* loss_out) {
+                                                  unsigned rows_blocks, int nslot) {
+  extern __shared__ float sm_w[];
   if (blockIdx.x >= rows_blocks) {
-    wsum_one(a, (int64_t)(blockIdx.x - rows_blocks) * 256 + threadIdx.x, nslot, npass, part, loss_out);
+    const int x = (int)(blockIdx.x - rows_blocks);
+    if (a.d % 16 == 0) wgrad_group<true>(a, x % nslot, x / nslot, nslot, sm_w);
+    else wgrad_group<false>(a, x % nslot, x / nslot, nslot, sm_w);
     return;
   }
   __shared__ int32_t s_idx[2][RCH];
@@ -842,6 +956,7 @@ struct acf_neumf_ctx {
   int32_t d = 0, maxB = 0;
   Layout L;
   float *contrib = nullptr, *delta = nullptr;
+  float *h0 = nullptr, *a1 = nullptr, *dz1 = nullptr, *dz2 = nullptr;  // weight-gradient operands
   float* wpart = nullptr;  // [2 passes][slots][weight-gradient outputs]
   int32_t nslot = 0;       // workgroups (slots) of a training pass at max_batch
   int32_t *owner = nullptr, *err = nullptr;
@@ -904,6 +1019,9 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
     *p = static_cast<std::remove_reference_t<decltype(*p)>>(q);
   };
   A(&c->contrib, B * 4 * dd); A(&c->delta, B * 4 * dd); A(&c->owner, 2 * B); A(&c->err, 4);
+  // two sets (clean / adversarial pass): the clean pass's gradient workgroups read theirs
+  // while the adversarial k_nmf_inst writes its own
+  A(&c->h0, 2 * B * 2 * dd); A(&c->a1, 2 * B * 2 * dd); A(&c->dz1, 2 * B * 2 * dd); A(&c->dz2, 2 * B * dd);
   c->nslot = (int32_t)std::min<int64_t>(((int64_t)maxB + MR - 1) / MR, NSLOT);
   A(&c->wpart, 2 * (size_t)c->nslot * (size_t)wout(d).n);
   if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
@@ -923,6 +1041,7 @@ static NArgs make_args(acf_neumf_ctx* c, const float* P, float* G, const int32_t
   a.U1 = c->U1; a.I1 = c->I1; a.B = B; a.d = c->d;
   a.scale_over_B = (float)((double)scale / (double)B);
   a.contrib = c->contrib; a.wpart = c->wpart;
+  a.h0 = c->h0; a.a1 = c->a1; a.dz1 = c->dz1; a.dz2 = c->dz2;
   a.delta = c->delta; a.owner = c->owner; a.pred = nullptr; a.err = c->err;
   return a;
 }
@@ -945,6 +1064,9 @@ static int set_inst_smem_limit() {
                        reinterpret_cast<const void*>(&k_nmf_inst<1, DFAST>),
                        reinterpret_cast<const void*>(&k_nmf_inst<2, DFAST>)};
   for (const void* f : fns) HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  // k_nmf_rows: 16 KB of indices + the gradient workgroups' operands (d = 128: 58 KB)
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_rows),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)wgrad_smem(128)));
   done = 1;
   return ACF_OK;
 }
@@ -958,36 +1080,50 @@ static int read_err(acf_neumf_ctx* c, hipStream_t s) {
   return ACF_OK;
 }
 
+// grid = inst workgroups + (optional) the previous pass's weight-gradient workgroups (args wg)
 template <int MODE>
-static void launch_inst(const NArgs& a, unsigned grid, hipStream_t s) {
+static void launch_inst(const NArgs& a, unsigned inst_blocks, hipStream_t s, const NArgs* wg = nullptr,
+                        unsigned wg_blocks = 0) {
+  const NArgs& w = wg ? *wg : a;
+  const unsigned grid = inst_blocks + (wg ? wg_blocks : 0u);
   if (a.d == DFAST)
-    k_nmf_inst<MODE, DFAST><<<grid, 256, inst_smem(a.d), s>>>(a);
+    k_nmf_inst<MODE, DFAST><<<grid, 256, inst_smem(a.d), s>>>(a, w, inst_blocks);
   else
-    k_nmf_inst<MODE, 0><<<grid, 256, inst_smem(a.d), s>>>(a);
+    k_nmf_inst<MODE, 0><<<grid, 256, inst_smem(a.d), s>>>(a, w, inst_blocks);
 }
 
-// clean pass: k_nmf_inst<0> -> k_nmf_rows (owners, rows, delta); adversarial
-// pass: k_nmf_inst<1> -> k_nmf_rows; the last k_nmf_rows launch also sums the
-// passes' weight-gradient slots into G (wsum), unless the caller leaves that to
+// clean pass: k_nmf_inst<0> -> k_nmf_rows (owners, rows, delta; + the pass's
+// weight-gradient tiles); adversarial pass: k_nmf_inst<1> -> k_nmf_rows; then
+// k_nmf_wsum sums the passes' slots into G, unless the caller leaves that to
 // k_nmf_adam (acf_neumf_train)
 static int launch_grad(acf_neumf_ctx* c, const float* P, float* G, const int32_t* u, const int32_t* i,
                        const float* y, int32_t B, const acf_neumf_hparams* hp, float* loss_out,
                        hipStream_t s, bool wsum = true) {
   const unsigned gi = (unsigned)std::min<int64_t>(((int64_t)B + MR - 1) / MR, NSLOT);
   const unsigned gr = (unsigned)((2 * (int64_t)B + 3) / 4);
+  const unsigned gw = gi * (unsigned)((wtiles(c->d) + WG_TILES - 1) / WG_TILES);  // gradient workgroups
+  const size_t sw = wgrad_smem(c->d);
   const WOut o = wout(c->d);
-  const unsigned gs = wsum ? (unsigned)((o.n + 255) / 256) : 0u;
   const int npass = hp->adver ? 2 : 1;
   NArgs a = make_args(c, P, G, u, i, y, B, 1.0f);
   launch_inst<0>(a, gi, s);
-  k_nmf_rows<<<gr + (npass == 1 ? gs : 0), 256, 0, s>>>(a, c->owner, c->delta, hp->adver ? 1 : 0, hp->eps, gr,
-                                                       (int)gi, npass, c->wpart, loss_out);
+  // APR-style: the clean pass's gradient workgroups ride in the adversarial
+  // k_nmf_inst (32 workgroups at B = 512: the other CUs are idle); BPR-style
+  // (no adversary) in its k_nmf_rows
+  k_nmf_rows<<<gr + (hp->adver ? 0u : gw), 256, sw, s>>>(a, c->owner, c->delta, hp->adver ? 1 : 0, hp->eps, gr,
+                                                        (int)gi);
   HIP_TRY(hipGetLastError());
   if (hp->adver) {
     NArgs b = make_args(c, P, G, u, i, y, B, hp->reg_adv);
     b.wpart = c->wpart + (int64_t)gi * o.n;
-    launch_inst<1>(b, gi, s);
-    k_nmf_rows<<<gr + gs, 256, 0, s>>>(b, c->owner, c->delta, 0, 0.f, gr, (int)gi, npass, c->wpart, loss_out);
+    const int64_t ab = (int64_t)c->maxB;  // the second activation buffer
+    b.h0 += ab * 2 * c->d; b.a1 += ab * 2 * c->d; b.dz1 += ab * 2 * c->d; b.dz2 += ab * c->d;
+    launch_inst<1>(b, gi, s, &a, gw);
+    k_nmf_rows<<<gr + gw, 256, sw, s>>>(b, c->owner, c->delta, 0, 0.f, gr, (int)gi);
+    HIP_TRY(hipGetLastError());
+  }
+  if (wsum) {
+    k_nmf_wsum<<<(unsigned)((o.n + 255) / 256), 256, 0, s>>>(a, (int)gi, npass, c->wpart, loss_out);
     HIP_TRY(hipGetLastError());
   }
   return ACF_OK;
@@ -1061,6 +1197,7 @@ extern "C" int acf_neumf_diag_stamps(uint64_t* out) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nmf_stamps), 16 * sizeof(uint64_t)));
   HIP_TRY(hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_nmf_rstamps), 8 * sizeof(uint64_t)));
+  HIP_TRY(hipMemcpyFromSymbol(out + 24, HIP_SYMBOL(g_nmf_wstamps), 8 * sizeof(uint64_t)));
   return ACF_OK;
 }
 #endif

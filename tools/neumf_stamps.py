@@ -26,7 +26,7 @@ for rep in range(5):
     y = (rng.random(B) < 0.5).astype(np.float32)
     ctx.grad(u, i, y, ctx.hparams(adver=1))
     torch.cuda.synchronize()
-    buf = (ctypes.c_uint64 * 24)()
+    buf = (ctypes.c_uint64 * 32)()
     lib.acf_neumf_diag_stamps(buf)
     t = np.array(buf[:11], dtype=np.int64)
     dt = np.diff(t) * 10 / 1000.0  # us
@@ -35,3 +35,7 @@ for rep in range(5):
     rd = np.diff(rt) * 10 / 1000.0
     print("    rows", " ".join(f"{n}={x:.2f}" for n, x in zip(["stage", "first", "accum", "g_store", "delta"], rd)),
           f"total={rd.sum():.2f}us", f"(starts {(rt[0] - t[-1]) * 10 / 1000.0:.2f}us after inst wg0 end)")
+    wt = np.array(buf[24:28], dtype=np.int64)
+    wd = np.diff(wt) * 10 / 1000.0
+    print("    wgrad", " ".join(f"{n}={x:.2f}" for n, x in zip(["loads", "lds+sync", "tiles"], wd)),
+          f"(starts {(wt[0] - t[0]) * 10 / 1000.0:.2f}us after inst wg0 start)")
