@@ -84,7 +84,12 @@ def test_sharded_rccl_world1_matches_oracle(ops, oracle, dev, fp32_parity, shape
         fp32_parity(g, w, n)
 
 
-def _worker(rank, world, port, out_dir, adver, exchange="all_to_all"):
+# two-rank problems: (U1, I1, d, B, nb, zipf, chunk); "pinterest" is BASELINE configs[2]'s
+# shape (the reference's global batch of 512 split over the ranks)
+SHAPES2 = {"zipf": (20_000, 9_000, 64, 4096, 4, 1.2, 3), "pinterest": (55_188, 9_917, 64, 512, 10, None, 4)}
+
+
+def _worker(rank, world, port, out_dir, adver, exchange="all_to_all", shape="zipf"):
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda", 0)
@@ -92,10 +97,11 @@ def _worker(rank, world, port, out_dir, adver, exchange="all_to_all"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     D_ = importlib.import_module(PKG + ".distributed")
     ops = importlib.import_module(PKG + ".ops")
-    P, Q, u, i, j = _problem(7 + adver, 20_000, 9_000, 64, 4096, 4, 1.2)
-    sh = D_.ShardedAPR(20_000, 9_000, 64, 4096, device=dev, init_P=P, init_Q=Q, item_exchange=exchange)
+    U1, I1, d, B, nb, z, chunk = SHAPES2[shape]
+    P, Q, u, i, j = _problem(7 + adver, U1, I1, d, B, nb, z)
+    sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, item_exchange=exchange)
     uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
-    sh.train(uu, ii, jj, ops.StepHParams(adver=adver), chunk=3)
+    sh.train(uu, ii, jj, ops.StepHParams(adver=adver), chunk=chunk)
     full = sh.full_tables()
     if rank == 0:
         np.savez(os.path.join(out_dir, "w2.npz"), *[t.cpu().numpy() for t in full])
@@ -104,13 +110,18 @@ def _worker(rank, world, port, out_dir, adver, exchange="all_to_all"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("adver,exchange", [(1, "all_to_all"), (0, "all_to_all"), (1, "allgather")])
-def test_sharded_two_ranks_one_gpu_matches_oracle(oracle, fp32_parity, tmp_path, adver, exchange):
+@pytest.mark.parametrize("adver,exchange,shape", [(1, "all_to_all", "zipf"), (0, "all_to_all", "zipf"),
+                                                  (1, "allgather", "zipf"), (1, "all_to_all", "pinterest"),
+                                                  (1, "allgather", "pinterest")])
+def test_sharded_two_ranks_one_gpu_matches_oracle(oracle, fp32_parity, tmp_path, adver, exchange, shape):
+    """shape "pinterest": configs[2] (55,187 x 9,916, d = 64, global batch 512) split over two
+    ranks, both E1 forms."""
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), adver, exchange), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), adver, exchange, shape), nprocs=world, join=True)
     got = np.load(os.path.join(tmp_path, "w2.npz"))
-    P, Q, u, i, j = _problem(7 + adver, 20_000, 9_000, 64, 4096, 4, 1.2)
-    want = _want(oracle, P, Q, u, i, j, 4096, adver)
+    U1, I1, d, B, nb, z, _ = SHAPES2[shape]
+    P, Q, u, i, j = _problem(7 + adver, U1, I1, d, B, nb, z)
+    want = _want(oracle, P, Q, u, i, j, B, adver)
     for k, (w, n) in enumerate(zip(want, ("P", "Q", "accP", "accQ"))):
         fp32_parity(got[f"arr_{k}"], w, n)
     runs = [np.load(os.path.join(tmp_path, f"n{r}.npy")) for r in range(world)]
