@@ -34,6 +34,7 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--reps", type=int, default=5, help="timed repetitions (each on fresh batches)")
+    p.add_argument("--failsafe", type=int, default=1, help="verified streamed calls (1, default) or not (0)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -47,6 +48,7 @@ def main():
     tabs = bench.init_tables(U1, I1, d, dev, seed=0)
     chunk = a.steps
     pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=None)
+    pipe.set_failsafe(bool(a.failsafe))
     hp = ops.StepHParams(lr=0.05, eps=0.5, reg=0.0, reg_adv=1.0, adver=1)
     pipe.run(tabs, hp, u, i, j, 0, max(a.warmup, 2 * chunk))
     torch.cuda.synchronize(dev)
