@@ -24,6 +24,12 @@
 //                       row's moments decay and every row moves): one HBM
 //                       stream of p, g, m, v, zeroing g behind it.
 //
+// acf_neumf_train splits that Adam (same arithmetic per element): k_nmf_adam_next
+// steps the rows the next batch gathers and the MLP / head parameters on the
+// caller's stream; k_nmf_adam_rest steps every other row on a side stream,
+// beside the next step's latency-bound kernels (and reads no g for rows the
+// step's batch did not touch).
+//
 // The MLP is tiny per instance (2d x 2d and 2d x d at d = 64) and the step is
 // bound by the dense Adam stream over the tables, not by the GEMMs.
 
@@ -678,11 +684,12 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
   if (bad) atomicOr(a.err, bad);
 }
 
-// Weight gradients of the step: slot element x summed over the passes' slots in
-// slot order (deterministic, no atomics); G += clean sum, then += adversarial sum;
-// the loss element gives the passes' mean losses.  k_nmf_adam does the same sums
-// in-line when it is handed the slots (acf_neumf_train).
-// (loads issued SB at a time, added in slot order)
+// Weight gradients of the step: slot element x summed over the passes' slots
+// (deterministic, no atomics): groups of SB consecutive slots summed in slot
+// order, then the group sums in group order; G += clean sum, then += adversarial
+// sum; the loss element gives the passes' mean losses.  acf_neumf_train does the
+// same sums with a lane per group (k_nmf_adam_next), so train == grad + adam bit
+// for bit.
 constexpr int SB = 8;
 
 __device__ __forceinline__ float slot_sum(const float* part, int p, int nslot, int64_t nout, int64_t x) {
@@ -692,30 +699,43 @@ __device__ __forceinline__ float slot_sum(const float* part, int p, int nslot, i
     float v[SB];
 #pragma unroll
     for (int j = 0; j < SB; ++j) v[j] = s0 + j < nslot ? q[(int64_t)(s0 + j) * nout] : 0.f;
+    float gs = 0.f;
 #pragma unroll
     for (int j = 0; j < SB; ++j)
-      if (s0 + j < nslot) acc = acc + v[j];
+      if (s0 + j < nslot) gs = gs + v[j];
+    acc = acc + gs;
   }
   return acc;
 }
 
-// four consecutive elements (x a multiple of 4, nout a multiple of 4)
-__device__ __forceinline__ float4 slot_sum4(const float* part, int p, int nslot, int64_t nout, int64_t x) {
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+// group gi's sum of four consecutive elements (x a multiple of 4, nout a multiple of 4)
+__device__ __forceinline__ float4 slot_group4(const float* part, int p, int nslot, int64_t nout, int64_t x, int gi) {
   const float4* q = reinterpret_cast<const float4*>(part + (int64_t)p * nslot * nout + x);
   const int64_t st = nout / 4;
-  for (int s0 = 0; s0 < nslot; s0 += SB) {
-    float4 v[SB];
+  const int s0 = gi * SB;
+  float4 v[SB];
 #pragma unroll
-    for (int j = 0; j < SB; ++j) v[j] = s0 + j < nslot ? q[(s0 + j) * st] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = 0; j < SB; ++j) v[j] = s0 + j < nslot ? q[(s0 + j) * st] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 gs = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int j = 0; j < SB; ++j)
-      if (s0 + j < nslot) {
-        acc.x = acc.x + v[j].x;
-        acc.y = acc.y + v[j].y;
-        acc.z = acc.z + v[j].z;
-        acc.w = acc.w + v[j].w;
-      }
+  for (int j = 0; j < SB; ++j)
+    if (s0 + j < nslot) {
+      gs.x = gs.x + v[j].x;
+      gs.y = gs.y + v[j].y;
+      gs.z = gs.z + v[j].z;
+      gs.w = gs.w + v[j].w;
+    }
+  return gs;
+}
+
+__device__ __forceinline__ float4 slot_sum4(const float* part, int p, int nslot, int64_t nout, int64_t x) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int gi = 0; gi * SB < nslot; ++gi) {
+    const float4 gs = slot_group4(part, p, nslot, nout, x, gi);
+    acc.x = acc.x + gs.x;
+    acc.y = acc.y + gs.y;
+    acc.z = acc.z + gs.z;
+    acc.w = acc.w + gs.w;
   }
   return acc;
 }
@@ -901,50 +921,208 @@ struct AdamSlots {
   float B = 1.f;  // the batch, for the mean losses
 };
 
-// Keras 2.2 Adam (keras/optimizers.py Adam.get_updates), dense, float4 stream:
+// Keras 2.2 Adam (keras/optimizers.py Adam.get_updates) of float4 x:
 // m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g^2; p -= lr_t*m / (sqrt(v) + eps); g = 0.
+// With slots (ws.part) the float4s from base4 on first get the slot sums of
+// k_nmf_inst added to their gradient (wsum_one's arithmetic); the loss element
+// goes to loss_out.
+struct AdamK {
+  float b1, b2, lr_t, eps;
+};
+
+// the float4's operands, loaded together (a wave issues them before its slot
+// sums or its row claim resolve)
+struct Adam4V {
+  float4 g, m, v, p;
+};
+
+__device__ __forceinline__ Adam4V adam4_load(const float4* p, const float4* g, const float4* m, const float4* v,
+                                             int64_t x) {
+  return Adam4V{g[x], m[x], v[x], p[x]};
+}
+
+// the slot sums s4[pass] of float4 x (x >= ws.base4) added to its gradient; the loss element
+__device__ __forceinline__ void adam4_fold(float4& gg, int64_t x, const AdamSlots& ws, const float4* s4) {
+  const int64_t e0 = 4 * (x - ws.base4);
+  const int64_t loss_x = ws.nout - 3;
+  const float sum[2][4] = {{s4[0].x, s4[0].y, s4[0].z, s4[0].w}, {s4[1].x, s4[1].y, s4[1].z, s4[1].w}};
+  float* gc = &gg.x;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (e0 + c < loss_x) {
+      float t = gc[c] + sum[0][c];
+      if (ws.npass > 1) t = t + sum[1][c];
+      gc[c] = t;
+    } else if (e0 + c == loss_x && ws.loss_out) {
+      ws.loss_out[0] = sum[0][c] / ws.B;
+      ws.loss_out[1] = ws.npass > 1 ? sum[1][c] / ws.B : 0.f;
+    }
+  }
+}
+
+template <bool GZ = false>  // GZ: g is known to be 0 (neither loaded nor cleared)
+__device__ __forceinline__ void adam4_store(float4* p, float4* g, float4* m, float4* v, int64_t x, const AdamK& k,
+                                            Adam4V a) {
+  const float c1 = 1.0f - k.b1, c2 = 1.0f - k.b2;
+#define ACF_ADAM(c)                                          \
+  a.m.c = k.b1 * a.m.c + c1 * a.g.c;                         \
+  a.v.c = k.b2 * a.v.c + c2 * (a.g.c * a.g.c);               \
+  a.p.c = a.p.c - (k.lr_t * a.m.c) / (sqrtf(a.v.c) + k.eps);
+  ACF_ADAM(x) ACF_ADAM(y) ACF_ADAM(z) ACF_ADAM(w)
+#undef ACF_ADAM
+  m[x] = a.m;
+  v[x] = a.v;
+  p[x] = a.p;
+  if (!GZ) g[x] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ void adam4(float4* __restrict__ p, float4* __restrict__ g, float4* __restrict__ m,
+                                      float4* __restrict__ v, int64_t x, const AdamK& k, const AdamSlots& ws) {
+  Adam4V a = adam4_load(p, g, m, v, x);
+  if (ws.part && x >= ws.base4) {
+    const int64_t e0 = 4 * (x - ws.base4);
+    float4 s4[2];
+    s4[0] = slot_sum4(ws.part, 0, ws.nslot, ws.nout, e0);
+    s4[1] = ws.npass > 1 ? slot_sum4(ws.part, 1, ws.nslot, ws.nout, e0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    adam4_fold(a.g, x, ws, s4);
+  }
+  adam4_store(p, g, m, v, x, k, a);
+}
+
+// dense, float4 stream; with slots the stream runs from the top down: the slot
+// range (the buffer's tail) is summed in the first sweep, under the rest of it
 __global__ void __launch_bounds__(256) k_nmf_adam(float4* __restrict__ p, float4* __restrict__ g,
                                                   float4* __restrict__ m, float4* __restrict__ v,
                                                   int64_t n4, float b1, float b2, float lr_t,
                                                   float eps, AdamSlots ws = AdamSlots()) {
-  const float c1 = 1.0f - b1, c2 = 1.0f - b2;
-  // with slots the stream runs from the top down: the slot range (the buffer's
-  // tail) is summed in the first sweep, under the rest of the stream
+  const AdamK k{b1, b2, lr_t, eps};
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t x = ws.part ? n4 - 1 - i : i;
-    float4 gg = g[x];
-    if (ws.part && x >= ws.base4) {
-      const int64_t e0 = 4 * (x - ws.base4);
-      const int64_t loss_x = ws.nout - 3;
-      float4 s4[2];
-      s4[0] = slot_sum4(ws.part, 0, ws.nslot, ws.nout, e0);
-      s4[1] = ws.npass > 1 ? slot_sum4(ws.part, 1, ws.nslot, ws.nout, e0) : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float sum[2][4] = {{s4[0].x, s4[0].y, s4[0].z, s4[0].w}, {s4[1].x, s4[1].y, s4[1].z, s4[1].w}};
-      float* gc = &gg.x;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (e0 + c < loss_x) {
-          float t = gc[c] + sum[0][c];
-          if (ws.npass > 1) t = t + sum[1][c];
-          gc[c] = t;
-        } else if (e0 + c == loss_x && ws.loss_out) {
-          ws.loss_out[0] = sum[0][c] / ws.B;
-          ws.loss_out[1] = ws.npass > 1 ? sum[1][c] / ws.B : 0.f;
-        }
+       i += (int64_t)gridDim.x * blockDim.x)
+    adam4(p, g, m, v, ws.part ? n4 - 1 - i : i, k, ws);
+}
+
+// acf_neumf_train splits each step's dense Adam in two (same arithmetic per
+// element, each element stepped once):
+//  k_nmf_adam_next  (caller's stream) the rows the NEXT batch gathers -- a wave per
+//                   (instance, side) claims its user / item row (mark = tag, first
+//                   claimer updates both tables' rows) -- and the parameter tail
+//                   (MLP / head, with the slot sums and the losses);
+//  k_nmf_adam_rest  (a side stream) every other embedding row, skipping the
+//                   claimed ones, beside the next step's latency-bound kernels.
+constexpr int64_t REST_WG = 192;
+
+struct AdamSplit {
+  int64_t U1, I1, d4;         // rows; float4s per row
+  int64_t emb4;               // float4s of the four embedding tables (= off[S_W1] / 4)
+  int32_t* mark_u;            // [U1] last tag that claimed the user row
+  int32_t* mark_i;            // [I1]
+  int32_t tag;
+  int32_t prev_tag;  // the tag the previous step's next-part claimed this batch's rows with
+  int32_t g_known;   // 1: a row not marked prev_tag has g = 0 (its batch did not touch it)
+};
+
+__global__ void __launch_bounds__(256) k_nmf_adam_next(float4* __restrict__ p, float4* __restrict__ g,
+                                                       float4* __restrict__ m, float4* __restrict__ v,
+                                                       int64_t n4, AdamK k, AdamSlots ws, AdamSplit sp,
+                                                       const int32_t* __restrict__ un,
+                                                       const int32_t* __restrict__ in, int32_t Bn,
+                                                       unsigned row_blocks) {
+  if (blockIdx.x >= row_blocks) {  // the parameter tail: a wave per float4, a lane per (pass, slot group)
+    const int64_t t4 = n4 - sp.emb4;
+    const int lane = threadIdx.x & 63, pass = lane >> 5, gi = lane & 31;
+    const int ng = (ws.nslot + SB - 1) / SB;  // <= 32 (nslot <= NSLOT)
+    const int64_t w0 = ((blockIdx.x - row_blocks) * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)(gridDim.x - row_blocks) * blockDim.x) >> 6;
+    for (int64_t i = w0; i < t4; i += nw) {
+      const int64_t x = sp.emb4 + i;
+      Adam4V a{};
+      if (lane == 0) a = adam4_load(p, g, m, v, x);
+      float4 gs = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gi < ng && pass < ws.npass) gs = slot_group4(ws.part, pass, ws.nslot, ws.nout, 4 * i, gi);
+      // the group sums in group order (slot_sum4's arithmetic), by lanes 0 and 32
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int j = 0; j < ng; ++j) {
+        const int src = (lane & 32) + j;
+        acc.x = acc.x + __shfl(gs.x, src, 64);
+        acc.y = acc.y + __shfl(gs.y, src, 64);
+        acc.z = acc.z + __shfl(gs.z, src, 64);
+        acc.w = acc.w + __shfl(gs.w, src, 64);
+      }
+      float4 sums[2];
+      sums[0] = acc;
+      sums[1] = make_float4(__shfl(acc.x, 32, 64), __shfl(acc.y, 32, 64), __shfl(acc.z, 32, 64),
+                            __shfl(acc.w, 32, 64));
+      if (ws.npass < 2) sums[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lane == 0) {
+        adam4_fold(a.g, x, ws, sums);
+        adam4_store(p, g, m, v, x, k, a);
       }
     }
-    float4 mm = m[x], vv = v[x], pp = p[x];
-#define ACF_ADAM(c)                                        \
-  mm.c = b1 * mm.c + c1 * gg.c;                            \
-  vv.c = b2 * vv.c + c2 * (gg.c * gg.c);                   \
-  pp.c = pp.c - (lr_t * mm.c) / (sqrtf(vv.c) + eps);
-    ACF_ADAM(x) ACF_ADAM(y) ACF_ADAM(z) ACF_ADAM(w)
-#undef ACF_ADAM
-    m[x] = mm;
-    v[x] = vv;
-    p[x] = pp;
-    g[x] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= 2 * (int64_t)Bn) return;
+  const int b = (int)(wave >> 1), side = (int)(wave & 1);
+  const int64_t nrows = side ? sp.I1 : sp.U1;
+  int32_t r = side ? in[b] : un[b];
+  if (r < 0 || r >= nrows) r = 0;  // the step flags bad indices; row 0 stays a valid address
+  int32_t* mk = (side ? sp.mark_i : sp.mark_u) + r;
+  int old = 0;
+  if (lane == 0) old = atomicExch(mk, sp.tag);
+  // the row's float4s in its two tables (MF_x then MLP_x), loaded beside the claim:
+  // nothing else writes the row before the claimer's stores
+  const int64_t d4 = sp.d4;
+  const int64_t mf = side ? sp.U1 * d4 + r * d4 : r * d4;                  // S_MF_U / S_MF_I
+  const int64_t mlp = side ? (2 * sp.U1 + sp.I1) * d4 + r * d4 : (sp.U1 + sp.I1) * d4 + r * d4;  // S_MLP_x
+  if (d4 <= 32) {  // one float4 a lane (d <= 128)
+    const int64_t x = lane < d4 ? mf + lane : mlp + (lane - d4);
+    Adam4V a{};
+    if (lane < 2 * d4) a = adam4_load(p, g, m, v, x);
+    old = __shfl(old, 0, 64);
+    if (old == sp.tag) return;  // another occurrence claimed the row
+    if (lane < 2 * d4) adam4_store(p, g, m, v, x, k, a);
+    return;
+  }
+  old = __shfl(old, 0, 64);
+  if (old == sp.tag) return;
+  for (int64_t q = lane; q < 2 * d4; q += 64) adam4(p, g, m, v, q < d4 ? mf + q : mlp + (q - d4), k, AdamSlots());
+}
+
+__global__ void __launch_bounds__(256) k_nmf_adam_rest(float4* __restrict__ p, float4* __restrict__ g,
+                                                       float4* __restrict__ m, float4* __restrict__ v, AdamK k,
+                                                       AdamSplit sp) {
+  const int64_t d4 = sp.d4, U4 = sp.U1 * d4, I4 = sp.I1 * d4;
+  constexpr int R = 4;  // float4s in flight per thread
+  const int64_t st = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t x0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x0 < sp.emb4; x0 += R * st) {
+    bool live[R], gz[R];
+    Adam4V a[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int64_t x = x0 + j * st;
+      live[j] = x < sp.emb4;
+      if (!live[j]) continue;
+      // segments: MF_U [0, U4), MF_I [U4, U4+I4), MLP_U [.., 2U4+I4), MLP_I [.., emb4)
+      int32_t mk;
+      if (x < U4) mk = sp.mark_u[x / d4];
+      else if (x < U4 + I4) mk = sp.mark_i[(x - U4) / d4];
+      else if (x < 2 * U4 + I4) mk = sp.mark_u[(x - U4 - I4) / d4];
+      else mk = sp.mark_i[(x - 2 * U4 - I4) / d4];
+      live[j] = mk != sp.tag;  // else k_nmf_adam_next stepped it
+      // a row the step's batch did not gather has g = 0: no g traffic (25% of the bytes)
+      gz[j] = sp.g_known && mk != sp.prev_tag;
+      if (live[j]) {
+        if (gz[j]) a[j] = Adam4V{make_float4(0.f, 0.f, 0.f, 0.f), m[x], v[x], p[x]};
+        else a[j] = adam4_load(p, g, m, v, x);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (live[j]) {
+        if (gz[j]) adam4_store<true>(p, g, m, v, x0 + j * st, k, a[j]);
+        else adam4_store(p, g, m, v, x0 + j * st, k, a[j]);
+      }
   }
 }
 
@@ -960,6 +1138,11 @@ struct acf_neumf_ctx {
   float* wpart = nullptr;  // [2 passes][slots][weight-gradient outputs]
   int32_t nslot = 0;       // workgroups (slots) of a training pass at max_batch
   int32_t *owner = nullptr, *err = nullptr;
+  // acf_neumf_train's split Adam: row claims, the side stream and its events
+  int32_t *mark_u = nullptr, *mark_i = nullptr;
+  int32_t tag = 0;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_next = nullptr, ev_rest = nullptr;
   std::vector<void*> allocs;
 };
 
@@ -989,7 +1172,11 @@ extern "C" int acf_neumf_param_offsets(int64_t U1, int64_t I1, int32_t d, int64_
 
 extern "C" int acf_neumf_destroy(acf_neumf_ctx* c) {
   if (!c) return ACF_OK;
+  if (c->side) (void)hipStreamSynchronize(c->side);
   for (void* p : c->allocs) (void)hipFree(p);
+  if (c->ev_next) (void)hipEventDestroy(c->ev_next);
+  if (c->ev_rest) (void)hipEventDestroy(c->ev_rest);
+  if (c->side) (void)hipStreamDestroy(c->side);
   delete c;
   return ACF_OK;
 }
@@ -1022,6 +1209,13 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
   // two sets (clean / adversarial pass): the clean pass's gradient workgroups read theirs
   // while the adversarial k_nmf_inst writes its own
   A(&c->h0, 2 * B * 2 * dd); A(&c->a1, 2 * B * 2 * dd); A(&c->dz1, 2 * B * 2 * dd); A(&c->dz2, 2 * B * dd);
+  A(&c->mark_u, (size_t)U1); A(&c->mark_i, (size_t)I1);
+  if (r == ACF_OK && (hipMemset(c->mark_u, 0, (size_t)U1 * 4) != hipSuccess ||
+                      hipMemset(c->mark_i, 0, (size_t)I1 * 4) != hipSuccess ||
+                      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+                      hipEventCreateWithFlags(&c->ev_next, hipEventDisableTiming) != hipSuccess ||
+                      hipEventCreateWithFlags(&c->ev_rest, hipEventDisableTiming) != hipSuccess))
+    r = set_error(ACF_E_HIP, "split-Adam setup failed");
   c->nslot = (int32_t)std::min<int64_t>(((int64_t)maxB + MR - 1) / MR, NSLOT);
   A(&c->wpart, 2 * (size_t)c->nslot * (size_t)wout(d).n);
   if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
@@ -1142,11 +1336,15 @@ extern "C" int acf_neumf_grad(acf_neumf_ctx* c, const float* P, float* G, const 
   return ACF_OK;
 }
 
+// lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t), evaluated in float32 as Keras does
+static float adam_lr_t(const acf_neumf_hparams* hp, int64_t t) {
+  const float tt = (float)t;
+  return hp->lr * (sqrtf(1.0f - powf(hp->beta2, tt)) / (1.0f - powf(hp->beta1, tt)));
+}
+
 static int launch_adam(acf_neumf_ctx* c, float* P, float* G, float* m, float* v, int64_t t,
                        const acf_neumf_hparams* hp, hipStream_t s, const AdamSlots& ws = AdamSlots()) {
-  // lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t), evaluated in float32 as Keras does
-  const float tt = (float)t;
-  const float lr_t = hp->lr * (sqrtf(1.0f - powf(hp->beta2, tt)) / (1.0f - powf(hp->beta1, tt)));
+  const float lr_t = adam_lr_t(hp, t);
   const int64_t n4 = c->L.total / 4;
   const unsigned grid = (unsigned)std::min<int64_t>((n4 + 255) / 256, 256 * 32);
   k_nmf_adam<<<grid, 256, 0, s>>>(reinterpret_cast<float4*>(P), reinterpret_cast<float4*>(G),
@@ -1172,23 +1370,60 @@ extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, f
   ACF_CHECK(n >= 0 && t_first >= 1, ACF_E_INVALID, "bad instance count or Adam iteration");
   hipStream_t s = static_cast<hipStream_t>(stream_);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  float4 *P4 = reinterpret_cast<float4*>(P), *G4 = reinterpret_cast<float4*>(G);
+  float4 *m4 = reinterpret_cast<float4*>(m), *v4 = reinterpret_cast<float4*>(v);
+  const int64_t n4 = c->L.total / 4;
+  AdamSplit sp;
+  sp.U1 = c->U1; sp.I1 = c->I1; sp.d4 = c->d / 4; sp.emb4 = c->L.off[S_W1] / 4;
+  sp.mark_u = c->mark_u; sp.mark_i = c->mark_i;
+  const unsigned tail_blocks = (unsigned)std::min<int64_t>((n4 - sp.emb4 + 3) / 4, 2048);  // a wave per float4
+  // the rest runs beside the step's latency-bound kernels: 3 workgroups per 4 CUs
+  // (yelp shape, d 64, B 512: 8192 WGs 5.65M instances/s, 512 5.79M, 256 6.59M,
+  // 192 6.71M, 128 5.52M -- fewer and the rest outlasts the step)
+  const unsigned rest_grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((sp.emb4 + 255) / 256, REST_WG));
   int64_t k = 0;
   for (int64_t o = 0; o < n; o += batch, ++k) {
     const int32_t B = (int32_t)std::min<int64_t>(batch, n - o);
-    // the weight-gradient slot sums ride on the Adam stream (same arithmetic as
-    // acf_neumf_grad's wsum, so train == grad + adam bit for bit)
     int r = launch_grad(c, P, G, u + o, i + o, y + o, B, hp, nullptr, s, false);
+    if (r != ACF_OK) {
+      if (k > 0) (void)hipStreamWaitEvent(s, c->ev_rest, 0);
+      return r;
+    }
+    // Adam of step k in two parts (k_nmf_adam_next / k_nmf_adam_rest): first the
+    // rows batch k+1 gathers and the parameter tail, with the weight-gradient slot
+    // sums (acf_neumf_grad's wsum arithmetic, so train == grad + adam bit for
+    // bit); then, on the side stream and beside step k+1, every other row.  The
+    // next part of step k waits for the rest of step k-1 (a row it claims may be
+    // one step k-1's rest still has to step first).
     AdamSlots ws;
     ws.part = c->wpart;
     ws.nslot = (int)std::min<int64_t>(((int64_t)B + MR - 1) / MR, NSLOT);
     ws.npass = hp->adver ? 2 : 1;
-    ws.base4 = c->L.off[S_W1] / 4;
+    ws.base4 = sp.emb4;
     ws.nout = wout(c->d).n;
     ws.loss_out = losses ? losses + 2 * k : nullptr;
     ws.B = (float)B;
-    if (r == ACF_OK) r = launch_adam(c, P, G, m, v, t_first + k, hp, s, ws);
-    if (r != ACF_OK) return r;
+    const AdamK ak{hp->beta1, hp->beta2, adam_lr_t(hp, t_first + k), hp->adam_eps};
+    const int64_t on = o + batch;
+    const int32_t Bn = on < n ? (int32_t)std::min<int64_t>(batch, n - on) : 0;
+    // step k's batch rows were claimed with the previous tag by step k-1's next
+    // part (step 0's G may hold anything the caller accumulated: read it all)
+    sp.prev_tag = c->tag;
+    sp.g_known = k > 0;
+    if (++c->tag == 0) ++c->tag;  // 0 = never claimed
+    sp.tag = c->tag;
+    const unsigned row_blocks = (unsigned)((2 * (int64_t)Bn * 64 + 255) / 256);
+    if (k > 0) HIP_TRY(hipStreamWaitEvent(s, c->ev_rest, 0));
+    k_nmf_adam_next<<<row_blocks + tail_blocks, 256, 0, s>>>(P4, G4, m4, v4, n4, ak, ws, sp, u + on, i + on, Bn,
+                                                            row_blocks);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev_next, s));
+    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_next, 0));
+    k_nmf_adam_rest<<<rest_grid, 256, 0, c->side>>>(P4, G4, m4, v4, ak, sp);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev_rest, c->side));
   }
+  if (k > 0) HIP_TRY(hipStreamWaitEvent(s, c->ev_rest, 0));  // the caller's stream sees every update
   return read_err(c, s);
 }
 

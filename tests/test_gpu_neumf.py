@@ -142,12 +142,16 @@ def test_recommender_surface(nm, dev):
         assert s.shape == (5, 1) and np.all((s > 0) & (s < 1))
 
 
-def test_train_epoch_equals_stepwise(nm, dev):
-    """acf_neumf_train (native batch loop) == grad + adam per batch, bit for bit,
-    including the trailing partial batch."""
+@pytest.mark.parametrize("B", [96, 300])
+def test_train_epoch_equals_stepwise(nm, dev, B):
+    """acf_neumf_train (native batch loop, split Adam: next batch's rows + MLP on
+    the stream, every other row on a side stream) == grad + dense adam per batch,
+    bit for bit, including the trailing partial batch.  41 users / 37 items: every
+    batch re-gathers rows the previous one touched; B = 300 sums 19 weight-gradient
+    slots in three groups."""
     P, _, _, _ = _problem(21, d=64)
     rng = np.random.default_rng(9)
-    n, B = 1000, 96
+    n = 1000
     u = rng.integers(0, 41, n).astype(np.int32)
     i = rng.integers(0, 37, n).astype(np.int32)
     y = (rng.random(n) < 0.5).astype(np.float32)
@@ -162,7 +166,9 @@ def test_train_epoch_equals_stepwise(nm, dev):
             cb.adam(hp)
         torch.cuda.synchronize()
         assert a.t == b.t == (n + B - 1) // B
-        assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(la, lb)
+        assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+        assert torch.equal(la, lb)
+        assert not a.grad.any() and not b.grad.any()
 
 
 def test_neumf_ranker_in_evaluation_protocol(nm, acf, dev):
