@@ -24,14 +24,15 @@
 //                       row's moments decay and every row moves): one HBM
 //                       stream of p, g, m, v, zeroing g behind it.
 //
-// acf_neumf_train splits that Adam (same arithmetic per element): k_nmf_adam_next
-// steps the rows the next batch gathers and the MLP / head parameters on the
-// caller's stream; k_nmf_adam_rest steps every other row on a side stream,
-// beside the next step's latency-bound kernels (and reads no g for rows the
-// step's batch did not touch).
+// acf_neumf_train runs that Adam lazily, with the same arithmetic per element
+// (bit-identical results): a row's zero-gradient iterations are deferred until
+// the next batch gathers it (k_nmf_adam_next, with the MLP / head parameters on
+// the caller's stream) or a rotating catch-up slice on a side stream reaches it
+// (k_nmf_adam_catchup, beside the next step's latency-bound kernels), so a step
+// moves the rows it touches instead of the whole tables.
 //
-// The MLP is tiny per instance (2d x 2d and 2d x d at d = 64) and the step is
-// bound by the dense Adam stream over the tables, not by the GEMMs.
+// The MLP is tiny per instance (2d x 2d and 2d x d at d = 64); the step is a
+// latency-bound chain (gather -> 4 MFMA layers -> weight gradients -> rows).
 
 #include <hip/hip_runtime.h>
 
@@ -960,20 +961,24 @@ __device__ __forceinline__ void adam4_fold(float4& gg, int64_t x, const AdamSlot
   }
 }
 
-template <bool GZ = false>  // GZ: g is known to be 0 (neither loaded nor cleared)
-__device__ __forceinline__ void adam4_store(float4* p, float4* g, float4* m, float4* v, int64_t x, const AdamK& k,
-                                            Adam4V a) {
+// one Adam iteration of the float4 with learning rate lr_t (every path's arithmetic)
+__device__ __forceinline__ void adam_math(Adam4V& a, const AdamK& k, float lr_t) {
   const float c1 = 1.0f - k.b1, c2 = 1.0f - k.b2;
 #define ACF_ADAM(c)                                          \
   a.m.c = k.b1 * a.m.c + c1 * a.g.c;                         \
   a.v.c = k.b2 * a.v.c + c2 * (a.g.c * a.g.c);               \
-  a.p.c = a.p.c - (k.lr_t * a.m.c) / (sqrtf(a.v.c) + k.eps);
+  a.p.c = a.p.c - (lr_t * a.m.c) / (sqrtf(a.v.c) + k.eps);
   ACF_ADAM(x) ACF_ADAM(y) ACF_ADAM(z) ACF_ADAM(w)
 #undef ACF_ADAM
+}
+
+__device__ __forceinline__ void adam4_store(float4* p, float4* g, float4* m, float4* v, int64_t x, const AdamK& k,
+                                            Adam4V a) {
+  adam_math(a, k, k.lr_t);
   m[x] = a.m;
   v[x] = a.v;
   p[x] = a.p;
-  if (!GZ) g[x] = make_float4(0.f, 0.f, 0.f, 0.f);
+  g[x] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 __device__ __forceinline__ void adam4(float4* __restrict__ p, float4* __restrict__ g, float4* __restrict__ m,
@@ -1001,48 +1006,96 @@ __global__ void __launch_bounds__(256) k_nmf_adam(float4* __restrict__ p, float4
     adam4(p, g, m, v, ws.part ? n4 - 1 - i : i, k, ws);
 }
 
-// acf_neumf_train splits each step's dense Adam in two (same arithmetic per
-// element, each element stepped once):
-//  k_nmf_adam_next  (caller's stream) the rows the NEXT batch gathers -- a wave per
-//                   (instance, side) claims its user / item row (mark = tag, first
-//                   claimer updates both tables' rows) -- and the parameter tail
-//                   (MLP / head, with the slot sums and the losses);
-//  k_nmf_adam_rest  (a side stream) every other embedding row, skipping the
-//                   claimed ones, beside the next step's latency-bound kernels.
-constexpr int64_t REST_WG = 192;
+// acf_neumf_train runs Keras's dense Adam lazily with the same per-element
+// arithmetic, so train == grad + adam bit for bit.  Each row holds in G the
+// gradient of at most one pending iteration pend[r] (the step that gathered it);
+// at every other iteration its gradient is 0, and such an iteration (m = b1 m,
+// v = b2 v, p -= lr_t m / (sqrt(v) + eps)) depends on (p, m, v) and lr_t only.
+// So a row's iterations can run later, in order, all at once, as long as that
+// happens before anything reads the row or adds to its G:
+//  k_nmf_adam_next    (caller's stream, after step k's gradients: iteration t)
+//                     the rows of batch k+1, which step k+1 gathers and adds
+//                     gradients to: a wave per (instance, side) claims its user /
+//                     item row (atomicExch of the row's last iteration: the first
+//                     claimer runs it) and runs the row's iterations up to t in
+//                     both of its tables (MF_x, MLP_x), the pending one with G;
+//                     pend = t + 1.  And the parameter tail (MLP / head) with the
+//                     slot sums and the losses, every iteration;
+//  k_nmf_adam_catchup (side stream, beside step k+1's kernels) slice k % LAZY_S
+//                     of the rows brought to iteration t, so no row is more than
+//                     LAZY_S iterations behind; after the call's last step, every
+//                     row (caller's stream).
+constexpr int LAZY_S = 8;   // catch-up period: a row is at most LAZY_S iterations behind
+constexpr int LAZY_W = 16;  // lr_t window (> LAZY_S)
+// workgroups of a step's catch-up slice, beside the step's kernels (yelp shape,
+// d 64, B 512: 32 WGs 3.9M instances/s (the slice outlasts the step), 64 5.6M,
+// 96 7.55M, 128 7.3M, 192 7.45M, 256 7.35M)
+constexpr int64_t CATCHUP_WG = 96;
+static_assert(LAZY_W > LAZY_S, "lr window");
 
-struct AdamSplit {
-  int64_t U1, I1, d4;         // rows; float4s per row
-  int64_t emb4;               // float4s of the four embedding tables (= off[S_W1] / 4)
-  int32_t* mark_u;            // [U1] last tag that claimed the user row
-  int32_t* mark_i;            // [I1]
-  int32_t tag;
-  int32_t prev_tag;  // the tag the previous step's next-part claimed this batch's rows with
-  int32_t g_known;   // 1: a row not marked prev_tag has g = 0 (its batch did not touch it)
+struct AdamLazy {
+  int64_t U1, I1, d4;
+  int32_t* last_u;   // [U1] the last Adam iteration the user's rows have taken
+  int32_t* last_i;   // [I1]
+  int32_t* pend_u;   // [U1] the iteration whose gradient G holds for the user's rows (<= last: none)
+  int32_t* pend_i;   // [I1]
+  int32_t* err;      // bit 8: a row more than LAZY_W - 1 iterations behind (never, by construction)
+  int32_t t;         // this step's Adam iteration
+  float lr[LAZY_W];  // lr[x] = lr_t of iteration t - (LAZY_W - 1) + x
+
+  // the row's float4 q (q < d4: MF table, else MLP table)
+  __device__ int64_t at(int side, int64_t r, int64_t q) const {
+    if (q < d4) return side ? U1 * d4 + r * d4 + q : r * d4 + q;                            // S_MF_U / S_MF_I
+    return side ? (2 * U1 + I1) * d4 + r * d4 + (q - d4) : (U1 + I1) * d4 + r * d4 + (q - d4);  // S_MLP_x
+  }
 };
+
+// iterations (from, t] of a float4 (from >= t - LAZY_W), a.g the gradient of
+// iteration gp, 0 at the others; unrolled so that every lr[x] is a kernel-argument load
+__device__ __forceinline__ void lazy_iters(Adam4V& a, const AdamK& k, const AdamLazy& z, int32_t from,
+                                           int32_t gp) {
+  const float4 g = a.g;
+#pragma unroll
+  for (int x = 0; x < LAZY_W; ++x) {
+    const int32_t tau = z.t - (LAZY_W - 1) + x;
+    if (tau > from) {
+      a.g = tau == gp ? g : make_float4(0.f, 0.f, 0.f, 0.f);
+      adam_math(a, k, z.lr[x]);
+    }
+  }
+}
 
 __global__ void __launch_bounds__(256) k_nmf_adam_next(float4* __restrict__ p, float4* __restrict__ g,
                                                        float4* __restrict__ m, float4* __restrict__ v,
-                                                       int64_t n4, AdamK k, AdamSlots ws, AdamSplit sp,
-                                                       const int32_t* __restrict__ un,
+                                                       int64_t n4, int64_t emb4, AdamK k, AdamSlots ws,
+                                                       AdamLazy z, const int32_t* __restrict__ un,
                                                        const int32_t* __restrict__ in, int32_t Bn,
                                                        unsigned row_blocks) {
-  if (blockIdx.x >= row_blocks) {  // the parameter tail: a wave per float4, a lane per (pass, slot group)
-    const int64_t t4 = n4 - sp.emb4;
-    const int lane = threadIdx.x & 63, pass = lane >> 5, gi = lane & 31;
+  if (blockIdx.x >= row_blocks) {
+    // the parameter tail: a lane per (float4, pass, slot group), 64 / (2 gp) float4s
+    // per wave (gp = slot groups rounded up to a power of two)
+    const int64_t t4 = n4 - emb4;
+    const int lane = threadIdx.x & 63;
     const int ng = (ws.nslot + SB - 1) / SB;  // <= 32 (nslot <= NSLOT)
+    int gp = 1;
+    while (gp < ng) gp <<= 1;
+    const int fpw = 32 / gp;  // float4s per wave
+    const int f = lane / (2 * gp), pass = (lane / gp) & 1, gi = lane & (gp - 1);
+    const int lead = f * 2 * gp;  // the float4's pass-0 leader; pass 1's is lead + gp
     const int64_t w0 = ((blockIdx.x - row_blocks) * (int64_t)blockDim.x + threadIdx.x) >> 6;
     const int64_t nw = ((int64_t)(gridDim.x - row_blocks) * blockDim.x) >> 6;
-    for (int64_t i = w0; i < t4; i += nw) {
-      const int64_t x = sp.emb4 + i;
+    for (int64_t i0 = w0 * fpw; i0 < t4; i0 += nw * fpw) {
+      const int64_t i = i0 + f;
+      const int64_t x = emb4 + i;
+      const bool live = i < t4;
       Adam4V a{};
-      if (lane == 0) a = adam4_load(p, g, m, v, x);
+      if (live && lane == lead) a = adam4_load(p, g, m, v, x);
       float4 gs = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gi < ng && pass < ws.npass) gs = slot_group4(ws.part, pass, ws.nslot, ws.nout, 4 * i, gi);
-      // the group sums in group order (slot_sum4's arithmetic), by lanes 0 and 32
+      if (live && gi < ng && pass < ws.npass) gs = slot_group4(ws.part, pass, ws.nslot, ws.nout, 4 * i, gi);
+      // the group sums in group order (slot_sum4's arithmetic), by the pass leaders
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
       for (int j = 0; j < ng; ++j) {
-        const int src = (lane & 32) + j;
+        const int src = (lane & ~(gp - 1)) + j;
         acc.x = acc.x + __shfl(gs.x, src, 64);
         acc.y = acc.y + __shfl(gs.y, src, 64);
         acc.z = acc.z + __shfl(gs.z, src, 64);
@@ -1050,10 +1103,10 @@ __global__ void __launch_bounds__(256) k_nmf_adam_next(float4* __restrict__ p, f
       }
       float4 sums[2];
       sums[0] = acc;
-      sums[1] = make_float4(__shfl(acc.x, 32, 64), __shfl(acc.y, 32, 64), __shfl(acc.z, 32, 64),
-                            __shfl(acc.w, 32, 64));
+      sums[1] = make_float4(__shfl(acc.x, lead + gp, 64), __shfl(acc.y, lead + gp, 64),
+                            __shfl(acc.z, lead + gp, 64), __shfl(acc.w, lead + gp, 64));
       if (ws.npass < 2) sums[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lane == 0) {
+      if (live && lane == lead) {
         adam4_fold(a.g, x, ws, sums);
         adam4_store(p, g, m, v, x, k, a);
       }
@@ -1064,66 +1117,102 @@ __global__ void __launch_bounds__(256) k_nmf_adam_next(float4* __restrict__ p, f
   const int lane = threadIdx.x & 63;
   if (wave >= 2 * (int64_t)Bn) return;
   const int b = (int)(wave >> 1), side = (int)(wave & 1);
-  const int64_t nrows = side ? sp.I1 : sp.U1;
+  const int64_t nrows = side ? z.I1 : z.U1;
   int32_t r = side ? in[b] : un[b];
   if (r < 0 || r >= nrows) r = 0;  // the step flags bad indices; row 0 stays a valid address
-  int32_t* mk = (side ? sp.mark_i : sp.mark_u) + r;
-  int old = 0;
-  if (lane == 0) old = atomicExch(mk, sp.tag);
-  // the row's float4s in its two tables (MF_x then MLP_x), loaded beside the claim:
-  // nothing else writes the row before the claimer's stores
-  const int64_t d4 = sp.d4;
-  const int64_t mf = side ? sp.U1 * d4 + r * d4 : r * d4;                  // S_MF_U / S_MF_I
-  const int64_t mlp = side ? (2 * sp.U1 + sp.I1) * d4 + r * d4 : (sp.U1 + sp.I1) * d4 + r * d4;  // S_MLP_x
-  if (d4 <= 32) {  // one float4 a lane (d <= 128)
-    const int64_t x = lane < d4 ? mf + lane : mlp + (lane - d4);
-    Adam4V a{};
-    if (lane < 2 * d4) a = adam4_load(p, g, m, v, x);
-    old = __shfl(old, 0, 64);
-    if (old == sp.tag) return;  // another occurrence claimed the row
-    if (lane < 2 * d4) adam4_store(p, g, m, v, x, k, a);
-    return;
+  int32_t* lst = (side ? z.last_i : z.last_u) + r;
+  int32_t* pnd = (side ? z.pend_i : z.pend_u) + r;
+  int32_t old = 0;
+  if (lane == 0) old = atomicExch(lst, z.t);
+  const int32_t gp = *pnd;
+  // the row's float4s, loaded beside the claim: nothing else writes the row
+  // before the claimer's stores
+  const int64_t d4 = z.d4;
+  for (int64_t q = lane; q < 2 * d4; q += 64) {
+    const int64_t x = z.at(side, r, q);
+    Adam4V a = adam4_load(p, g, m, v, x);
+    const int32_t from = __shfl(old, 0, 64);
+    if (from == z.t) return;  // another occurrence claimed the row
+    if (z.t - from > LAZY_W) {
+      if (lane == 0) atomicOr(z.err, 256);
+      return;
+    }
+    lazy_iters(a, k, z, from, gp);
+    m[x] = a.m;
+    v[x] = a.v;
+    p[x] = a.p;
+    g[x] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  old = __shfl(old, 0, 64);
-  if (old == sp.tag) return;
-  for (int64_t q = lane; q < 2 * d4; q += 64) adam4(p, g, m, v, q < d4 ? mf + q : mlp + (q - d4), k, AdamSlots());
+  if (lane == 0) *pnd = z.t + 1;  // step k+1's gradient
 }
 
-__global__ void __launch_bounds__(256) k_nmf_adam_rest(float4* __restrict__ p, float4* __restrict__ g,
-                                                       float4* __restrict__ m, float4* __restrict__ v, AdamK k,
-                                                       AdamSplit sp) {
-  const int64_t d4 = sp.d4, U4 = sp.U1 * d4, I4 = sp.I1 * d4;
-  constexpr int R = 4;  // float4s in flight per thread
-  const int64_t st = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t x0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x0 < sp.emb4; x0 += R * st) {
-    bool live[R], gz[R];
-    Adam4V a[R];
+// rows [lo, hi) of the (users, then items) row space brought to iteration t; a
+// lane-group of 32 (2 d4 <= 32) or 64 lanes per row, CR rows per lane-group in
+// flight (2: 103 VGPRs and no faster beside the step)
+constexpr int CR = 1;
+
+__global__ void __launch_bounds__(256) k_nmf_adam_catchup(float4* __restrict__ p, float4* __restrict__ g,
+                                                          float4* __restrict__ m, float4* __restrict__ v,
+                                                          AdamK k, AdamLazy z, int64_t lo, int64_t hi) {
+  const int64_t d4 = z.d4;
+  const int lpr = 2 * d4 <= 32 ? 32 : 64;
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t groups = (int64_t)gridDim.x * blockDim.x / lpr;
+  const int l = (int)(threadIdx.x & (lpr - 1));
+  for (int64_t r0 = lo + gid / lpr; r0 < hi; r0 += CR * groups) {
+    int32_t from[CR], gp[CR];
+    int64_t rr[CR];
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int64_t x = x0 + j * st;
-      live[j] = x < sp.emb4;
-      if (!live[j]) continue;
-      // segments: MF_U [0, U4), MF_I [U4, U4+I4), MLP_U [.., 2U4+I4), MLP_I [.., emb4)
-      int32_t mk;
-      if (x < U4) mk = sp.mark_u[x / d4];
-      else if (x < U4 + I4) mk = sp.mark_i[(x - U4) / d4];
-      else if (x < 2 * U4 + I4) mk = sp.mark_u[(x - U4 - I4) / d4];
-      else mk = sp.mark_i[(x - 2 * U4 - I4) / d4];
-      live[j] = mk != sp.tag;  // else k_nmf_adam_next stepped it
-      // a row the step's batch did not gather has g = 0: no g traffic (25% of the bytes)
-      gz[j] = sp.g_known && mk != sp.prev_tag;
-      if (live[j]) {
-        if (gz[j]) a[j] = Adam4V{make_float4(0.f, 0.f, 0.f, 0.f), m[x], v[x], p[x]};
-        else a[j] = adam4_load(p, g, m, v, x);
+    for (int j = 0; j < CR; ++j) {
+      rr[j] = r0 + j * groups;
+      from[j] = z.t;
+      gp[j] = 0;
+      if (rr[j] < hi) {
+        const int side = rr[j] >= z.U1 ? 1 : 0;
+        const int64_t r = side ? rr[j] - z.U1 : rr[j];
+        from[j] = (side ? z.last_i : z.last_u)[r];
+        gp[j] = (side ? z.pend_i : z.pend_u)[r];
       }
     }
+    for (int64_t q = l; q < 2 * d4; q += lpr) {
+      Adam4V a[CR];
+      int64_t x[CR];
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-      if (live[j]) {
-        if (gz[j]) adam4_store<true>(p, g, m, v, x0 + j * st, k, a[j]);
-        else adam4_store(p, g, m, v, x0 + j * st, k, a[j]);
+      for (int j = 0; j < CR; ++j) {  // all loads first
+        if (from[j] >= z.t || z.t - from[j] > LAZY_W) continue;  // claimed at t / (never) too far behind
+        const int side = rr[j] >= z.U1 ? 1 : 0;
+        x[j] = z.at(side, side ? rr[j] - z.U1 : rr[j], q);
+        const bool wg = gp[j] > from[j] && gp[j] <= z.t;  // G holds a gradient of the range
+        a[j] = Adam4V{wg ? g[x[j]] : make_float4(0.f, 0.f, 0.f, 0.f), m[x[j]], v[x[j]], p[x[j]]};
       }
+#pragma unroll
+      for (int j = 0; j < CR; ++j) {
+        if (from[j] >= z.t || z.t - from[j] > LAZY_W) continue;
+        lazy_iters(a[j], k, z, from[j], gp[j]);
+        m[x[j]] = a[j].m;
+        v[x[j]] = a[j].v;
+        p[x[j]] = a[j].p;
+        if (gp[j] > from[j] && gp[j] <= z.t) g[x[j]] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    if (l == 0) {
+#pragma unroll
+      for (int j = 0; j < CR; ++j) {
+        if (from[j] >= z.t) continue;
+        if (z.t - from[j] > LAZY_W) {
+          atomicOr(z.err, 256);
+          continue;
+        }
+        const int side = rr[j] >= z.U1 ? 1 : 0;
+        (side ? z.last_i : z.last_u)[side ? rr[j] - z.U1 : rr[j]] = z.t;  // read again only after this launch
+      }
+    }
   }
+}
+
+__global__ void k_nmf_fill_i32(int32_t* __restrict__ a, int64_t n, int32_t val) {
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x < n) a[x] = val;
 }
 
 // ---------------------------------------------------------------------------
@@ -1138,9 +1227,8 @@ struct acf_neumf_ctx {
   float* wpart = nullptr;  // [2 passes][slots][weight-gradient outputs]
   int32_t nslot = 0;       // workgroups (slots) of a training pass at max_batch
   int32_t *owner = nullptr, *err = nullptr;
-  // acf_neumf_train's split Adam: row claims, the side stream and its events
-  int32_t *mark_u = nullptr, *mark_i = nullptr;
-  int32_t tag = 0;
+  // acf_neumf_train's lazy Adam: each row's last iteration, the side stream and its events
+  int32_t *last_u = nullptr, *last_i = nullptr, *pend_u = nullptr, *pend_i = nullptr;
   hipStream_t side = nullptr;
   hipEvent_t ev_next = nullptr, ev_rest = nullptr;
   std::vector<void*> allocs;
@@ -1209,13 +1297,11 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
   // two sets (clean / adversarial pass): the clean pass's gradient workgroups read theirs
   // while the adversarial k_nmf_inst writes its own
   A(&c->h0, 2 * B * 2 * dd); A(&c->a1, 2 * B * 2 * dd); A(&c->dz1, 2 * B * 2 * dd); A(&c->dz2, 2 * B * dd);
-  A(&c->mark_u, (size_t)U1); A(&c->mark_i, (size_t)I1);
-  if (r == ACF_OK && (hipMemset(c->mark_u, 0, (size_t)U1 * 4) != hipSuccess ||
-                      hipMemset(c->mark_i, 0, (size_t)I1 * 4) != hipSuccess ||
-                      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+  A(&c->last_u, (size_t)U1); A(&c->last_i, (size_t)I1); A(&c->pend_u, (size_t)U1); A(&c->pend_i, (size_t)I1);
+  if (r == ACF_OK && (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
                       hipEventCreateWithFlags(&c->ev_next, hipEventDisableTiming) != hipSuccess ||
                       hipEventCreateWithFlags(&c->ev_rest, hipEventDisableTiming) != hipSuccess))
-    r = set_error(ACF_E_HIP, "split-Adam setup failed");
+    r = set_error(ACF_E_HIP, "lazy-Adam setup failed");
   c->nslot = (int32_t)std::min<int64_t>(((int64_t)maxB + MR - 1) / MR, NSLOT);
   A(&c->wpart, 2 * (size_t)c->nslot * (size_t)wout(d).n);
   if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
@@ -1269,6 +1355,7 @@ static int read_err(acf_neumf_ctx* c, hipStream_t s) {
   int32_t herr = 0;
   HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  ACF_CHECK(!(herr & 256), ACF_E_HIP, "lazy Adam: a row fell behind the learning-rate window (internal)");
   ACF_CHECK(herr == 0, ACF_E_RANGE, "index out of range (%s%s)", (herr & 1) ? "user >= num_user_rows " : "",
             (herr & 2) ? "item >= num_item_rows" : "");
   return ACF_OK;
@@ -1372,58 +1459,85 @@ extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, f
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
   float4 *P4 = reinterpret_cast<float4*>(P), *G4 = reinterpret_cast<float4*>(G);
   float4 *m4 = reinterpret_cast<float4*>(m), *v4 = reinterpret_cast<float4*>(v);
-  const int64_t n4 = c->L.total / 4;
-  AdamSplit sp;
-  sp.U1 = c->U1; sp.I1 = c->I1; sp.d4 = c->d / 4; sp.emb4 = c->L.off[S_W1] / 4;
-  sp.mark_u = c->mark_u; sp.mark_i = c->mark_i;
-  const unsigned tail_blocks = (unsigned)std::min<int64_t>((n4 - sp.emb4 + 3) / 4, 2048);  // a wave per float4
-  // the rest runs beside the step's latency-bound kernels: 3 workgroups per 4 CUs
-  // (yelp shape, d 64, B 512: 8192 WGs 5.65M instances/s, 512 5.79M, 256 6.59M,
-  // 192 6.71M, 128 5.52M -- fewer and the rest outlasts the step)
-  const unsigned rest_grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((sp.emb4 + 255) / 256, REST_WG));
+  const int64_t n4 = c->L.total / 4, emb4 = c->L.off[S_W1] / 4;
+  const int64_t nsteps = (n + batch - 1) / batch;
+  ACF_CHECK(t_first + nsteps < INT32_MAX, ACF_E_INVALID, "Adam iteration overflows int32");
+  AdamLazy z;
+  z.U1 = c->U1; z.I1 = c->I1; z.d4 = c->d / 4;
+  z.last_u = c->last_u; z.last_i = c->last_i; z.pend_u = c->pend_u; z.pend_i = c->pend_i; z.err = c->err;
+  // every row has taken iteration t_first - 1, and G holds its gradient of
+  // iteration t_first (what the caller accumulated, plus step 0's)
+  k_nmf_fill_i32<<<(unsigned)((c->U1 + 255) / 256), 256, 0, s>>>(c->last_u, c->U1, (int32_t)(t_first - 1));
+  k_nmf_fill_i32<<<(unsigned)((c->I1 + 255) / 256), 256, 0, s>>>(c->last_i, c->I1, (int32_t)(t_first - 1));
+  k_nmf_fill_i32<<<(unsigned)((c->U1 + 255) / 256), 256, 0, s>>>(c->pend_u, c->U1, (int32_t)t_first);
+  k_nmf_fill_i32<<<(unsigned)((c->I1 + 255) / 256), 256, 0, s>>>(c->pend_i, c->I1, (int32_t)t_first);
+  HIP_TRY(hipGetLastError());
+  const int64_t nrows = c->U1 + c->I1;
+  // k_nmf_adam_next's tail: 32 / gp float4s per wave, gp = the slot groups of a full
+  // batch rounded up to a power of two (a smaller last batch packs more per wave)
+  const int ng_max = (int)((std::min<int64_t>((batch + MR - 1) / MR, NSLOT) + SB - 1) / SB);
+  int gp2 = 1;
+  while (gp2 < ng_max) gp2 <<= 1;
+  const int64_t tail_waves = (n4 - emb4 + 32 / gp2 - 1) / (32 / gp2);
+  const unsigned tail_blocks = (unsigned)std::min<int64_t>((tail_waves + 3) / 4, 2048);
+  const int lpr = 2 * z.d4 <= 32 ? 32 : 64;
+  auto rows_grid = [&](int64_t rows, int64_t cap) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((rows * lpr + 255) / 256, cap));
+  };
+  const int64_t slice = (nrows + LAZY_S - 1) / LAZY_S;
+  bool side_pending = false;
+  AdamK ak{};
   int64_t k = 0;
   for (int64_t o = 0; o < n; o += batch, ++k) {
     const int32_t B = (int32_t)std::min<int64_t>(batch, n - o);
     int r = launch_grad(c, P, G, u + o, i + o, y + o, B, hp, nullptr, s, false);
     if (r != ACF_OK) {
-      if (k > 0) (void)hipStreamWaitEvent(s, c->ev_rest, 0);
+      if (side_pending) (void)hipStreamWaitEvent(s, c->ev_rest, 0);
       return r;
     }
-    // Adam of step k in two parts (k_nmf_adam_next / k_nmf_adam_rest): first the
-    // rows batch k+1 gathers and the parameter tail, with the weight-gradient slot
-    // sums (acf_neumf_grad's wsum arithmetic, so train == grad + adam bit for
-    // bit); then, on the side stream and beside step k+1, every other row.  The
-    // next part of step k waits for the rest of step k-1 (a row it claims may be
-    // one step k-1's rest still has to step first).
+    // Adam iteration t of step k: batch k+1's rows (up to t) and the parameter tail
+    // now, with the weight-gradient slot sums (acf_neumf_grad's wsum arithmetic);
+    // every other row's iterations later (k_nmf_adam_catchup)
     AdamSlots ws;
     ws.part = c->wpart;
     ws.nslot = (int)std::min<int64_t>(((int64_t)B + MR - 1) / MR, NSLOT);
     ws.npass = hp->adver ? 2 : 1;
-    ws.base4 = sp.emb4;
+    ws.base4 = emb4;
     ws.nout = wout(c->d).n;
     ws.loss_out = losses ? losses + 2 * k : nullptr;
     ws.B = (float)B;
-    const AdamK ak{hp->beta1, hp->beta2, adam_lr_t(hp, t_first + k), hp->adam_eps};
+    const int64_t t = t_first + k;
+    ak = AdamK{hp->beta1, hp->beta2, adam_lr_t(hp, t), hp->adam_eps};
+    z.t = (int32_t)t;
+    for (int x = 0; x < LAZY_W; ++x) {
+      const int64_t tau = t - (LAZY_W - 1) + x;
+      z.lr[x] = tau >= 1 ? adam_lr_t(hp, tau) : 0.f;
+    }
     const int64_t on = o + batch;
     const int32_t Bn = on < n ? (int32_t)std::min<int64_t>(batch, n - on) : 0;
-    // step k's batch rows were claimed with the previous tag by step k-1's next
-    // part (step 0's G may hold anything the caller accumulated: read it all)
-    sp.prev_tag = c->tag;
-    sp.g_known = k > 0;
-    if (++c->tag == 0) ++c->tag;  // 0 = never claimed
-    sp.tag = c->tag;
     const unsigned row_blocks = (unsigned)((2 * (int64_t)Bn * 64 + 255) / 256);
-    if (k > 0) HIP_TRY(hipStreamWaitEvent(s, c->ev_rest, 0));
-    k_nmf_adam_next<<<row_blocks + tail_blocks, 256, 0, s>>>(P4, G4, m4, v4, n4, ak, ws, sp, u + on, i + on, Bn,
-                                                            row_blocks);
+    if (side_pending) HIP_TRY(hipStreamWaitEvent(s, c->ev_rest, 0));  // the catch-up of step k-1
+    k_nmf_adam_next<<<row_blocks + tail_blocks, 256, 0, s>>>(P4, G4, m4, v4, n4, emb4, ak, ws, z, u + on, i + on,
+                                                            Bn, row_blocks);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(c->ev_next, s));
-    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_next, 0));
-    k_nmf_adam_rest<<<rest_grid, 256, 0, c->side>>>(P4, G4, m4, v4, ak, sp);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(c->ev_rest, c->side));
+    side_pending = false;
+    if (Bn > 0) {  // slice k % LAZY_S of the rows, beside step k+1
+      const int64_t lo = (k % LAZY_S) * slice, hi = std::min<int64_t>(lo + slice, nrows);
+      if (lo < hi) {
+        HIP_TRY(hipEventRecord(c->ev_next, s));
+        HIP_TRY(hipStreamWaitEvent(c->side, c->ev_next, 0));
+        k_nmf_adam_catchup<<<rows_grid(hi - lo, CATCHUP_WG), 256, 0, c->side>>>(P4, G4, m4, v4, ak, z, lo, hi);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev_rest, c->side));
+        side_pending = true;
+      }
+    }
   }
-  if (k > 0) HIP_TRY(hipStreamWaitEvent(s, c->ev_rest, 0));  // the caller's stream sees every update
+  if (side_pending) HIP_TRY(hipStreamWaitEvent(s, c->ev_rest, 0));
+  if (k > 0) {  // every row to the last iteration
+    k_nmf_adam_catchup<<<rows_grid(nrows, 256 * 16), 256, 0, s>>>(P4, G4, m4, v4, ak, z, 0, nrows);
+    HIP_TRY(hipGetLastError());
+  }
   return read_err(c, s);
 }
 

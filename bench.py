@@ -425,8 +425,10 @@ def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
 def neumf_bench(acf, dev):
     """BASELINE configs[3]: adversarial NeuMF (GMF + MLP towers perturbed) on
     yelp-sort-shaped synthetic data, d = 64, batch 512 (run.py --bs default), one
-    epoch of Keras-style training (libacf_neumf.so).  Dominant kernel: the dense
-    Adam stream over the flat parameter buffer (8 x 4 B per parameter per step)."""
+    epoch of Keras-style training (libacf_neumf.so).  The epoch (acf_neumf_train)
+    runs Keras's dense Adam lazily (bit-identical) and is a
+    latency-bound chain of small launches; the roofline is the dense Adam kernel
+    of the stepwise API (acf_neumf_adam: 8 x 4 B per parameter per step)."""
     import scipy.sparse as sp
     nm = importlib.import_module(PKG + ".neumf")
     ds = acf.yelp_like()

@@ -68,7 +68,10 @@ int acf_neumf_adam(acf_neumf_ctx* ctx, float* params, float* grad, float* m, flo
  * of `batch` (the last one partial), each acf_neumf_grad + acf_neumf_adam with
  * Adam iterations t_first, t_first+1, ...  losses (device, [ceil(n/batch)][2],
  * may be NULL): per-batch clean / adversarial mean loss.  Indices are validated
- * once at the end (ACF_E_RANGE; out-of-range rows were read as row 0). */
+ * once at the end (ACF_E_RANGE; out-of-range rows were read as row 0).  The
+ * result is bit-identical to that grad + adam sequence; inside the call each
+ * embedding row's zero-gradient Adam iterations run late (when a batch gathers
+ * the row, or in a rotating catch-up), and every row is current on return. */
 int acf_neumf_train(acf_neumf_ctx* ctx, float* params, float* grad, float* m, float* v,
                     const int32_t* user, const int32_t* item, const float* label, int64_t n,
                     int32_t batch, int64_t t_first, const acf_neumf_hparams* hp, float* losses,

@@ -142,30 +142,38 @@ def test_recommender_surface(nm, dev):
         assert s.shape == (5, 1) and np.all((s > 0) & (s < 1))
 
 
-@pytest.mark.parametrize("B", [96, 300])
-def test_train_epoch_equals_stepwise(nm, dev, B):
-    """acf_neumf_train (native batch loop, split Adam: next batch's rows + MLP on
-    the stream, every other row on a side stream) == grad + dense adam per batch,
-    bit for bit, including the trailing partial batch.  41 users / 37 items: every
-    batch re-gathers rows the previous one touched; B = 300 sums 19 weight-gradient
-    slots in three groups."""
-    P, _, _, _ = _problem(21, d=64)
+@pytest.mark.parametrize("B,U1,I1,n,d,calls", [
+    (96, 41, 37, 1000, 64, 1),     # every batch re-gathers rows the previous one touched
+    (300, 41, 37, 1000, 64, 1),    # 19 weight-gradient slots, summed in three groups
+    (16, 500, 300, 640, 16, 2),    # most rows idle for many steps; two calls (t continues)
+    (64, 200, 150, 1200, 128, 1),  # a full wave per row
+])
+def test_train_epoch_equals_stepwise(nm, dev, B, U1, I1, n, d, calls):
+    """acf_neumf_train (native batch loop, lazy Adam: batch k's and k+1's rows and
+    the MLP at step k, every other row's zero-gradient iterations later in a
+    rotating catch-up slice and at the end of the call) == grad + dense adam per
+    batch, bit for bit, including the trailing partial batch."""
+    P, _, _, _ = _problem(21, U1=U1, I1=I1, d=d)
     rng = np.random.default_rng(9)
-    n = 1000
-    u = rng.integers(0, 41, n).astype(np.int32)
-    i = rng.integers(0, 37, n).astype(np.int32)
+    u = rng.integers(0, U1, n).astype(np.int32)
+    i = rng.integers(0, I1, n).astype(np.int32)
     y = (rng.random(n) < 0.5).astype(np.float32)
+    cut = [0, n] if calls == 1 else [0, (n // B // 2) * B, n]
     for adver in (0, 1):
         a, b = _state(nm, P, dev), _state(nm, P, dev)
         ca, cb = nm.NeuMFContext(a, B), nm.NeuMFContext(b, B)
         hp = ca.hparams(adver=adver)
-        la = ca.train(u, i, y, B, hp)
+        la = torch.cat([ca.train(u[c0:c1], i[c0:c1], y[c0:c1], B, hp) for c0, c1 in zip(cut, cut[1:])])
         lb = torch.zeros_like(la)
-        for k, o in enumerate(range(0, n, B)):
-            cb.grad(u[o:o + B], i[o:o + B], y[o:o + B], hp, lb[k])
-            cb.adam(hp)
+        k = 0
+        for c0, c1 in zip(cut, cut[1:]):
+            for o in range(c0, c1, B):
+                e = min(o + B, c1)
+                cb.grad(u[o:e], i[o:e], y[o:e], hp, lb[k])
+                cb.adam(hp)
+                k += 1
         torch.cuda.synchronize()
-        assert a.t == b.t == (n + B - 1) // B
+        assert a.t == b.t == k
         assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
         assert torch.equal(la, lb)
         assert not a.grad.any() and not b.grad.any()
