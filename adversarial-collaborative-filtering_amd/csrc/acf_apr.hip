@@ -3773,6 +3773,13 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->plan_kind2 = all_dt;
   c->plan_kb = kb;
   c->tri = packed && !c->shard && c->fusion;
+  if (c->shard) {
+    // Shard plans are replayed inside captured step graphs (distributed.ShardedAPR),
+    // where a step's generation repeats from one replay to the next: clear the
+    // inline records so that a slot this plan does not write never reads as
+    // current (k_flush scans every slot of the batch).
+    HIP_TRY(hipMemsetAsync(c->inl, 0, (size_t)nb * 3 * B * sizeof(OccRec), s));
+  }
   if (packed) {  // k_records writes the slot flags of the slots it finds; the rest read 0
     HIP_TRY(hipMemsetAsync(c->key_in, 0, (size_t)3 * E * sizeof(uint64_t), s));
     HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));

@@ -33,10 +33,26 @@ and configs[2] name -- an RCCL all_gather of every rank's Q shard (the small
 pinterest item table replicated for the step), from which each rank takes the
 rows its negatives and positives need.  E2-E4 are the same in both.
 
+Static step layout.  Every exchange buffer has a fixed shape: G blocks of C rows
+(C = the chunk's largest per-peer request count, rounded up and only ever
+grown), block o holding what this rank exchanges with rank o, plus one trash
+row.  The routing of a chunk of T steps (one host sync, for the counts) writes
+per-step index maps into persistent buffers at fixed per-step offsets:
+``wsrc`` (working-set entry -> received row), ``winv`` (exchange row ->
+working-set entry), ``srv`` (exchange row -> owned row), and the owner's
+segments ``seg`` / ``pos`` / ``own`` (rows padded with empty segments on a
+trash row of the Q storage).  A step therefore has no host-side sizes, so a
+chunk's steps are captured as hipGraphs once and replayed:
+
+  * world 1: the exchanges are the identity (no collective), the whole chunk is
+    ONE graph;
+  * world > 1: the local work between two collectives is a captured segment;
+    the collectives (fixed-size RCCL all_to_all / all_gather) are issued between
+    the segment replays.
+
 The working sets and the exchange plans of a whole chunk of steps are built on
-device in one go (one host sync per chunk, for the all_to_all split sizes).
-Every rank sees the same global triplet stream (the sampler is seeded
-identically) and keeps its users' triplets, in stream order.
+device in one go.  Every rank sees the same global triplet stream (the sampler
+is seeded identically) and keeps its users' triplets, in stream order.
 
 The local compute is pluggable: :class:`HipLocal` (the product path: the step
 kernels in shard mode, include/acf_apr.h) on GPUs; the CPU tests plug in the
@@ -45,6 +61,7 @@ exchanges over gloo.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -54,6 +71,8 @@ import torch.distributed as dist
 
 class HipLocal:
     """One rank's local passes and owner reductions on the HIP kernels."""
+
+    graphable = True  # every call is a fixed-shape launch sequence (no host sync)
 
     def __init__(self, sh: "ShardedAPR"):
         from . import ops
@@ -86,7 +105,8 @@ class HipLocal:
         self.ops.shard_reduce_delta(recv, seg, pos, hp, G0, reply)
 
     def reduce_apply(self, hp, recv, seg, pos, G0, rows, count):
-        self.ops.shard_reduce_apply(self.sh.Q, self.sh.accQ, recv, seg, pos, hp, G0, rows, count,
+        # rows of padded segments name the trash row ni of the Q storage
+        self.ops.shard_reduce_apply(self.sh._Qst, self.sh._aQst, recv, seg, pos, hp, G0, rows, count,
                                     reg_batch=self.sh.B)
 
     def step_errors(self) -> int:
@@ -94,8 +114,45 @@ class HipLocal:
 
 
 class _Chunk:
-    """Device-side routing of one chunk of T global batches for this rank, plus
-    the host copies of the split sizes."""
+    """Host copies of one chunk's counts (the device maps live in ShardedAPR._buf)."""
+
+
+class _Buffers:
+    """Persistent per-chunk maps and per-step exchange buffers (fixed addresses, so
+    captured step graphs stay valid from one chunk to the next)."""
+
+
+def _hp_key(hp) -> tuple:
+    return tuple(sorted((k, v) for k, v in vars(hp).items() if isinstance(v, (int, float, bool))))
+
+
+class _SegmentRecorder:
+    """Captures a step sequence as hipGraph segments cut at every collective."""
+
+    def __init__(self, stream, pool):
+        self.stream, self.pool = stream, pool
+        self.segs = []  # [(graph, collective or None)]
+        self._g = None
+
+    def begin(self):
+        self._g = torch.cuda.CUDAGraph()
+        self._g.capture_begin(pool=self.pool)
+
+    def cut(self, fn):
+        self._g.capture_end()
+        self.segs.append((self._g, fn))
+        self.begin()
+
+    def end(self):
+        self._g.capture_end()
+        self.segs.append((self._g, None))
+        self._g = None
+
+    def replay(self):
+        for g, fn in self.segs:
+            g.replay()
+            if fn is not None:
+                fn()
 
 
 class ShardedAPR:
@@ -103,11 +160,13 @@ class ShardedAPR:
     split APR step.  ``batch_size`` is the GLOBAL batch (the reference's
     ``--batch_size``); each rank processes the triplets of its users.
     ``local_batch``: triplets are routed at sampling time (train_routed), each
-    rank holding exactly this many of every global batch (= G x local_batch)."""
+    rank holding exactly this many of every global batch (= G x local_batch).
+    ``graph``: capture a chunk's steps as hipGraphs (None = whenever the local
+    passes are the HIP ones on a GPU and the collectives are RCCL)."""
 
     def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, batch_size: int, device=None,
                  group=None, init_P=None, init_Q=None, acc0: float = 0.1, local=None,
-                 local_batch: int | None = None, item_exchange: str = "all_to_all"):
+                 local_batch: int | None = None, item_exchange: str = "all_to_all", graph: bool | None = None):
         if item_exchange not in ("all_to_all", "allgather"):
             raise ValueError(f"item_exchange must be 'all_to_all' or 'allgather', got {item_exchange!r}")
         self.item_exchange = item_exchange
@@ -122,30 +181,85 @@ class ShardedAPR:
         G, r = self.G, self.rank
         f = dict(dtype=torch.float32, device=self.device)
         nu, ni = len(range(r, self.U1, G)), len(range(r, self.I1, G))
+        self.ni = ni
         self.P = torch.empty(nu, dim, **f)
-        self.Q = torch.empty(ni, dim, **f)
+        # Q / accQ storage carries one trash row (index ni) for the padded owner segments
+        self._Qst = torch.zeros(ni + 1, dim, **f)
+        self._aQst = torch.full((ni + 1, dim), acc0, **f)
+        self.Q, self.accQ = self._Qst[:ni], self._aQst[:ni]
         if init_P is not None:
             self.P.copy_(torch.as_tensor(np.asarray(init_P, np.float32)[r::G]))
             self.Q.copy_(torch.as_tensor(np.asarray(init_Q, np.float32)[r::G]))
         self.accP = torch.full((nu, dim), acc0, **f)
-        self.accQ = torch.full((ni, dim), acc0, **f)
         if local_batch is not None and local_batch * self.G != self.B:
             raise ValueError(f"local_batch {local_batch} x {self.G} ranks != batch_size {self.B}")
         self.b_max = int(local_batch) if local_batch is not None else self.B  # triplets of a rank per batch
         self.routed = local_batch is not None
         self.max_items = 2 * self.b_max  # a rank's working set of one batch: <= 2 x its triplets
         self.Qc = torch.zeros(self.max_items, dim, **f)
-        self._send = torch.empty(self.max_items, dim, **f)
-        self._dlt = torch.empty(self.max_items, dim, **f)
-        self._recv = torch.empty(0, dim, **f)
         self._qcap = (self.I1 + G - 1) // G  # rows of the largest Q shard (all_gather slots)
-        self._qpad = torch.zeros(self._qcap, dim, **f) if item_exchange == "allgather" else None
-        self._qall = torch.empty(G * self._qcap, dim, **f) if item_exchange == "allgather" else None
+        self._qpad = torch.zeros(self._qcap, dim, **f) if item_exchange == "allgather" and G > 1 else None
+        self._qall = torch.empty(G * self._qcap, dim, **f) if item_exchange == "allgather" and G > 1 else None
         self.local = local(self) if local is not None else HipLocal(self)
-        self.stats = {"steps": 0, "items_requested": 0, "rows_served": 0, "triplets": 0, "route_s": 0.0}
+        can_graph = (self.device.type == "cuda" and not self._stage and getattr(self.local, "graphable", False))
+        if graph is None:  # ACF_SHARD_GRAPH=0: eager steps (A/B of the captured graphs)
+            graph = os.environ.get("ACF_SHARD_GRAPH", "1") != "0"
+        self.graph = bool(graph) and can_graph
+        self._C = 0   # per-peer block rows of the exchange buffers (only grows)
+        self._T = 0   # steps the per-chunk maps hold
+        self._buf = None
+        self._graphs = {}
+        self._pool = None
+        self._cap_stream = None
+        self._rec = None  # the segment recorder while capturing
+        self.stats = {"steps": 0, "items_requested": 0, "rows_served": 0, "triplets": 0, "route_s": 0.0,
+                      "graph_replays": 0}
+
+    # -- buffers -------------------------------------------------------------------
+    def _ensure(self, T: int, C: int) -> None:
+        if C <= self._C and T <= self._T:
+            return
+        if C > self._C:  # headroom: chunk-to-chunk growth should not re-capture
+            self._C = max(64, -(-int(C * 1.0625) // 64) * 64)
+        self._T = max(self._T, T)
+        self._graphs.clear()
+        G, C, T, M, d = self.G, self._C, self._T, self.max_items, self.d
+        GC = G * C
+        dev = self.device
+        li = dict(dtype=torch.int64, device=dev)
+        ii = dict(dtype=torch.int32, device=dev)
+        fl = dict(dtype=torch.float32, device=dev)
+        b = _Buffers()
+        b.u_rows = torch.zeros(T, self.b_max, **ii)
+        b.wi = torch.zeros(T, self.b_max, **ii)
+        b.wj = torch.zeros(T, self.b_max, **ii)
+        b.wsrc = torch.empty(T, M, **li)        # working-set entry -> row of the received E1/E3 block
+        b.winv = torch.empty(T, GC + 1, **li)   # exchange row -> working-set entry (trash: M)
+        b.srv = torch.empty(T, GC + 1, **li)    # exchange row -> owned Q row (trash: ni)
+        b.wslot = torch.zeros(T, M, **li) if self.item_exchange == "allgather" else None
+        b.seg = torch.empty(T, GC + 1, **ii)
+        b.pos = torch.zeros(T, GC, **ii)
+        b.own = torch.empty(T, GC, **ii)
+        b.count = torch.zeros(T, GC, **ii)
+        b.S1 = torch.empty(GC + 1, d, **fl)
+        b.R1 = torch.empty(GC + 1, d, **fl)
+        b.part = torch.zeros(M + 1, d, **fl)
+        b.S = torch.empty(GC + 1, d, **fl)
+        b.R = torch.empty(GC + 1, d, **fl)
+        b.G0 = torch.empty(GC, d, **fl)
+        b.reply = torch.zeros(GC + 1, d, **fl)
+        b.R3 = torch.zeros(GC + 1, d, **fl)
+        b.dlt = torch.empty(M, d, **fl)
+        self._buf = b
 
     # -- collectives ---------------------------------------------------------------
-    def _a2a(self, out, inp, out_splits, in_splits):
+    def _collective(self, fn) -> None:
+        if self._rec is not None:  # capturing: the collective runs between segment replays
+            self._rec.cut(fn)
+        else:
+            fn()
+
+    def _a2a(self, out, inp, out_splits=None, in_splits=None):
         if self._stage:  # gloo with device tensors (rehearsal of several ranks on one GPU)
             o = torch.empty(out.shape, dtype=out.dtype)
             dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
@@ -153,21 +267,35 @@ class ShardedAPR:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
+    def _exchange(self, out, inp):
+        """Fixed-size exchange of G blocks of C rows (block o to / from rank o);
+        the identity at world 1.  Returns the tensor holding the received rows."""
+        if self.G == 1:
+            return inp
+        n = self.G * self._C
+        self._collective(lambda: self._a2a(out[:n], inp[:n]))
+        return out
+
     def _gather_q(self):
         """E1, "allgather" form: every rank's Q shard to every rank (RCCL all_gather);
-        row i is then at _qall[(i % G) * cap + i // G]."""
-        n = self.Q.shape[0]
-        self._qpad[:n] = self.Q
-        if self._stage:
-            parts = [torch.empty(self._qcap, self.d) for _ in range(self.G)]
-            dist.all_gather(parts, self._qpad.cpu(), group=self.group)
-            self._qall.copy_(torch.cat(parts))
-        else:
-            dist.all_gather_into_tensor(self._qall, self._qpad, group=self.group)
+        row i is then at _qall[(i % G) * cap + i // G].  World 1: Q itself."""
+        if self.G == 1:
+            return self._Qst
+        self._qpad[: self.ni] = self.Q
+
+        def gather():
+            if self._stage:
+                parts = [torch.empty(self._qcap, self.d) for _ in range(self.G)]
+                dist.all_gather(parts, self._qpad.cpu(), group=self.group)
+                self._qall.copy_(torch.cat(parts))
+            else:
+                dist.all_gather_into_tensor(self._qall, self._qpad, group=self.group)
+        self._collective(gather)
+        return self._qall
 
     # -- routing (one chunk of T global batches) -----------------------------------
     def _route(self, u, i, j, T: int) -> _Chunk:
-        G, r, I1 = self.G, self.rank, self.I1
+        G, r, I1, ni = self.G, self.rank, self.I1, self.ni
         B = self.b_max if self.routed else self.B  # triplets per batch in the stream given
         dev = self.device
         u, i, j = (torch.as_tensor(x, device=dev).reshape(-1)[: T * B].long() for x in (u, i, j))
@@ -188,11 +316,10 @@ class ShardedAPR:
         sel = torch.arange(u.numel(), device=dev) if self.routed else torch.nonzero(u % G == r).squeeze(1)
         st = sel // B
         n = sel.numel()
-        c.u_rows = (u[sel] // G).to(torch.int32)
         items = torch.cat([i[sel], j[sel]])
         ist = torch.cat([st, st])
         # working set per step: unique items, ordered by (owner, id) so that each
-        # owner's rows are one contiguous block of the all_to_all buffers
+        # owner's rows are one contiguous block
         uk, inv = torch.unique((ist * G + items % G) * I1 + items, return_inverse=True)
         wstep, wown, wid = uk // (G * I1), (uk // I1) % G, uk % I1
         cnt = torch.bincount(wstep * G + wown, minlength=T * G).view(T, G)
@@ -200,9 +327,8 @@ class ShardedAPR:
         nW = cnt.sum(1)
         wstart = torch.cumsum(nW, 0) - nW
         widx = (inv - wstart[ist]).to(torch.int32)
-        c.wi, c.wj = widx[:n], widx[n:]
-        if self.item_exchange == "allgather":  # where each working-set row sits in the gathered table
-            c.wslot = ((wid % G) * self._qcap + wid // G).long()
+        wk = torch.arange(uk.numel(), device=dev) - wstart[wstep]        # entry inside its step's set
+        kblk = wk - (torch.cumsum(cnt, 1) - cnt)[wstep, wown]             # entry inside its owner block
         # the requests of the whole chunk, owner-major, in one exchange
         order = torch.argsort((wown * T + wstep) * I1 + wid)
         req = (wid // G)[order]
@@ -221,109 +347,139 @@ class ShardedAPR:
         c.cnt = host[: T * G].reshape(T, G)           # my requests per (step, owner)
         c.rc = host[T * G: 2 * T * G].reshape(G, T)   # requests to me per (requester, step)
         c.nloc = host[2 * T * G: -G]
+        self._ensure(T, int(max(c.cnt.max(initial=0), c.rc.max(initial=0), 1)))
+        bf, C, M = self._buf, self._C, self.max_items
+        GC = G * C
+        # local triplets at a fixed stride of b_max per step
+        lo = torch.cumsum(nloc, 0) - nloc
+        slot = st * self.b_max + (torch.arange(n, device=dev) - lo[st])
+        bf.u_rows[:T].view(-1)[slot] = (u[sel] // G).to(torch.int32)
+        bf.wi[:T].view(-1)[slot] = widx[:n]
+        bf.wj[:T].view(-1)[slot] = widx[n:]
+        # requester maps: working-set entry <-> row of the exchange blocks
+        xrow = wown * C + kblk
+        bf.wsrc[:T].fill_(GC)
+        bf.wsrc[:T].view(-1)[wstep * M + wk] = xrow
+        bf.winv[:T].fill_(M)
+        bf.winv[:T].view(-1)[wstep * (GC + 1) + xrow] = wk
+        if bf.wslot is not None:  # where each working-set row sits in the gathered table
+            bf.wslot[:T].view(-1)[wstep * M + wk] = (wid % G) * self._qcap + wid // G if G > 1 else wid
+        # rows I serve, received in (requester o, step t, k) order
         rows = torch.empty(int(c.rc.sum()), dtype=req.dtype, device=dev)
         self._a2a(rows, req, c.rc.sum(1).tolist(), c.cnt.sum(0).tolist())
-        # received rows in per-step all_to_all order: step, then requester, then id
-        c.R = c.rc.sum(0)                                   # rows I serve per step
-        c.Rs = np.concatenate([[0], np.cumsum(c.R)])
-        pstart = np.cumsum(c.rc, 0) - c.rc                  # [G, T] requester offset inside a step
-        blk_start = (c.Rs[:-1][None, :] + pstart).reshape(-1)  # block (requester o, step t) -> position
-        blk_len = c.rc.reshape(-1)
-        src_pos = np.concatenate([[0], np.cumsum(blk_len)])[:-1]
-        k = torch.arange(rows.numel(), device=dev) - torch.as_tensor(np.repeat(src_pos, blk_len), device=dev)
-        q = torch.as_tensor(np.repeat(blk_start, blk_len), device=dev) + k
-        served = torch.empty_like(rows)
-        served[q] = rows
-        c.served = served                                   # owner-local rows, step-major
+        blk_len = torch.as_tensor(c.rc.reshape(-1), device=dev)        # block (o, t) -> rows
+        blk = torch.repeat_interleave(torch.arange(G * T, device=dev), blk_len, output_size=rows.numel())
+        o_e, t_e = blk // T, blk % T
+        k_e = torch.arange(rows.numel(), device=dev) - (torch.cumsum(blk_len, 0) - blk_len)[blk]
+        bf.srv[:T].fill_(ni)
+        bf.srv[:T].view(-1)[t_e * (GC + 1) + o_e * C + k_e] = rows
         # owner reduction segments: per (step, row), positions in requester order
-        step_of = torch.as_tensor(np.repeat(np.arange(T), c.R), device=dev)
-        key = step_of * (self.Q.shape[0] + 1) + served
-        skey, spos = torch.sort(key, stable=True)
-        head = torch.ones_like(skey, dtype=torch.bool)
-        if skey.numel() > 1:
-            head[1:] = skey[1:] != skey[:-1]
-        starts = torch.nonzero(head).squeeze(1)
-        c.seg = torch.cat([starts, torch.tensor([skey.numel()], device=dev)]).to(torch.int32)
-        c.pos = (spos - torch.as_tensor(c.Rs[:-1], device=dev)[step_of[spos]]).to(torch.int32)
-        c.own_rows = served[spos[starts]].to(torch.int32)
-        nseg = torch.bincount(step_of[spos[starts]], minlength=T) if starts.numel() else torch.zeros(T)
-        c.Sa = np.concatenate([[0], np.cumsum(nseg.cpu().numpy())]).astype(np.int64)
-        c.lo = np.concatenate([[0], np.cumsum(c.nloc)])
+        key = (t_e * (ni + 1) + rows) * G + o_e
+        skey, sp = torch.sort(key)
+        srow = skey // G
+        head = torch.ones_like(srow, dtype=torch.bool)
+        if srow.numel() > 1:
+            head[1:] = srow[1:] != srow[:-1]
+        ts = t_e[sp]
+        Rt = torch.bincount(t_e, minlength=T)
+        nseg = torch.bincount(ts[head], minlength=T)
+        p_in = torch.arange(rows.numel(), device=dev) - (torch.cumsum(Rt, 0) - Rt)[ts]
+        s_in = torch.cumsum(head.long(), 0) - 1 - (torch.cumsum(nseg, 0) - nseg)[ts]
+        bf.pos[:T].view(-1)[ts * GC + p_in] = (o_e * C + k_e)[sp].to(torch.int32)
+        bf.seg[:T].copy_(Rt.to(torch.int32)[:, None].expand(T, GC + 1))
+        hs = ts[head]
+        bf.seg[:T].view(-1)[hs * (GC + 1) + s_in[head]] = p_in[head].to(torch.int32)
+        bf.own[:T].fill_(ni)
+        c.own_rows = (srow[head] % (ni + 1))
+        c.own_flat = hs * GC + s_in[head]
+        bf.own[:T].view(-1)[c.own_flat] = c.own_rows.to(torch.int32)
+        c.has_count = False
+        c.R = c.rc.sum(0)                                   # rows I serve per step
         c.nW = c.cnt.sum(1)
-        c.w0 = np.concatenate([[0], np.cumsum(c.nW)])  # working-set start of each step (host)
-        c.count = None
         self._chunk_items = (i, j)
         return c
 
-    def _counts(self, c: _Chunk, i, j):
+    def _counts(self, c: _Chunk, i, j) -> None:
         """Occurrences of every owned row of each step in the GLOBAL batch (the
         reg * mean(w^2) gradient counts them, APR.py:153-154)."""
         G, B, T = self.G, self.B, c.T
         items = torch.cat([i, j])
         st = torch.cat([torch.arange(T * B, device=self.device) // B] * 2)
         mine = items % G == self.rank
-        nrow = self.Q.shape[0] + 1
+        nrow = self.ni + 1
         cnt = torch.bincount(st[mine] * nrow + items[mine] // G, minlength=T * nrow)
-        seg_step = torch.as_tensor(np.repeat(np.arange(T), np.diff(c.Sa)), device=self.device)
-        return cnt[seg_step * nrow + c.own_rows.long()].to(torch.int32)
+        seg_step = c.own_flat // (G * self._C)
+        cf = self._buf.count[:T]
+        cf.zero_()
+        cf.view(-1)[c.own_flat] = cnt[seg_step * nrow + c.own_rows].to(torch.int32)
+        c.has_count = True
 
-    # -- one step ------------------------------------------------------------------
-    def _step(self, c: _Chunk, t: int, hp):
-        d = self.d
-        cnt, rc = c.cnt[t].tolist(), c.rc[:, t].tolist()
-        b, nw, R = int(c.nloc[t]), int(c.nW[t]), int(c.R[t])
-        if self._recv.shape[0] < R:
-            self._recv = torch.empty(max(R, 2 * self._recv.shape[0]), d, dtype=torch.float32, device=self.device)
-        lo = int(c.lo[t])
-        served = c.served[c.Rs[t]: c.Rs[t] + R]
-        seg = c.seg[c.Sa[t]: c.Sa[t + 1] + 1]
-        own_rows = c.own_rows[c.Sa[t]: c.Sa[t + 1]]
-        count = None if c.count is None else c.count[c.Sa[t]: c.Sa[t + 1]]
-        nseg = seg.numel() - 1
-        recv, reply = self._recv[:R], self._recv_reply(R)
-        part = self._send[:nw]
+    # -- one step (fixed shapes: every size is the buffers') -----------------------
+    def _step(self, t: int, b: int, hp, count: bool) -> None:
+        bf, M = self._buf, self.max_items
         # E1: current item rows of my working set from their owners
         if self.item_exchange == "allgather":
-            self._gather_q()
-            w0 = int(c.w0[t])
-            torch.index_select(self._qall, 0, c.wslot[w0: w0 + nw], out=self.Qc[:nw])
+            torch.index_select(self._gather_q(), 0, bf.wslot[t], out=self.Qc)
         else:
-            self._a2a(self.Qc[:nw], self.Q.index_select(0, served.long()), cnt, rc)
+            torch.index_select(self._Qst, 0, bf.srv[t], out=bf.S1)
+            torch.index_select(self._exchange(bf.R1, bf.S1), 0, bf.wsrc[t], out=self.Qc)
+        part = bf.part[: 2 * b]
         if b:
-            self.local.plan(c.u_rows[lo: lo + b], c.wi[lo: lo + b], c.wj[lo: lo + b])
+            self.local.plan(bf.u_rows[t, :b], bf.wi[t, :b], bf.wj[t, :b])
             self.local.clean(hp, part)
         # E2: partial clean item sums -> owners
-        self._a2a(recv, part, rc, cnt)
-        G0 = self._g0(nseg)
+        torch.index_select(bf.part, 0, bf.winv[t], out=bf.S)
+        recv = self._exchange(bf.R, bf.S)
+        cnt = bf.count[t] if count else None
         if hp.adver:
-            self.local.reduce_delta(hp, recv, seg, c.pos, G0, reply)
+            self.local.reduce_delta(hp, recv, bf.seg[t], bf.pos[t], bf.G0, bf.reply)
             # E3: deltas -> requesters
-            self._a2a(self._dlt[:nw], reply, cnt, rc)
+            torch.index_select(self._exchange(bf.R3, bf.reply), 0, bf.wsrc[t], out=bf.dlt)
             if b:
-                self.local.set_item_delta(self._dlt[:nw])
+                self.local.set_item_delta(bf.dlt[: 2 * b])
                 self.local.adv(hp, part)
             # E4: partial adversarial item sums -> owners, who apply Adagrad
-            self._a2a(recv, part, rc, cnt)
-            self.local.reduce_apply(hp, recv, seg, c.pos, G0, own_rows, count)
+            torch.index_select(bf.part, 0, bf.winv[t], out=bf.S)
+            recv = self._exchange(bf.R, bf.S)
+            self.local.reduce_apply(hp, recv, bf.seg[t], bf.pos[t], bf.G0, bf.own[t], cnt)
         else:
-            self.local.reduce_apply(hp, recv, seg, c.pos, None, own_rows, count)
-        st = self.stats
-        st["steps"] += 1
-        st["items_requested"] += nw
-        st["rows_served"] += R
-        st["triplets"] += b
+            self.local.reduce_apply(hp, recv, bf.seg[t], bf.pos[t], None, bf.own[t], cnt)
 
-    def _recv_reply(self, R):
-        buf = getattr(self, "_reply", None)
-        if buf is None or buf.shape[0] < R:
-            self._reply = buf = torch.empty(max(R, 1), self.d, dtype=torch.float32, device=self.device)
-        return buf[:R]
+    def _run(self, c: _Chunk, hp) -> None:
+        T = c.T
+        bs = set(int(x) for x in c.nloc)
+        key = None
+        if self.graph and len(bs) == 1 and min(bs) > 0:
+            key = (T, min(bs), self._C, c.has_count, _hp_key(hp))
+        rec = self._graphs.get(key) if key is not None else None
+        if rec is not None:
+            rec.replay()
+            self.stats["graph_replays"] += 1
+            return
+        for t in range(T):
+            self._step(t, int(c.nloc[t]), hp, c.has_count)
+        if key is not None:  # capture for the next chunk of this shape (capturing runs nothing)
+            self._graphs[key] = self._capture(T, min(bs), hp, c.has_count)
 
-    def _g0(self, n):
-        buf = getattr(self, "_g0buf", None)
-        if buf is None or buf.shape[0] < n:
-            self._g0buf = buf = torch.empty(max(n, 1), self.d, dtype=torch.float32, device=self.device)
-        return buf[:n]
+    def _capture(self, T: int, b: int, hp, count: bool) -> _SegmentRecorder:
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+            self._cap_stream = torch.cuda.Stream(self.device)
+        main = torch.cuda.current_stream(self.device)
+        rec = _SegmentRecorder(self._cap_stream, self._pool)
+        torch.cuda.synchronize(self.device)
+        self._cap_stream.wait_stream(main)
+        with torch.cuda.stream(self._cap_stream):
+            self._rec = rec
+            try:
+                rec.begin()
+                for t in range(T):
+                    self._step(t, b, hp, count)
+                rec.end()
+            finally:
+                self._rec = None
+        main.wait_stream(self._cap_stream)
+        return rec
 
     # -- public --------------------------------------------------------------------
     def train(self, u, i, j, hp, chunk: int = 64) -> int:
@@ -337,13 +493,17 @@ class ShardedAPR:
             s = slice(c0 * bs, (c0 + T) * bs)
             t0 = time.perf_counter()
             c = self._route(u[s], i[s], j[s], T)
-            self.stats["route_s"] += time.perf_counter() - t0
             if hp.reg:  # the owners count their rows in the GLOBAL batch
                 if self.routed:
                     raise ValueError("reg != 0 needs the global stream on every rank (train, not train_routed)")
-                c.count = self._counts(c, *self._chunk_items)
-            for t in range(T):
-                self._step(c, t, hp)
+                self._counts(c, *self._chunk_items)
+            self.stats["route_s"] += time.perf_counter() - t0
+            self._run(c, hp)
+            st = self.stats
+            st["steps"] += T
+            st["items_requested"] += int(c.nW.sum())
+            st["rows_served"] += int(c.R.sum())
+            st["triplets"] += int(c.nloc.sum())
         return n
 
     def train_routed(self, u, i, j, hp, chunk: int = 64) -> int:

@@ -385,34 +385,44 @@ def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
             "xgmi_egress_GBs_rank0": round(4 * req * d * 4 * (world - 1) / world / (el / steps) / 1e9, 2),
             "items_per_rank_step": round(req, 1),
             "route_ms_rank0": round(1e3 * (sh.stats["route_s"] - st0["route_s"]), 3),
+            "launch": "hipGraph" if sh.stats["graph_replays"] > st0["graph_replays"] else "eager",
             "step_errors": sh.step_errors()}
         del sh, u, i, j
         torch.cuda.empty_cache()
 
-        # configs[2], strong scaling: the reference's global batch of 512
+        # configs[2], strong scaling: the reference's global batch of 512, B / N triplets
+        # of it per rank, routed at sampling time (each rank samples its own users), so
+        # every step has the same shape and the chunk replays as captured hipGraphs
         B, d = 512, 64
+        bl = B // world
         ds = acf.pinterest_like(seed=2019)
-        psamp = acf.DeviceSampler(ds, B, dev, seed=3)
+        pu = ds.pair_user % world == rank
+        sub = type(ds)(ds.num_users, ds.num_items, ds.pair_user[pu], ds.pair_item[pu], ds.test_items,
+                       name="pinterest-20-synthetic-rank")
+        psamp = acf.DeviceSampler(sub, bl, dev, seed=3 + rank)
         ep = psamp.epoch(0)
         steps_p = 200
-        warm = steps_p  # as above: one untimed chunk of the timed size
-        n = (warm + steps_p) * B
+        warm = steps_p  # as above: one untimed chunk of the timed size (graphs captured after it)
+        n = (warm + steps_p) * bl
         u, i, j = (x[:n].contiguous() for x in (ep.user, ep.item_pos, ep.item_neg))
         for key, exchange in (("pinterest", "all_to_all"), ("pinterest_allgather", "allgather")):
-            sh = D_.ShardedAPR(ds.num_users + 1, ds.num_items + 1, d, B, device=dev, item_exchange=exchange)
+            sh = D_.ShardedAPR(ds.num_users + 1, ds.num_items + 1, d, B, device=dev, item_exchange=exchange,
+                               local_batch=bl)
             sh.P.normal_(0, 0.01, generator=g)
             sh.Q.normal_(0, 0.01, generator=g)
-            sh.train(u[: warm * B], i[: warm * B], j[: warm * B], hp, chunk=warm)
-            s = slice(warm * B, n)
-            el, tot = timed(sh, lambda: sh.train(u[s], i[s], j[s], hp, chunk=steps_p), steps_p * B / world)
+            sh.train_routed(u[: warm * bl], i[: warm * bl], j[: warm * bl], hp, chunk=warm)
+            s = slice(warm * bl, n)
+            r0 = sh.stats["graph_replays"]
+            el, tot = timed(sh, lambda: sh.train_routed(u[s], i[s], j[s], hp, chunk=steps_p), steps_p * bl)
             out[key] = {
                 "metric": "APR triplets/sec, split step (users/items sharded over the ranks)",
-                "value": round(steps_p * B / el, 1), "unit": "triplets/s", "n_gpus": world, "steps": steps_p,
+                "value": round(tot / el, 1), "unit": "triplets/s", "n_gpus": world, "steps": steps_p,
                 "ms_per_step": round(1e3 * el / steps_p, 4), "scaling": "strong", "dtype": "f32",
-                "data": "synthetic pinterest-20-shaped (55,187 x 9,916), device sampler",
+                "data": "synthetic pinterest-20-shaped (55,187 x 9,916), device sampler per rank",
                 "config": {"workload": "APR, BASELINE configs[2] split over the ranks", "users": ds.num_users,
-                           "items": ds.num_items, "dim": d, "global_batch": B,
+                           "items": ds.num_items, "dim": d, "global_batch": B, "per_gpu_batch": bl,
                            "parallelism": f"user/item row shards x{world}, E1 by {exchange}, all_to_all x3"},
+                "launch": "hipGraph" if sh.stats["graph_replays"] > r0 else "eager",
                 "step_errors": sh.step_errors()}
             del sh
             torch.cuda.empty_cache()

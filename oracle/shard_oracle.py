@@ -122,7 +122,8 @@ class OracleShardLocal:
     def reduce_apply(self, hp, recv, seg, pos, G0, rows, count):
         S, seg, _ = self._seg_sums(recv, seg, pos)
         G = (G0.numpy() + f32(hp.reg_adv) * S).astype(f32) if hp.adver else S
-        Q, A, rows = self.sh.Q.numpy(), self.sh.accQ.numpy(), rows.numpy()
+        # the storage with the trash row that padded segments name (distributed.py)
+        Q, A, rows = self.sh._Qst.numpy(), self.sh._aQst.numpy(), rows.numpy()
         if hp.reg:
             coef = f32(2.0 * hp.reg / (self.sh.B * self.sh.d)) * f32(2 if hp.adver else 1)
             cnt = count.numpy()

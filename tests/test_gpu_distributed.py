@@ -84,6 +84,37 @@ def test_sharded_rccl_world1_matches_oracle(ops, oracle, dev, fp32_parity, shape
         fp32_parity(g, w, n)
 
 
+@pytest.mark.parametrize("exchange,adver,reg,routed", [("all_to_all", 1, 0.0, False), ("allgather", 1, 0.0, True),
+                                                       ("all_to_all", 0, 0.01, False), ("all_to_all", 1, 0.0, True)])
+def test_sharded_graph_replay_bit_identical(ops, dev, exchange, adver, reg, routed):
+    """The captured step graphs (one hipGraph per chunk at world 1, distributed.py
+    "Static step layout") replay the eager step sequence bit for bit, on
+    pinterest-20-shaped data (configs[2]), 3 chunks of 4 steps: the first is run
+    eagerly and captured, the next ones replay."""
+    D_ = importlib.import_module(PKG + ".distributed")
+    U1, I1, d, B, nb = 55_188, 9_917, 64, 512, 12
+    P, Q, u, i, j = _problem(5 + adver, U1, I1, d, B, nb)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    outs, replays = [], []
+    try:
+        uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
+        for graph in (False, True):
+            sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, item_exchange=exchange, graph=graph,
+                               local_batch=B if routed else None)
+            hp = ops.StepHParams(adver=adver, reg=reg)
+            (sh.train_routed if routed else sh.train)(uu, ii, jj, hp, chunk=4)
+            torch.cuda.synchronize(dev)
+            assert sh.step_errors() == 0
+            outs.append(sh.full_tables())
+            replays.append(sh.stats["graph_replays"])
+    finally:
+        dist.destroy_process_group()
+    assert replays[0] == 0 and replays[1] >= 1, replays
+    for g, e, n in zip(outs[1], outs[0], ("P", "Q", "accP", "accQ")):
+        assert torch.equal(g, e), n
+
+
 # two-rank problems: (U1, I1, d, B, nb, zipf, chunk); "pinterest" is BASELINE configs[2]'s
 # shape (the reference's global batch of 512 split over the ranks)
 SHAPES2 = {"zipf": (20_000, 9_000, 64, 4096, 4, 1.2, 3), "pinterest": (55_188, 9_917, 64, 512, 10, None, 4)}
