@@ -136,7 +136,8 @@ class _SegmentRecorder:
 
     def begin(self):
         self._g = torch.cuda.CUDAGraph()
-        self._g.capture_begin(pool=self.pool)
+        # thread-local: the process group's watchdog thread may query its events meanwhile
+        self._g.capture_begin(pool=self.pool, capture_error_mode="thread_local")
 
     def cut(self, fn):
         self._g.capture_end()
