@@ -501,22 +501,16 @@ __device__ __forceinline__ void slot_flag(uint64_t* __restrict__ sflags, const H
 // its batch is "single" (its triplet's lane-group steps it: SINGLE bit, and
 // INPLACE by fuse_info's rule), and every triplet gets a record in trec with
 // the single bits 16 / 32 / 64 (u / i / j) beside the fused / in-place flags.
-__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb, int32_t no_fuse,
-                          int32_t tri,
-                          const int4* __restrict__ tsl, const int4* __restrict__ tpos,
-                          const int4* __restrict__ uinfo, const int4* __restrict__ iinfo,
-                          const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
-                          OccRec* __restrict__ urec, OccRec* __restrict__ irec,
-                          OccRec* __restrict__ inl, OccRec* __restrict__ trec,
-                          int32_t* __restrict__ gen_ptr, uint64_t* __restrict__ sflags, HotLists hl) {
-  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (e == 0) *gen_ptr = gen;
-  if (e >= E) return;
+// the records of triplet e of batch t (its user slots start at ub0, its item slots
+// at ib0, nU user slots); shared by k_records and the one-workgroup shard plan
+__device__ __forceinline__ void records_one(int64_t e, int32_t t, int32_t ub0, int32_t nU, int32_t ib0, int32_t S,
+                                            int32_t R, int32_t gen, int32_t kb, int32_t no_fuse, int32_t tri,
+                                            const int4* tsl, const int4* tpos, const int4* uinfo, const int4* iinfo,
+                                            OccRec* urec, OccRec* irec, OccRec* inl, OccRec* trec,
+                                            uint64_t* sflags, const HotLists& hl) {
   const int4 sl = tsl[e], ps = tpos[e];
   const int4 U = uinfo[sl.x], I = iinfo[sl.y], J = iinfo[sl.z];
-  const int32_t t = (int32_t)(e / B);
-  const int32_t nU = ubs[t + 1] - ubs[t];
-  const int32_t k = sl.x - ubs[t], ki = nU + (sl.y - ibs[t]), kj = nU + (sl.z - ibs[t]);
+  const int32_t k = sl.x - ub0, ki = nU + (sl.y - ib0), kj = nU + (sl.z - ib0);
   FuseInfo f = fuse_info(U, I, J, kb);
   if (no_fuse) f.fused = f.in_u = f.in_i = f.in_j = 0;  // shard mode: item counts are rank-local
   const int su = info_count(U) == 1, si = info_count(I) == 1, sj = info_count(J) == 1;
@@ -568,6 +562,22 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
     q.pb_slot = (int32_t)e; q.gen = gen;
     trec[e] = q;
   }
+}
+
+__global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb, int32_t no_fuse,
+                          int32_t tri,
+                          const int4* __restrict__ tsl, const int4* __restrict__ tpos,
+                          const int4* __restrict__ uinfo, const int4* __restrict__ iinfo,
+                          const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
+                          OccRec* __restrict__ urec, OccRec* __restrict__ irec,
+                          OccRec* __restrict__ inl, OccRec* __restrict__ trec,
+                          int32_t* __restrict__ gen_ptr, uint64_t* __restrict__ sflags, HotLists hl) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e == 0) *gen_ptr = gen;
+  if (e >= E) return;
+  const int32_t t = (int32_t)(e / B);
+  records_one(e, t, ubs[t], ubs[t + 1] - ubs[t], ibs[t], S, R, gen, kb, no_fuse, tri, tsl, tpos, uinfo, iinfo,
+              urec, irec, inl, trec, sflags, hl);
 }
 
 __global__ void k_slot_lists(const uint64_t* __restrict__ flags, const uint64_t* __restrict__ incl,
@@ -810,6 +820,193 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
     p.berr[t] = s_err;
   }
   STAMP(t, tid >> 6, 4);
+}
+
+// ---------------------------------------------------------------------------
+// One-workgroup shard plan (shard mode, one batch of B <= 1,024 triplets:
+// distributed.ShardedAPR's per-step plan).  It writes what the device-wide sort
+// plan writes for nb = 1 -- unique rows and CSR offsets, slot info, the triplets'
+// slots and CSR positions, occurrence records, slot flags, hot lists and the
+// slot / write-back lists -- in ONE launch instead of ~17 (stage, radix sort,
+// head flags, two scans, compaction, slot info, four clears, records, list
+// scan), which a captured split step replays every step.  Same keys and the
+// same stable order (users by row, then items by row, occurrence order inside a
+// row), so the records are the sort plan's bit for bit
+// (test_shard_plan_small_matches_sort_plan).
+// ---------------------------------------------------------------------------
+struct SPlanArgs {
+  const int32_t* user;
+  const int32_t* ipos;
+  const int32_t* ineg;
+  int64_t U1, I1;
+  int32_t B, rb, kb, gen;
+  int32_t *uuniq, *uoff, *ubs, *iuniq, *ioff, *ibs;
+  int32_t *tsl, *tpos;  // [E][4]
+  int4 *uinfo, *iinfo;
+  OccRec *urec, *irec, *inl, *trec;
+  int32_t *gen_ptr, *err;
+  uint64_t* sflags;
+  HotLists hl;
+  int32_t *slot_list, *flush_list, *slot_cnt, *flush_cnt;
+};
+
+template <int BS, int IPT>
+__global__ void __launch_bounds__(BS) k_shard_plan(SPlanArgs p) {
+  constexpr int N = BS * IPT;
+  using Sort = rocprim::block_radix_sort<uint32_t, BS, IPT, int32_t>;
+  using Scan = rocprim::block_scan<int32_t, BS>;
+  using Scan64 = rocprim::block_scan<uint64_t, BS>;
+  __shared__ union {
+    typename Sort::storage_type sort;
+    struct {
+      uint32_t key[N];
+      int32_t start[N + 1];
+    } a;
+    typename Scan64::storage_type scan64;
+  } sm;
+  __shared__ typename Scan::storage_type scan_st;
+  __shared__ int32_t s_err, s_nu;
+  const int tid = threadIdx.x, B = p.B, S3 = 3 * B;
+  // what the sort plan clears: slot flags, inline records (shard plans), hot counters
+  for (int x = tid; x < S3; x += BS) {
+    p.sflags[x] = 0;
+    p.inl[x] = OccRec{};
+  }
+  for (int x = tid; x < p.hl.piece_stride; x += BS) p.hl.arrive[x] = 0;
+  if (tid == 0) {
+    p.hl.cnt[0] = 0;
+    p.hl.pcnt[0] = 0;
+    *p.gen_ptr = p.gen;
+    s_err = 0;
+    s_nu = 0;
+  }
+  // keys: users [0, B) by row, items B + 2e + role after them (side bit)
+  const uint32_t side_bit = 1u << p.rb;
+  uint32_t keys[IPT];
+  int32_t vals[IPT], raw[IPT];
+  int err = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int o = tid * IPT + k;
+    raw[k] = 0;
+    if (o < B) {
+      raw[k] = p.user[o];
+    } else if (o < S3) {
+      const int v = o - B;
+      raw[k] = ((v & 1) ? p.ineg : p.ipos)[v >> 1];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int o = tid * IPT + k;
+    uint32_t key = ~0u;  // padding sorts after every key (stable: after equal ones too)
+    int32_t x = raw[k];
+    if (o < B) {
+      if (x < 0 || x >= p.U1) { err |= 1; x = 0; }
+      key = (uint32_t)x;
+    } else if (o < S3) {
+      if (x < 0 || x >= p.I1) { err |= 2; x = 0; }
+      key = side_bit | (uint32_t)x;
+    }
+    keys[k] = key;
+    vals[k] = o;
+  }
+  __syncthreads();
+  if (err) atomicOr(&s_err, err);
+  Sort().sort(keys, vals, sm.sort, 0, p.rb + 1);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) sm.a.key[tid * IPT + k] = keys[k];
+  __syncthreads();
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int q = tid * IPT + k;
+    cnt += (q < S3 && (q == 0 || keys[k] != sm.a.key[q - 1])) ? 1 : 0;
+  }
+  int32_t excl = 0, total = 0;
+  Scan().exclusive_scan(cnt, excl, 0, total, scan_st);
+  int32_t sl[IPT];
+  int32_t s = excl - 1;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int q = tid * IPT + k;
+    sl[k] = -1;
+    if (q >= S3) continue;
+    if (q == 0 || keys[k] != sm.a.key[q - 1]) {
+      ++s;
+      sm.a.start[s] = q;
+      if (q == B) s_nu = s;  // position B holds the first item occurrence: a head
+    }
+    sl[k] = s;
+  }
+  if (tid == 0) sm.a.start[total] = S3;
+  __syncthreads();
+  const int nU = s_nu, nI = total - nU;
+  // unique rows, CSR offsets and slot info (user part [0, B), item part [0, 2B));
+  // every triplet's slots and CSR positions
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int q = tid * IPT + k;
+    if (q >= S3) continue;
+    const int32_t sk = sl[k];
+    const int32_t row = (int32_t)(keys[k] & (side_bit - 1));
+    if (sm.a.start[sk] == q) {
+      const int32_t c = sm.a.start[sk + 1] - q;
+      if (q < B) {
+        p.uuniq[sk] = row;
+        p.uoff[sk] = q;
+        p.uinfo[sk] = make_int4(row, row, c, q);
+      } else {
+        p.iuniq[sk - nU] = row;
+        p.ioff[sk - nU] = q - B;
+        p.iinfo[sk - nU] = make_int4(row, row, c, q - B);
+      }
+    }
+    const int o = vals[k];
+    if (o < B) {
+      p.tsl[o * 4] = sk;
+      p.tpos[o * 4] = q;
+    } else {
+      const int v = o - B;
+      const int at = (v >> 1) * 4 + 1 + (v & 1);
+      p.tsl[at] = sk - nU;
+      p.tpos[at] = q - B;
+    }
+  }
+  if (tid == 0) {
+    p.uoff[nU] = B;
+    p.ioff[nI] = 2 * B;
+    p.ubs[0] = 0;
+    p.ubs[1] = nU;
+    p.ibs[0] = 0;
+    p.ibs[1] = nI;
+    *p.err = s_err;
+  }
+  __syncthreads();  // the slot info and triplet slots above, for the records
+  for (int e = tid; e < B; e += BS)
+    records_one(e, 0, 0, nU, 0, S3, 1, p.gen, p.kb, 1, 0, reinterpret_cast<const int4*>(p.tsl),
+                reinterpret_cast<const int4*>(p.tpos), p.uinfo, p.iinfo, p.urec, p.irec, p.inl, p.trec,
+                p.sflags, p.hl);
+  __syncthreads();  // the slot flags, for the lists
+  uint64_t f[IPT], inc[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int x = tid * IPT + k;
+    f[k] = x < S3 ? p.sflags[x] : 0ull;
+  }
+  Scan64().inclusive_scan(f, inc, sm.scan64, rocprim::plus<uint64_t>());
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int x = tid * IPT + k;
+    if (x >= S3) continue;
+    if (f[k] >> 32) p.slot_list[(inc[k] >> 32) - 1] = x;
+    if (f[k] & 0xFFFFFFFFull) p.flush_list[(inc[k] & 0xFFFFFFFFull) - 1] = x;
+    if (x == S3 - 1) {
+      *p.slot_cnt = (int32_t)(inc[k] >> 32);
+      *p.flush_cnt = (int32_t)(inc[k] & 0xFFFFFFFFull);
+    }
+  }
 }
 
 template <int BS, int MAXB>
@@ -3662,6 +3859,47 @@ static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, 
   return ACF_OK;
 }
 
+// shard mode, one batch of B <= 1,024: the one-workgroup plan (k_shard_plan)
+static int shard_plan_small(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg,
+                            int32_t B, int32_t gen, int32_t check, hipStream_t s) {
+  const int32_t kb = (int32_t)bits_for((uint64_t)3 * B + 1);
+  SPlanArgs p;
+  p.user = user; p.ipos = ipos; p.ineg = ineg;
+  p.U1 = c->U1; p.I1 = c->I1;
+  p.B = B;
+  p.rb = (int32_t)bits_for((uint64_t)std::max(c->U1, c->I1));
+  p.kb = kb;
+  p.gen = gen;
+  p.uuniq = c->uuniq; p.uoff = c->uoff; p.ubs = c->ubs;
+  p.iuniq = c->iuniq; p.ioff = c->ioff; p.ibs = c->ibs;
+  p.tsl = c->tsl; p.tpos = c->tpos;
+  p.uinfo = c->uinfo; p.iinfo = c->iinfo;
+  p.urec = c->urec; p.irec = c->irec; p.inl = c->inl; p.trec = c->trec;
+  p.gen_ptr = c->gen_dev; p.err = c->err;
+  p.sflags = c->key_in;
+  p.hl = c->hot;
+  p.slot_list = c->slot_list; p.flush_list = c->flush_list;
+  p.slot_cnt = c->slot_cnt; p.flush_cnt = c->flush_cnt;
+  k_shard_plan<1024, 3><<<1, 1024, 0, s>>>(p);
+  HIP_TRY(hipGetLastError());
+  c->plan_R = 1;
+  c->plan_kind2 = 0;
+  c->plan_kb = kb;
+  c->tri = 0;
+  c->task_lists = 0;
+  c->lists = 1;
+  if (check) {
+    int32_t herr = 0;
+    HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ACF_CHECK(herr == 0, ACF_E_RANGE, "triplet index out of range (%s%s)",
+              (herr & 1) ? "user >= num_user_rows " : "", (herr & 2) ? "item >= num_item_rows" : "");
+  }
+  c->B = B;
+  c->nb = 1;
+  return ACF_OK;
+}
+
 // sorted keys -> head flags -> one scan -> per-side compaction
 template <class KT>
 static int plan_groups(acf_apr_ctx* c, const KT& ku, const KT& ki, int64_t E, int32_t nb,
@@ -3701,6 +3939,9 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
     if (!packed && c->plan_mode == 0 && B <= 1024 && kb + bits_for((uint64_t)nb + 1) <= 31 && bplan_ready(c))
       return batch_plan(c, user, ipos, ineg, B, nb, gen, kb, check, s);
   }
+  if (c->shard && nb == 1 && B <= 1024 && c->plan_mode == 0 &&
+      bits_for((uint64_t)std::max(c->U1, c->I1)) <= 30)
+    return shard_plan_small(c, user, ipos, ineg, B, gen, check, s);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
   // 32-bit keys (segment only, occurrence as the sort value) when they fit
   const uint32_t sb = std::max(bits_for((uint64_t)nb * (uint64_t)c->U1),
@@ -4511,18 +4752,26 @@ extern "C" int acf_apr_shard_pass(acf_apr_ctx* c, const acf_apr_tables* tb, cons
 }
 
 // item slot rows of the current one-batch plan (slots nU .. nU + n, nU read
-// on device): dir 0 copies g0 -> buf, dir 1 copies buf -> delta
+// on device): dir 0 copies g0 -> buf, dir 1 copies buf -> delta; with a map,
+// working-set entry w sits in buf row map[w] (the split step's exchange rows)
 __global__ void k_shard_items(float* __restrict__ g0, float* __restrict__ delta, const int32_t* __restrict__ ubs,
-                              float* __restrict__ buf, int64_t n4, int32_t d4, int32_t dir) {
+                              float* __restrict__ buf, const int64_t* __restrict__ map, int64_t n4, int32_t d4,
+                              int32_t dir) {
   const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (x >= n4) return;
   const int64_t off = (int64_t)(ubs[1] - ubs[0]) * d4;
-  float4* b = reinterpret_cast<float4*>(buf) + x;
+  int64_t bx = x;
+  if (map) {
+    const int64_t w = x / d4;
+    bx = map[w] * d4 + (x - w * d4);
+  }
+  float4* b = reinterpret_cast<float4*>(buf) + bx;
   if (dir == 0) *b = reinterpret_cast<const float4*>(g0)[off + x];
   else reinterpret_cast<float4*>(delta)[off + x] = *b;
 }
 
-extern "C" int acf_apr_shard_items(acf_apr_ctx* c, int32_t dir, float* buf, int64_t n_items, void* stream_) {
+extern "C" int acf_apr_shard_items_mapped(acf_apr_ctx* c, int32_t dir, float* buf, const int64_t* map,
+                                          int64_t n_items, void* stream_) {
   ACF_CHECK(c && (buf || n_items == 0), ACF_E_INVALID, "NULL argument");
   ACF_CHECK(c->shard && c->nb == 1, ACF_E_STATE, "shard items need shard mode and a one-batch plan");
   ACF_CHECK(dir == 0 || dir == 1, ACF_E_INVALID, "dir must be 0 or 1");
@@ -4531,9 +4780,13 @@ extern "C" int acf_apr_shard_items(acf_apr_ctx* c, int32_t dir, float* buf, int6
   if (n_items == 0) return ACF_OK;
   hipStream_t s = static_cast<hipStream_t>(stream_);
   const int64_t n4 = n_items * (c->d / 4);
-  k_shard_items<<<grid_for(n4), 256, 0, s>>>(c->g0, c->delta, c->ubs, buf, n4, c->d / 4, dir);
+  k_shard_items<<<grid_for(n4), 256, 0, s>>>(c->g0, c->delta, c->ubs, buf, map, n4, c->d / 4, dir);
   HIP_TRY(hipGetLastError());
   return ACF_OK;
+}
+
+extern "C" int acf_apr_shard_items(acf_apr_ctx* c, int32_t dir, float* buf, int64_t n_items, void* stream_) {
+  return acf_apr_shard_items_mapped(c, dir, buf, nullptr, n_items, stream_);
 }
 
 // Owner side: the partial rows the requesters sent, grouped per owned row by

@@ -38,8 +38,9 @@ Static step layout.  Every exchange buffer has a fixed shape: G blocks of C rows
 grown), block o holding what this rank exchanges with rank o, plus one trash
 row.  The routing of a chunk of T steps (one host sync, for the counts) writes
 per-step index maps into persistent buffers at fixed per-step offsets:
-``wsrc`` (working-set entry -> received row), ``winv`` (exchange row ->
-working-set entry), ``srv`` (exchange row -> owned row), and the owner's
+``wsrc`` (working-set entry -> its row of the exchange blocks: the passes
+write the item sums there and read the deltas from there), ``srv`` (exchange
+row -> owned row), and the owner's
 segments ``seg`` / ``pos`` / ``own`` (rows padded with empty segments on a
 trash row of the Q storage).  A step therefore has no host-side sizes, so a
 chunk's steps are captured as hipGraphs once and replayed:
@@ -90,16 +91,18 @@ class HipLocal:
     def plan(self, u_rows, wi, wj):
         self.ctx.plan(u_rows, wi, wj, u_rows.numel(), check=False)
 
-    def clean(self, hp, out):
+    def clean(self, hp, out, rows):
+        """pass 0; working-set entry w's partial clean sum -> out[rows[w]]"""
         self.ctx.shard_pass(self._tables(), hp, 0)
-        self.ctx.shard_items_out(out)
+        self.ctx.shard_items_mapped(0, out, rows)
 
-    def set_item_delta(self, delta):
-        self.ctx.shard_items_delta(delta)
+    def set_item_delta(self, src, rows):
+        """the owners' delta of working-set entry w <- src[rows[w]]"""
+        self.ctx.shard_items_mapped(1, src, rows)
 
-    def adv(self, hp, out):
+    def adv(self, hp, out, rows):
         self.ctx.shard_pass(self._tables(), hp, 1)
-        self.ctx.shard_items_out(out)
+        self.ctx.shard_items_mapped(0, out, rows)
 
     def reduce_delta(self, hp, recv, seg, pos, G0, reply):
         self.ops.shard_reduce_delta(recv, seg, pos, hp, G0, reply)
@@ -234,9 +237,9 @@ class ShardedAPR:
         b.u_rows = torch.zeros(T, self.b_max, **ii)
         b.wi = torch.zeros(T, self.b_max, **ii)
         b.wj = torch.zeros(T, self.b_max, **ii)
-        b.wsrc = torch.empty(T, M, **li)        # working-set entry -> row of the received E1/E3 block
-        b.winv = torch.empty(T, GC + 1, **li)   # exchange row -> working-set entry (trash: M)
+        b.wsrc = torch.empty(T, M, **li)        # working-set entry -> its row of the exchange blocks
         b.srv = torch.empty(T, GC + 1, **li)    # exchange row -> owned Q row (trash: ni)
+        b.wq = torch.empty(T, M, **li) if G == 1 else None  # world 1: working-set entry -> Q row
         b.wslot = torch.zeros(T, M, **li) if self.item_exchange == "allgather" else None
         b.seg = torch.empty(T, GC + 1, **ii)
         b.pos = torch.zeros(T, GC, **ii)
@@ -244,13 +247,11 @@ class ShardedAPR:
         b.count = torch.zeros(T, GC, **ii)
         b.S1 = torch.empty(GC + 1, d, **fl)
         b.R1 = torch.empty(GC + 1, d, **fl)
-        b.part = torch.zeros(M + 1, d, **fl)
-        b.S = torch.empty(GC + 1, d, **fl)
+        b.S = torch.zeros(GC + 1, d, **fl)
         b.R = torch.empty(GC + 1, d, **fl)
         b.G0 = torch.empty(GC, d, **fl)
         b.reply = torch.zeros(GC + 1, d, **fl)
         b.R3 = torch.zeros(GC + 1, d, **fl)
-        b.dlt = torch.empty(M, d, **fl)
         self._buf = b
 
     # -- collectives ---------------------------------------------------------------
@@ -261,7 +262,9 @@ class ShardedAPR:
             fn()
 
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
-        if self._stage:  # gloo with device tensors (rehearsal of several ranks on one GPU)
+        if self.G == 1:  # one rank: the exchange is a copy
+            out.copy_(inp)
+        elif self._stage:  # gloo with device tensors (rehearsal of several ranks on one GPU)
             o = torch.empty(out.shape, dtype=out.dtype)
             dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
             out.copy_(o)
@@ -361,8 +364,6 @@ class ShardedAPR:
         xrow = wown * C + kblk
         bf.wsrc[:T].fill_(GC)
         bf.wsrc[:T].view(-1)[wstep * M + wk] = xrow
-        bf.winv[:T].fill_(M)
-        bf.winv[:T].view(-1)[wstep * (GC + 1) + xrow] = wk
         if bf.wslot is not None:  # where each working-set row sits in the gathered table
             bf.wslot[:T].view(-1)[wstep * M + wk] = (wid % G) * self._qcap + wid // G if G > 1 else wid
         # rows I serve, received in (requester o, step t, k) order
@@ -374,6 +375,8 @@ class ShardedAPR:
         k_e = torch.arange(rows.numel(), device=dev) - (torch.cumsum(blk_len, 0) - blk_len)[blk]
         bf.srv[:T].fill_(ni)
         bf.srv[:T].view(-1)[t_e * (GC + 1) + o_e * C + k_e] = rows
+        if bf.wq is not None:  # world 1: E1 in one gather (the exchange is the identity)
+            torch.gather(bf.srv[:T], 1, bf.wsrc[:T], out=bf.wq[:T])
         # owner reduction segments: per (step, row), positions in requester order
         key = (t_e * (ni + 1) + rows) * G + o_e
         skey, sp = torch.sort(key)
@@ -417,30 +420,30 @@ class ShardedAPR:
 
     # -- one step (fixed shapes: every size is the buffers') -----------------------
     def _step(self, t: int, b: int, hp, count: bool) -> None:
-        bf, M = self._buf, self.max_items
+        bf = self._buf
         # E1: current item rows of my working set from their owners
         if self.item_exchange == "allgather":
             torch.index_select(self._gather_q(), 0, bf.wslot[t], out=self.Qc)
+        elif bf.wq is not None:
+            torch.index_select(self._Qst, 0, bf.wq[t], out=self.Qc)
         else:
             torch.index_select(self._Qst, 0, bf.srv[t], out=bf.S1)
             torch.index_select(self._exchange(bf.R1, bf.S1), 0, bf.wsrc[t], out=self.Qc)
-        part = bf.part[: 2 * b]
+        rows = bf.wsrc[t, : 2 * b]  # working-set entry -> its exchange row
         if b:
             self.local.plan(bf.u_rows[t, :b], bf.wi[t, :b], bf.wj[t, :b])
-            self.local.clean(hp, part)
+            self.local.clean(hp, bf.S, rows)
         # E2: partial clean item sums -> owners
-        torch.index_select(bf.part, 0, bf.winv[t], out=bf.S)
         recv = self._exchange(bf.R, bf.S)
         cnt = bf.count[t] if count else None
         if hp.adver:
             self.local.reduce_delta(hp, recv, bf.seg[t], bf.pos[t], bf.G0, bf.reply)
             # E3: deltas -> requesters
-            torch.index_select(self._exchange(bf.R3, bf.reply), 0, bf.wsrc[t], out=bf.dlt)
+            dl = self._exchange(bf.R3, bf.reply)
             if b:
-                self.local.set_item_delta(bf.dlt[: 2 * b])
-                self.local.adv(hp, part)
+                self.local.set_item_delta(dl, rows)
+                self.local.adv(hp, bf.S, rows)
             # E4: partial adversarial item sums -> owners, who apply Adagrad
-            torch.index_select(bf.part, 0, bf.winv[t], out=bf.S)
             recv = self._exchange(bf.R, bf.S)
             self.local.reduce_apply(hp, recv, bf.seg[t], bf.pos[t], bf.G0, bf.own[t], cnt)
         else:

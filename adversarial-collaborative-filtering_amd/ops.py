@@ -312,6 +312,16 @@ class APRContext:
         with torch.cuda.device(self.device):
             call("acf_apr_shard_items", self._ptr, 1, delta.data_ptr(), delta.shape[0], _stream_ptr(self.device))
 
+    def shard_items_mapped(self, dir_: int, buf: torch.Tensor, rows: torch.Tensor) -> None:
+        """Working-set entry w <-> row rows[w] of buf, for w < rows.numel(): dir 0
+        writes the item slots' partial sums there, dir 1 takes the owners'
+        deltas from there (the split step's exchange rows)."""
+        _require(buf, "buf", torch.float32, self.device, 2)
+        _require(rows, "rows", torch.int64, self.device, 1)
+        with torch.cuda.device(self.device):
+            call("acf_apr_shard_items_mapped", self._ptr, int(dir_), buf.data_ptr(), rows.data_ptr(), rows.numel(),
+                 _stream_ptr(self.device))
+
     def step_errors(self) -> int:
         """Read and clear the step error words (bit 0: an overlapped step gave up
         waiting for a row, or an unverified streamed call gave up -- set_failsafe)."""

@@ -232,6 +232,13 @@ int acf_apr_shard_pass(acf_apr_ctx* ctx, const acf_apr_tables* tables, const acf
  * their delta rows (the owners' deltas, before pass 1). */
 int acf_apr_shard_items(acf_apr_ctx* ctx, int32_t dir, float* buf, int64_t n_items, void* stream);
 
+/* As acf_apr_shard_items, with working-set entry w at row map[w] of buf (int64
+ * row indices): the split step moves the item partial sums and deltas straight
+ * between the slots and its fixed-layout exchange rows (distributed.py "Static
+ * step layout"), with no gather or scatter pass of its own. */
+int acf_apr_shard_items_mapped(acf_apr_ctx* ctx, int32_t dir, float* buf, const int64_t* map, int64_t n_items,
+                               void* stream);
+
 /* Owner side, per owned row s of the step: the partial rows recv[pos[p]] for p
  * in [seg[s], seg[s+1]) (requester order) are summed in that order.
  * reduce_delta (APR.py:183-191): G0[s] = the sum; reply[pos[p]] = eps *

@@ -67,11 +67,12 @@ class OracleShardLocal:
         x = ((p * qi).astype(f32).sum(1, dtype=f32) - (p * qj).astype(f32).sum(1, dtype=f32)).astype(f32)
         return p, qi, qj, x
 
-    def clean(self, hp, out):
+    def clean(self, hp, out, rows):
+        """working-set entry w's partial clean sum -> out[rows[w]]"""
         sh, d = self.sh, self.sh.d
         p, qi, qj, x = self._rows()
         g = _bpr_coef(x, hp.clip_lo, hp.clip_hi)
-        GP, GQ = _sums(self.u, self.wi, self.wj, p, qi, qj, g, sh.P.shape[0], out.shape[0], d)
+        GP, GQ = _sums(self.u, self.wi, self.wj, p, qi, qj, g, sh.P.shape[0], rows.numel(), d)
         self.GPc, self.users, self.p0 = GP, np.unique(self.u), p
         if hp.adver:  # the delta follows the clean loss only (APR.py:180-191)
             self.dP = np.zeros_like(GP) if hp.zero_delta else (_l2_normalize(GP) * f32(hp.eps)).astype(f32)
@@ -79,26 +80,27 @@ class OracleShardLocal:
             if hp.reg:
                 self._reg(GP, p, hp)
             _adagrad(sh.P.numpy(), sh.accP.numpy(), self.users, GP, hp.lr)
-        out.copy_(__import__("torch").from_numpy(GQ))
+        out.numpy()[rows.numpy()] = GQ
 
     def _reg(self, GP, p, hp):
         coef = f32(2.0 * hp.reg / (self.sh.B * self.sh.d)) * f32(2 if hp.adver else 1)
         for b in range(len(self.u)):
             GP[self.u[b]] = GP[self.u[b]] + (coef * p[b]).astype(f32)
 
-    def set_item_delta(self, delta):
-        self.dQ = delta.numpy().copy()
+    def set_item_delta(self, src, rows):
+        """the owners' delta of working-set entry w <- src[rows[w]]"""
+        self.dQ = src.numpy()[rows.numpy()].copy()
 
-    def adv(self, hp, out):
+    def adv(self, hp, out, rows):
         sh, d = self.sh, self.sh.d
         p, qi, qj, x = self._rows(self.dP, self.dQ)
         g = _bpr_coef(x, hp.clip_lo, hp.clip_hi)
-        GP, GQ = _sums(self.u, self.wi, self.wj, p, qi, qj, g, sh.P.shape[0], out.shape[0], d)
+        GP, GQ = _sums(self.u, self.wi, self.wj, p, qi, qj, g, sh.P.shape[0], rows.numel(), d)
         G = (self.GPc + f32(hp.reg_adv) * GP).astype(f32)
         if hp.reg:
             self._reg(G, self.p0, hp)
         _adagrad(sh.P.numpy(), sh.accP.numpy(), self.users, G, hp.lr)
-        out.copy_(__import__("torch").from_numpy(GQ))
+        out.numpy()[rows.numpy()] = GQ
 
     # -- owner side ------------------------------------------------------------------
     @staticmethod

@@ -115,6 +115,34 @@ def test_sharded_graph_replay_bit_identical(ops, dev, exchange, adver, reg, rout
         assert torch.equal(g, e), n
 
 
+@pytest.mark.parametrize("adver", [1, 0])
+def test_shard_plan_small_matches_sort_plan(ops, dev, adver):
+    """The one-workgroup shard plan (k_shard_plan, one batch of B <= 1,024) against
+    the device-wide sort plan (plan mode 1) in shard mode: the same bits after 6
+    split steps on pinterest-20-shaped data, with a hot item in every batch (hot
+    lists, pieces) and i == j triplets."""
+    D_ = importlib.import_module(PKG + ".distributed")
+    U1, I1, d, B, nb = 55_188, 9_917, 64, 512, 6
+    P, Q, u, i, j = _problem(11 + adver, U1, I1, d, B, nb)
+    i[::5] = 17
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    outs = []
+    try:
+        uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
+        for mode in (0, 1):
+            sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, graph=False)
+            sh.local.ctx.set_plan_mode(mode)
+            sh.train(uu, ii, jj, ops.StepHParams(adver=adver), chunk=3)
+            torch.cuda.synchronize(dev)
+            assert sh.step_errors() == 0
+            outs.append(sh.full_tables())
+    finally:
+        dist.destroy_process_group()
+    for a, b, n in zip(outs[0], outs[1], ("P", "Q", "accP", "accQ")):
+        assert torch.equal(a, b), n
+
+
 # two-rank problems: (U1, I1, d, B, nb, zipf, chunk); "pinterest" is BASELINE configs[2]'s
 # shape (the reference's global batch of 512 split over the ranks)
 SHAPES2 = {"zipf": (20_000, 9_000, 64, 4096, 4, 1.2, 3), "pinterest": (55_188, 9_917, 64, 512, 10, None, 4)}
