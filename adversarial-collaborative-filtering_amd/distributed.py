@@ -336,13 +336,16 @@ class ShardedAPR:
         # the requests of the whole chunk, owner-major, in one exchange
         order = torch.argsort((wown * T + wstep) * I1 + wid)
         req = (wid // G)[order]
-        # split sizes (T per owner) + this rank's error flags, to every rank in one exchange
-        send = torch.cat([cnt.t(), bad.reshape(1, 1).expand(G, 1)], 1).contiguous()
+        # split sizes (T per owner) + this rank's error flags + its largest request count
+        # (the exchange blocks' C must be the same on every rank), to every rank in one exchange
+        send = torch.cat([cnt.t(), bad.reshape(1, 1).expand(G, 1), cnt.max().reshape(1, 1).expand(G, 1)],
+                         1).contiguous()
         recv = torch.empty_like(send)
-        self._a2a(recv.view(-1), send.view(-1), [T + 1] * G, [T + 1] * G)
+        self._a2a(recv.view(-1), send.view(-1), [T + 2] * G, [T + 2] * G)
         rc = recv[:, :T]
-        host = torch.cat([cnt.reshape(-1), rc.reshape(-1), nloc, recv[:, T]]).cpu().numpy()  # one sync
+        host = torch.cat([cnt.reshape(-1), rc.reshape(-1), nloc, recv[:, T + 1], recv[:, T]]).cpu().numpy()  # one sync
         flags = host[-G:]
+        cmax = int(host[-2 * G: -G].max())  # the largest request count of any rank and step
         if flags.any():
             who = [o for o in range(G) if flags[o]]
             if np.bitwise_or.reduce(flags) & 1:
@@ -350,8 +353,8 @@ class ShardedAPR:
             raise ValueError(f"train_routed: a triplet of another rank's user (rank(s) {who})")
         c.cnt = host[: T * G].reshape(T, G)           # my requests per (step, owner)
         c.rc = host[T * G: 2 * T * G].reshape(G, T)   # requests to me per (requester, step)
-        c.nloc = host[2 * T * G: -G]
-        self._ensure(T, int(max(c.cnt.max(initial=0), c.rc.max(initial=0), 1)))
+        c.nloc = host[2 * T * G: -2 * G]
+        self._ensure(T, max(cmax, 1))
         bf, C, M = self._buf, self._C, self.max_items
         GC = G * C
         # local triplets at a fixed stride of b_max per step

@@ -131,3 +131,53 @@ def test_bad_triplet_on_one_rank_raises_on_every_rank(tmp_path, kind, want):
     for r in range(world):
         with open(os.path.join(tmp_path, f"res{r}.txt")) as f:
             assert f.read() == want, f"rank {r}"
+
+
+def _skew_worker(rank, world, port, out_dir):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from apr_oracle import HParams
+    from shard_oracle import OracleShardLocal
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D_ = importlib.import_module(PKG + ".distributed")
+    P, Q, u, i, j = _skew_problem()
+    sh = D_.ShardedAPR(SK_U1, SK_I1, D, SK_B, init_P=P, init_Q=Q, local=OracleShardLocal)
+    sh.train(u, i, j, HParams(adver=1), chunk=2)
+    full = sh.full_tables()
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "skew.npz"), *[t.numpy() for t in full])
+    np.save(os.path.join(out_dir, f"C{rank}.npy"), np.array([sh._C]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+SK_U1, SK_I1, SK_B, SK_NB = 64, 400, 256, 4
+
+
+def _skew_problem():
+    rng = np.random.default_rng(21)
+    P = (rng.standard_normal((SK_U1, D)) * 0.2).astype(np.float32)
+    Q = (rng.standard_normal((SK_I1, D)) * 0.2).astype(np.float32)
+    u = rng.integers(0, SK_U1, SK_NB * SK_B).astype(np.int32)
+    u[rng.random(u.size) < 0.9] &= ~1  # 90% of the triplets on rank 0's (even) users
+    i = rng.integers(0, SK_I1, SK_NB * SK_B).astype(np.int32)
+    j = rng.integers(0, SK_I1, SK_NB * SK_B).astype(np.int32)
+    return P, Q, u, i, j
+
+
+def test_split_step_skewed_ranks_share_block_size(tmp_path, oracle, fp32_parity):
+    """One rank requests many more item rows per step than the other: the fixed
+    exchange blocks (distributed.py "Static step layout") must still have ONE size on
+    every rank, or the equal-split all_to_alls would disagree."""
+    from apr_oracle import HParams
+    world = 2
+    mp.spawn(_skew_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    Cs = [int(np.load(os.path.join(tmp_path, f"C{r}.npy"))[0]) for r in range(world)]
+    assert Cs[0] == Cs[1] and Cs[0] > 64, Cs
+    got = np.load(os.path.join(tmp_path, "skew.npz"))
+    P, Q, u, i, j = _skew_problem()
+    aP, aQ = np.full_like(P, 0.1), np.full_like(Q, 0.1)
+    oracle.apr_train(P, Q, aP, aQ, u, i, j, SK_B, HParams(adver=1))
+    for k, (want, n) in enumerate(zip((P, Q, aP, aQ), ("P", "Q", "accP", "accQ"))):
+        fp32_parity(got[f"arr_{k}"], want, n)
