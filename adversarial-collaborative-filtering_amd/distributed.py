@@ -64,6 +64,7 @@ from __future__ import annotations
 
 import os
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -126,7 +127,7 @@ class _Buffers:
 
 
 def _hp_key(hp) -> tuple:
-    return tuple(sorted((k, v) for k, v in vars(hp).items() if isinstance(v, (int, float, bool))))
+    return tuple(sorted((k, v) for k, v in vars(hp).items() if isinstance(v, (int, float, bool, str))))
 
 
 class _SegmentRecorder:
@@ -151,6 +152,16 @@ class _SegmentRecorder:
         self._g.capture_end()
         self.segs.append((self._g, None))
         self._g = None
+
+    def abort(self):
+        """End a capture that failed half-way (the segments are dropped)."""
+        if self._g is not None:
+            try:
+                self._g.capture_end()
+            except RuntimeError:
+                pass
+            self._g = None
+        self.segs = []
 
     def replay(self):
         for g, fn in self.segs:
@@ -466,7 +477,11 @@ class ShardedAPR:
         for t in range(T):
             self._step(t, int(c.nloc[t]), hp, c.has_count)
         if key is not None:  # capture for the next chunk of this shape (capturing runs nothing)
-            self._graphs[key] = self._capture(T, min(bs), hp, c.has_count)
+            try:
+                self._graphs[key] = self._capture(T, min(bs), hp, c.has_count)
+            except RuntimeError as e:  # the chunk ran eagerly; later chunks stay eager
+                warnings.warn(f"ShardedAPR: step capture failed ({e}); continuing without graphs")
+                self.graph = False
 
     def _capture(self, T: int, b: int, hp, count: bool) -> _SegmentRecorder:
         if self._pool is None:
@@ -483,6 +498,9 @@ class ShardedAPR:
                 for t in range(T):
                     self._step(t, b, hp, count)
                 rec.end()
+            except BaseException:
+                rec.abort()
+                raise
             finally:
                 self._rec = None
         main.wait_stream(self._cap_stream)
