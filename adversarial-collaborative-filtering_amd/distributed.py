@@ -335,7 +335,11 @@ class ShardedAPR:
         ist = torch.cat([st, st])
         # working set per step: unique items, ordered by (owner, id) so that each
         # owner's rows are one contiguous block
-        uk, inv = torch.unique((ist * G + items % G) * I1 + items, return_inverse=True)
+        # 32-bit sort keys whenever the key range fits (half the radix passes of 64-bit ones)
+        k32 = T * G * I1 < 2 ** 31
+        wkey = (ist * G + items % G) * I1 + items
+        uk, inv = torch.unique(wkey.to(torch.int32) if k32 else wkey, return_inverse=True)
+        uk = uk.long()
         wstep, wown, wid = uk // (G * I1), (uk // I1) % G, uk % I1
         cnt = torch.bincount(wstep * G + wown, minlength=T * G).view(T, G)
         nloc = torch.bincount(st, minlength=T)
@@ -345,8 +349,11 @@ class ShardedAPR:
         wk = torch.arange(uk.numel(), device=dev) - wstart[wstep]        # entry inside its step's set
         kblk = wk - (torch.cumsum(cnt, 1) - cnt)[wstep, wown]             # entry inside its owner block
         # the requests of the whole chunk, owner-major, in one exchange
-        order = torch.argsort((wown * T + wstep) * I1 + wid)
-        req = (wid // G)[order]
+        if G == 1:  # the working sets are already in (owner, step, id) order
+            req = wid
+        else:
+            okey = (wown * T + wstep) * I1 + wid
+            req = (wid // G)[torch.argsort(okey.to(torch.int32) if k32 else okey)]
         # split sizes (T per owner) + this rank's error flags + its largest request count
         # (the exchange blocks' C must be the same on every rank), to every rank in one exchange
         send = torch.cat([cnt.t(), bad.reshape(1, 1).expand(G, 1), cnt.max().reshape(1, 1).expand(G, 1)],
@@ -393,7 +400,8 @@ class ShardedAPR:
             torch.gather(bf.srv[:T], 1, bf.wsrc[:T], out=bf.wq[:T])
         # owner reduction segments: per (step, row), positions in requester order
         key = (t_e * (ni + 1) + rows) * G + o_e
-        skey, sp = torch.sort(key)
+        skey, sp = torch.sort(key.to(torch.int32) if T * (ni + 1) * G < 2 ** 31 else key)
+        skey = skey.long()
         srow = skey // G
         head = torch.ones_like(srow, dtype=torch.bool)
         if srow.numel() > 1:
