@@ -118,7 +118,7 @@ class HipLocal:
 
 
 class _Chunk:
-    """Host copies of one chunk's counts (the device maps live in ShardedAPR._buf)."""
+    """Host copies of one chunk's counts (the device maps live in ShardedAPR._maps[mset])."""
 
 
 class _Buffers:
@@ -223,6 +223,7 @@ class ShardedAPR:
         self._C = 0   # per-peer block rows of the exchange buffers (only grows)
         self._T = 0   # steps the per-chunk maps hold
         self._buf = None
+        self._maps = None
         self._graphs = {}
         self._pool = None
         self._cap_stream = None
@@ -234,6 +235,8 @@ class ShardedAPR:
     def _ensure(self, T: int, C: int) -> None:
         if C <= self._C and T <= self._T:
             return
+        if self.device.type == "cuda":  # the old buffers may still be in use by enqueued steps
+            torch.cuda.synchronize(self.device)
         if C > self._C:  # headroom: chunk-to-chunk growth should not re-capture
             self._C = max(64, -(-int(C * 1.0625) // 64) * 64)
         self._T = max(self._T, T)
@@ -244,18 +247,30 @@ class ShardedAPR:
         li = dict(dtype=torch.int64, device=dev)
         ii = dict(dtype=torch.int32, device=dev)
         fl = dict(dtype=torch.float32, device=dev)
-        b = _Buffers()
-        b.u_rows = torch.zeros(T, self.b_max, **ii)
-        b.wi = torch.zeros(T, self.b_max, **ii)
-        b.wj = torch.zeros(T, self.b_max, **ii)
-        b.wsrc = torch.empty(T, M, **li)        # working-set entry -> its row of the exchange blocks
-        b.srv = torch.empty(T, GC + 1, **li)    # exchange row -> owned Q row (trash: ni)
-        b.wq = torch.empty(T, M, **li) if G == 1 else None  # world 1: working-set entry -> Q row
-        b.wslot = torch.zeros(T, M, **li) if self.item_exchange == "allgather" else None
-        b.seg = torch.empty(T, GC + 1, **ii)
-        b.pos = torch.zeros(T, GC, **ii)
-        b.own = torch.empty(T, GC, **ii)
-        b.count = torch.zeros(T, GC, **ii)
+        maps = []
+        for _ in range(2):  # chunk k routes into set k % 2 while chunk k - 1 runs on the other
+            m = _Buffers()
+            m.u_rows = torch.zeros(T, self.b_max, **ii)
+            m.wi = torch.zeros(T, self.b_max, **ii)
+            m.wj = torch.zeros(T, self.b_max, **ii)
+            m.wsrc = torch.empty(T, M, **li)        # working-set entry -> its row of the exchange blocks
+            m.srv = torch.empty(T, GC + 1, **li)    # exchange row -> owned Q row (trash: ni)
+            m.wq = torch.empty(T, M, **li) if G == 1 else None  # world 1: working-set entry -> Q row
+            m.wslot = torch.zeros(T, M, **li) if self.item_exchange == "allgather" else None
+            # seg / own / count: flat storage with one dump element at the end (routing
+            # scatters the entries it does not want there instead of compacting)
+            m.seg_flat = torch.empty(T * (GC + 1) + 1, **ii)
+            m.seg = m.seg_flat[:-1].view(T, GC + 1)
+            m.dump_at = T * (GC + 1)
+            m.pos = torch.zeros(T, GC, **ii)
+            m.own_flat = torch.empty(T * GC + 1, **ii)
+            m.own = m.own_flat[:-1].view(T, GC)
+            m.dump_own = T * GC
+            m.count_flat = torch.zeros(T * GC + 1, **ii)
+            m.count = m.count_flat[:-1].view(T, GC)
+            maps.append(m)
+        self._maps = maps
+        b = _Buffers()  # per-step exchange scratch (steps run one after another on one stream)
         b.S1 = torch.empty(GC + 1, d, **fl)
         b.R1 = torch.empty(GC + 1, d, **fl)
         b.S = torch.zeros(GC + 1, d, **fl)
@@ -309,7 +324,7 @@ class ShardedAPR:
         return self._qall
 
     # -- routing (one chunk of T global batches) -----------------------------------
-    def _route(self, u, i, j, T: int) -> _Chunk:
+    def _route(self, u, i, j, T: int, mset: int = 0) -> _Chunk:
         G, r, I1, ni = self.G, self.rank, self.I1, self.ni
         B = self.b_max if self.routed else self.B  # triplets per batch in the stream given
         dev = self.device
@@ -327,33 +342,48 @@ class ShardedAPR:
         u, i, j = u.clamp(0, self.U1 - 1), i.clamp(0, I1 - 1), j.clamp(0, I1 - 1)
         c = _Chunk()
         c.T = T
+        c.mset = mset
         # this rank's triplets, stream order
         sel = torch.arange(u.numel(), device=dev) if self.routed else torch.nonzero(u % G == r).squeeze(1)
         st = sel // B
         n = sel.numel()
         items = torch.cat([i[sel], j[sel]])
         ist = torch.cat([st, st])
-        # working set per step: unique items, ordered by (owner, id) so that each
-        # owner's rows are one contiguous block
-        # 32-bit sort keys whenever the key range fits (half the radix passes of 64-bit ones)
+        # Working set per step: the unique items, ordered by (owner, id) so that each
+        # owner's rows are one contiguous block.  No step below waits on the device
+        # before the one host copy of the counts: a unique is a sort + head flags,
+        # counts are scatter-adds, and arrays keep their full length (entries past
+        # the U uniques are don't-cares, sliced off once U is known on the host).
+        # 32-bit sort keys whenever the key range fits (half the radix passes).
         k32 = T * G * I1 < 2 ** 31
         wkey = (ist * G + items % G) * I1 + items
-        uk, inv = torch.unique(wkey.to(torch.int32) if k32 else wkey, return_inverse=True)
-        uk = uk.long()
+        sk, perm = torch.sort(wkey.to(torch.int32) if k32 else wkey)
+        sk = sk.long()
+        hd = torch.ones_like(sk, dtype=torch.bool)
+        if sk.numel() > 1:
+            hd[1:] = sk[1:] != sk[:-1]
+        uid = torch.cumsum(hd, 0) - 1                       # unique index of each sorted occurrence
+        inv = torch.empty_like(uid)
+        inv[perm] = uid                                     # occurrence -> unique index
+        uk = torch.zeros_like(sk).scatter_(0, uid, sk)      # unique keys first (same value per segment)
+        valid = torch.arange(sk.numel(), device=dev) <= uid[-1:]
         wstep, wown, wid = uk // (G * I1), (uk // I1) % G, uk % I1
-        cnt = torch.bincount(wstep * G + wown, minlength=T * G).view(T, G)
-        nloc = torch.bincount(st, minlength=T)
+        ones = torch.ones_like(wstep)
+        cnt = torch.zeros(T * G + 1, dtype=torch.long, device=dev).scatter_add_(
+            0, torch.where(valid, wstep * G + wown, T * G), ones)[: T * G].view(T, G)
+        nloc = (torch.full((T,), B, dtype=torch.long, device=dev) if self.routed else
+                torch.zeros(T, dtype=torch.long, device=dev).scatter_add_(0, st, torch.ones_like(st)))
         nW = cnt.sum(1)
         wstart = torch.cumsum(nW, 0) - nW
         widx = (inv - wstart[ist]).to(torch.int32)
         wk = torch.arange(uk.numel(), device=dev) - wstart[wstep]        # entry inside its step's set
         kblk = wk - (torch.cumsum(cnt, 1) - cnt)[wstep, wown]             # entry inside its owner block
-        # the requests of the whole chunk, owner-major, in one exchange
+        # the requests of the whole chunk, owner-major (valid entries first), in one exchange
         if G == 1:  # the working sets are already in (owner, step, id) order
             req = wid
         else:
-            okey = (wown * T + wstep) * I1 + wid
-            req = (wid // G)[torch.argsort(okey.to(torch.int32) if k32 else okey)]
+            okey = torch.where(valid, (wown * T + wstep) * I1 + wid, T * G * I1)
+            req = (wid // G)[torch.argsort(okey.to(torch.int32) if k32 and T * G * I1 < 2 ** 31 - 1 else okey)]
         # split sizes (T per owner) + this rank's error flags + its largest request count
         # (the exchange blocks' C must be the same on every rank), to every rank in one exchange
         send = torch.cat([cnt.t(), bad.reshape(1, 1).expand(G, 1), cnt.max().reshape(1, 1).expand(G, 1)],
@@ -372,8 +402,9 @@ class ShardedAPR:
         c.cnt = host[: T * G].reshape(T, G)           # my requests per (step, owner)
         c.rc = host[T * G: 2 * T * G].reshape(G, T)   # requests to me per (requester, step)
         c.nloc = host[2 * T * G: -2 * G]
+        U = int(c.cnt.sum())                          # my working-set entries over the chunk
         self._ensure(T, max(cmax, 1))
-        bf, C, M = self._buf, self._C, self.max_items
+        bf, C, M = self._maps[mset], self._C, self.max_items
         GC = G * C
         # local triplets at a fixed stride of b_max per step
         lo = torch.cumsum(nloc, 0) - nloc
@@ -382,23 +413,30 @@ class ShardedAPR:
         bf.wi[:T].view(-1)[slot] = widx[:n]
         bf.wj[:T].view(-1)[slot] = widx[n:]
         # requester maps: working-set entry <-> row of the exchange blocks
+        wstep, wown, wid, wk, kblk = wstep[:U], wown[:U], wid[:U], wk[:U], kblk[:U]
         xrow = wown * C + kblk
         bf.wsrc[:T].fill_(GC)
         bf.wsrc[:T].view(-1)[wstep * M + wk] = xrow
         if bf.wslot is not None:  # where each working-set row sits in the gathered table
             bf.wslot[:T].view(-1)[wstep * M + wk] = (wid % G) * self._qcap + wid // G if G > 1 else wid
         # rows I serve, received in (requester o, step t, k) order
-        rows = torch.empty(int(c.rc.sum()), dtype=req.dtype, device=dev)
-        self._a2a(rows, req, c.rc.sum(1).tolist(), c.cnt.sum(0).tolist())
-        blk_len = torch.as_tensor(c.rc.reshape(-1), device=dev)        # block (o, t) -> rows
-        blk = torch.repeat_interleave(torch.arange(G * T, device=dev), blk_len, output_size=rows.numel())
+        Rn = int(c.rc.sum())
+        rows = torch.empty(Rn, dtype=req.dtype, device=dev)
+        self._a2a(rows, req[:U], c.rc.sum(1).tolist(), c.cnt.sum(0).tolist())
+        Rt = c.rc.sum(0)                                              # rows I serve per step (host)
+        Rstart = np.concatenate([[0], np.cumsum(Rt)])
+        # the host-side counts this routing needs on the device, in ONE upload
+        meta = torch.as_tensor(np.concatenate([c.rc.reshape(-1), Rstart[:-1], Rt]).astype(np.int64), device=dev)
+        blk_len, rstart_d, rt_d = meta[: G * T], meta[G * T: G * T + T], meta[G * T + T:]
+        blk = torch.repeat_interleave(torch.arange(G * T, device=dev), blk_len, output_size=Rn)
         o_e, t_e = blk // T, blk % T
-        k_e = torch.arange(rows.numel(), device=dev) - (torch.cumsum(blk_len, 0) - blk_len)[blk]
+        k_e = torch.arange(Rn, device=dev) - (torch.cumsum(blk_len, 0) - blk_len)[blk]
         bf.srv[:T].fill_(ni)
         bf.srv[:T].view(-1)[t_e * (GC + 1) + o_e * C + k_e] = rows
         if bf.wq is not None:  # world 1: E1 in one gather (the exchange is the identity)
             torch.gather(bf.srv[:T], 1, bf.wsrc[:T], out=bf.wq[:T])
-        # owner reduction segments: per (step, row), positions in requester order
+        # owner reduction segments: per (step, row), positions in requester order;
+        # non-head entries write to the maps' dump element (no compaction, no sync)
         key = (t_e * (ni + 1) + rows) * G + o_e
         skey, sp = torch.sort(key.to(torch.int32) if T * (ni + 1) * G < 2 ** 31 else key)
         skey = skey.long()
@@ -407,20 +445,21 @@ class ShardedAPR:
         if srow.numel() > 1:
             head[1:] = srow[1:] != srow[:-1]
         ts = t_e[sp]
-        Rt = torch.bincount(t_e, minlength=T)
-        nseg = torch.bincount(ts[head], minlength=T)
-        p_in = torch.arange(rows.numel(), device=dev) - (torch.cumsum(Rt, 0) - Rt)[ts]
-        s_in = torch.cumsum(head.long(), 0) - 1 - (torch.cumsum(nseg, 0) - nseg)[ts]
+        hcum = torch.zeros(Rn + 1, dtype=torch.long, device=dev)
+        hcum[1:] = torch.cumsum(head.long(), 0)                       # heads before each position
+        segstart = hcum[rstart_d]                                     # first segment of each step
+        p_in = torch.arange(Rn, device=dev) - rstart_d[ts]
+        s_in = hcum[1:] - 1 - segstart[ts]
         bf.pos[:T].view(-1)[ts * GC + p_in] = (o_e * C + k_e)[sp].to(torch.int32)
-        bf.seg[:T].copy_(Rt.to(torch.int32)[:, None].expand(T, GC + 1))
-        hs = ts[head]
-        bf.seg[:T].view(-1)[hs * (GC + 1) + s_in[head]] = p_in[head].to(torch.int32)
+        bf.seg[:T].copy_(rt_d.to(torch.int32)[:, None].expand(T, GC + 1))
+        dump = bf.dump_at
+        bf.seg_flat[torch.where(head, ts * (GC + 1) + s_in, dump)] = p_in.to(torch.int32)
         bf.own[:T].fill_(ni)
-        c.own_rows = (srow[head] % (ni + 1))
-        c.own_flat = hs * GC + s_in[head]
-        bf.own[:T].view(-1)[c.own_flat] = c.own_rows.to(torch.int32)
+        c.own_rows = srow % (ni + 1)
+        c.own_flat = torch.where(head, ts * GC + s_in, bf.dump_own)
+        bf.own_flat[c.own_flat] = c.own_rows.to(torch.int32)
         c.has_count = False
-        c.R = c.rc.sum(0)                                   # rows I serve per step
+        c.R = Rt                                          # rows I serve per step
         c.nW = c.cnt.sum(1)
         self._chunk_items = (i, j)
         return c
@@ -431,35 +470,38 @@ class ShardedAPR:
         G, B, T = self.G, self.B, c.T
         items = torch.cat([i, j])
         st = torch.cat([torch.arange(T * B, device=self.device) // B] * 2)
-        mine = items % G == self.rank
         nrow = self.ni + 1
-        cnt = torch.bincount(st[mine] * nrow + items[mine] // G, minlength=T * nrow)
-        seg_step = c.own_flat // (G * self._C)
-        cf = self._buf.count[:T]
-        cf.zero_()
-        cf.view(-1)[c.own_flat] = cnt[seg_step * nrow + c.own_rows].to(torch.int32)
+        # other ranks' items count into the trash row ni of their step (never read)
+        local = torch.where(items % G == self.rank, items // G, self.ni)
+        cnt = torch.zeros(T * nrow, dtype=torch.long, device=self.device).scatter_add_(
+            0, st * nrow + local, torch.ones_like(st))
+        m = self._maps[c.mset]
+        seg_step = torch.clamp(c.own_flat // (G * self._C), max=T - 1)
+        m.count[:T].zero_()
+        m.count_flat[c.own_flat] = cnt[seg_step * nrow + c.own_rows].to(torch.int32)
         c.has_count = True
 
-    # -- one step (fixed shapes: every size is the buffers') -----------------------
-    def _step(self, t: int, b: int, hp, count: bool) -> None:
+    # -- one step ------------------------------------------------------------------
+    def _step(self, m, t: int, b: int, hp, count: bool) -> None:
+        """Step t of a chunk routed into map set m (fixed shapes: every size is the buffers')."""
         bf = self._buf
         # E1: current item rows of my working set from their owners
         if self.item_exchange == "allgather":
-            torch.index_select(self._gather_q(), 0, bf.wslot[t], out=self.Qc)
-        elif bf.wq is not None:
-            torch.index_select(self._Qst, 0, bf.wq[t], out=self.Qc)
+            torch.index_select(self._gather_q(), 0, m.wslot[t], out=self.Qc)
+        elif m.wq is not None:
+            torch.index_select(self._Qst, 0, m.wq[t], out=self.Qc)
         else:
-            torch.index_select(self._Qst, 0, bf.srv[t], out=bf.S1)
-            torch.index_select(self._exchange(bf.R1, bf.S1), 0, bf.wsrc[t], out=self.Qc)
-        rows = bf.wsrc[t, : 2 * b]  # working-set entry -> its exchange row
+            torch.index_select(self._Qst, 0, m.srv[t], out=bf.S1)
+            torch.index_select(self._exchange(bf.R1, bf.S1), 0, m.wsrc[t], out=self.Qc)
+        rows = m.wsrc[t, : 2 * b]  # working-set entry -> its exchange row
         if b:
-            self.local.plan(bf.u_rows[t, :b], bf.wi[t, :b], bf.wj[t, :b])
+            self.local.plan(m.u_rows[t, :b], m.wi[t, :b], m.wj[t, :b])
             self.local.clean(hp, bf.S, rows)
         # E2: partial clean item sums -> owners
         recv = self._exchange(bf.R, bf.S)
-        cnt = bf.count[t] if count else None
+        cnt = m.count[t] if count else None
         if hp.adver:
-            self.local.reduce_delta(hp, recv, bf.seg[t], bf.pos[t], bf.G0, bf.reply)
+            self.local.reduce_delta(hp, recv, m.seg[t], m.pos[t], bf.G0, bf.reply)
             # E3: deltas -> requesters
             dl = self._exchange(bf.R3, bf.reply)
             if b:
@@ -467,31 +509,32 @@ class ShardedAPR:
                 self.local.adv(hp, bf.S, rows)
             # E4: partial adversarial item sums -> owners, who apply Adagrad
             recv = self._exchange(bf.R, bf.S)
-            self.local.reduce_apply(hp, recv, bf.seg[t], bf.pos[t], bf.G0, bf.own[t], cnt)
+            self.local.reduce_apply(hp, recv, m.seg[t], m.pos[t], bf.G0, m.own[t], cnt)
         else:
-            self.local.reduce_apply(hp, recv, bf.seg[t], bf.pos[t], None, bf.own[t], cnt)
+            self.local.reduce_apply(hp, recv, m.seg[t], m.pos[t], None, m.own[t], cnt)
 
     def _run(self, c: _Chunk, hp) -> None:
         T = c.T
         bs = set(int(x) for x in c.nloc)
         key = None
         if self.graph and len(bs) == 1 and min(bs) > 0:
-            key = (T, min(bs), self._C, c.has_count, _hp_key(hp))
+            key = (c.mset, T, min(bs), self._C, c.has_count, _hp_key(hp))
         rec = self._graphs.get(key) if key is not None else None
         if rec is not None:
             rec.replay()
             self.stats["graph_replays"] += 1
             return
+        m = self._maps[c.mset]
         for t in range(T):
-            self._step(t, int(c.nloc[t]), hp, c.has_count)
+            self._step(m, t, int(c.nloc[t]), hp, c.has_count)
         if key is not None:  # capture for the next chunk of this shape (capturing runs nothing)
             try:
-                self._graphs[key] = self._capture(T, min(bs), hp, c.has_count)
+                self._graphs[key] = self._capture(m, T, min(bs), hp, c.has_count)
             except RuntimeError as e:  # the chunk ran eagerly; later chunks stay eager
                 warnings.warn(f"ShardedAPR: step capture failed ({e}); continuing without graphs")
                 self.graph = False
 
-    def _capture(self, T: int, b: int, hp, count: bool) -> _SegmentRecorder:
+    def _capture(self, m, T: int, b: int, hp, count: bool) -> _SegmentRecorder:
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
             self._cap_stream = torch.cuda.Stream(self.device)
@@ -504,7 +547,7 @@ class ShardedAPR:
             try:
                 rec.begin()
                 for t in range(T):
-                    self._step(t, b, hp, count)
+                    self._step(m, t, b, hp, count)
                 rec.end()
             except BaseException:
                 rec.abort()
@@ -518,26 +561,64 @@ class ShardedAPR:
     def train(self, u, i, j, hp, chunk: int = 64) -> int:
         """Train consecutive global batches of the stream (u, i, j), identical on
         every rank (length a multiple of the batch size; train_routed: this rank's
-        triplets only, local_batch per batch).  Returns the batches run."""
+        triplets only, local_batch per batch).  Returns the batches run.
+
+        On a GPU the routing of chunk k + 1 runs on a side stream while chunk k's
+        steps run on the caller's stream (the two chunks use the two map sets)."""
         bs = self.b_max if self.routed else self.B
         n = len(u) // bs
-        for c0 in range(0, n, chunk):
-            T = min(chunk, n - c0)
+        spans = [(c0, min(chunk, n - c0)) for c0 in range(0, n, chunk)]
+        cuda = self.device.type == "cuda"
+        main = torch.cuda.current_stream(self.device) if cuda else None
+        if cuda and getattr(self, "_route_stream", None) is None:
+            self._route_stream = torch.cuda.Stream(self.device)
+        side = self._route_stream if cuda else None
+        done = [None, None]  # event after the last chunk enqueued on map set k % 2
+
+        def route(k):
+            c0, T = spans[k]
             s = slice(c0 * bs, (c0 + T) * bs)
             t0 = time.perf_counter()
-            c = self._route(u[s], i[s], j[s], T)
-            if hp.reg:  # the owners count their rows in the GLOBAL batch
-                if self.routed:
-                    raise ValueError("reg != 0 needs the global stream on every rank (train, not train_routed)")
-                self._counts(c, *self._chunk_items)
+            if cuda:
+                if k == 0:  # the triplets come from the caller's stream
+                    side.wait_stream(main)
+                if done[k % 2] is not None:  # the set's previous chunk has run
+                    side.wait_event(done[k % 2])
+                with torch.cuda.stream(side):
+                    c = self._route(u[s], i[s], j[s], T, k % 2)
+                    if hp.reg:
+                        self._reg_counts(c)
+                    c.ready = torch.cuda.Event()
+                    c.ready.record(side)
+            else:
+                c = self._route(u[s], i[s], j[s], T, k % 2)
+                if hp.reg:
+                    self._reg_counts(c)
             self.stats["route_s"] += time.perf_counter() - t0
+            return c
+
+        c = route(0) if spans else None
+        for k in range(len(spans)):
+            if cuda:
+                main.wait_event(c.ready)
             self._run(c, hp)
+            if cuda:
+                done[k % 2] = torch.cuda.Event()
+                done[k % 2].record(main)
             st = self.stats
-            st["steps"] += T
+            st["steps"] += c.T
             st["items_requested"] += int(c.nW.sum())
             st["rows_served"] += int(c.R.sum())
             st["triplets"] += int(c.nloc.sum())
+            if k + 1 < len(spans):
+                c = route(k + 1)
         return n
+
+    def _reg_counts(self, c: _Chunk) -> None:
+        # the owners count their rows in the GLOBAL batch
+        if self.routed:
+            raise ValueError("reg != 0 needs the global stream on every rank (train, not train_routed)")
+        self._counts(c, *self._chunk_items)
 
     def train_routed(self, u, i, j, hp, chunk: int = 64) -> int:
         """As train, for triplets routed at sampling time: this rank's users only,
