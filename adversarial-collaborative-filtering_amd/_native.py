@@ -84,6 +84,8 @@ SIGNATURES = {
     "acf_apr_shard_pass": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _P]),
     "acf_apr_shard_items": (ctypes.c_int, [_P, _I32, _P, _I64, _P]),
     "acf_apr_shard_items_mapped": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),
+    "acf_apr_shard_pass_export": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _P, _P,
+                                                 _I64, _P]),
     "acf_shard_reduce_delta": (ctypes.c_int, [_P, _P, _P, _I32, _I32, ctypes.POINTER(HParams), _P, _P, _P]),
     "acf_shard_reduce_apply": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, ctypes.POINTER(HParams), _P, _P,
                                               _P, _I32, _P]),

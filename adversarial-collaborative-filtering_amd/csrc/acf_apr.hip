@@ -1265,6 +1265,15 @@ struct StepArgs {
   // exchange instead of Adagrad, and item rows are never written back
   int32_t shard;
   int32_t reg_B;       // batch size of reg * mean(w^2) (the global batch in shard mode)
+  // shard mode with export (acf_apr_shard_pass_export): an item slot's partial sum
+  // also goes to xbuf row xmap[slot - nU] (the split step's exchange rows): the hot
+  // combine stores its hot slots there, and its last xblocks workgroups copy the
+  // other item slots' sums from g0 (no separate copy launch)
+  float* xbuf;
+  const int64_t* xmap;
+  const int32_t* xubs;  // the plan's user / item slot bounds (one batch)
+  const int32_t* xibs;
+  int32_t xn, xblocks;
   // triplet-centric list step (k_tri_*): per-occurrence contributions of shared rows
   const int4* tpos;    // [E] CSR positions of a triplet's three occurrences
   float* contrib;      // users [B][2][d] (positive, negative branch), then items [2B][d]
@@ -2691,6 +2700,8 @@ __device__ __forceinline__ void hot_combine_slot(const StepArgs& a, const int4 e
     const int32_t row = r.own_row();
     const float* own_tab = is_item ? a.Q : a.P;
     float* acc_tab = is_item ? a.accQ : a.accP;
+    if (a.shard && is_item && a.xbuf)  // the owner's partial sum, straight to its exchange row
+      store_row<LPR, NV>(a.xbuf, a.xmap[k - (a.xubs[1] - a.xubs[0])], d, l, G);
     if (MODE != 0 && a.shard && is_item) {  // partial item sum for the owner
       store_row<LPR, NV>(a.g0, k, d, l, G);
     } else if (MODE == 0) {
@@ -2717,13 +2728,37 @@ __device__ __forceinline__ void hot_combine_slot(const StepArgs& a, const int4 e
   __syncthreads();
 }
 
+// Export workgroups of the shard-mode combine: one lane-group per item slot of
+// the batch (strided), the non-hot slots' partial sums g0 -> their exchange rows
+// (hot slots are exported by the workgroup that combines them).
+template <int LPR, int NV>
+__device__ __forceinline__ void shard_export_rest(const StepArgs& a, int bx) {
+  const int l = threadIdx.x & (LPR - 1), d = a.d;
+  const int nU = a.xubs[1] - a.xubs[0], nI = a.xibs[1] - a.xibs[0];
+  const int n = nI < a.xn ? nI : a.xn;
+  const int stride = a.xblocks * (256 / LPR);
+  for (int w = bx * (256 / LPR) + (int)threadIdx.x / LPR; w < n; w += stride) {
+    const int k = nU + w;
+    const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
+    const int cnt = r.meta() & ACF_COUNT_MASK;
+    if (!(r.meta() & ACF_SINGLE_BIT) && cnt > ACF_HOT_MIN) continue;  // a hot slot: its combine exports it
+    store_row<LPR, NV>(a.xbuf, a.xmap[w], d, l, load_row<LPR, NV>(a.g0, k, d, l));
+  }
+}
+
 // Hot-slot combine: one workgroup per hot slot (strided); see hot_combine_slot.
+// With export (shard mode), the last a.xblocks workgroups run shard_export_rest.
 template <int LPR, int NV, int MODE>
 __global__ void __launch_bounds__(256) k_hot_combine(StepArgs a) {
   __shared__ float4 red[NV * 256];
+  const int cb = (int)gridDim.x - a.xblocks;  // combining workgroups
+  if ((int)blockIdx.x >= cb) {
+    shard_export_rest<LPR, NV>(a, (int)blockIdx.x - cb);
+    return;
+  }
   const int n = a.hot.cnt[a.t];
   const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
-  for (int hx = blockIdx.x; hx < n; hx += gridDim.x) hot_combine_slot<LPR, NV, MODE, false>(a, hl[hx], red);
+  for (int hx = blockIdx.x; hx < n; hx += cb) hot_combine_slot<LPR, NV, MODE, false>(a, hl[hx], red);
 }
 
 template <int LPR, int NV, bool FUSE_APPLY>
@@ -4107,6 +4142,10 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.hot_waves = 0;
   a.hot_blocks = 0;
   a.shard = c->shard;
+  a.xbuf = nullptr;  // shard export: set by acf_apr_shard_pass_export
+  a.xmap = nullptr;
+  a.xubs = a.xibs = nullptr;
+  a.xn = a.xblocks = 0;
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
   a.contrib = c->contrib;
@@ -4716,13 +4755,17 @@ extern "C" int acf_apr_set_shard_mode(acf_apr_ctx* c, int32_t on, int32_t reg_ba
   return ACF_OK;
 }
 
-extern "C" int acf_apr_shard_pass(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
-                                  int32_t pass, void* stream_) {
+extern "C" int acf_apr_shard_pass_export(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
+                                         int32_t pass, float* xbuf, const int64_t* xmap, int64_t n_items,
+                                         void* stream_) {
   ACF_RET(check_step(c, tb, hp, 0));
   ACF_CHECK(c->shard && c->lists && c->nb == 1, ACF_E_STATE,
             "shard pass needs shard mode and a one-batch plan");
   ACF_CHECK(pass == 0 || (pass == 1 && hp->adver), ACF_E_INVALID, "pass must be 0, or 1 for APR");
   ACF_CHECK(hp->adv_mode == 0, ACF_E_INVALID, "shard mode supports adv = grad only");
+  ACF_CHECK((xbuf == nullptr) == (xmap == nullptr), ACF_E_INVALID, "xbuf and xmap go together");
+  ACF_CHECK(n_items >= 0 && n_items <= 2 * (int64_t)c->B, ACF_E_INVALID, "n_items %lld outside [0, 2B]",
+            (long long)n_items);
   hipStream_t s = static_cast<hipStream_t>(stream_);
   Kernels K;
   ACF_RET(get_kernels(c, &K, 0));
@@ -4741,14 +4784,29 @@ extern "C" int acf_apr_shard_pass(acf_apr_ctx* c, const acf_apr_tables* tb, cons
     ACF_RET(launch(K.adv, a, SW + HW, s));
   }
   StepArgs ah = a;
-  ah.slot_waves = 4 * HB;  // k_hot_combine: workgroups stride over the hot slots
-  ACF_RET(launch(pass == 1 ? K.hot_adv : (hp->adver ? K.hot_clean : K.hot_bpr), ah, 4 * HB, s));
+  int XB = 0;
+  if (xbuf && n_items > 0) {  // export workgroups after the combining ones
+    XB = (int)std::min<int64_t>((n_items * c->lpr + 255) / 256, 64);
+    ah.xbuf = xbuf;
+    ah.xmap = xmap;
+    ah.xubs = c->ubs;
+    ah.xibs = c->ibs;
+    ah.xn = (int32_t)n_items;
+    ah.xblocks = XB;
+  }
+  ah.slot_waves = 4 * (HB + XB);  // k_hot_combine: workgroups stride over the hot slots
+  ACF_RET(launch(pass == 1 ? K.hot_adv : (hp->adver ? K.hot_clean : K.hot_bpr), ah, 4 * (HB + XB), s));
   if (pass == 1 || !hp->adver) {  // user rows W scratch -> the user shard
     a.slot_waves = S;
     a.hot_waves = 0;
     ACF_RET(launch(K.flush, a, S, s));
   }
   return ACF_OK;
+}
+
+extern "C" int acf_apr_shard_pass(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
+                                  int32_t pass, void* stream_) {
+  return acf_apr_shard_pass_export(c, tb, hp, pass, nullptr, nullptr, 0, stream_);
 }
 
 // item slot rows of the current one-batch plan (slots nU .. nU + n, nU read

@@ -94,16 +94,14 @@ class HipLocal:
 
     def clean(self, hp, out, rows):
         """pass 0; working-set entry w's partial clean sum -> out[rows[w]]"""
-        self.ctx.shard_pass(self._tables(), hp, 0)
-        self.ctx.shard_items_mapped(0, out, rows)
+        self.ctx.shard_pass_export(self._tables(), hp, 0, out, rows)
 
     def set_item_delta(self, src, rows):
         """the owners' delta of working-set entry w <- src[rows[w]]"""
         self.ctx.shard_items_mapped(1, src, rows)
 
     def adv(self, hp, out, rows):
-        self.ctx.shard_pass(self._tables(), hp, 1)
-        self.ctx.shard_items_mapped(0, out, rows)
+        self.ctx.shard_pass_export(self._tables(), hp, 1, out, rows)
 
     def reduce_delta(self, hp, recv, seg, pos, G0, reply):
         self.ops.shard_reduce_delta(recv, seg, pos, hp, G0, reply)

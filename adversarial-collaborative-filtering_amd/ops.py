@@ -300,6 +300,16 @@ class APRContext:
             call("acf_apr_shard_pass", self._ptr, ctypes.byref(tb), ctypes.byref(h), int(pass_),
                  _stream_ptr(self.device))
 
+    def shard_pass_export(self, tables, hp: StepHParams, pass_: int, buf: torch.Tensor, rows: torch.Tensor) -> None:
+        """shard_pass, with working-set entry w's partial item sum also written to
+        buf[rows[w]] by the pass's own launches (the split step's exchange rows)."""
+        tb, h = self._tables(*tables), hp.to_c()
+        _require(buf, "buf", torch.float32, self.device, 2)
+        _require(rows, "rows", torch.int64, self.device, 1)
+        with torch.cuda.device(self.device):
+            call("acf_apr_shard_pass_export", self._ptr, ctypes.byref(tb), ctypes.byref(h), int(pass_),
+                 buf.data_ptr(), rows.data_ptr(), rows.numel(), _stream_ptr(self.device))
+
     def shard_items_out(self, out: torch.Tensor) -> None:
         """The item slots' partial sums (working-set order) -> out [n_items, d]."""
         _require(out, "out", torch.float32, self.device, 2)

@@ -232,6 +232,13 @@ int acf_apr_shard_pass(acf_apr_ctx* ctx, const acf_apr_tables* tables, const acf
  * their delta rows (the owners' deltas, before pass 1). */
 int acf_apr_shard_items(acf_apr_ctx* ctx, int32_t dir, float* buf, int64_t n_items, void* stream);
 
+/* acf_apr_shard_pass, and the item slots' partial sums of the pass also written to
+ * row map[w] of buf for working-set entry w < n_items (what acf_apr_shard_items_mapped
+ * dir 0 does after the pass), by the pass's own combine launch (export workgroups):
+ * the split step hands its exchange rows to the pass and needs no copy launch. */
+int acf_apr_shard_pass_export(acf_apr_ctx* ctx, const acf_apr_tables* tables, const acf_apr_hparams* hp,
+                              int32_t pass, float* buf, const int64_t* map, int64_t n_items, void* stream);
+
 /* As acf_apr_shard_items, with working-set entry w at row map[w] of buf (int64
  * row indices): the split step moves the item partial sums and deltas straight
  * between the slots and its fixed-layout exchange rows (distributed.py "Static
