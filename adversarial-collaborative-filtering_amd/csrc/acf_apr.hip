@@ -4786,7 +4786,7 @@ extern "C" int acf_apr_shard_pass_export(acf_apr_ctx* c, const acf_apr_tables* t
   StepArgs ah = a;
   int XB = 0;
   if (xbuf && n_items > 0) {  // export workgroups after the combining ones
-    XB = (int)std::min<int64_t>((n_items * c->lpr + 255) / 256, 64);
+    XB = (int)((n_items * c->lpr + 255) / 256);  // one lane-group per item slot
     ah.xbuf = xbuf;
     ah.xmap = xmap;
     ah.xubs = c->ubs;
