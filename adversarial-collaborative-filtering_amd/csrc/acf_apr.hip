@@ -1274,6 +1274,10 @@ struct StepArgs {
   const int32_t* xubs;  // the plan's user / item slot bounds (one batch)
   const int32_t* xibs;
   int32_t xn, xblocks;
+  // ... and, for the pass that updates the users, the user rows' write-back (the
+  // k_flush of the pass): hot user slots go to their table in the combine, the
+  // last xflush of the xblocks workgroups copy the others from W scratch
+  int32_t xflush;
   // triplet-centric list step (k_tri_*): per-occurrence contributions of shared rows
   const int4* tpos;    // [E] CSR positions of a triplet's three occurrences
   float* contrib;      // users [B][2][d] (positive, negative branch), then items [2B][d]
@@ -2721,7 +2725,9 @@ __device__ __forceinline__ void hot_combine_slot(const StepArgs& a, const int4 e
         adagrad_row(a, G0, own, acc, e.w, wout);
       }
       store_row<LPR, NV>(acc_tab, row, d, l, acc);
-      if (a.inplace) store_row<LPR, NV>(is_item ? a.Q : a.P, row, d, l, wout);
+      // (a shard pass with the write-back in this launch: nothing reads the user
+      // rows any more, so a hot user slot goes straight to its table)
+      if (a.inplace || (a.xflush && !is_item)) store_row<LPR, NV>(is_item ? a.Q : a.P, row, d, l, wout);
       else store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
     }
   }
@@ -2735,8 +2741,19 @@ template <int LPR, int NV>
 __device__ __forceinline__ void shard_export_rest(const StepArgs& a, int bx) {
   const int l = threadIdx.x & (LPR - 1), d = a.d;
   const int nU = a.xubs[1] - a.xubs[0], nI = a.xibs[1] - a.xibs[0];
+  const int xb = a.xblocks - a.xflush;  // item-export workgroups, then user write-back ones
+  if (bx >= xb) {
+    const int ustride = a.xflush * (256 / LPR);
+    for (int k = (bx - xb) * (256 / LPR) + (int)threadIdx.x / LPR; k < nU; k += ustride) {
+      const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
+      const int cnt = r.meta() & ACF_COUNT_MASK;
+      if (!(r.meta() & ACF_SINGLE_BIT) && cnt > ACF_HOT_MIN) continue;  // hot: written by its combine
+      store_row<LPR, NV>(a.P, r.own_row(), d, l, load_row<LPR, NV>(a.wnew_cur, k, d, l));
+    }
+    return;
+  }
   const int n = nI < a.xn ? nI : a.xn;
-  const int stride = a.xblocks * (256 / LPR);
+  const int stride = xb * (256 / LPR);
   for (int w = bx * (256 / LPR) + (int)threadIdx.x / LPR; w < n; w += stride) {
     const int k = nU + w;
     const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
@@ -4145,7 +4162,7 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.xbuf = nullptr;  // shard export: set by acf_apr_shard_pass_export
   a.xmap = nullptr;
   a.xubs = a.xibs = nullptr;
-  a.xn = a.xblocks = 0;
+  a.xn = a.xblocks = a.xflush = 0;
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
   a.contrib = c->contrib;
@@ -4785,18 +4802,21 @@ extern "C" int acf_apr_shard_pass_export(acf_apr_ctx* c, const acf_apr_tables* t
   }
   StepArgs ah = a;
   int XB = 0;
-  if (xbuf && n_items > 0) {  // export workgroups after the combining ones
-    XB = (int)((n_items * c->lpr + 255) / 256);  // one lane-group per item slot
+  const bool users_done = pass == 1 || !hp->adver;  // this pass updates the user rows
+  if (xbuf) {  // export (and write-back) workgroups after the combining ones
+    const int XF = users_done ? (c->B * c->lpr + 255) / 256 : 0;  // one lane-group per user slot
+    XB = (int)((n_items * c->lpr + 255) / 256) + XF;                 // one lane-group per item slot
     ah.xbuf = xbuf;
     ah.xmap = xmap;
     ah.xubs = c->ubs;
     ah.xibs = c->ibs;
     ah.xn = (int32_t)n_items;
     ah.xblocks = XB;
+    ah.xflush = XF;
   }
   ah.slot_waves = 4 * (HB + XB);  // k_hot_combine: workgroups stride over the hot slots
   ACF_RET(launch(pass == 1 ? K.hot_adv : (hp->adver ? K.hot_clean : K.hot_bpr), ah, 4 * (HB + XB), s));
-  if (pass == 1 || !hp->adver) {  // user rows W scratch -> the user shard
+  if (users_done && !xbuf) {  // user rows W scratch -> the user shard
     a.slot_waves = S;
     a.hot_waves = 0;
     ACF_RET(launch(K.flush, a, S, s));
