@@ -1,6 +1,6 @@
 """configs[2]'s split step alone (world 1, pinterest-20-shaped, B = 512, d = 64), graph
 replay vs eager, with the routing time of a chunk and the replay time apart:
-   python3 tools/shard_pinterest.py [steps]
+   python3 tools/shard_pinterest.py [steps] [chunks]
    rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/pp -o pp -- python3 tools/shard_pinterest.py"""
 import importlib
 import json
@@ -24,6 +24,7 @@ os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+nchunks = int(sys.argv[2]) if len(sys.argv) > 2 else 1  # > 1: routing of chunk k + 1 beside chunk k
 B, d = 512, 64
 ds = acf.pinterest_like(seed=2019)
 ep = acf.DeviceSampler(ds, B, dev, seed=3).epoch(0)
@@ -36,7 +37,7 @@ for graph in (True, False):
     g = torch.Generator(device=dev).manual_seed(5)
     sh.P.normal_(0, 0.01, generator=g)
     sh.Q.normal_(0, 0.01, generator=g)
-    ck = steps
+    ck = steps // nchunks
     sh.train_routed(u[: steps * B], i[: steps * B], j[: steps * B], hp, chunk=ck)  # eager + capture (both sets)
     s = slice(steps * B, 2 * steps * B)
     torch.cuda.synchronize(dev)
