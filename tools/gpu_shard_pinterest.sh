@@ -7,7 +7,6 @@ cat $OUT/times.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o pp -- python3 tools/shard_pinterest.py > $OUT/prof.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
 f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1)
 cp "$f" $OUT/kernel_stats.csv
-find $OUT/prof -name "*kernel_trace.csv" -exec cp {} $OUT/kernel_trace.csv \;
 rm -rf $OUT/prof
 python3 - <<PY
 import csv
