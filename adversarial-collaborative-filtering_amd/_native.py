@@ -9,6 +9,8 @@ import ctypes
 import os
 import threading
 
+from . import build_native
+
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libacf_apr.so")
 
@@ -40,6 +42,7 @@ class HParams(ctypes.Structure):
 SIGNATURES = {
     "acf_apr_abi_version": (ctypes.c_int, []),
     "acf_apr_last_error": (ctypes.c_char_p, []),
+    "acf_apr_build_hash": (ctypes.c_char_p, []),
     "acf_apr_create": (ctypes.c_int, [ctypes.POINTER(_P), _I64, _I64, _I32, _I32, _I32]),
     "acf_apr_destroy": (ctypes.c_int, [_P]),
     "acf_apr_plan": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P]),
@@ -108,22 +111,36 @@ _lib = None
 _lock = threading.Lock()
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load the HIP library (once).  Raises ImportError if it was never built."""
+def _open(path: str, name: str, sigs: dict, hash_fn: str, root: str) -> ctypes.CDLL:
+    """dlopen a library after checking that it was built from the sources under
+    ``root`` as they are now (build_native.verify: ImportError otherwise), and
+    check the hash it reports once loaded."""
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: the HIP extension is not built. Run "
+            "`python adversarial-collaborative-filtering_amd/build_native.py` "
+            "(or __graft_entry__.build()). There is no CPU fallback.")
+    build_native.verify(name, path, root)
+    lib = ctypes.CDLL(path)
+    for fname, (res, args) in sigs.items():
+        fn = getattr(lib, fname)
+        fn.restype = res
+        fn.argtypes = args
+    got = getattr(lib, hash_fn)().decode().split("=", 1)[-1]
+    if got != build_native.source_hash(name, root):
+        raise ImportError(f"{path} reports build hash {got}, not its sources' ({path} was replaced "
+                          "after the check?): rebuild it")
+    return lib
+
+
+def load(path: str = LIB_PATH, root: str = build_native.REPO) -> ctypes.CDLL:
+    """Load the HIP library (once).  Raises ImportError if it was never built or
+    was built from other sources than those under ``root``."""
     global _lib
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(path):
-            raise ImportError(
-                f"{path} not found: the HIP extension is not built. Run "
-                "`python adversarial-collaborative-filtering_amd/build_native.py` "
-                "(or __graft_entry__.build()). There is no CPU fallback.")
-        lib = ctypes.CDLL(path)
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
+        lib = _open(path, "apr", SIGNATURES, "acf_apr_build_hash", root)
         ver = lib.acf_apr_abi_version()
         if ver != ABI_VERSION:
             raise ImportError(f"libacf_apr ABI {ver} != expected {ABI_VERSION}; rebuild it")
@@ -159,6 +176,7 @@ class NeuMFHParams(ctypes.Structure):
 
 NEUMF_SIGNATURES = {
     "acf_neumf_last_error": (ctypes.c_char_p, []),
+    "acf_neumf_build_hash": (ctypes.c_char_p, []),
     "acf_neumf_param_count": (_I64, [_I64, _I64, _I32]),
     "acf_neumf_param_offsets": (ctypes.c_int, [_I64, _I64, _I32, ctypes.POINTER(_I64)]),
     "acf_neumf_create": (ctypes.c_int, [ctypes.POINTER(_P), _I64, _I64, _I32, _I32]),
@@ -186,23 +204,15 @@ NEUMF_SIGNATURES = {
 _neumf = None
 
 
-def load_neumf(path: str = NEUMF_LIB_PATH) -> ctypes.CDLL:
-    """Load libacf_neumf.so (once).  Raises ImportError if it was never built."""
+def load_neumf(path: str = NEUMF_LIB_PATH, root: str = build_native.REPO) -> ctypes.CDLL:
+    """Load libacf_neumf.so (once).  Raises ImportError if it was never built or
+    was built from other sources than those under ``root``."""
     global _neumf
     with _lock:
         if _neumf is not None:
             return _neumf
-        if not os.path.exists(path):
-            raise ImportError(f"{path} not found: the HIP extension is not built. Run "
-                              "`python adversarial-collaborative-filtering_amd/build_native.py`. "
-                              "There is no CPU fallback.")
-        lib = ctypes.CDLL(path)
-        for name, (res, args) in NEUMF_SIGNATURES.items():
-            fn = getattr(lib, name)
-            fn.restype = res
-            fn.argtypes = args
-        _neumf = lib
-        return lib
+        _neumf = _open(path, "neumf", NEUMF_SIGNATURES, "acf_neumf_build_hash", root)
+        return _neumf
 
 
 def call_neumf(name: str, *args) -> None:

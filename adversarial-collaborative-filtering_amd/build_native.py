@@ -1,26 +1,46 @@
 """Build the in-tree HIP libraries with ``hipcc --offload-arch=gfx950``:
 ``lib/libacf_apr.so`` (APR path, C-ABI of ``include/acf_apr.h``) and
-``lib/libacf_neumf.so`` (NeuMF path, ``include/acf_neumf.h``).  They land inside
-the repository so that ``gpurun`` ships them to the GPU box.
+``lib/libacf_neumf.so`` (NeuMF path, ``include/acf_neumf.h``), plus the
+``TORCH_LIBRARY(acf)`` op library ``lib/libacf_torch.so``.  They land inside the
+repository so that ``gpurun`` ships them to the GPU box.
+
+Every library carries the hash of what it was built from: the bytes of its
+sources and of the headers they include, and the compile flags
+(``source_hash``).  The hash is compiled in as the string
+``ACF_BUILD_HASH=<hex>`` (exported by ``acf_*_build_hash()``), so a library can
+be tied to its sources without loading it (``embedded_hash`` scans the file).
+``build`` rebuilds exactly the libraries whose embedded hash differs from the
+sources on disk (no mtimes: a pushed tree's mtimes say nothing), and the
+loaders (``_native.load`` / ``load_neumf``, ``torch_ops.load``) refuse a library
+whose hash does not match (``verify``).
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
-HIP_SRC = os.path.join(PKG_DIR, "csrc", "acf_apr.hip")
-OPS_SRC = os.path.join(PKG_DIR, "csrc", "acf_ops.hip")
-ROWS_H = os.path.join(PKG_DIR, "csrc", "acf_rows.h")
-HIP_LIB = os.path.join(PKG_DIR, "lib", "libacf_apr.so")
-HEADER = os.path.join(REPO, "include", "acf_apr.h")
-NEUMF_SRC = os.path.join(PKG_DIR, "csrc", "acf_neumf.hip")
-NEUMF_LIB = os.path.join(PKG_DIR, "lib", "libacf_neumf.so")
-NEUMF_HEADER = os.path.join(REPO, "include", "acf_neumf.h")
-# (sources, library, headers it depends on)
-TARGETS = [([HIP_SRC, OPS_SRC], HIP_LIB, [HEADER, ROWS_H]), ([NEUMF_SRC], NEUMF_LIB, [HEADER, NEUMF_HEADER])]
+PKG = os.path.basename(PKG_DIR)
+
+# per library: sources (compiled), headers (included; hashed), relative to REPO
+LIBS = {
+    "apr": {"lib": f"{PKG}/lib/libacf_apr.so",
+            "srcs": [f"{PKG}/csrc/acf_apr.hip", f"{PKG}/csrc/acf_ops.hip"],
+            "headers": ["include/acf_apr.h", f"{PKG}/csrc/acf_rows.h"]},
+    "neumf": {"lib": f"{PKG}/lib/libacf_neumf.so",
+              "srcs": [f"{PKG}/csrc/acf_neumf.hip"],
+              "headers": ["include/acf_apr.h", "include/acf_neumf.h"]},
+    "torch": {"lib": f"{PKG}/lib/libacf_torch.so",
+              "srcs": [f"{PKG}/csrc/acf_torch.cpp"],
+              "headers": ["include/acf_apr.h"]},
+}
+HIP_LIB = os.path.join(REPO, LIBS["apr"]["lib"])
+NEUMF_LIB = os.path.join(REPO, LIBS["neumf"]["lib"])
+TORCH_LIB = os.path.join(REPO, LIBS["torch"]["lib"])
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -32,22 +52,67 @@ HIPCC_FLAGS = [
     "-Wall",
     "-Wno-unused-result",
 ]
+TORCH_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared"]
+_HASH_RE = re.compile(rb"ACF_BUILD_HASH=([0-9a-f]{32})")
 
 
-def _stale(target: str, sources: list[str]) -> bool:
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(s) > t for s in sources if os.path.exists(s))
+def _flags(name: str) -> list[str]:
+    return TORCH_FLAGS if name == "torch" else HIPCC_FLAGS
+
+
+def source_hash(name: str, root: str = REPO) -> str:
+    """Hash of library ``name``'s sources, headers and compile flags under ``root``."""
+    spec = LIBS[name]
+    h = hashlib.sha256()
+    for rel in [*spec["srcs"], *spec["headers"]]:
+        h.update(rel.encode() + b"\0")
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(" ".join(_flags(name)).encode())
+    return h.hexdigest()[:32]
+
+
+def embedded_hash(path: str) -> str | None:
+    """The ``ACF_BUILD_HASH`` a built library carries (None: none, or no file)."""
+    try:
+        with open(path, "rb") as f:
+            m = _HASH_RE.search(f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def verify(name: str, path: str | None = None, root: str = REPO) -> None:
+    """Raise ImportError unless the library at ``path`` was built from the
+    sources under ``root`` as they are now."""
+    path = path or os.path.join(root, LIBS[name]["lib"])
+    got, want = embedded_hash(path), source_hash(name, root)
+    if got != want:
+        raise ImportError(
+            f"{path} was built from other sources (embedded hash {got}, sources {want}): "
+            "rebuild it with `python adversarial-collaborative-filtering_amd/build_native.py` "
+            "(or __graft_entry__.build())")
+
+
+def _stale(name: str) -> bool:
+    return embedded_hash(os.path.join(REPO, LIBS[name]["lib"])) != source_hash(name)
+
+
+def _define(name: str) -> str:
+    return f'-DACF_BUILD_HASH="{source_hash(name)}"'
 
 
 def build_hip(force: bool = False, verbose: bool = True) -> str:
-    for srcs, lib, headers in TARGETS:
-        if force or _stale(lib, [*srcs, *headers, __file__]):
+    for name in ("apr", "neumf"):
+        if force or _stale(name):
+            spec = LIBS[name]
+            lib = os.path.join(REPO, spec["lib"])
             os.makedirs(os.path.dirname(lib), exist_ok=True)
             hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
             tmp = lib + ".tmp"
-            cmd = [hipcc, *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), *srcs, "-o", tmp]
+            cmd = [hipcc, *HIPCC_FLAGS, _define(name), "-I", os.path.join(REPO, "include"),
+                   *[os.path.join(REPO, s) for s in spec["srcs"]], "-o", tmp]
             if verbose:
                 print("[build]", " ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
@@ -55,24 +120,21 @@ def build_hip(force: bool = False, verbose: bool = True) -> str:
     return HIP_LIB
 
 
-TORCH_SRC = os.path.join(PKG_DIR, "csrc", "acf_torch.cpp")
-TORCH_LIB = os.path.join(PKG_DIR, "lib", "libacf_torch.so")
-
-
 def build_torch_ops(force: bool = False, verbose: bool = True) -> str:
     """lib/libacf_torch.so: the TORCH_LIBRARY(acf, m) custom ops over libacf_apr.so
     (host code only: g++ against the installed torch's headers and libraries)."""
     import torch
 
-    if not (force or _stale(TORCH_LIB, [TORCH_SRC, HEADER, HIP_LIB, __file__])):
+    if not (force or _stale("torch")):
         return TORCH_LIB
     tdir = os.path.dirname(torch.__file__)
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     tmp = TORCH_LIB + ".tmp"
-    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+    cmd = ["g++", *TORCH_FLAGS, _define("torch"), f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
            "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
            "-I", os.path.join(tdir, "include"), "-I", os.path.join(tdir, "include", "torch", "csrc", "api", "include"),
-           "-I", "/opt/rocm/include", "-I", os.path.join(REPO, "include"), TORCH_SRC, "-o", tmp,
+           "-I", "/opt/rocm/include", "-I", os.path.join(REPO, "include"),
+           os.path.join(REPO, LIBS["torch"]["srcs"][0]), "-o", tmp,
            "-L", os.path.join(tdir, "lib"), "-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip", "-ltorch_hip",
            "-L", os.path.dirname(HIP_LIB), "-lacf_apr", "-Wl,-rpath,$ORIGIN"]
     if verbose:

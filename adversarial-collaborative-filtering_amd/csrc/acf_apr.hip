@@ -3717,6 +3717,11 @@ static int check_dim(int d) {
 
 extern "C" int acf_apr_abi_version(void) { return ACF_APR_ABI_VERSION; }
 
+#ifndef ACF_BUILD_HASH
+#define ACF_BUILD_HASH "unhashed"
+#endif
+extern "C" const char* acf_apr_build_hash(void) { return "ACF_BUILD_HASH=" ACF_BUILD_HASH; }
+
 extern "C" const char* acf_apr_last_error(void) { return g_last_error.c_str(); }
 
 extern "C" int acf_apr_destroy(acf_apr_ctx* c) {

@@ -1236,6 +1236,11 @@ struct acf_neumf_ctx {
 
 extern "C" const char* acf_neumf_last_error(void) { return g_neumf_error.c_str(); }
 
+#ifndef ACF_BUILD_HASH
+#define ACF_BUILD_HASH "unhashed"
+#endif
+extern "C" const char* acf_neumf_build_hash(void) { return "ACF_BUILD_HASH=" ACF_BUILD_HASH; }
+
 static int check_dims(int64_t U1, int64_t I1, int32_t d) {
   ACF_CHECK(U1 > 0 && I1 > 0 && U1 < (1ll << 31) && I1 < (1ll << 31), ACF_E_INVALID,
             "table rows must be in [1, 2^31): got %lld, %lld", (long long)U1, (long long)I1);

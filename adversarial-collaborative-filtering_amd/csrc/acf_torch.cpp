@@ -326,6 +326,12 @@ at::Tensor score_rank_all(const at::Tensor& P, const at::Tensor& Q, const at::Te
 
 }  // namespace
 
+#ifndef ACF_BUILD_HASH
+#define ACF_BUILD_HASH "unhashed"
+#endif
+// "ACF_BUILD_HASH=<32 hex>" of this library's sources (build_native.source_hash)
+extern "C" const char* acf_torch_build_hash(void) { return "ACF_BUILD_HASH=" ACF_BUILD_HASH; }
+
 TORCH_LIBRARY(acf, m) {
   m.def("bpr_apr_step(Tensor(a!) P, Tensor(b!) Q, Tensor(c!) accP, Tensor(d!) accQ, Tensor u, Tensor i, "
         "Tensor j, float lr=0.05, float eps=0.5, float reg=0., float reg_adv=1., bool adver=True, "

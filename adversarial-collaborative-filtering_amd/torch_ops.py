@@ -26,6 +26,8 @@ import threading
 
 import torch
 
+from . import build_native
+
 LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libacf_torch.so")
 OPS = ("bpr_apr_step", "apr_train", "gather_bpr_fwd_bwd", "row_segment_sum", "l2norm_perturb",
        "sparse_adagrad_apply", "score_rank", "score_rank_all",
@@ -42,6 +44,7 @@ def load():
             if not os.path.exists(LIB):
                 raise ImportError(f"{LIB} not found: build it with __graft_entry__.build() "
                                   "(build_native.build_torch_ops); there is no CPU fallback")
+            build_native.verify("torch", LIB)  # built from these sources (ImportError otherwise)
             torch.ops.load_library(LIB)
             _loaded = True
     return torch.ops.acf

@@ -71,6 +71,9 @@ typedef struct acf_apr_hparams {
 /* ---- library ------------------------------------------------------------ */
 int acf_apr_abi_version(void);
 const char* acf_apr_last_error(void);
+/* "ACF_BUILD_HASH=<32 hex>": hash of the sources, headers and flags the library
+ * was built from (build_native.source_hash); the loaders refuse a mismatch. */
+const char* acf_apr_build_hash(void);
 
 /* ---- context ------------------------------------------------------------ */
 /* Allocates the workspace for plans of up to max_batches_per_plan batches of up

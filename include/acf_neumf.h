@@ -39,6 +39,8 @@ typedef struct {
 } acf_neumf_hparams;
 
 const char* acf_neumf_last_error(void);
+/* "ACF_BUILD_HASH=<32 hex>" of this library's sources (see acf_apr_build_hash). */
+const char* acf_neumf_build_hash(void);
 
 /* Number of floats of the flat parameter buffer, and the 10 segment offsets. */
 int64_t acf_neumf_param_count(int64_t num_user_rows, int64_t num_item_rows, int32_t dim);
