@@ -63,6 +63,8 @@ SIGNATURES = {
     "acf_apr_set_failsafe": (ctypes.c_int, [_P, _I32]),
     "acf_apr_set_spin_limit": (ctypes.c_int, [_P, _I32]),
     "acf_apr_stream_recoveries": (ctypes.c_int, [_P, ctypes.POINTER(_I64)]),
+    "acf_apr_resolve": (ctypes.c_int, [_P]),
+    "acf_apr_share_failsafe": (ctypes.c_int, [_P, _P]),
     "acf_apr_copy_losses": (ctypes.c_int, [_P, _P, _P, _P]),
     "acf_apr_delta_scatter": (ctypes.c_int, [_P, _P, _P, _P]),
     "acf_bpr_forward": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _P, _I32, _I32, _F, _F, _P, _P,
@@ -153,9 +155,14 @@ def call(name: str, *args) -> None:
     lib = load()
     rc = getattr(lib, name)(*args)
     if rc != ACF_OK:
-        msg = lib.acf_apr_last_error().decode("utf-8", "replace")
-        cls = NativeIndexError if rc == ACF_E_RANGE else NativeError
-        raise cls(rc, name, msg)
+        call_failed(rc, name)
+
+
+def call_failed(rc: int, name: str) -> None:
+    """Raise the NativeError of a failed C-ABI call (status rc)."""
+    msg = load().acf_apr_last_error().decode("utf-8", "replace")
+    cls = NativeIndexError if rc == ACF_E_RANGE else NativeError
+    raise cls(rc, name, msg)
 
 
 def exported_symbols(path: str = LIB_PATH) -> set[str]:

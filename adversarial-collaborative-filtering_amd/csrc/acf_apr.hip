@@ -44,6 +44,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -702,6 +703,8 @@ struct BPlanArgs {
   int32_t* nextt;
   int32_t* task_list;
   int32_t* task_cnt;
+  int2* final_list;   // slots no later batch of the plan touches (k_stream's tail write-back)
+  int32_t* final_cnt;
 };
 
 // Workgroup barrier for LDS data only.  __syncthreads() also waits for every
@@ -731,6 +734,7 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
   const int t = blockIdx.x, tid = threadIdx.x, B = p.B, S3 = 3 * B;
   STAMP(t, tid >> 6, 0);
   if (tid == 0) { s_err = 0; s_nu = -1; }
+  if (t == 0 && tid == 0) *p.final_cnt = 0;  // k_bplan_build appends to it
   const uint32_t side_bit = 1u << p.rb;
   uint32_t keys[IPT];
   int32_t vals[IPT];
@@ -1016,9 +1020,11 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
   __shared__ uint8_t single[3 * MAXB];
   __shared__ uint8_t gflag[MAXB];
   __shared__ typename Scan::storage_type scan_st;
+  __shared__ int32_t s_fin, s_fbase;
   const int t = blockIdx.x, tid = threadIdx.x, B = p.B, S = p.S;
   const int G = (B + p.opw - 1) / p.opw;
   STAMP(t, 16 + (tid >> 6), 0);
+  if (tid == 0) s_fin = 0;
   const int2 n = p.bn[t];
   const int64_t rbase = (int64_t)t * S;
   // the triplet's occurrence slots, loaded now (k_bplan_sort wrote them): off
@@ -1091,6 +1097,14 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
   }
   for (int g = tid; g < G; g += BS) gflag[g] = 0;
   lds_barrier();  // info (LDS); the nextt stores stay in flight
+  // final slots (no later batch of the plan touches the row): their place in
+  // this batch's share of the final-slot list
+  int32_t fidx[SPT];
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    fidx[q] = -1;
+    if (tid + q * BS < n.x && tn[q] == 0x7fffffff) fidx[q] = atomicAdd(&s_fin, 1);
+  }
   const int gen = p.gen;
   STAMP(t, 16 + (tid >> 6), 3);
   static_assert(MAXB <= BS, "k_bplan_build: one triplet per thread");
@@ -1139,6 +1153,10 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
   }
   lds_barrier();
   STAMP(t, 16 + (tid >> 6), 4);
+  // the batch's share of the final-slot list: the atomic stays in flight over
+  // the task-list scans below (they wait on LDS only)
+  int32_t fret = 0;
+  if (tid == 0 && s_fin > 0) fret = atomicAdd(p.final_cnt, s_fin);
   // task list: the non-fused slots in slot order, then the groups holding a fused triplet
   int32_t base = 0;
   for (int y0 = 0; y0 < S + G; y0 += BS) {
@@ -1153,12 +1171,17 @@ __global__ void __launch_bounds__(BS) k_bplan_build(BPlanArgs p) {
     lds_barrier();  // scan storage reuse
   }
   STAMP(t, 16 + (tid >> 6), 5);
+  if (tid == 0) s_fbase = fret;
+  lds_barrier();
   // every global store of the kernel from here on: on gfx950 vmcnt counts stores
   // too, so an earlier store would have held up the loads the phases above wait for
 #pragma unroll
   for (int q = 0; q < SPT; ++q) {
     const int s = tid + q * BS;
     if (s < S) p.nextt[rbase + s] = s < n.x ? tn[q] : 0;  // 0: no row, never written back
+    if (fidx[q] >= 0)
+      p.final_list[s_fbase + fidx[q]] =
+          make_int2((int32_t)(rbase + s), (int32_t)(key[q] & (side_bit - 1)) | ((key[q] & side_bit) ? (int32_t)0x80000000 : 0));
   }
   if (tid < B) {
     (ar >= 0 ? p.inl[ar] : p.urec[-1 - ar]) = r;
@@ -1248,12 +1271,37 @@ struct StepArgs {
   const int32_t* task_cnt;   // [nb]
   int32_t task_stride, max_depth;
   int32_t poll_sleep;  // k_stream: s_sleep between polls of a version (0-3; 4/5/6 = 8/16/32)
-  // k_stream's give-ups: the call's failure word (bit 0: a version wait gave up
-  // after spin_limit polls) -- k_stream_flush writes nothing when it is set, so a
-  // failed call leaves the tables as they were and can be replayed exactly
+  // k_stream's give-ups: a version wait that gave up after spin_limit polls
+  // stores the launch's seq into the failure word `fail` (so the word needs no
+  // reset between calls: a launch failed iff *fail == its seq).  The write-back
+  // of a failed launch writes nothing, so the tables are as before the call.
   int32_t* fail;
   int32_t spin_limit;
-  int32_t* fail_host;  // host-mapped copy of the failure word (written by the flush)
+  // (r04) the end of a streamed call, decided once per launch (stream_end):
+  //  - seq: the host's number of this launch (status ring slot seq % 8);
+  //  - verify: a failed call is replayed by the host later (acf_apr_resolve):
+  //    the decider sets the group's gate, so every later streamed launch of the
+  //    group runs nothing until the replays, and leaves the epoch alone; an
+  //    unverified failure sets step_err bit 0 and bumps the epoch;
+  //  - tail: the launch ends in a barrier over an arrival counter (workgroups
+  //    arrive once each; arrive_target = the host's running total), the first
+  //    workgroup to reach the decide word records COMMIT / FAIL for seq, and on
+  //    COMMIT every workgroup writes back its share of the plan's final-slot
+  //    list (the rows' last versions) -- no k_stream_flush launch;
+  //  - status: host-mapped ring where the decider reports (seq << 2) | failed.
+  uint32_t seq;
+  int32_t verify;
+  int32_t* gate;
+  unsigned long long* decide;
+  unsigned long long decide_prev;  // the decide word as the host expects it (the last tail launch committed)
+  unsigned long long* arrive;  // two sets (by tail_par) of a top counter + 8 shard counters, 128 B apart
+  int32_t tail_par;
+  int32_t tail;
+  int32_t flushers;  // tail: workgroups [0, flushers) wait for the outcome and write back
+  unsigned long long* tail_diag;  // ACF_TAIL_DIAG: s_memrealtime stamps of the tail (tools/tail_diag.py)
+  const int2* final_list;   // [n] {t * S + slot, row | item << 31}: slots no later batch of the plan touches
+  const int32_t* final_cnt;
+  unsigned long long* status;
   // hot slots of list plans (k_records): piece waves [slot_waves, slot_waves +
   // hot_waves) of a list kernel stride over the batch's pieces; partial sums in hot_part
   HotLists hot;
@@ -2109,11 +2157,12 @@ __device__ __forceinline__ void store_ver(u64* dst, int d, int l, const RowV<NV>
 __device__ __forceinline__ bool wait_round(const StepArgs& a, bool ok, int it) {
   if (__all(ok)) return true;
   if (it >= a.spin_limit) {
-    if ((threadIdx.x & 63) == 0) atomicOr(a.fail, 1);
+    if ((threadIdx.x & 63) == 0)
+      __hip_atomic_store(a.fail, (int32_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
   }
   if ((it & 31) == 31 &&
-      __any(__hip_atomic_load(a.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
+      __any(__hip_atomic_load(a.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int32_t)a.seq))
     return true;  // another wave gave up: the launch is failing, drain it
   switch (a.poll_sleep) {  // s_sleep takes an immediate
     case 0: break;
@@ -2480,6 +2529,155 @@ __device__ __forceinline__ void stream_single(const StepArgs& a, int b, int l, u
   store_ver<LPR, NV>(const_cast<u64*>(vrow(a.ver_a, a, a.t, r.b.y)), d, l, cj, tag);
 }
 
+// The end of a streamed call, decided once: thread 0 of the deciding workgroup
+// (the first to record an outcome for a.seq) moves the epoch on after a COMMIT,
+// sets the group's gate after a verified failure (the host replays the call
+// later) or step_err bit 0 after an unverified one (the call is dropped), and
+// reports the outcome in the host-mapped status ring.  A verified failure leaves
+// the epoch alone: the replay reads the same call counter (random delta) and
+// bumps it as this call would have; the failed launch's granules keep their
+// tag, and the next streamed launch of the context has a later one.
+__device__ __forceinline__ void stream_decided(const StepArgs& a, bool failed) {
+  uint32_t* ep = const_cast<uint32_t*>(a.epoch);
+  if (!failed) {
+    atomicAdd(ep, 1u);
+  } else if (a.verify) {
+    __hip_atomic_store(a.gate, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    atomicOr(a.step_err, 1);
+    atomicAdd(ep, 1u);
+  }
+  if (a.verify && a.status)
+    __hip_atomic_store(a.status + (a.seq & 7), ((unsigned long long)a.seq << 2) | (failed ? 1ull : 0ull),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Record the outcome of launch a.seq in the decide word unless one is recorded
+// already; returns the recorded outcome (bit 0: failed) and, through *me,
+// whether this call recorded it (the decider runs stream_decided).
+__device__ __forceinline__ int stream_decide(const StepArgs& a, bool failed, bool* me) {
+  const unsigned long long want = ((unsigned long long)a.seq << 1) | (failed ? 1ull : 0ull);
+  // first attempt against the host's guess of the current word (one round trip)
+  unsigned long long cur = a.decide_prev;
+  *me = false;
+  while ((cur >> 1) != (unsigned long long)a.seq) {
+    unsigned long long exp = cur;
+    if (__hip_atomic_compare_exchange_strong(a.decide, &exp, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+      cur = want;
+      *me = true;
+      break;
+    }
+    cur = exp;
+  }
+  return (int)(cur & 1);
+}
+
+// k_stream's tail (a.tail): every workgroup, once its four waves have no
+// version store in flight, arrives: an agent-scope add to its shard counter
+// (blockIdx % 8; the Guideline 16 counter form: every handed-off byte stored
+// and loaded sc1), and the shard's last arrival adds to the top counter (one
+// counter for 512 arrivals serialised ~6 us at the end of a call).  The last
+// arrival at the top decides the launch's outcome (COMMIT unless a wait gave up
+// or the launch was gated).  Workgroups [0, a.flushers) then poll the decide
+// word (bounded: a launch that cannot become fully resident times out and
+// fails) and, on COMMIT, write back the plan's final-slot list, lane-group gw
+// taking entries gw, gw + G, ... two at a time: the row's last version in the
+// launch -> weights and Adagrad slot (the granules k_stream_flush copies).
+// Every other workgroup leaves after it has arrived.  The counters come in two
+// sets used by alternate tail launches; each launch's block 0 zeroes the set
+// the previous tail launch used (that launch has ended: kernel boundary).
+template <int LPR>
+__device__ __forceinline__ void stream_tail(const StepArgs& a, uint32_t tag, bool gated, int32_t fcnt) {
+  __shared__ int s_out;
+  const int flushers = max(1, min((int)gridDim.x, a.flushers));
+  const bool flusher = (int)blockIdx.x < flushers;
+  unsigned long long* set = a.arrive + a.tail_par * 144;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a.tail_diag) atomicMax(a.tail_diag + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    const int G = (int)gridDim.x, k = (int)(blockIdx.x & 7);
+    const unsigned long long nk = (unsigned long long)(G / 8 + (k < G % 8 ? 1 : 0));
+    const unsigned long long nsh = (unsigned long long)min(G, 8);
+    bool last = false;
+    if (__hip_atomic_fetch_add(set + 16 * (k + 1), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == nk)
+      last = __hip_atomic_fetch_add(set, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == nsh;
+    int out = -1;
+    bool me = false;
+    if (last) {
+      if (a.tail_diag) a.tail_diag[2] = __builtin_amdgcn_s_memrealtime();
+      const bool failed =
+          gated || __hip_atomic_load(a.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int32_t)a.seq;
+      out = stream_decide(a, failed, &me);
+      if (a.tail_diag) a.tail_diag[3] = __builtin_amdgcn_s_memrealtime();
+      if (me) stream_decided(a, out != 0);
+      if (a.tail_diag) a.tail_diag[4] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (flusher && out < 0) {
+      const int64_t lim = (int64_t)a.spin_limit * 8;
+      for (int64_t it = 0;; ++it) {
+        const unsigned long long v = __hip_atomic_load(a.decide, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 1) == (unsigned long long)a.seq) { out = (int)(v & 1); break; }
+        if (it >= lim) {  // never all resident: fail the launch (and drain its late waves)
+          __hip_atomic_store(a.fail, (int32_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          out = stream_decide(a, true, &me);
+          if (me) stream_decided(a, out != 0);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+    s_out = out;
+    if (a.tail_diag && flusher && blockIdx.x == 0) a.tail_diag[5] = __builtin_amdgcn_s_memrealtime();
+  }
+  __syncthreads();
+  if (!flusher || s_out != 0) return;
+  const int64_t groups = (int64_t)flushers * (blockDim.x / LPR);
+  const int l = (int)(threadIdx.x & (LPR - 1));
+  const int d4 = a.d >> 2;
+  for (int64_t e = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / LPR; e < fcnt; e += 2 * groups) {
+    const bool two = e + groups < fcnt;
+    const int2 f0 = a.final_list[e];
+    const int2 f1 = two ? a.final_list[e + groups] : f0;
+    if (l >= d4) continue;
+    u64 w[2][4], c[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int2 f = h ? f1 : f0;
+      const u64* vw = a.ver_w + (int64_t)f.x * a.d;
+      const u64* va = a.ver_a + (int64_t)f.x * a.d;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        w[h][k] = __hip_atomic_load((gu64_ptr)(vw + l + k * d4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c[h][k] = __hip_atomic_load((gu64_ptr)(va + l + k * d4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h && !two) break;
+      const int2 f = h ? f1 : f0;
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        ok = ok && (uint32_t)(w[h][k] >> 32) == tag && (uint32_t)(c[h][k] >> 32) == tag;
+      if (!ok) atomicOr(a.step_err, 4);  // a final version missing after the barrier: never expected
+      const int item = f.y < 0;
+      const int64_t off = (int64_t)(f.y & 0x7fffffff) * a.d + 4 * l;
+      *reinterpret_cast<float4*>((item ? a.Q : a.P) + off) =
+          make_float4(__uint_as_float((uint32_t)w[h][0]), __uint_as_float((uint32_t)w[h][1]),
+                      __uint_as_float((uint32_t)w[h][2]), __uint_as_float((uint32_t)w[h][3]));
+      *reinterpret_cast<float4*>((item ? a.accQ : a.accP) + off) =
+          make_float4(__uint_as_float((uint32_t)c[h][0]), __uint_as_float((uint32_t)c[h][1]),
+                      __uint_as_float((uint32_t)c[h][2]), __uint_as_float((uint32_t)c[h][3]));
+    }
+  }
+  if (a.tail_diag && blockIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) a.tail_diag[6] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
 // The work of a batch is a list of tasks: task k < S is slot k, task S + g the
 // group of 64/LPR consecutive triplets g*64/LPR, ... (its fused ones).  With the
 // plan's task lists (fusion on) a batch's tasks are its non-fused slots, then
@@ -2487,7 +2685,8 @@ __device__ __forceinline__ void stream_single(const StepArgs& a, int b, int l, u
 // count of its batches positions; without them (fusion off) position p is task
 // p of every batch, P = `positions`.  depth = min(max_depth, waves / P) waves
 // share a position, taking every depth-th batch; a wave loads its next task
-// while it runs the current one.
+// while it runs the current one.  A gated launch (a failed verified call of the
+// group awaits its replay) runs no task.
 template <int LPR, int NV, int TEAM>
 __global__ void __launch_bounds__(256, 2) k_stream(StepArgs a, int32_t positions) {
   static_assert(TEAM * LPR == 64, "k_stream: one wave per slot");
@@ -2504,44 +2703,59 @@ __global__ void __launch_bounds__(256, 2) k_stream(StepArgs a, int32_t positions
   const int waves = (int)((gridDim.x * (int64_t)blockDim.x) >> 6);
   const int depth = min(a.max_depth, waves / P);
   const int pos = q.wave % P, phase = q.wave / P;
-  if (phase >= depth) return;
-  const uint32_t tag = *a.epoch;
-  int32_t t = a.first + phase;
-  int32_t nxt = pos, ncnt = positions;
-  if (a.task_list && t < a.t_end) {
-    nxt = a.task_list[(int64_t)t * a.task_stride + pos];
-    ncnt = a.task_cnt[t];
+  // version tag: the launch's seq, never reused by the context, so a granule a
+  // late wave of a failed launch stores can never match a later launch
+  const uint32_t tag = a.seq;
+  const bool gated = *a.gate != 0;  // set by an earlier launch (kernel boundary)
+  int32_t fcnt = 0;
+  if (a.tail) {
+    if ((int)blockIdx.x < a.flushers) fcnt = *a.final_cnt;  // the plan's (an earlier launch)
+    if (blockIdx.x == 0 && threadIdx.x < 9)  // the counter set the previous tail launch used
+      __hip_atomic_store(a.arrive + (a.tail_par ^ 1) * 144 + 16 * threadIdx.x, 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
-  for (; t < a.t_end; t += depth) {
-    const int32_t task = nxt, cnt = ncnt;
-    if (a.task_list && t + depth < a.t_end) {
-      nxt = a.task_list[(int64_t)(t + depth) * a.task_stride + pos];
-      ncnt = a.task_cnt[t + depth];
+  if (a.tail_diag && blockIdx.x == 0 && threadIdx.x == 0) a.tail_diag[0] = __builtin_amdgcn_s_memrealtime();
+  if (phase < depth && !gated) {
+    int32_t t = a.first + phase;
+    int32_t nxt = pos, ncnt = positions;
+    if (a.task_list && t < a.t_end) {
+      nxt = a.task_list[(int64_t)t * a.task_stride + pos];
+      ncnt = a.task_cnt[t];
     }
-    if (pos >= cnt) continue;
-    StepArgs b = a;
-    b.t = t;
-    if (task < a.S) {
-      stream_slot<LPR, NV, TEAM>(b, task, q.m, q.l, q.leader, tag);
-    } else {
-      STAMP(t, task, 0);
-      stream_single<LPR, NV>(b, (task - a.S) * (64 / LPR) + lane / LPR, q.l, tag);
-      STAMP(t, task, 5);
+    for (; t < a.t_end; t += depth) {
+      const int32_t task = nxt, cnt = ncnt;
+      if (a.task_list && t + depth < a.t_end) {
+        nxt = a.task_list[(int64_t)(t + depth) * a.task_stride + pos];
+        ncnt = a.task_cnt[t + depth];
+      }
+      if (pos >= cnt) continue;
+      StepArgs b = a;
+      b.t = t;
+      if (task < a.S) {
+        stream_slot<LPR, NV, TEAM>(b, task, q.m, q.l, q.leader, tag);
+      } else {
+        STAMP(t, task, 0);
+        stream_single<LPR, NV>(b, (task - a.S) * (64 / LPR) + lane / LPR, q.l, tag);
+        STAMP(t, task, 5);
+      }
     }
+  }
+  if (a.tail) {
+    stream_tail<LPR>(a, tag, gated, fcnt);
+  } else if (a.tail_diag && (threadIdx.x & 63) == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    atomicMax(a.tail_diag + 1, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   }
 }
 
-// After k_stream: the last version of every row the launch updated goes to the
-// tables (weights and Adagrad slot); then the epoch moves on.  One lane-group
-// per slot of the range: lane c gathers granules c, c + d/4, c + d/2, c + 3d/4
-// (elements 4c .. 4c+3 in the component-major order) of both versions and
-// stores them as one float4 each, so every slot's loads are in flight at once.
-// A failed launch (a.fail set: some wait gave up) writes nothing: the tables are
-// as before the call.  A verified call (fail_host set) leaves the epoch alone too:
-// the host replays the chunk on the two-kernel schedule, which reads the same
-// call counter and bumps the epoch as this flush would have (stale granules of
-// the failed launch carry the old tag and never match again).  An unverified
-// one bumps it, so the next launch cannot match the failed launch's granules.
+// After a k_stream launch without a tail (a partial range of the plan, a plan
+// without a final-slot list, a captured or timed call): the last version of
+// every row the launch updated goes to the tables (weights and Adagrad slot).
+// One lane-group per slot of the range: lane c gathers granules c, c + d/4,
+// c + d/2, c + 3d/4 (elements 4c .. 4c+3 in the component-major order) of both
+// versions and stores them as one float4 each, so every slot's loads are in
+// flight at once.  A failed launch (a wait gave up: *fail == seq) or a gated one
+// writes nothing; thread 0 decides the call's end as stream_tail's decider does.
 template <int LPR>
 __global__ void __launch_bounds__(256) k_stream_flush(StepArgs a, uint32_t* __restrict__ epoch) {
   constexpr int OPW = 64 / LPR;
@@ -2549,11 +2763,11 @@ __global__ void __launch_bounds__(256) k_stream_flush(StepArgs a, uint32_t* __re
   const int64_t x = (gid >> 6) * OPW + (int64_t)((threadIdx.x & 63) / LPR);
   const int l = (int)(threadIdx.x & (LPR - 1));
   const int64_t n = (int64_t)(a.t_end - a.first) * a.S;
-  const int32_t failed = *a.fail;  // k_stream has ended (kernel boundary)
-  if (gid == 0) {
-    if (!failed || !a.fail_host) atomicAdd(epoch, 1u);  // every k_stream wave has read it
-    if (a.fail_host) *a.fail_host = failed;
-  }
+  // k_stream has ended (kernel boundary); the gate is only set below, by
+  // thread 0, for this same failed call
+  const bool failed = *a.fail == (int32_t)a.seq || *a.gate != 0;
+  (void)epoch;
+  if (gid == 0) stream_decided(a, failed);
   if (failed || x >= n) return;
   const int32_t t = a.first + (int32_t)(x / a.S);
   const int32_t k = (int32_t)(x - (int64_t)(t - a.first) * a.S);
@@ -3576,6 +3790,33 @@ struct GraphKey {
   bool operator<(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
 
+// (r04) Verified streamed calls are checked lazily, without a host sync per
+// call.  Each one is queued on its group's FIFO (the contexts that train the same
+// tables on one stream: a PlanPipeline's two contexts share one group); its
+// launch reports COMMIT / FAIL in the context's host-mapped status ring.  A
+// failed call applied nothing and set the group's gate, so every later streamed
+// launch of the group ran nothing either (and applied nothing).  acf_apr_resolve
+// (and every entry point that needs settled tables or re-plans a context with a
+// queued call) walks the FIFO: committed calls leave it; at the first failed one
+// the gate is cleared and that call and every later queued call are replayed,
+// in order, on the two-kernel schedule, which waits on nothing -- exact, as
+// k_stream is bit-identical to it.  A context keeps its plan while it has a
+// queued call (acf_apr_plan resolves the context's calls first).
+struct acf_apr_ctx;
+struct Pending {
+  acf_apr_ctx* c;
+  uint32_t seq;
+  int32_t first, n;
+  acf_apr_tables tb;
+  acf_apr_hparams hp;
+  hipStream_t s;
+};
+struct FailGroup {
+  int32_t* gate = nullptr;  // device word, see StepArgs.gate
+  std::deque<Pending> q;
+  int refs = 0;
+};
+
 struct acf_apr_ctx {
   int64_t U1 = 0, I1 = 0;
   int32_t d = 0, maxB = 0, maxNB = 0, lpr = 0, nv = 0, R = 0;
@@ -3623,9 +3864,20 @@ struct acf_apr_ctx {
   int32_t poll_sleep = 2;    // ACF_POLL_SLEEP: s_sleep between version polls (0-3; 4/5/6 = 8/16/32)
   int32_t spin_limit = ACF_SPIN_LIMIT;  // k_stream version polls before a give-up (acf_apr_set_spin_limit)
   int32_t failsafe = 1;      // verify every streamed call, replay a failed one (acf_apr_set_failsafe)
-  int32_t* fail_host = nullptr;      // host-mapped failure word of the last streamed call
-  int32_t* fail_host_dev = nullptr;  // its device address
+  unsigned long long* status = nullptr;      // host-mapped ring of 8: (seq << 2) | failed, per streamed launch
+  unsigned long long* status_dev = nullptr;  // its device address
   int64_t recoveries = 0;    // streamed calls replayed on the two-kernel schedule
+  uint32_t seq = 0;          // streamed launches so far (StepArgs.seq)
+  uint32_t last_tail_seq = 0;  // seq of the last launch with a tail (StepArgs.decide_prev)
+  int32_t tail_on = 1;         // ACF_TAIL=0: write-back by k_stream_flush always (A/B)
+  int32_t tail_flushers = 128; // ACF_TAIL_FLUSHERS: workgroups of the tail write-back
+  unsigned long long* tail_diag = nullptr;  // ACF_TAIL_DIAG=1: tail stamps (acf_apr_diag_tail)
+  unsigned long long* decide = nullptr;  // [0] decide word, [16, 16 + 288) the tail's arrival counters
+  uint32_t tail_launches = 0;            // launches with a tail so far (StepArgs.tail_par)
+  FailGroup* grp = nullptr;  // contexts whose streamed calls are verified together (PlanPipeline)
+  int2* final_list = nullptr;  // the batch plan's final slots (k_stream's tail write-back)
+  int32_t* final_cnt = nullptr;
+  int32_t final_ok = 0;        // the current plan wrote final_list
   int32_t stream_ok = -1;    // -1 unknown, 0 unavailable (allocation / occupancy), 1 ready
   int64_t stream_max_waves = 0;
   unsigned long long *ver_w = nullptr, *ver_a = nullptr, *ver_d = nullptr;
@@ -3724,15 +3976,23 @@ extern "C" const char* acf_apr_build_hash(void) { return "ACF_BUILD_HASH=" ACF_B
 
 extern "C" const char* acf_apr_last_error(void) { return g_last_error.c_str(); }
 
+static int resolve(acf_apr_ctx* c, int mode);
+static void leave_group(acf_apr_ctx* c);
+
 extern "C" int acf_apr_destroy(acf_apr_ctx* c) {
   if (!c) return ACF_OK;
+  int r = ACF_OK;
+  if (c->grp) {
+    r = resolve(c, 2);  // the group's queued calls still need this context's plan
+    leave_group(c);
+  }
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   c->graphs.clear();
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
-  if (c->fail_host) (void)hipHostFree(c->fail_host);
+  if (c->status) (void)hipHostFree(c->status);
   delete c;
-  return ACF_OK;
+  return r;
 }
 
 extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t d,
@@ -3774,7 +4034,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->iinfo, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
-  A(&c->err, 4); A(&c->gen_dev, 4); A(&c->epoch, 4);
+  A(&c->err, 4); A(&c->gen_dev, 4); A(&c->epoch, 4); A(&c->decide, 16 + 2 * 144);
   A(&c->g0, 2 * S * d); A(&c->delta, 2 * S * d);  // by batch parity (k_ovl: clean(t+1) beside adv(t))
   A(&c->flags, 3 * maxE);
   A(&c->nextt, 3 * maxE);
@@ -3810,12 +4070,125 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (hipMemset(c->inl, 0, (size_t)maxNB * S * c->R * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->trec, 0, (size_t)maxE * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->gen_dev, 0, 16) != hipSuccess ||
+      hipMemset(c->decide, 0, (16 + 2 * 144) * 8) != hipSuccess ||
       hipMemcpy(c->epoch, &kOne, sizeof(kOne), hipMemcpyHostToDevice) != hipSuccess || hipMemset(c->nextt, 0, 3 * maxE * sizeof(int32_t)) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipMemset failed");
   }
+  if (const char* e = getenv("ACF_TAIL")) c->tail_on = atoi(e) != 0;
+  if (const char* e = getenv("ACF_TAIL_FLUSHERS")) c->tail_flushers = std::max(1, atoi(e));
+  if (const char* e = getenv("ACF_TAIL_DIAG"))
+    if (atoi(e) && dalloc(c, &c->tail_diag, 8) == ACF_OK) (void)hipMemset(c->tail_diag, 0, 64);
+  c->grp = new FailGroup();
+  c->grp->refs = 1;
+  if (hipMalloc(&c->grp->gate, 16) != hipSuccess || hipMemset(c->grp->gate, 0, 16) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    (void)hipGetLastError();
+    acf_apr_destroy(c);
+    return set_error(ACF_E_NOMEM, "failure-gate allocation failed");
+  }
   *out = c;
+  return ACF_OK;
+}
+
+static void leave_group(acf_apr_ctx* c) {
+  FailGroup* g = c->grp;
+  c->grp = nullptr;
+  if (!g) return;
+  for (auto it = g->q.begin(); it != g->q.end();)
+    it = it->c == c ? g->q.erase(it) : it + 1;
+  if (--g->refs == 0) {
+    if (g->gate) (void)hipFree(g->gate);
+    delete g;
+  }
+}
+
+static bool decided(const Pending& p, bool* failed) {
+  const unsigned long long v = *(volatile unsigned long long*)(p.c->status + (p.seq & 7));
+  *failed = (v & 1) != 0;
+  return (v >> 2) == (unsigned long long)p.seq;
+}
+
+static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
+                    int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds,
+                    int allow_overlap, int tri_phases);
+
+// Settle the queued verified streamed calls of c's group (see FailGroup), front
+// to back.  mode 0: only calls that have already reported; 1: block until every
+// call of c itself has been settled; 2: block until the queue is empty.
+static int resolve(acf_apr_ctx* c, int mode) {
+  FailGroup* g = c->grp;
+  if (!g) return ACF_OK;
+  while (!g->q.empty()) {
+    const Pending p = g->q.front();
+    bool failed = false;
+    if (!decided(p, &failed)) {
+      bool need = mode == 2;
+      for (const auto& x : g->q) need = need || (mode == 1 && x.c == c);
+      if (!need) return ACF_OK;
+      HIP_TRY(hipStreamSynchronize(p.s));
+      if (!decided(p, &failed))
+        return set_error(ACF_E_STATE, "streamed call %u reported no outcome", p.seq);
+    }
+    if (!failed) {
+      g->q.pop_front();
+      continue;
+    }
+    // every later queued call ran gated: wait until each has reported, then
+    // clear the gate and replay them all, in order
+    for (const auto& x : g->q) {
+      bool f2 = false;
+      if (!decided(x, &f2)) {
+        HIP_TRY(hipStreamSynchronize(x.s));
+        if (!decided(x, &f2)) return set_error(ACF_E_STATE, "streamed call %u reported no outcome", x.seq);
+      }
+    }
+    std::deque<Pending> todo;
+    todo.swap(g->q);
+    HIP_TRY(hipMemsetAsync(g->gate, 0, sizeof(int32_t), todo.front().s));
+    hipStream_t prev = todo.front().s;
+    for (auto& x : todo) {
+      if (x.s != prev) HIP_TRY(hipStreamSynchronize(prev));  // one stream per group in practice
+      prev = x.s;
+      ACF_RET(run_loop(x.c, &x.tb, &x.hp, x.first, x.n, x.s, nullptr, nullptr, 0, 3));
+      ++x.c->recoveries;
+    }
+  }
+  return ACF_OK;
+}
+
+// diagnostic (ACF_TAIL_DIAG=1, tools/tail_diag.py): the last tail's stamps
+// (s_memrealtime, 100 MHz): [0] kernel start (block 0), [1] last workgroup done,
+// [2] last arrival's add returned, [3] decided, [4] decider's actions issued,
+// [5] last flusher saw the outcome, [6] last flusher wave done; zeroed after reading
+extern "C" int acf_apr_diag_tail(acf_apr_ctx* c, uint64_t* out, void* stream_) {
+  ACF_CHECK(c && out, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(c->tail_diag, ACF_E_STATE, "ACF_TAIL_DIAG was not set when the context was created");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  HIP_TRY(hipMemcpyAsync(out, c->tail_diag, 64, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemsetAsync(c->tail_diag, 0, 64, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_resolve(acf_apr_ctx* c) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  return resolve(c, 2);
+}
+
+extern "C" int acf_apr_share_failsafe(acf_apr_ctx* c, acf_apr_ctx* peer) {
+  ACF_CHECK(c && peer, ACF_E_INVALID, "ctx is NULL");
+  if (c->grp == peer->grp) return ACF_OK;
+  ACF_RET(resolve(c, 2));
+  ACF_RET(resolve(peer, 2));
+  FailGroup* g = c->grp;
+  c->grp = peer->grp;
+  ++c->grp->refs;
+  if (--g->refs == 0) {
+    (void)hipFree(g->gate);
+    delete g;
+  }
   return ACF_OK;
 }
 
@@ -3841,7 +4214,8 @@ static bool bplan_ready(acf_apr_ctx* c) {
   bool ok = A(&c->bmask[0], mask_words) && A(&c->bmask[1], mask_words) &&
             A(&c->slot_of, (size_t)rows * c->maxNB) && A(&c->bkey, (size_t)c->maxNB * S) &&
             A(&c->bstart, (size_t)c->maxNB * (S + 1)) && A(&c->bocc, (size_t)c->maxNB * S) &&
-            A(&c->bn, (size_t)c->maxNB) && A(&c->berr, (size_t)c->maxNB);
+            A(&c->bn, (size_t)c->maxNB) && A(&c->berr, (size_t)c->maxNB) &&
+            A(&c->final_list, (size_t)std::min<int64_t>(rows, (int64_t)c->maxNB * S)) && A(&c->final_cnt, 4);
   ok = ok && hipMemset(c->bmask[0], 0, mask_words * 8) == hipSuccess &&
        hipMemset(c->bmask[1], 0, mask_words * 8) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
   if (!ok) {  // give back what was allocated; the sort plan stays in use
@@ -3851,6 +4225,8 @@ static bool bplan_ready(acf_apr_ctx* c) {
       c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), p));
     }
     c->bmask[0] = c->bmask[1] = nullptr;
+    c->final_list = nullptr;
+    c->final_cnt = nullptr;
     return false;
   }
   c->bmask_words = mask_words;
@@ -3885,6 +4261,7 @@ static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, 
   p.urec = c->urec; p.irec = c->irec; p.inl = c->inl; p.trec = c->trec;
   p.nextt = c->nextt;
   p.task_list = c->task_list; p.task_cnt = c->task_cnt;
+  p.final_list = c->final_list; p.final_cnt = c->final_cnt;
   // 3 occurrences per thread in the sort, one thread per slot / triplet in the
   // build: ~24 us for a 20-batch plan against ~32 us for 6 per thread / 256-thread
   // builds (per-thread loops serialise the build's dependent loads)
@@ -3904,6 +4281,7 @@ static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, 
   c->task_lists = 1;
   c->task_stride = p.stride;
   c->lists = 0;
+  c->final_ok = (int64_t)c->maxNB * 3 * c->maxB < (1ll << 31) ? 1 : 0;
   if (check) {
     int32_t herr = 0;
     HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -3986,9 +4364,11 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   const uint32_t eb_i = ob_i + bits_for((uint64_t)nb * (uint64_t)c->I1);
   const uint32_t eb = std::max(eb_u, eb_i);  // item keys carry bit eb
   ACF_CHECK(eb < 64, ACF_E_INVALID, "plan key does not fit 64 bits");
+  ACF_RET(resolve(c, 1));  // a queued streamed call of this context still needs its plan
   c->B = 0;
   c->nb = 0;
   c->last_delta_batch = -1;
+  c->final_ok = 0;  // set by the batch plan
   const int32_t gen = ++c->gen;
   {
     const int packed = is_packed(c, B);
@@ -4156,9 +4536,13 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.epoch = c->epoch; a.nextt = c->nextt;
   a.task_list = nullptr; a.task_cnt = c->task_cnt; a.task_stride = 0; a.max_depth = 1;
   a.poll_sleep = c->poll_sleep;
-  a.fail = c->err + 1;  // k_stream launches: the call's own word (err + 2)
+  a.fail = c->err + 2;  // seq of a streamed launch that gave up
   a.spin_limit = c->spin_limit;
-  a.fail_host = nullptr;
+  a.seq = 0; a.verify = 0; a.tail = 0; a.flushers = 1; a.decide_prev = 0; a.tail_diag = c->tail_diag;
+  a.gate = c->grp ? c->grp->gate : nullptr;
+  a.decide = c->decide; a.arrive = c->decide + 16; a.tail_par = 0;
+  a.final_list = c->final_list; a.final_cnt = c->final_cnt;
+  a.status = c->status_dev;
   a.hot = c->hot;
   a.hot_part = c->hot_part;
   a.hot_waves = 0;
@@ -4368,8 +4752,8 @@ static int stream_ready(acf_apr_ctx* c, const Kernels& K) {
     (void)hipGetLastError();
     return 0;
   }
-  // the host-mapped failure word the flush reports to (verified calls)
-  if (!c->fail_host) {
+  // the host-mapped status ring the end of a verified call reports to
+  if (!c->status) {
     void* h = nullptr;
     void* dptr = nullptr;
     if (hipHostMalloc(&h, 64, hipHostMallocMapped) != hipSuccess || hipHostGetDevicePointer(&dptr, h, 0) != hipSuccess) {
@@ -4377,9 +4761,9 @@ static int stream_ready(acf_apr_ctx* c, const Kernels& K) {
       if (h) (void)hipHostFree(h);
       return 0;
     }
-    c->fail_host = static_cast<int32_t*>(h);
-    c->fail_host_dev = static_cast<int32_t*>(dptr);
-    *c->fail_host = 0;
+    c->status = static_cast<unsigned long long*>(h);
+    c->status_dev = static_cast<unsigned long long*>(dptr);
+    memset(h, 0, 64);
   }
   c->stream_ok = 1;
   return 1;
@@ -4444,6 +4828,19 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     // resident maximum; otherwise P x depth waves
     const int64_t waves = lists ? c->stream_max_waves
                                 : std::min<int64_t>(c->stream_max_waves, (int64_t)P * c->stream_depth);
+    const int cap = capturing(s);
+    // verified: queued for acf_apr_resolve (no host sync here); a timed or
+    // captured call is unverified (a give-up sets step_err bit 0, the call is dropped)
+    const bool verify = c->failsafe && !events && cap == 0;
+    // the write-back in k_stream's tail: the whole plan in one launch (the final-
+    // slot list is the plan's), and a launch the host counts (not captured)
+    const bool tail = c->tail_on && c->final_ok && first == 0 && n == c->nb && cap == 0;
+    if (verify) {  // at most 8 queued calls per context (its status ring)
+      int mine = 0;
+      for (const auto& x : c->grp->q) mine += x.c == c;
+      if (mine >= 8) ACF_RET(resolve(c, 1));
+    }
+    const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
     StepArgs a = make_args(c, tb, hp, first, 0);
     a.use_single = fuse;
     a.slot_waves = S;
@@ -4453,41 +4850,44 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     a.task_stride = c->task_stride;
     a.max_depth = c->stream_depth;
     a.poll_sleep = c->poll_sleep;
-    a.fail = c->err + 2;  // this call's failure word (zero: reset after every failure)
-    const bool verify = c->failsafe && !events && capturing(s) == 0;
-    a.fail_host = verify ? c->fail_host_dev : nullptr;
+    if (++c->seq == 0) ++c->seq;  // seq 0 is never a launch's (zeroed words)
+    a.seq = c->seq;
+    a.verify = verify ? 1 : 0;
+    if (tail) {
+      a.tail_par = (int32_t)(c->tail_launches++ & 1);
+      a.tail = 1;
+      a.flushers = c->tail_flushers;
+      a.decide_prev = (unsigned long long)c->last_tail_seq << 1;
+      c->last_tail_seq = a.seq;
+    }
     hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
     if (kinds) kinds[li] = 4;
     ++li;
     typedef void (*SK)(StepArgs, int32_t);
-    const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
     if (e0)
       hipExtLaunchKernelGGL(reinterpret_cast<SK>(K.stream), grid, block, 0, s, e0, e1, 0, a, (int32_t)P);
     else
       hipLaunchKernelGGL(reinterpret_cast<SK>(K.stream), grid, block, 0, s, a, (int32_t)P);
     HIP_TRY(hipGetLastError());
-    e0 = events ? events[2 * li] : nullptr;
-    e1 = events ? events[2 * li + 1] : nullptr;
-    if (kinds) kinds[li] = 2;
-    ++li;
-    typedef void (*FK)(StepArgs, uint32_t*);
-    const dim3 fgrid(grid_for((int64_t)n * S * c->lpr));  // one lane-group per slot
-    if (e0)
-      hipExtLaunchKernelGGL(reinterpret_cast<FK>(K.stream_flush), fgrid, block, 0, s, e0, e1, 0, a, c->epoch);
-    else
-      hipLaunchKernelGGL(reinterpret_cast<FK>(K.stream_flush), fgrid, block, 0, s, a, c->epoch);
-    HIP_TRY(hipGetLastError());
-    if (!verify) return ACF_OK;  // a give-up stays in err + 2: acf_apr_step_errors reports it
-    // Verified call: k_stream needs all of its waves resident (another process or
-    // a concurrent persistent kernel on the device can starve its hand-offs).  A
-    // give-up left the tables untouched (gated flush): replay the chunk on the
-    // two-kernel schedule, which waits on nothing.
-    HIP_TRY(hipStreamSynchronize(s));
-    if (*(volatile int32_t*)c->fail_host == 0) return ACF_OK;
-    *(volatile int32_t*)c->fail_host = 0;
-    HIP_TRY(hipMemsetAsync(c->err + 2, 0, sizeof(int32_t), s));
-    ++c->recoveries;
-    return run_loop(c, tb, hp, first, n, s, nullptr, nullptr, 0, tri_phases);
+    if (!tail) {
+      e0 = events ? events[2 * li] : nullptr;
+      e1 = events ? events[2 * li + 1] : nullptr;
+      if (kinds) kinds[li] = 2;
+      ++li;
+      typedef void (*FK)(StepArgs, uint32_t*);
+      const dim3 fgrid(grid_for((int64_t)n * S * c->lpr));  // one lane-group per slot
+      if (e0)
+        hipExtLaunchKernelGGL(reinterpret_cast<FK>(K.stream_flush), fgrid, block, 0, s, e0, e1, 0, a, c->epoch);
+      else
+        hipLaunchKernelGGL(reinterpret_cast<FK>(K.stream_flush), fgrid, block, 0, s, a, c->epoch);
+      HIP_TRY(hipGetLastError());
+    }
+    if (verify) {
+      Pending p;
+      p.c = c; p.seq = a.seq; p.first = first; p.n = n; p.tb = *tb; p.hp = *hp; p.s = s;
+      c->grp->q.push_back(p);
+    }
+    return ACF_OK;
   }
   if (allow_overlap && use_overlap(c, K, hp)) {
     HIP_TRY(hipMemsetAsync(c->flags + (size_t)first * S, 0, (size_t)n * S * sizeof(int32_t), s));
@@ -4587,6 +4987,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
 extern "C" int acf_apr_delta_update(acf_apr_ctx* c, const acf_apr_tables* tb,
                                     const acf_apr_hparams* hp, int32_t t, void* stream_) {
   ACF_RET(check_step(c, tb, hp, t));
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(hp->adver, ACF_E_INVALID, "delta_update needs hparams.adver = 1 (APR graph)");
   hipStream_t s = static_cast<hipStream_t>(stream_);
   if (c->tri) {  // triplet-centric plan: its clean phase
@@ -4607,6 +5008,7 @@ extern "C" int acf_apr_delta_update(acf_apr_ctx* c, const acf_apr_tables* tb,
 extern "C" int acf_apr_optimizer_step(acf_apr_ctx* c, const acf_apr_tables* tb,
                                       const acf_apr_hparams* hp, int32_t t, void* stream_) {
   ACF_RET(check_step(c, tb, hp, t));
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   hipStream_t s = static_cast<hipStream_t>(stream_);
   if (c->tri) {  // triplet-centric plan: its adversarial (or BPR) phase, rows in place
     ACF_CHECK(!hp->adver || c->last_delta_batch == t, ACF_E_STATE,
@@ -4640,12 +5042,13 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   hipStream_t s = static_cast<hipStream_t>(stream_);
   c->last_delta_batch = -1;
   prepare_stream(c, hp);
-  if (!graph_mode) return run_loop(c, tb, hp, first, n, s, nullptr, nullptr);
-  {  // the streamed step is two launches: a graph buys nothing
-    Kernels K;
-    if (get_kernels(c, &K, c->fusion) == ACF_OK && use_stream(c, K, hp))
-      return run_loop(c, tb, hp, first, n, s, nullptr, nullptr);
-  }
+  Kernels K;
+  const bool streamed = get_kernels(c, &K, c->fusion) == ACF_OK && use_stream(c, K, hp);
+  // a streamed call runs gated behind a queued call of the group that may have
+  // failed; any other schedule needs the tables settled first
+  ACF_RET(resolve(c, streamed ? 0 : 2));
+  // the streamed step is one or two launches: a graph buys nothing
+  if (!graph_mode || streamed) return run_loop(c, tb, hp, first, n, s, nullptr, nullptr);
   GraphKey key;
   memset(&key, 0, sizeof(key));
   key.ptrs[0] = tb->P; key.ptrs[1] = tb->Q; key.ptrs[2] = tb->accP; key.ptrs[3] = tb->accQ;
@@ -4685,6 +5088,7 @@ extern "C" int acf_apr_train(acf_apr_ctx* c, const acf_apr_tables* tb, const acf
 static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp, int32_t first,
                         int32_t n, double* ms_out, int32_t* launches_out, void* stream_, int nkinds) {
   ACF_CHECK(c && tb && hp && ms_out && launches_out, ACF_E_INVALID, "NULL argument");
+  ACF_RET(resolve(c, 2));
   ACF_CHECK(n > 0 && first >= 0 && first + n <= c->nb, ACF_E_INVALID,
             "batch range [%d, %d) outside planned range [0, %d)", first, first + n, c->nb);
   ACF_RET(check_step(c, tb, hp, first));
@@ -4722,6 +5126,7 @@ extern "C" int acf_apr_time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb,
 
 extern "C" int acf_apr_set_slot_mapping(acf_apr_ctx* c, int32_t mode) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(mode >= 0 && mode <= 2, ACF_E_INVALID, "slot mapping must be 0 (auto), 1 or 2, got %d", mode);
   c->mapping = mode;
   return ACF_OK;
@@ -4729,6 +5134,7 @@ extern "C" int acf_apr_set_slot_mapping(acf_apr_ctx* c, int32_t mode) {
 
 extern "C" int acf_apr_set_plan_mode(acf_apr_ctx* c, int32_t mode) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(mode == 0 || mode == 1, ACF_E_INVALID, "plan mode must be 0 (auto) or 1 (sort plan)");
   c->plan_mode = mode;
   return ACF_OK;
@@ -4736,6 +5142,7 @@ extern "C" int acf_apr_set_plan_mode(acf_apr_ctx* c, int32_t mode) {
 
 extern "C" int acf_apr_set_fusion(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "fusion must be 0 or 1, got %d", on);
   c->fusion = on;
   return ACF_OK;
@@ -4743,12 +5150,14 @@ extern "C" int acf_apr_set_fusion(acf_apr_ctx* c, int32_t on) {
 
 extern "C" int acf_apr_set_stream(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   c->stream = on != 0;
   return ACF_OK;
 }
 
 extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);
   c->overlap = on;
   return ACF_OK;
@@ -4770,6 +5179,7 @@ extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
 // ---------------------------------------------------------------------------
 extern "C" int acf_apr_set_shard_mode(acf_apr_ctx* c, int32_t on, int32_t reg_batch) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(reg_batch >= 0, ACF_E_INVALID, "reg_batch must be >= 0");
   c->shard = on != 0;
   c->reg_batch = reg_batch;
@@ -4781,6 +5191,7 @@ extern "C" int acf_apr_shard_pass_export(acf_apr_ctx* c, const acf_apr_tables* t
                                          int32_t pass, float* xbuf, const int64_t* xmap, int64_t n_items,
                                          void* stream_) {
   ACF_RET(check_step(c, tb, hp, 0));
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(c->shard && c->lists && c->nb == 1, ACF_E_STATE,
             "shard pass needs shard mode and a one-batch plan");
   ACF_CHECK(pass == 0 || (pass == 1 && hp->adver), ACF_E_INVALID, "pass must be 0, or 1 for APR");
@@ -4856,6 +5267,7 @@ __global__ void k_shard_items(float* __restrict__ g0, float* __restrict__ delta,
 extern "C" int acf_apr_shard_items_mapped(acf_apr_ctx* c, int32_t dir, float* buf, const int64_t* map,
                                           int64_t n_items, void* stream_) {
   ACF_CHECK(c && (buf || n_items == 0), ACF_E_INVALID, "NULL argument");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(c->shard && c->nb == 1, ACF_E_STATE, "shard items need shard mode and a one-batch plan");
   ACF_CHECK(dir == 0 || dir == 1, ACF_E_INVALID, "dir must be 0 or 1");
   ACF_CHECK(n_items >= 0 && n_items <= 2 * (int64_t)c->B, ACF_E_INVALID, "n_items %lld outside [0, 2B]",
@@ -4979,17 +5391,19 @@ extern "C" int acf_shard_reduce_apply(float* Q, float* accQ, const float* recv, 
 
 extern "C" int acf_apr_step_errors(acf_apr_ctx* c, int32_t* out, void* stream_) {
   ACF_CHECK(c && out, ACF_E_INVALID, "NULL argument");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  int32_t w[2] = {0, 0};
-  HIP_TRY(hipMemcpyAsync(w, c->err + 1, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemsetAsync(c->err + 1, 0, 2 * sizeof(int32_t), s));
+  int32_t w = 0;
+  HIP_TRY(hipMemcpyAsync(&w, c->err + 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemsetAsync(c->err + 1, 0, sizeof(int32_t), s));
   HIP_TRY(hipStreamSynchronize(s));
-  *out = w[0] | w[1];  // step waits, and unverified streamed calls that gave up
+  *out = w;  // sticky: step waits that gave up, and unverified streamed calls that did (dropped)
   return ACF_OK;
 }
 
 extern "C" int acf_apr_set_failsafe(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "failsafe must be 0 or 1, got %d", on);
   c->failsafe = on;
   return ACF_OK;
@@ -4997,6 +5411,7 @@ extern "C" int acf_apr_set_failsafe(acf_apr_ctx* c, int32_t on) {
 
 extern "C" int acf_apr_set_spin_limit(acf_apr_ctx* c, int32_t polls) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(polls >= 0, ACF_E_INVALID, "spin limit must be >= 0, got %d", polls);
   c->spin_limit = polls;
   return ACF_OK;
@@ -5004,12 +5419,14 @@ extern "C" int acf_apr_set_spin_limit(acf_apr_ctx* c, int32_t polls) {
 
 extern "C" int acf_apr_stream_recoveries(acf_apr_ctx* c, int64_t* out) {
   ACF_CHECK(c && out, ACF_E_INVALID, "NULL argument");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   *out = c->recoveries;
   return ACF_OK;
 }
 
 extern "C" int acf_apr_copy_losses(acf_apr_ctx* c, float* lc, float* la, void* stream_) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(c->nb > 0, ACF_E_STATE, "no batches planned");
   hipStream_t s = static_cast<hipStream_t>(stream_);
   const size_t n = (size_t)c->B * c->nb * sizeof(float);
@@ -5020,6 +5437,7 @@ extern "C" int acf_apr_copy_losses(acf_apr_ctx* c, float* lc, float* la, void* s
 
 extern "C" int acf_apr_delta_scatter(acf_apr_ctx* c, float* dP, float* dQ, void* stream_) {
   ACF_CHECK(c && dP && dQ, ACF_E_INVALID, "NULL argument");
+  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(c->last_delta_batch >= 0, ACF_E_STATE, "no delta computed since the last step");
   hipStream_t s = static_cast<hipStream_t>(stream_);
   acf_apr_tables tb{nullptr, nullptr, nullptr, nullptr};

@@ -267,12 +267,23 @@ class APRContext:
         call("acf_apr_set_step_overlap", self._ptr, int(bool(on)))
 
     def set_failsafe(self, on: bool) -> None:
-        """Verified streamed steps (default on): each streamed call syncs its stream
-        once and, when a hand-off wait gave up (k_stream needs all its waves
-        resident), replays the chunk on the two-kernel schedule -- exact, the
-        tables are untouched by a failed launch.  Off: calls stay asynchronous and
-        a give-up is reported by step_errors() (the chunk is then not applied)."""
+        """Verified streamed steps (default on): a streamed call stays asynchronous
+        and is queued; if a hand-off wait gave up (k_stream needs all its waves
+        resident), the call applied nothing and gated the later streamed calls of
+        its group, and the next settling point (resolve(), step_errors(),
+        stream_recoveries(), losses(), a re-plan of this context, ...) replays
+        them in order on the two-kernel schedule -- exact.  Off: a give-up is
+        reported by step_errors() and that call is not applied."""
         call("acf_apr_set_failsafe", self._ptr, int(bool(on)))
+
+    def resolve(self) -> None:
+        """Settle the queued streamed calls of this context's group (blocking)."""
+        call("acf_apr_resolve", self._ptr)
+
+    def share_failsafe(self, peer: "APRContext") -> None:
+        """Verify this context's streamed calls together with peer's (contexts
+        training the same tables on one stream)."""
+        call("acf_apr_share_failsafe", self._ptr, peer._ptr)
 
     def set_spin_limit(self, polls: int) -> None:
         """Version polls before a k_stream wait gives up (default 65,536; tests use
@@ -387,10 +398,12 @@ class PlanPipeline:
         self.batch_size, self.chunk = int(batch_size), int(chunk)
         self.ctx = [APRContext(num_user_rows, num_item_rows, dim, batch_size, chunk, self.device)
                     for _ in range(2)]
+        self.ctx[1].share_failsafe(self.ctx[0])  # one verification queue for both (acf_apr.h)
         # default priority: a high-priority plan stream halved the configs[4] rate
         # (608M -> 313M triplets/s at d = 64, tools/large_prio.py, r03)
         self.side = torch.cuda.Stream(self.device)
         self._free = [None, None]  # event: the last training on ctx[k] has been issued before it
+        self._memo = None  # the last single-chunk call, validated (_repeat)
 
     def set_fusion(self, on: bool) -> None:
         for c in self.ctx:
@@ -421,6 +434,9 @@ class PlanPipeline:
     def stream_recoveries(self) -> int:
         return sum(c.stream_recoveries() for c in self.ctx)
 
+    def resolve(self) -> None:
+        self.ctx[0].resolve()
+
     def set_slot_mapping(self, mode) -> None:
         for c in self.ctx:
             c.set_slot_mapping(mode)
@@ -428,6 +444,19 @@ class PlanPipeline:
     def set_plan_mode(self, mode) -> None:
         for c in self.ctx:
             c.set_plan_mode(mode)
+
+    def _remember(self, tables, hp, user, item_pos, item_neg, first_batch, n_batches, graph) -> None:
+        c = self.ctx[0]
+        P, Q, aP, aQ = tables
+        tb, h = c._tables(P, Q, aP, aQ), hp.to_c()
+        off = first_batch * self.batch_size * 4
+        args = (c._ptr, ctypes.byref(tb), ctypes.byref(h), user.data_ptr() + off, item_pos.data_ptr() + off,
+                item_neg.data_ptr() + off, self.batch_size, n_batches, 0, int(bool(graph)))
+        self._memo = (user, item_pos, item_neg, hp, first_batch, n_batches, graph, P, Q, aP, aQ, dict(hp.__dict__),
+                      (P.data_ptr(), Q.data_ptr(), aP.data_ptr(), aQ.data_ptr(), user.data_ptr(),
+                       item_pos.data_ptr(), item_neg.data_ptr(), P.shape, Q.shape, aP.shape, aQ.shape,
+                       user.shape, item_pos.shape, item_neg.shape),
+                      _native.load().acf_apr_train, args, c, tb, h)
 
     def _plan(self, k, u, i, j, b, n, check):
         B, c = self.batch_size, self.ctx[k % 2]
@@ -443,9 +472,36 @@ class PlanPipeline:
             ev.record(self.side)
         return ev
 
+    def _repeat(self, tables, hp, user, item_pos, item_neg, first_batch, n_batches, graph) -> bool:
+        """The exact call the last run made (same tensor objects, storage, shapes
+        and hyper-parameters; one chunk): issue it straight to the C-ABI with the
+        arguments validated then.  Saves the per-call validation (~10 us of host
+        time in front of the first kernel of a short call)."""
+        m = self._memo
+        if not (m[0] is user and m[1] is item_pos and m[2] is item_neg and m[3] is hp and m[4] == first_batch
+                and m[5] == n_batches and m[6] == graph):
+            return False
+        P, Q, aP, aQ = tables
+        if not (P is m[7] and Q is m[8] and aP is m[9] and aQ is m[10] and hp.__dict__ == m[11]
+                and m[12] == (P.data_ptr(), Q.data_ptr(), aP.data_ptr(), aQ.data_ptr(), user.data_ptr(),
+                              item_pos.data_ptr(), item_neg.data_ptr(), P.shape, Q.shape, aP.shape, aQ.shape,
+                              user.shape, item_pos.shape, item_neg.shape)
+                and torch.cuda.current_device() == self.device.index):
+            return False
+        fn, args, ctx = m[13], m[14], m[15]
+        rc = fn(*args, torch.cuda.current_stream(self.device).cuda_stream)
+        if rc:
+            _native.call_failed(rc, "acf_apr_train")
+        ctx._staged = (user, item_pos, item_neg)
+        return True
+
     def run(self, tables, hp: StepHParams, user, item_pos, item_neg, first_batch: int = 0,
             n_batches: int | None = None, graph: bool = True, check: bool = False) -> None:
         """Train batches [first_batch, first_batch + n_batches) of the stream."""
+        if self._memo is not None and not check and self._repeat(tables, hp, user, item_pos, item_neg, first_batch,
+                                                                 n_batches, graph):
+            return
+        self._memo = None
         B = self.batch_size
         u, i, j = (_idx(x, n, self.device) for x, n in ((user, "user"), (item_pos, "item_pos"),
                                                        (item_neg, "item_neg")))
@@ -462,6 +518,8 @@ class PlanPipeline:
             for k, (b, n) in enumerate(chunks):
                 self.ctx[k % 2].train_range(tables, hp, u, i, j, B, b, n, graph=graph, check=check, _checked=True)
             self._staged = (u, i, j)
+            if len(chunks) == 1 and not check and u is user and i is item_pos and j is item_neg:
+                self._remember(tables, hp, user, item_pos, item_neg, first_batch, n_batches, graph)
             return
         if self._ov:
             ready = torch.cuda.Event()

@@ -198,16 +198,31 @@ int acf_apr_set_stream(acf_apr_ctx* ctx, int32_t on);
  * its waves resident; when a hand-off wait gives up (another process or a
  * concurrent persistent kernel on the device), its flush writes nothing, so the
  * tables are as before the call.  failsafe = 1 (default): every streamed call
- * synchronises its stream once at its end and, after a give-up, replays the
- * chunk on the two-kernel schedule (exact: same result as acf_apr_set_stream 0).
- * failsafe = 0: calls stay asynchronous; a give-up is reported by
- * acf_apr_step_errors (bit 0) and the chunk's rows are not applied.
+ * stays asynchronous and is queued for verification; its launch reports its
+ * outcome to host-mapped memory.  A failed call sets the group's gate, so every
+ * later streamed call of the group applies nothing either; the queue is settled
+ * by acf_apr_resolve and, implicitly, by every entry point that needs settled
+ * tables (the setters, acf_apr_step_errors, acf_apr_stream_recoveries,
+ * acf_apr_copy_losses, the two-phase and shard calls, a non-streamed
+ * train_planned) or that re-plans a context with a queued call (acf_apr_plan):
+ * the failed call and every later queued one are replayed, in order, on the
+ * two-kernel schedule (exact: same result as acf_apr_set_stream 0).
+ * failsafe = 0 (and timed or graph-captured calls): a give-up is reported by
+ * acf_apr_step_errors (bit 0, sticky until read) and that call's rows are not
+ * applied; later calls are applied normally.
  * acf_apr_set_spin_limit: version polls before a give-up (default 65,536; 0
  * gives up at the first unready poll -- tests force the replay with it).
  * acf_apr_stream_recoveries: streamed calls replayed so far. */
 int acf_apr_set_failsafe(acf_apr_ctx* ctx, int32_t on);
 int acf_apr_set_spin_limit(acf_apr_ctx* ctx, int32_t polls);
 int acf_apr_stream_recoveries(acf_apr_ctx* ctx, int64_t* out);
+/* Settle every queued verified streamed call of the context's group (blocks
+ * until they have all reported; replays failed ones, see above). */
+int acf_apr_resolve(acf_apr_ctx* ctx);
+/* ctx joins peer's verification group: contexts that train the same tables on
+ * one stream (a PlanPipeline's contexts) must share one, so that a failed call
+ * of either gates the later calls of both.  Settles both groups first. */
+int acf_apr_share_failsafe(acf_apr_ctx* ctx, acf_apr_ctx* peer);
 
 /* ---- shard mode: users and items row-sharded over the ranks of one node ----
  * SURVEY §8(e) (no reference counterpart: the reference trains on one CPU

@@ -744,9 +744,10 @@ def test_step_overlap_kernel_timing_kinds(ops, dev):
 
 @pytest.mark.parametrize("d", [16, 64, 256])
 def test_stream_kernel_timing_kinds(ops, dev, d):
-    """With streamed steps on, train_planned runs ONE k_stream launch plus its
-    write-back for the whole range (time_kernels reports exactly that), and the
-    result equals training."""
+    """With streamed steps on, train_planned runs ONE k_stream launch for the
+    whole plan, its write-back in the launch's tail (time_kernels reports exactly
+    that), and a partial range one k_stream plus a k_stream_flush launch; the
+    results equal training."""
     U1, I1, B, nb = 300, 200, 128, 9
     u, i, j = _sparse_stream(5, U1, I1, B, nb, hot=16, p_hot=0.3)
     rng = np.random.default_rng(1)
@@ -758,8 +759,13 @@ def test_stream_kernel_timing_kinds(ops, dev, d):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ta, tb = _gpu_tables(P, Q, dev), _gpu_tables(P, Q, dev)
     t = ctx.time_kernels(ta, hp)
-    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "ovl": 0, "adv": 0, "flush": 1, "stream": 1, "hot": 0}
+    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "ovl": 0, "adv": 0, "flush": 0, "stream": 1, "hot": 0}
     ctx.train_planned(tb, hp)
+    for x, y in zip(ta, tb):
+        assert torch.equal(x, y)
+    t = ctx.time_kernels(ta, hp, 2, nb - 2)
+    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "ovl": 0, "adv": 0, "flush": 1, "stream": 1, "hot": 0}
+    ctx.train_planned(tb, hp, 2, nb - 2)
     for x, y in zip(ta, tb):
         assert torch.equal(x, y)
     assert ctx.step_errors() == 0
@@ -813,5 +819,76 @@ def test_stream_give_up_replays_exactly(ops, acf, dev, fuse):
     ctx.train_planned(got, hp)
     torch.cuda.synchronize()
     assert ctx.step_errors() == 0 and ctx.stream_recoveries() == before
+    for x, y in zip(ref, got):
+        assert torch.equal(x, y)
+
+
+def test_unverified_give_up_reported_and_next_call_applied(ops, acf, dev):
+    """failsafe off: a streamed call that gives up is dropped and
+    reported; its failure word is the launch's own (seq-tagged), so the NEXT call
+    is applied normally, and the report stays until step_errors() reads it,
+    switching failsafe back on included."""
+    B, nb, d = 512, 12, 64
+    U1, I1, u, i, j = _overlap_stream("ml1m", acf, dev, B, 2 * nb, seed=13)
+    rng = np.random.default_rng(4)
+    P = (rng.standard_normal((U1, d)) * 0.2).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
+    hp = ops.StepHParams(adver=1)
+    first = [torch.tensor(x[:nb * B], device=dev) for x in (u, i, j)]
+    second = [torch.tensor(x[nb * B:], device=dev) for x in (u, i, j)]
+    # reference: the second call's batches alone, on the two-kernel schedule
+    ref = _gpu_tables(P, Q, dev)
+    rctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    rctx.set_stream(False)
+    rctx.plan(*second, B)
+    rctx.train_planned(ref, hp)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_failsafe(False)
+    got = _gpu_tables(P, Q, dev)
+    ctx.set_spin_limit(0)
+    ctx.plan(*first, B)
+    ctx.train_planned(got, hp)  # gives up: dropped
+    ctx.set_spin_limit(1 << 16)
+    ctx.plan(*second, B)
+    ctx.train_planned(got, hp)  # applied
+    torch.cuda.synchronize()
+    for x, y in zip(ref, got):
+        assert torch.equal(x, y)
+    ctx.set_failsafe(True)
+    assert ctx.step_errors() & 1  # the first call's report survived the second call and the toggle
+    assert ctx.step_errors() == 0 and ctx.stream_recoveries() == 0
+
+
+def test_pipeline_failed_chunks_gate_and_replay(ops, acf, dev):
+    """Verified calls without a host sync: with a spin limit of 0 every streamed
+    chunk of a PlanPipeline gives up; the first failure gates the later chunks
+    of both contexts, and the re-plan of a context (and the final settling)
+    replays them in order -- the tables equal the two-kernel schedule's bits."""
+    B, chunk, nb, d = 512, 4, 12, 64
+    U1, I1, u, i, j = _overlap_stream("ml1m", acf, dev, B, nb, seed=17)
+    rng = np.random.default_rng(5)
+    P = (rng.standard_normal((U1, d)) * 0.2).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
+    hp = ops.StepHParams(adver=1, reg=0.01)
+    tu, ti, tj = (torch.tensor(x, device=dev) for x in (u, i, j))
+    ref = _gpu_tables(P, Q, dev)
+    rp = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False)
+    rp.set_stream(False)
+    rp.run(ref, hp, tu, ti, tj)
+    pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False)
+    pipe.set_spin_limit(0)
+    got = _gpu_tables(P, Q, dev)
+    pipe.run(got, hp, tu, ti, tj)
+    pipe.resolve()
+    assert pipe.stream_recoveries() == nb // chunk
+    assert pipe.step_errors() == 0
+    for x, y in zip(ref, got):
+        assert torch.equal(x, y)
+    # and with a normal limit: nothing replayed, the same bits
+    pipe.set_spin_limit(1 << 16)
+    got = _gpu_tables(P, Q, dev)
+    pipe.run(got, hp, tu, ti, tj)
+    torch.cuda.synchronize()
+    assert pipe.stream_recoveries() == nb // chunk and pipe.step_errors() == 0
     for x, y in zip(ref, got):
         assert torch.equal(x, y)
