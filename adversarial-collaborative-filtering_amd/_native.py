@@ -71,7 +71,8 @@ SIGNATURES = {
                                        _P, _P, _P]),
     "acf_eval_positions_all": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I32, _I32, _P, _P, _P,
                                               _P]),
-    "acf_eval_set_kernel": (ctypes.c_int, [_I32]),
+    "acf_eval_positions_all_kernel": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I32, _I32, _P, _P, _P,
+                                                     _I32, _P]),
     "acf_eval_positions_list": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P]),
     "acf_sample_epoch": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P, _U64, _I32, _I32, _P, _P,
                                         _P, _P]),

@@ -535,23 +535,27 @@ __device__ __forceinline__ void records_one(int64_t e, int32_t t, int32_t ub0, i
   r.pb_slot = kj | (info_count(J) == 1 ? ACF_SOLO_BIT : 0);
   r.gen = gen;
   // the CSR records (occurrences past the first R) are read by the slot kernels
-  // only: the triplet-centric step reads a slot's first record and trec
+  // only: the triplet-centric step reads a shared slot's first record (its
+  // combine) and trec -- a single row's slot is read by nothing (its triplet
+  // steps it from trec), so tri plans write neither its record nor its slot
+  // flags (0, the cleared value: not listed, written in place), ~60% of
+  // k_records' scattered 48-B stores at configs[4]
   const int64_t base = (int64_t)t * S;
   int32_t rr = ps.x - U.w;
-  if (rr < R) inl[(base + k) * R + rr] = r;
+  if (rr < R) { if (!(tri && su)) inl[(base + k) * R + rr] = r; }
   else if (!tri) urec[ps.x] = r;
   const OccRec ri = item_rec(I, J, U, (int32_t)(2 * e), k, kj, xi, f.in_i, gen);
   rr = ps.y - I.w;
-  if (rr < R) inl[(base + ki) * R + rr] = ri;
+  if (rr < R) { if (!(tri && si)) inl[(base + ki) * R + rr] = ri; }
   else if (!tri) irec[ps.y] = ri;
   const OccRec rj = item_rec(J, I, U, (int32_t)(2 * e + 1), k, ki, xj, f.in_j, gen);
   rr = ps.z - J.w;
-  if (rr < R) inl[(base + kj) * R + rr] = rj;
+  if (rr < R) { if (!(tri && sj)) inl[(base + kj) * R + rr] = rj; }
   else if (!tri) irec[ps.z] = rj;
   if (sflags) {  // packed plans: the slot flags and hot lists, from each slot's first occurrence
-    if (ps.x == U.w) slot_flag(sflags, hl, t, S, k, info_count(U), xu, f.in_u);
-    if (ps.y == I.w) slot_flag(sflags, hl, t, S, ki, info_count(I), xi, f.in_i);
-    if (ps.z == J.w) slot_flag(sflags, hl, t, S, kj, info_count(J), xj, f.in_j);
+    if (ps.x == U.w && !(tri && su)) slot_flag(sflags, hl, t, S, k, info_count(U), xu, f.in_u);
+    if (ps.y == I.w && !(tri && si)) slot_flag(sflags, hl, t, S, ki, info_count(I), xi, f.in_i);
+    if (ps.z == J.w && !(tri && sj)) slot_flag(sflags, hl, t, S, kj, info_count(J), xj, f.in_j);
   }
   if (f.fused || tri) {  // other triplets' records read as absent (older generation)
     OccRec q;
@@ -3454,7 +3458,6 @@ __device__ __forceinline__ float seq_dot(const float* __restrict__ p, const floa
 }
 
 constexpr int EVAL_UB = 8;  // users per workgroup
-static int g_eval_valu = 0;  // acf_eval_set_kernel
 
 __global__ void __launch_bounds__(256) k_eval_all(const float* __restrict__ P,
                                                   const float* __restrict__ Q, int d,
@@ -3508,7 +3511,9 @@ __global__ void __launch_bounds__(256) k_eval_all(const float* __restrict__ P,
   for (int uu = 0; uu < nu; ++uu) {
     const int64_t a0 = excl_off[u0 + uu], a1 = excl_off[u0 + uu + 1];
     for (int64_t x = a0 + threadIdx.x; x < a1; x += blockDim.x) {
-      const float s = seq_dot(smem + uu * d, Q + (int64_t)excl[x] * d, d);
+      const int32_t it = excl[x];
+      if (it < 0 || it >= num_cand) continue;  // never a candidate, never counted
+      const float s = seq_dot(smem + uu * d, Q + (int64_t)it * d, d);
       cnt[uu] -= s >= s_test[uu] ? 1 : 0;
     }
   }
@@ -3530,53 +3535,56 @@ __global__ void __launch_bounds__(256) k_eval_all(const float* __restrict__ P,
 // s_mfma - E > t is counted, one with s_mfma + E < t is not, and the rare one in
 // between is rescored with seq_dot and compared exactly.  Positions are
 // therefore bit-identical to k_eval_all's.
-__global__ void __launch_bounds__(256) k_eval_prep(const float* __restrict__ P, const float* __restrict__ Q, int d,
-                                                   const int32_t* __restrict__ users,
-                                                   const int32_t* __restrict__ tests, int n_users, int num_cand,
-                                                   float* __restrict__ tscore, float* __restrict__ pnorm,
-                                                   float* __restrict__ qnorm) {
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  auto norm = [&](const float* r) {
-    double ss = 0.0;
-    for (int k = 0; k < d; ++k) ss += (double)r[k] * (double)r[k];
-    return (float)(sqrt(ss) * (1.0 + 1e-6));  // rounded up
-  };
-  if (x < n_users) {
-    const float* p = P + (int64_t)users[x] * d;
-    tscore[x] = seq_dot(p, Q + (int64_t)tests[x] * d, d);
-    pnorm[x] = norm(p);
-  }
-  if (x < num_cand) qnorm[x] = norm(Q + x * d);
-}
-
 constexpr int EVM_U = 64, EVM_C = 128, EVM_KC = 32;
 
-__global__ void __launch_bounds__(256) k_eval_mfma(const float* __restrict__ P, const float* __restrict__ Q, int d,
-                                                   const int32_t* __restrict__ users, int n_users, int num_cand,
-                                                   const float* __restrict__ tscore, const float* __restrict__ pnorm,
-                                                   const float* __restrict__ qnorm, float eb, float floor_e,
-                                                   int32_t* __restrict__ positions) {
+// (r04) The whole ranking is ONE kernel (after a memset of the positions): each
+// workgroup forms what it needs itself -- the test scores of its 64 users
+// (seq_dot, the exact reference rounding), the norms of its 64 users and 128
+// candidates (double sums of the tiles it stages anyway, rounded up) -- and
+// applies the exclusion lists as a bitmap of its 128-candidate window per user
+// (set semantics, as utils.py:209-214 builds item_input: set(range(num_items))
+// - set(trainList[u]) - {test}), so no excluded candidate is counted and no
+// exclusion score is computed.  (r03 ran a prep kernel, the sweep and an
+// exclusion-correction kernel that rescored every trainList item with seq_dot.)
+__global__ void __launch_bounds__(256) k_eval_fused(const float* __restrict__ P, const float* __restrict__ Q, int d,
+                                                    const int32_t* __restrict__ users,
+                                                    const int32_t* __restrict__ tests, int n_users, int num_cand,
+                                                    const int64_t* __restrict__ excl_off,
+                                                    const int32_t* __restrict__ excl, float eb, float floor_e,
+                                                    int32_t* __restrict__ positions) {
   __shared__ float sP[EVM_U][EVM_KC + 1];
   __shared__ float sQ[EVM_C][EVM_KC + 1];
   __shared__ int s_cnt[EVM_U];
-  __shared__ float s_t[EVM_U], s_pn[EVM_U];
+  __shared__ float s_t[EVM_U], s_pn[EVM_U], s_qn[EVM_C];
   __shared__ int32_t s_row[EVM_U];
+  __shared__ uint32_t s_ex[EVM_U][EVM_C / 32];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63;
   const int u0 = blockIdx.y * EVM_U, c0 = blockIdx.x * EVM_C;
+  float tsc = 0.f;
   if (tid < EVM_U) {
     const bool ok = u0 + tid < n_users;
     s_cnt[tid] = 0;
     s_row[tid] = ok ? users[u0 + tid] : -1;
-    s_t[tid] = ok ? tscore[u0 + tid] : 0.f;
-    s_pn[tid] = ok ? pnorm[u0 + tid] : 0.f;
+    if (ok) tsc = seq_dot(P + (int64_t)users[u0 + tid] * d, Q + (int64_t)tests[u0 + tid] * d, d);
   }
+  for (int x = tid; x < EVM_U * (EVM_C / 32); x += 256) (&s_ex[0][0])[x] = 0u;
+  __syncthreads();
+  // exclusion bitmap of the window [c0, c0 + 128): wave w scans users w, w + 4, ...
+  for (int ur = wave; ur < EVM_U && u0 + ur < n_users; ur += 4) {
+    const int64_t a0 = excl_off[u0 + ur], a1 = excl_off[u0 + ur + 1];
+    for (int64_t x = a0 + l; x < a1; x += 64) {
+      const int32_t it = excl[x] - c0;
+      if (it >= 0 && it < EVM_C) atomicOr(&s_ex[ur][it >> 5], 1u << (it & 31));
+    }
+  }
+  double ss = 0.0;  // tid < 64: user tid's squared norm; 64 <= tid < 192: candidate tid - 64's
   f32x4 acc[4][2];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < 2; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int k0 = 0; k0 < d; k0 += EVM_KC) {
-    __syncthreads();  // s_row (first pass) / the previous chunk's reads
+    __syncthreads();  // the previous chunk's reads
     constexpr int C4 = EVM_KC / 4;
 #pragma unroll
     for (int j = 0; j < EVM_U * C4 / 256; ++j) {
@@ -3596,6 +3604,11 @@ __global__ void __launch_bounds__(256) k_eval_mfma(const float* __restrict__ P, 
     }
     __syncthreads();
     const int kend = min(EVM_KC, d - k0);
+    if (tid < EVM_U) {
+      for (int k = 0; k < kend; ++k) ss += (double)sP[tid][k] * (double)sP[tid][k];
+    } else if (tid < EVM_U + EVM_C) {
+      for (int k = 0; k < kend; ++k) ss += (double)sQ[tid - EVM_U][k] * (double)sQ[tid - EVM_U][k];
+    }
     for (int kk = 0; kk < kend; kk += 4) {
       float a[4], b[2];
 #pragma unroll
@@ -3608,14 +3621,17 @@ __global__ void __launch_bounds__(256) k_eval_mfma(const float* __restrict__ P, 
         for (int c = 0; c < 2; ++c) acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[r], b[c], acc[r][c], 0, 0, 0);
     }
   }
-  // epilogue: lane l holds users 16r + 4(l >> 4) + reg, candidate 16c + (l & 15)
-  float qn[2];
-  int cand[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    cand[c] = c0 + wave * 32 + 16 * c + (l & 15);
-    qn[c] = cand[c] < num_cand ? qnorm[cand[c]] : 0.f;
+  if (tid < EVM_U) {
+    s_t[tid] = tsc;
+    s_pn[tid] = (float)(sqrt(ss) * (1.0 + 1e-6));  // rounded up
+  } else if (tid < EVM_U + EVM_C) {
+    s_qn[tid - EVM_U] = (float)(sqrt(ss) * (1.0 + 1e-6));
   }
+  __syncthreads();
+  // epilogue: lane l holds users 16r + 4(l >> 4) + reg, candidate 16c + (l & 15)
+  int cl[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) cl[c] = wave * 32 + 16 * c + (l & 15);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -3626,13 +3642,14 @@ __global__ void __launch_bounds__(256) k_eval_mfma(const float* __restrict__ P, 
         const float t = s_t[ur];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          if (cand[c] >= num_cand) continue;
+          const int cand = c0 + cl[c];
+          if (cand >= num_cand || ((s_ex[ur][cl[c] >> 5] >> (cl[c] & 31)) & 1u)) continue;
           const float sm = acc[r][c][reg];
-          const float e = eb * s_pn[ur] * qn[c] + floor_e;
+          const float e = eb * s_pn[ur] * s_qn[cl[c]] + floor_e;
           if (sm - e > t) {
             ++cnt;
           } else if (sm + e >= t) {  // within the error band: the exact score decides
-            cnt += seq_dot(P + (int64_t)s_row[ur] * d, Q + (int64_t)cand[c] * d, d) >= t ? 1 : 0;
+            cnt += seq_dot(P + (int64_t)s_row[ur] * d, Q + (int64_t)cand * d, d) >= t ? 1 : 0;
           }
         }
       }
@@ -3643,28 +3660,6 @@ __global__ void __launch_bounds__(256) k_eval_mfma(const float* __restrict__ P, 
   }
   __syncthreads();
   if (tid < EVM_U && s_cnt[tid]) atomicAdd(positions + u0 + tid, s_cnt[tid]);
-}
-
-// the exclusion correction of k_eval_mfma's counts (trainList[u] and the test
-// item, utils.py:211-215): one wave per user, exact seq_dot scores
-__global__ void __launch_bounds__(256) k_eval_excl(const float* __restrict__ P, const float* __restrict__ Q, int d,
-                                                   const int32_t* __restrict__ users, int n_users, int num_cand,
-                                                   const float* __restrict__ tscore,
-                                                   const int64_t* __restrict__ excl_off,
-                                                   const int32_t* __restrict__ excl, int32_t* __restrict__ positions) {
-  const int64_t w = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int l = threadIdx.x & 63;
-  if (w >= n_users) return;
-  const float* p = P + (int64_t)users[w] * d;
-  const float t = tscore[w];
-  int cnt = 0;
-  for (int64_t x = excl_off[w] + l; x < excl_off[w + 1]; x += 64) {
-    const int32_t it = excl[x];
-    if (it >= 0 && it < num_cand) cnt += seq_dot(p, Q + (int64_t)it * d, d) >= t ? 1 : 0;
-  }
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) cnt += __shfl_xor(cnt, m, 64);
-  if (l == 0 && cnt) positions[w] -= cnt;
 }
 
 __global__ void __launch_bounds__(256) k_eval_list(const float* __restrict__ P,
@@ -5469,47 +5464,55 @@ extern "C" int acf_bpr_forward(const float* P, const float* Q, int64_t U1, int64
   return ACF_OK;
 }
 
-extern "C" int acf_eval_positions_all(const float* P, const float* Q, int64_t U1, int64_t I1,
-                                      int32_t d, const int32_t* users, const int32_t* tests,
-                                      int32_t n_users, int32_t num_cand, const int64_t* excl_off,
-                                      const int32_t* excl, int32_t* positions, void* stream_) {
+// kernel: 0 auto (ACF_EVAL_AUTO_VALU_PAIRS), 1 the fused MFMA sweep, 2 the VALU
+// sweep k_eval_all (A/B and tests); positions are identical.
+#define ACF_EVAL_VALU_PAIRS 0  // auto: the VALU sweep below this many user x candidate pairs
+
+static int eval_positions_all(const float* P, const float* Q, int64_t U1, int64_t I1, int32_t d,
+                              const int32_t* users, const int32_t* tests, int32_t n_users, int32_t num_cand,
+                              const int64_t* excl_off, const int32_t* excl, int32_t* positions, int32_t kernel,
+                              void* stream_) {
   ACF_RET(check_dim(d));
   ACF_CHECK(P && Q && users && tests && excl_off && positions, ACF_E_INVALID, "NULL argument");
   ACF_CHECK(num_cand >= 0 && num_cand <= I1, ACF_E_INVALID, "num_candidates %d > item rows", num_cand);
+  ACF_CHECK(kernel >= 0 && kernel <= 2, ACF_E_INVALID, "kernel must be 0 (auto), 1 (MFMA) or 2 (VALU), got %d",
+            kernel);
   if (n_users <= 0) return ACF_OK;
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  if (g_eval_valu) {  // the VALU sweep (acf_eval_set_kernel(0): A/B only)
+  if (kernel == 0) kernel = (int64_t)n_users * num_cand < ACF_EVAL_VALU_PAIRS ? 2 : 1;
+  if (kernel == 2) {
     const size_t lds = (size_t)EVAL_UB * d * sizeof(float);
     k_eval_all<<<(n_users + EVAL_UB - 1) / EVAL_UB, 256, lds, s>>>(P, Q, d, users, tests, n_users,
                                                                     num_cand, excl_off, excl, positions);
     HIP_TRY(hipGetLastError());
     return ACF_OK;
   }
-  float* scr = nullptr;
-  const size_t nf = 2 * (size_t)n_users + (size_t)std::max(num_cand, 1);
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scr), nf * sizeof(float), s));
-  float *tscore = scr, *pnorm = scr + n_users, *qnorm = scr + 2 * (size_t)n_users;
   HIP_TRY(hipMemsetAsync(positions, 0, (size_t)n_users * sizeof(int32_t), s));
-  k_eval_prep<<<grid_for(std::max<int64_t>(n_users, num_cand)), 256, 0, s>>>(P, Q, d, users, tests, n_users,
-                                                                            num_cand, tscore, pnorm, qnorm);
   if (num_cand > 0) {
     const float eb = 4.0f * (float)(d + 2) * 5.9604645e-8f;  // 4 (d + 2) 2^-24
     const float floor_e = (float)d * 1.1754944e-38f * 4.0f;   // denormal products flushed by MFMA
     const dim3 grid((unsigned)((num_cand + EVM_C - 1) / EVM_C), (unsigned)((n_users + EVM_U - 1) / EVM_U));
-    k_eval_mfma<<<grid, 256, 0, s>>>(P, Q, d, users, n_users, num_cand, tscore, pnorm, qnorm, eb, floor_e,
-                                     positions);
+    k_eval_fused<<<grid, 256, 0, s>>>(P, Q, d, users, tests, n_users, num_cand, excl_off, excl, eb, floor_e,
+                                      positions);
   }
-  k_eval_excl<<<grid_for((int64_t)n_users * 64), 256, 0, s>>>(P, Q, d, users, n_users, num_cand, tscore, excl_off,
-                                                               excl, positions);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipFreeAsync(scr, s));
   return ACF_OK;
 }
 
-// test / A-B only: 1 (default) the MFMA sweep, 0 the VALU sweep k_eval_all
-extern "C" int acf_eval_set_kernel(int32_t mfma) {
-  g_eval_valu = mfma ? 0 : 1;
-  return ACF_OK;
+extern "C" int acf_eval_positions_all(const float* P, const float* Q, int64_t U1, int64_t I1,
+                                      int32_t d, const int32_t* users, const int32_t* tests,
+                                      int32_t n_users, int32_t num_cand, const int64_t* excl_off,
+                                      const int32_t* excl, int32_t* positions, void* stream_) {
+  return eval_positions_all(P, Q, U1, I1, d, users, tests, n_users, num_cand, excl_off, excl, positions, 0,
+                            stream_);
+}
+
+extern "C" int acf_eval_positions_all_kernel(const float* P, const float* Q, int64_t U1, int64_t I1, int32_t d,
+                                             const int32_t* users, const int32_t* tests, int32_t n_users,
+                                             int32_t num_cand, const int64_t* excl_off, const int32_t* excl,
+                                             int32_t* positions, int32_t kernel, void* stream_) {
+  return eval_positions_all(P, Q, U1, I1, d, users, tests, n_users, num_cand, excl_off, excl, positions, kernel,
+                            stream_);
 }
 
 extern "C" int acf_eval_positions_list(const float* P, const float* Q, int64_t U1, int64_t I1,

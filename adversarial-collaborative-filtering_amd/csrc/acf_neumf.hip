@@ -39,7 +39,9 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -1025,11 +1027,13 @@ __global__ void __launch_bounds__(256) k_nmf_adam(float4* __restrict__ p, float4
 //                     of the rows brought to iteration t, so no row is more than
 //                     LAZY_S iterations behind; after the call's last step, every
 //                     row (caller's stream).
-constexpr int LAZY_S = 8;   // catch-up period: a row is at most LAZY_S iterations behind
-constexpr int LAZY_W = 16;  // lr_t window (> LAZY_S)
+// catch-up period (acf_neumf_ctx::lazy_s, default LAZY_S; ACF_NMF_LAZY_S for A/B):
+// a row is at most lazy_s iterations behind; a step's slice is 1/lazy_s of the rows
+constexpr int LAZY_S = 8;
+constexpr int LAZY_W = 32;  // lr_t window (> the catch-up period)
 // workgroups of a step's catch-up slice, beside the step's kernels (yelp shape,
-// d 64, B 512: 32 WGs 3.9M instances/s (the slice outlasts the step), 64 5.6M,
-// 96 7.55M, 128 7.3M, 192 7.45M, 256 7.35M)
+// d 64, B 512, period 8: 32 WGs 3.9M instances/s (the slice outlasts the step),
+// 64 5.6M, 96 7.55M, 128 7.3M, 192 7.45M, 256 7.35M); ACF_NMF_CATCHUP_WG for A/B
 constexpr int64_t CATCHUP_WG = 96;
 static_assert(LAZY_W > LAZY_S, "lr window");
 
@@ -1231,6 +1235,8 @@ struct acf_neumf_ctx {
   int32_t *last_u = nullptr, *last_i = nullptr, *pend_u = nullptr, *pend_i = nullptr;
   hipStream_t side = nullptr;
   hipEvent_t ev_next = nullptr, ev_rest = nullptr;
+  int32_t lazy_s = LAZY_S;           // catch-up period (< LAZY_W)
+  int64_t catchup_wg = CATCHUP_WG;   // workgroups of a catch-up slice
   std::vector<void*> allocs;
 };
 
@@ -1284,6 +1290,8 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
   if (r != ACF_OK) return r;
   ACF_CHECK(maxB > 0 && maxB <= (1 << 24), ACF_E_INVALID, "max_batch must be in (0, 2^24], got %d", maxB);
   acf_neumf_ctx* c = new acf_neumf_ctx();
+  if (const char* e = getenv("ACF_NMF_LAZY_S")) c->lazy_s = std::min(std::max(1, atoi(e)), LAZY_W - 1);
+  if (const char* e = getenv("ACF_NMF_CATCHUP_WG")) c->catchup_wg = std::max(1, atoi(e));
   c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB;
   c->L = make_layout(U1, I1, d);
   const size_t B = (size_t)maxB, dd = (size_t)d;
@@ -1489,7 +1497,7 @@ extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, f
   auto rows_grid = [&](int64_t rows, int64_t cap) {
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>((rows * lpr + 255) / 256, cap));
   };
-  const int64_t slice = (nrows + LAZY_S - 1) / LAZY_S;
+  const int64_t slice = (nrows + c->lazy_s - 1) / c->lazy_s;
   bool side_pending = false;
   AdamK ak{};
   int64_t k = 0;
@@ -1527,11 +1535,11 @@ extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, f
     HIP_TRY(hipGetLastError());
     side_pending = false;
     if (Bn > 0) {  // slice k % LAZY_S of the rows, beside step k+1
-      const int64_t lo = (k % LAZY_S) * slice, hi = std::min<int64_t>(lo + slice, nrows);
+      const int64_t lo = (k % c->lazy_s) * slice, hi = std::min<int64_t>(lo + slice, nrows);
       if (lo < hi) {
         HIP_TRY(hipEventRecord(c->ev_next, s));
         HIP_TRY(hipStreamWaitEvent(c->side, c->ev_next, 0));
-        k_nmf_adam_catchup<<<rows_grid(hi - lo, CATCHUP_WG), 256, 0, c->side>>>(P4, G4, m4, v4, ak, z, lo, hi);
+        k_nmf_adam_catchup<<<rows_grid(hi - lo, c->catchup_wg), 256, 0, c->side>>>(P4, G4, m4, v4, ak, z, lo, hi);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev_rest, c->side));
         side_pending = true;

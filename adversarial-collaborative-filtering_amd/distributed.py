@@ -562,7 +562,12 @@ class ShardedAPR:
         triplets only, local_batch per batch).  Returns the batches run.
 
         On a GPU the routing of chunk k + 1 runs on a side stream while chunk k's
-        steps run on the caller's stream (the two chunks use the two map sets)."""
+        steps run on the caller's stream (the two chunks use the two map sets).
+        That overlap is complete only at world 1: above it, the routing's count
+        and row all_to_alls go through the same process group as chunk k's step
+        collectives, so they queue behind them (and the routing's host copy of
+        the counts waits for most of chunk k); the split-step figures of DESIGN
+        §7 are world-1 measurements."""
         bs = self.b_max if self.routed else self.B
         n = len(u) // bs
         spans = [(c0, min(chunk, n - c0)) for c0 in range(0, n, chunk)]

@@ -94,12 +94,13 @@ def init_eval_model(dataset, args, users=None, twin=False):
     return EvalPlan("sample", users, tests, n_neg, K, cand_off=co, cand=cand)
 
 
-def positions(P, Q, plan: EvalPlan):
-    """Per-user position (#candidates scoring >= the test item), on the GPU."""
+def positions(P, Q, plan: EvalPlan, kernel: str = "auto"):
+    """Per-user position (#candidates scoring >= the test item), on the GPU
+    (kernel: the all-items sweep, ops.eval_positions_all)."""
     dev = P.device
     u, t, o, c = plan.device_arrays(dev)
     if plan.mode == "all":
-        return ops.eval_positions_all(P, Q, u, t, plan.num_candidates, o, c)
+        return ops.eval_positions_all(P, Q, u, t, plan.num_candidates, o, c, kernel=kernel)
     return ops.eval_positions_list(P, Q, u, t, o, c)
 
 

@@ -566,14 +566,31 @@ def bpr_forward(P, Q, user, item_pos, item_neg, batch_size: int, clip_lo=CLIP_LO
     return bl, bc, op, on
 
 
+_RANGE_OK: dict = {}  # index tensors already range-checked, by (storage, version, bound)
+
+
 def _check_range(idx: torch.Tensor, rows: int, name: str) -> None:
+    """IndexError unless every index lies in [0, rows).  The check reads the
+    extremes back to the host (a device sync), so a tensor that passed is
+    remembered by (address, length, in-place version, bound): an evaluation plan
+    re-uses the same user / test tensors every epoch and pays the check once."""
+    key = (idx.data_ptr(), idx.numel(), idx._version, rows, idx.device)
+    if _RANGE_OK.get(key) is idx:
+        return
     if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= rows):
         raise _native.NativeIndexError(_native.ACF_E_RANGE, "range check",
                                        f"{name} index outside [0, {rows})")
+    if len(_RANGE_OK) > 64:
+        _RANGE_OK.clear()
+    _RANGE_OK[key] = idx
 
 
-def eval_positions_all(P, Q, users, test_items, num_candidates: int, excl_off, excl_items):
-    """_eval_by_user positions over all items minus the exclusion lists."""
+EVAL_KERNELS = {"auto": 0, "mfma": 1, "valu": 2}
+
+
+def eval_positions_all(P, Q, users, test_items, num_candidates: int, excl_off, excl_items, kernel: str = "auto"):
+    """_eval_by_user positions over all items minus the exclusion lists.  kernel:
+    'auto' | 'mfma' | 'valu' (acf_eval_positions_all_kernel; same positions)."""
     dev = P.device
     _require(P, "embedding_P", torch.float32, None, 2)
     _require(Q, "embedding_Q", torch.float32, dev, 2)
@@ -582,15 +599,17 @@ def eval_positions_all(P, Q, users, test_items, num_candidates: int, excl_off, e
     ex = _idx(excl_items, "excl_items", dev) if len(excl_items) else torch.zeros(1, dtype=torch.int32, device=dev)
     if off.numel() != u.numel() + 1:
         raise ValueError("excl_off must have len(users) + 1 entries")
+    if kernel not in EVAL_KERNELS:
+        raise ValueError(f"kernel must be one of {sorted(EVAL_KERNELS)}, got {kernel!r}")
     _check_range(u, P.shape[0], "user")
     _check_range(t, Q.shape[0], "test item")
     if num_candidates > Q.shape[0]:
         raise ValueError("num_candidates exceeds item rows")
     pos = torch.empty(u.numel(), dtype=torch.int32, device=dev)
-    with torch.cuda.device(dev):
-        call("acf_eval_positions_all", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
+    with _on(dev):
+        call("acf_eval_positions_all_kernel", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
              u.data_ptr(), t.data_ptr(), u.numel(), int(num_candidates), off.data_ptr(), ex.data_ptr(),
-             pos.data_ptr(), _stream_ptr(dev))
+             pos.data_ptr(), EVAL_KERNELS[kernel], _stream_ptr(dev))
     return pos
 
 

@@ -326,11 +326,17 @@ int acf_eval_positions_list(const float* P, const float* Q, int64_t num_user_row
                             const int64_t* cand_off, const int32_t* cand_items,
                             int32_t* positions, void* stream);
 
-/* Test / A-B only: 1 (default) acf_eval_positions_all sweeps the scores on MFMA
- * (v_mfma_f32_16x16x4_f32 tiles, exact rescoring of candidates within the f32
- * error band of the test score: positions identical to the VALU sweep); 0 the
- * VALU sweep.  Process-wide. */
-int acf_eval_set_kernel(int32_t mfma);
+/* acf_eval_positions_all with the sweep chosen per call: kernel 0 = auto (what
+ * acf_eval_positions_all runs), 1 = the MFMA sweep (one kernel:
+ * v_mfma_f32_16x16x4_f32 tiles, exact rescoring of candidates within the f32
+ * error band of the test score, exclusions as a per-tile bitmap), 2 = the VALU
+ * sweep.  Positions are identical for every kernel; no process-wide state. */
+int acf_eval_positions_all_kernel(const float* P, const float* Q, int64_t num_user_rows,
+                                  int64_t num_item_rows, int32_t dim, const int32_t* users,
+                                  const int32_t* test_items, int32_t n_users,
+                                  int32_t num_candidates, const int64_t* excl_off,
+                                  const int32_t* excl_items, int32_t* positions, int32_t kernel,
+                                  void* stream);
 
 /* ---- sampler: shuffle/_get_train_batch (APR.py:39-81) --------------------
  * Shuffles the n_pos positive pairs with a counter-based permutation of

@@ -283,13 +283,34 @@ def test_eval_mfma_exact_near_ties(ops, oracle, dev, d):
             torch.tensor(tests, device=dev), num_cand, off, excl)
     got = ops.eval_positions_all(*args).cpu().numpy()
     np.testing.assert_array_equal(got, want)
-    lib = importlib.import_module(PKG + "._native").load()
-    lib.acf_eval_set_kernel(0)
-    try:
-        valu = ops.eval_positions_all(*args).cpu().numpy()
-    finally:
-        lib.acf_eval_set_kernel(1)
-    np.testing.assert_array_equal(valu, want)
+    for kernel in ("mfma", "valu"):
+        np.testing.assert_array_equal(ops.eval_positions_all(*args, kernel=kernel).cpu().numpy(), want)
+
+
+def test_eval_exclusions_unsorted_and_out_of_range(ops, oracle, dev):
+    """The MFMA sweep applies the exclusion lists as a set (utils.py:209-214):
+    unsorted lists and entries outside [0, num_candidates) give the positions of
+    the sorted, in-range lists; the VALU sweep agrees."""
+    rng = np.random.default_rng(21)
+    U1, I1, d, num_cand = 300, 900, 64, 777
+    P = rng.standard_normal((U1, d)).astype(np.float32)
+    Q = rng.standard_normal((I1, d)).astype(np.float32)
+    users = rng.permutation(U1)[:211].astype(np.int32)
+    tests = rng.integers(0, num_cand, len(users)).astype(np.int32)
+    lists = [np.unique(np.append(rng.integers(0, I1, 40), t)).astype(np.int32) for t in tests]
+    clean = [x[x < num_cand] for x in lists]
+    off = np.zeros(len(users) + 1, np.int64)
+    np.cumsum([len(x) for x in clean], out=off[1:])
+    want = oracle.eval_positions_all(P, Q, users, tests, num_cand, off, np.concatenate(clean))
+    shuffled = [rng.permutation(x) for x in lists]
+    off2 = np.zeros(len(users) + 1, np.int64)
+    np.cumsum([len(x) for x in shuffled], out=off2[1:])
+    args = (torch.tensor(P, device=dev), torch.tensor(Q, device=dev), torch.tensor(users, device=dev),
+            torch.tensor(tests, device=dev), num_cand, off2, np.concatenate(shuffled))
+    for kernel in ("auto", "mfma", "valu"):
+        np.testing.assert_array_equal(ops.eval_positions_all(*args, kernel=kernel).cpu().numpy(), want)
+    with pytest.raises(ValueError):
+        ops.eval_positions_all(*args, kernel="gemm")
 
 
 def test_sampler_properties(ops, acf, dev):
