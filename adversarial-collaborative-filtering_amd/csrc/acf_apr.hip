@@ -3537,18 +3537,30 @@ __global__ void __launch_bounds__(256) k_eval_all(const float* __restrict__ P,
 // therefore bit-identical to k_eval_all's.
 constexpr int EVM_U = 64, EVM_C = 128, EVM_KC = 32;
 
-// (r04) The whole ranking is ONE kernel (after a memset of the positions): each
-// workgroup forms what it needs itself -- the test scores of its 64 users
-// (seq_dot, the exact reference rounding), the norms of its 64 users and 128
-// candidates (double sums of the tiles it stages anyway, rounded up) -- and
-// applies the exclusion lists as a bitmap of its 128-candidate window per user
+// (r04) The ranking is two kernels: k_eval_tscore (the test scores, positions
+// zeroed) and k_eval_fused, whose workgroups form the rest themselves -- the
+// norms of its 64 users and 128 candidates (double sums of the tiles it stages
+// anyway, rounded up) -- and apply the exclusion lists as a bitmap of its
+// 128-candidate window per user
 // (set semantics, as utils.py:209-214 builds item_input: set(range(num_items))
 // - set(trainList[u]) - {test}), so no excluded candidate is counted and no
 // exclusion score is computed.  (r03 ran a prep kernel, the sweep and an
 // exclusion-correction kernel that rescored every trainList item with seq_dot.)
+// the test scores (seq_dot: the reference rounding) once per user, and the
+// positions zeroed for k_eval_fused's per-tile adds
+__global__ void __launch_bounds__(256) k_eval_tscore(const float* __restrict__ P, const float* __restrict__ Q, int d,
+                                                     const int32_t* __restrict__ users,
+                                                     const int32_t* __restrict__ tests, int n_users,
+                                                     float* __restrict__ tscore, int32_t* __restrict__ positions) {
+  const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (w >= n_users) return;
+  tscore[w] = seq_dot(P + (int64_t)users[w] * d, Q + (int64_t)tests[w] * d, d);
+  positions[w] = 0;
+}
+
 __global__ void __launch_bounds__(256) k_eval_fused(const float* __restrict__ P, const float* __restrict__ Q, int d,
                                                     const int32_t* __restrict__ users,
-                                                    const int32_t* __restrict__ tests, int n_users, int num_cand,
+                                                    const float* __restrict__ tscore, int n_users, int num_cand,
                                                     const int64_t* __restrict__ excl_off,
                                                     const int32_t* __restrict__ excl, float eb, float floor_e,
                                                     int32_t* __restrict__ positions) {
@@ -3558,6 +3570,7 @@ __global__ void __launch_bounds__(256) k_eval_fused(const float* __restrict__ P,
   __shared__ float s_t[EVM_U], s_pn[EVM_U], s_qn[EVM_C];
   __shared__ int32_t s_row[EVM_U];
   __shared__ uint32_t s_ex[EVM_U][EVM_C / 32];
+  __shared__ int64_t s_off[EVM_U + 1];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63;
   const int u0 = blockIdx.y * EVM_U, c0 = blockIdx.x * EVM_C;
   float tsc = 0.f;
@@ -3565,16 +3578,34 @@ __global__ void __launch_bounds__(256) k_eval_fused(const float* __restrict__ P,
     const bool ok = u0 + tid < n_users;
     s_cnt[tid] = 0;
     s_row[tid] = ok ? users[u0 + tid] : -1;
-    if (ok) tsc = seq_dot(P + (int64_t)users[u0 + tid] * d, Q + (int64_t)tests[u0 + tid] * d, d);
+    if (ok) tsc = tscore[u0 + tid];
   }
   for (int x = tid; x < EVM_U * (EVM_C / 32); x += 256) (&s_ex[0][0])[x] = 0u;
+  const int nu = min(EVM_U, n_users - u0);
+  if (tid <= nu) s_off[tid] = excl_off[u0 + tid];
   __syncthreads();
-  // exclusion bitmap of the window [c0, c0 + 128): wave w scans users w, w + 4, ...
-  for (int ur = wave; ur < EVM_U && u0 + ur < n_users; ur += 4) {
-    const int64_t a0 = excl_off[u0 + ur], a1 = excl_off[u0 + ur + 1];
-    for (int64_t x = a0 + l; x < a1; x += 64) {
-      const int32_t it = excl[x] - c0;
-      if (it >= 0 && it < EVM_C) atomicOr(&s_ex[ur][it >> 5], 1u << (it & 31));
+  // exclusion bitmap of the window [c0, c0 + 128): the tile's users' lists are
+  // one contiguous span of excl (users in order); the workgroup strides over it
+  // (coalesced, independent loads, 4 in flight per thread) and finds each
+  // entry's user by a binary search of the offsets in LDS
+  {
+    const int64_t a0 = s_off[0], a1 = s_off[nu];
+    for (int64_t x0 = a0 + tid; x0 < a1; x0 += 4 * 256) {
+      int32_t v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = x0 + q * 256 < a1 ? excl[x0 + q * 256] : -1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t x = x0 + q * 256;
+        const int32_t it = v[q] - c0;
+        if (x >= a1 || it < 0 || it >= EVM_C) continue;
+        int lo = 0, hi = nu;  // the user: last ur with s_off[ur] <= x
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (s_off[mid] <= x) lo = mid; else hi = mid;
+        }
+        atomicOr(&s_ex[lo][it >> 5], 1u << (it & 31));
+      }
     }
   }
   double ss = 0.0;  // tid < 64: user tid's squared norm; 64 <= tid < 192: candidate tid - 64's
@@ -5487,15 +5518,18 @@ static int eval_positions_all(const float* P, const float* Q, int64_t U1, int64_
     HIP_TRY(hipGetLastError());
     return ACF_OK;
   }
-  HIP_TRY(hipMemsetAsync(positions, 0, (size_t)n_users * sizeof(int32_t), s));
+  float* tscore = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&tscore), (size_t)n_users * sizeof(float), s));
+  k_eval_tscore<<<grid_for(n_users), 256, 0, s>>>(P, Q, d, users, tests, n_users, tscore, positions);
   if (num_cand > 0) {
     const float eb = 4.0f * (float)(d + 2) * 5.9604645e-8f;  // 4 (d + 2) 2^-24
     const float floor_e = (float)d * 1.1754944e-38f * 4.0f;   // denormal products flushed by MFMA
     const dim3 grid((unsigned)((num_cand + EVM_C - 1) / EVM_C), (unsigned)((n_users + EVM_U - 1) / EVM_U));
-    k_eval_fused<<<grid, 256, 0, s>>>(P, Q, d, users, tests, n_users, num_cand, excl_off, excl, eb, floor_e,
+    k_eval_fused<<<grid, 256, 0, s>>>(P, Q, d, users, tscore, n_users, num_cand, excl_off, excl, eb, floor_e,
                                       positions);
   }
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipFreeAsync(tscore, s));
   return ACF_OK;
 }
 

@@ -1028,13 +1028,16 @@ __global__ void __launch_bounds__(256) k_nmf_adam(float4* __restrict__ p, float4
 //                     LAZY_S iterations behind; after the call's last step, every
 //                     row (caller's stream).
 // catch-up period (acf_neumf_ctx::lazy_s, default LAZY_S; ACF_NMF_LAZY_S for A/B):
-// a row is at most lazy_s iterations behind; a step's slice is 1/lazy_s of the rows
-constexpr int LAZY_S = 8;
+// a row is at most lazy_s iterations behind; a step's slice is 1/lazy_s of the
+// rows, so a longer period is a smaller slice beside each step (r04, yelp shape,
+// d 64, B 512, one box: period 8 6.47M instances/s, 16 7.10-7.15M, 24 6.91M, 31 6.74M)
+constexpr int LAZY_S = 16;
 constexpr int LAZY_W = 32;  // lr_t window (> the catch-up period)
-// workgroups of a step's catch-up slice, beside the step's kernels (yelp shape,
-// d 64, B 512, period 8: 32 WGs 3.9M instances/s (the slice outlasts the step),
-// 64 5.6M, 96 7.55M, 128 7.3M, 192 7.45M, 256 7.35M); ACF_NMF_CATCHUP_WG for A/B
-constexpr int64_t CATCHUP_WG = 96;
+// workgroups of a step's catch-up slice, beside the step's kernels (r03, period
+// 8: 32 WGs 3.9M instances/s (the slice outlasts the step), 64 5.6M, 96 7.55M,
+// 128 7.3M, 192 7.45M, 256 7.35M; r04, period 16: 48 5.1M, 64 5.8-6.0M, 96 7.10M,
+// 128 7.15M); ACF_NMF_CATCHUP_WG for A/B
+constexpr int64_t CATCHUP_WG = 128;
 static_assert(LAZY_W > LAZY_S, "lr window");
 
 struct AdamLazy {

@@ -47,9 +47,16 @@ chunk's steps are captured as hipGraphs once and replayed:
 
   * world 1: the exchanges are the identity (no collective), the whole chunk is
     ONE graph;
-  * world > 1: the local work between two collectives is a captured segment;
-    the collectives (fixed-size RCCL all_to_all / all_gather) are issued between
-    the segment replays.
+  * world > 1 (r04): the fixed-size RCCL all_to_all / all_gather calls are
+    captured INSIDE the graph too (``capture_collectives``, default on; a
+    one-off capture + replay of an all_reduce checks that the RCCL in use can
+    be captured first, and ACF_SHARD_RCCL_GRAPH=0 turns it off), so a chunk is
+    again ONE graph with no host round trip per exchange; with it off, the local
+    work between two collectives is a captured segment and the collectives are
+    issued between the segment replays (r03).  ``force_collectives`` routes the
+    exchanges through the process group even at world 1 (an RCCL self-exchange):
+    the one-GPU rehearsal of the captured collectives
+    (tests/test_gpu_distributed.py).
 
 The working sets and the exchange plans of a whole chunk of steps are built on
 device in one go.  Every rank sees the same global triplet stream (the sampler
@@ -72,22 +79,33 @@ import torch.distributed as dist
 
 
 class HipLocal:
-    """One rank's local passes and owner reductions on the HIP kernels."""
+    """One rank's local passes and owner reductions on the HIP kernels.  Two
+    step contexts (plan buffers + pass scratch) alternate by step parity, so the
+    plan of step t + 1 runs beside step t (ShardedAPR._step, r04)."""
 
     graphable = True  # every call is a fixed-shape launch sequence (no host sync)
+    pipelined = True  # plan_into / use: the next step's plan beside this step
 
     def __init__(self, sh: "ShardedAPR"):
         from . import ops
         self.ops = ops
         self.sh = sh
-        self.ctx = ops.APRContext(sh.P.shape[0], sh.max_items, sh.d, sh.b_max, 1, sh.device)
-        self.ctx.set_shard_mode(True, reg_batch=sh.B)
+        self.ctxs = [ops.APRContext(sh.P.shape[0], sh.max_items, sh.d, sh.b_max, 1, sh.device) for _ in range(2)]
+        for c in self.ctxs:
+            c.set_shard_mode(True, reg_batch=sh.B)
+        self.ctx = self.ctxs[0]  # the context the passes below use
         # the fetched item rows are never updated locally; their Adagrad slots are unused
         self.accQc = torch.full((sh.max_items, sh.d), 0.1, device=sh.device)
 
     def _tables(self):
         sh = self.sh
         return (sh.P, sh.Qc, sh.accP, self.accQc)
+
+    def use(self, k: int) -> None:
+        self.ctx = self.ctxs[k]
+
+    def plan_into(self, k: int, u_rows, wi, wj):
+        self.ctxs[k].plan(u_rows, wi, wj, u_rows.numel(), check=False)
 
     def plan(self, u_rows, wi, wj):
         self.ctx.plan(u_rows, wi, wj, u_rows.numel(), check=False)
@@ -112,7 +130,7 @@ class HipLocal:
                                     reg_batch=self.sh.B)
 
     def step_errors(self) -> int:
-        return self.ctx.step_errors()
+        return self.ctxs[0].step_errors() | self.ctxs[1].step_errors()
 
 
 class _Chunk:
@@ -179,7 +197,8 @@ class ShardedAPR:
 
     def __init__(self, num_user_rows: int, num_item_rows: int, dim: int, batch_size: int, device=None,
                  group=None, init_P=None, init_Q=None, acc0: float = 0.1, local=None,
-                 local_batch: int | None = None, item_exchange: str = "all_to_all", graph: bool | None = None):
+                 local_batch: int | None = None, item_exchange: str = "all_to_all", graph: bool | None = None,
+                 capture_collectives: bool | None = None, force_collectives: bool = False):
         if item_exchange not in ("all_to_all", "allgather"):
             raise ValueError(f"item_exchange must be 'all_to_all' or 'allgather', got {item_exchange!r}")
         self.item_exchange = item_exchange
@@ -191,6 +210,8 @@ class ShardedAPR:
             raise ValueError(f"tables of {self.U1} x {self.I1} rows cannot be split over {self.G} ranks")
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self._stage = self.device.type == "cuda" and dist.get_backend(group) == "gloo"
+        # exchanges through the process group even at world 1 (RCCL self-exchange: rehearsal)
+        self._force = bool(force_collectives) and not self._stage
         G, r = self.G, self.rank
         f = dict(dtype=torch.float32, device=self.device)
         nu, ni = len(range(r, self.U1, G)), len(range(r, self.I1, G))
@@ -211,13 +232,17 @@ class ShardedAPR:
         self.max_items = 2 * self.b_max  # a rank's working set of one batch: <= 2 x its triplets
         self.Qc = torch.zeros(self.max_items, dim, **f)
         self._qcap = (self.I1 + G - 1) // G  # rows of the largest Q shard (all_gather slots)
-        self._qpad = torch.zeros(self._qcap, dim, **f) if item_exchange == "allgather" and G > 1 else None
-        self._qall = torch.empty(G * self._qcap, dim, **f) if item_exchange == "allgather" and G > 1 else None
+        gq = item_exchange == "allgather" and (G > 1 or self._force)
+        self._qpad = torch.zeros(self._qcap, dim, **f) if gq else None
+        self._qall = torch.empty(G * self._qcap, dim, **f) if gq else None
         self.local = local(self) if local is not None else HipLocal(self)
         can_graph = (self.device.type == "cuda" and not self._stage and getattr(self.local, "graphable", False))
         if graph is None:  # ACF_SHARD_GRAPH=0: eager steps (A/B of the captured graphs)
             graph = os.environ.get("ACF_SHARD_GRAPH", "1") != "0"
         self.graph = bool(graph) and can_graph
+        if capture_collectives is None:
+            capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "1") != "0"
+        self._cap_coll = bool(capture_collectives) and self.graph and (self.G > 1 or self._force)
         self._C = 0   # per-peer block rows of the exchange buffers (only grows)
         self._T = 0   # steps the per-chunk maps hold
         self._buf = None
@@ -228,6 +253,8 @@ class ShardedAPR:
         self._rec = None  # the segment recorder while capturing
         self.stats = {"steps": 0, "items_requested": 0, "rows_served": 0, "triplets": 0, "route_s": 0.0,
                       "graph_replays": 0}
+        if self._cap_coll:  # here, where every rank is: the check is itself a collective
+            self._cap_coll = self._collectives_capturable()
 
     # -- buffers -------------------------------------------------------------------
     def _ensure(self, T: int, C: int) -> None:
@@ -280,13 +307,57 @@ class ShardedAPR:
 
     # -- collectives ---------------------------------------------------------------
     def _collective(self, fn) -> None:
-        if self._rec is not None:  # capturing: the collective runs between segment replays
+        if self._rec is not None and not self._cap_coll:  # the collective runs between segment replays
             self._rec.cut(fn)
-        else:
+        else:  # eager, or captured into the graph with the local work
             fn()
 
+    def _collectives_capturable(self) -> bool:
+        """One-off check, at construction (every rank is there), that this process
+        group's collectives can be captured into a graph and replayed (RCCL): an
+        all_reduce captured on the capture stream, then -- only if every rank
+        captured it -- replayed twice and checked.  Every rank takes the same
+        decision (the graphs must hold the same collectives); on any error the
+        chunks keep the collectives between graph segments."""
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+            self._cap_stream = torch.cuda.Stream(self.device)
+
+        def agree(ok: bool) -> bool:
+            flag = torch.tensor([1 if ok else 0], device=self.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+            return bool(flag.item())
+
+        x = torch.ones(64, device=self.device)
+        g = torch.cuda.CUDAGraph()
+        ok = True
+        try:
+            torch.cuda.synchronize(self.device)
+            self._cap_stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._cap_stream):
+                g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+                try:
+                    dist.all_reduce(x, group=self.group)
+                finally:
+                    g.capture_end()
+        except Exception as e:  # noqa: BLE001
+            warnings.warn(f"ShardedAPR: collectives cannot be captured ({e!r}); they stay between graph segments")
+            ok = False
+        if not agree(ok):
+            return False
+        try:
+            x.fill_(1.0)
+            g.replay()
+            g.replay()
+            torch.cuda.synchronize(self.device)
+            ok = bool((x == float(self.G) ** 2).all())
+        except Exception as e:  # noqa: BLE001
+            warnings.warn(f"ShardedAPR: a captured collective did not replay ({e!r}); collectives stay eager")
+            ok = False
+        return agree(ok)
+
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
-        if self.G == 1:  # one rank: the exchange is a copy
+        if self.G == 1 and not self._force:  # one rank: the exchange is a copy
             out.copy_(inp)
         elif self._stage:  # gloo with device tensors (rehearsal of several ranks on one GPU)
             o = torch.empty(out.shape, dtype=out.dtype)
@@ -298,7 +369,7 @@ class ShardedAPR:
     def _exchange(self, out, inp):
         """Fixed-size exchange of G blocks of C rows (block o to / from rank o);
         the identity at world 1.  Returns the tensor holding the received rows."""
-        if self.G == 1:
+        if self.G == 1 and not self._force:
             return inp
         n = self.G * self._C
         self._collective(lambda: self._a2a(out[:n], inp[:n]))
@@ -307,7 +378,7 @@ class ShardedAPR:
     def _gather_q(self):
         """E1, "allgather" form: every rank's Q shard to every rank (RCCL all_gather);
         row i is then at _qall[(i % G) * cap + i // G].  World 1: Q itself."""
-        if self.G == 1:
+        if self.G == 1 and not self._force:
             return self._Qst
         self._qpad[: self.ni] = self.Q
 
@@ -480,21 +551,69 @@ class ShardedAPR:
         c.has_count = True
 
     # -- one step ------------------------------------------------------------------
-    def _step(self, m, t: int, b: int, hp, count: bool) -> None:
+    def _pipelined(self) -> bool:
+        """The next step's plan beside this step: the local passes support it, and
+        no graph segment is cut between here and the next step (eager steps, or a
+        capture that holds its collectives)."""
+        return getattr(self.local, "pipelined", False) and (self._rec is None or self._cap_coll)
+
+    def _plan_step(self, m, t: int, nb: list, pipe: bool) -> None:
+        """The plan of step t (nb[t] local triplets): in line, or -- pipelined -- the
+        one made beside step t - 1 (step 0's in line), then step t + 1's forked
+        onto the side stream once step t - 1 has released its context."""
+        b = nb[t]
+        if not pipe:
+            self.local.plan(m.u_rows[t, :b], m.wi[t, :b], m.wj[t, :b])
+            return
+        main = torch.cuda.current_stream(self.device)
+        k = t & 1
+        if t == 0 or self._planned[k] is None:
+            self.local.plan_into(k, m.u_rows[t, :b], m.wi[t, :b], m.wj[t, :b])
+        else:
+            main.wait_event(self._planned[k])
+        self._planned[k] = None
+        self.local.use(k)
+        T = len(nb)
+        if t + 1 < T and nb[t + 1]:
+            k1 = k ^ 1
+            side = self._plan_stream
+            fork = self._free[k1]
+            if fork is None:  # nothing used that context yet in this chunk: fork from here
+                fork = torch.cuda.Event()
+                fork.record(main)
+            side.wait_event(fork)
+            with torch.cuda.stream(side):
+                b1 = nb[t + 1]
+                self.local.plan_into(k1, m.u_rows[t + 1, :b1], m.wi[t + 1, :b1], m.wj[t + 1, :b1])
+                ev = torch.cuda.Event()
+                ev.record(side)
+            self._planned[k1] = ev
+
+    def _release(self, t: int, pipe: bool) -> None:
+        """Step t's last use of its context: the plan of step t + 2 may overwrite it."""
+        if pipe:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._free[t & 1] = ev
+
+    def _step(self, m, t: int, nb: list, hp, count: bool, pipe: bool = False) -> None:
         """Step t of a chunk routed into map set m (fixed shapes: every size is the buffers')."""
+        b = nb[t]
         bf = self._buf
         # E1: current item rows of my working set from their owners
         if self.item_exchange == "allgather":
             torch.index_select(self._gather_q(), 0, m.wslot[t], out=self.Qc)
-        elif m.wq is not None:
+        elif m.wq is not None and not self._force:
             torch.index_select(self._Qst, 0, m.wq[t], out=self.Qc)
         else:
             torch.index_select(self._Qst, 0, m.srv[t], out=bf.S1)
             torch.index_select(self._exchange(bf.R1, bf.S1), 0, m.wsrc[t], out=self.Qc)
         rows = m.wsrc[t, : 2 * b]  # working-set entry -> its exchange row
         if b:
-            self.local.plan(m.u_rows[t, :b], m.wi[t, :b], m.wj[t, :b])
+            self._plan_step(m, t, nb, pipe)
             self.local.clean(hp, bf.S, rows)
+            if not hp.adver:
+                self._release(t, pipe)
         # E2: partial clean item sums -> owners
         recv = self._exchange(bf.R, bf.S)
         cnt = m.count[t] if count else None
@@ -505,6 +624,7 @@ class ShardedAPR:
             if b:
                 self.local.set_item_delta(dl, rows)
                 self.local.adv(hp, bf.S, rows)
+                self._release(t, pipe)
             # E4: partial adversarial item sums -> owners, who apply Adagrad
             recv = self._exchange(bf.R, bf.S)
             self.local.reduce_apply(hp, recv, m.seg[t], m.pos[t], bf.G0, m.own[t], cnt)
@@ -523,14 +643,24 @@ class ShardedAPR:
             self.stats["graph_replays"] += 1
             return
         m = self._maps[c.mset]
-        for t in range(T):
-            self._step(m, t, int(c.nloc[t]), hp, c.has_count)
+        self._run_steps(m, [int(x) for x in c.nloc[:T]], hp, c.has_count)
         if key is not None:  # capture for the next chunk of this shape (capturing runs nothing)
             try:
                 self._graphs[key] = self._capture(m, T, min(bs), hp, c.has_count)
             except RuntimeError as e:  # the chunk ran eagerly; later chunks stay eager
                 warnings.warn(f"ShardedAPR: step capture failed ({e}); continuing without graphs")
                 self.graph = False
+
+    def _run_steps(self, m, nb: list, hp, count: bool) -> None:
+        """The steps of a chunk, each step's plan beside the previous step where
+        the local passes allow it (_pipelined)."""
+        pipe = self.device.type == "cuda" and self._pipelined()
+        if pipe and getattr(self, "_plan_stream", None) is None:
+            self._plan_stream = torch.cuda.Stream(self.device)
+        self._planned, self._free = [None, None], [None, None]
+        for t in range(len(nb)):
+            self._step(m, t, nb, hp, count, pipe)
+        self._planned, self._free = [None, None], [None, None]
 
     def _capture(self, m, T: int, b: int, hp, count: bool) -> _SegmentRecorder:
         if self._pool is None:
@@ -544,8 +674,7 @@ class ShardedAPR:
             self._rec = rec
             try:
                 rec.begin()
-                for t in range(T):
-                    self._step(m, t, b, hp, count)
+                self._run_steps(m, [b] * T, hp, count)
                 rec.end()
             except BaseException:
                 rec.abort()

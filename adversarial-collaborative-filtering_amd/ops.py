@@ -39,6 +39,15 @@ def _stream_ptr(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_RAW = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _raw_stream(device: torch.device) -> int:
+    """The current stream of `device` as an integer handle (torch's raw accessor:
+    no Stream object per call)."""
+    return _RAW(device.index) if _RAW is not None else _stream_ptr(device)
+
+
 def _require(t: torch.Tensor, name: str, dtype: torch.dtype, device: torch.device | None = None,
              ndim: int | None = None) -> int:
     if not isinstance(t, torch.Tensor):
@@ -454,8 +463,7 @@ class PlanPipeline:
                 item_neg.data_ptr() + off, self.batch_size, n_batches, 0, int(bool(graph)))
         self._memo = (user, item_pos, item_neg, hp, first_batch, n_batches, graph, P, Q, aP, aQ, dict(hp.__dict__),
                       (P.data_ptr(), Q.data_ptr(), aP.data_ptr(), aQ.data_ptr(), user.data_ptr(),
-                       item_pos.data_ptr(), item_neg.data_ptr(), P.shape, Q.shape, aP.shape, aQ.shape,
-                       user.shape, item_pos.shape, item_neg.shape),
+                       item_pos.data_ptr(), item_neg.data_ptr()),
                       _native.load().acf_apr_train, args, c, tb, h)
 
     def _plan(self, k, u, i, j, b, n, check):
@@ -482,14 +490,15 @@ class PlanPipeline:
                 and m[5] == n_batches and m[6] == graph):
             return False
         P, Q, aP, aQ = tables
+        # the same tensor objects on the same storage (a storage swap moves data_ptr)
+        # and the same hyper-parameters; the launches go to the device's current
+        # stream, which selects the device
         if not (P is m[7] and Q is m[8] and aP is m[9] and aQ is m[10] and hp.__dict__ == m[11]
                 and m[12] == (P.data_ptr(), Q.data_ptr(), aP.data_ptr(), aQ.data_ptr(), user.data_ptr(),
-                              item_pos.data_ptr(), item_neg.data_ptr(), P.shape, Q.shape, aP.shape, aQ.shape,
-                              user.shape, item_pos.shape, item_neg.shape)
-                and torch.cuda.current_device() == self.device.index):
+                              item_pos.data_ptr(), item_neg.data_ptr())):
             return False
         fn, args, ctx = m[13], m[14], m[15]
-        rc = fn(*args, torch.cuda.current_stream(self.device).cuda_stream)
+        rc = fn(*args, _raw_stream(self.device))
         if rc:
             _native.call_failed(rc, "acf_apr_train")
         ctx._staged = (user, item_pos, item_neg)

@@ -115,6 +115,42 @@ def test_sharded_graph_replay_bit_identical(ops, dev, exchange, adver, reg, rout
         assert torch.equal(g, e), n
 
 
+@pytest.mark.parametrize("exchange,routed", [("all_to_all", False), ("allgather", True)])
+def test_sharded_collectives_captured_in_graph_world1(ops, dev, exchange, routed):
+    """The RCCL collectives of the split step captured INSIDE the step graph
+    (capture_collectives), rehearsed on one GPU: force_collectives issues every
+    exchange through a one-rank nccl group (an RCCL self-exchange) instead of the
+    world-1 identity.  The constructor's capture check passes, a chunk is ONE
+    graph segment, and eager / segments-between-collectives / collectives-in-graph
+    runs give identical bits (pinterest-20 shape, configs[2])."""
+    D_ = importlib.import_module(PKG + ".distributed")
+    U1, I1, d, B, nb = 55_188, 9_917, 64, 512, 12
+    P, Q, u, i, j = _problem(9, U1, I1, d, B, nb)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    outs, segs = [], []
+    try:
+        uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
+        for graph, cap in ((False, False), (True, False), (True, True)):
+            sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, item_exchange=exchange, graph=graph,
+                               local_batch=B if routed else None, force_collectives=True, capture_collectives=cap)
+            assert sh._cap_coll == cap
+            hp = ops.StepHParams(adver=1)
+            (sh.train_routed if routed else sh.train)(uu, ii, jj, hp, chunk=4)
+            torch.cuda.synchronize(dev)
+            assert sh.step_errors() == 0
+            outs.append(sh.full_tables())
+            segs.append([len(r.segs) for r in sh._graphs.values()])
+            assert not graph or sh.stats["graph_replays"] >= 1
+    finally:
+        dist.destroy_process_group()
+    assert segs[1] and min(segs[1]) > 1, segs  # cut at every collective
+    assert segs[2] == [1] * len(segs[2]) and segs[2], segs  # one graph per chunk
+    for o in outs[1:]:
+        for g, e, n in zip(o, outs[0], ("P", "Q", "accP", "accQ")):
+            assert torch.equal(g, e), n
+
+
 @pytest.mark.parametrize("adver", [1, 0])
 def test_shard_plan_small_matches_sort_plan(ops, dev, adver):
     """The one-workgroup shard plan (k_shard_plan, one batch of B <= 1,024) against
@@ -132,7 +168,8 @@ def test_shard_plan_small_matches_sort_plan(ops, dev, adver):
         uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
         for mode in (0, 1):
             sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, graph=False)
-            sh.local.ctx.set_plan_mode(mode)
+            for c in sh.local.ctxs:  # both step contexts (the next step is planned beside this one)
+                c.set_plan_mode(mode)
             sh.train(uu, ii, jj, ops.StepHParams(adver=adver), chunk=3)
             torch.cuda.synchronize(dev)
             assert sh.step_errors() == 0

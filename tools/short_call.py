@@ -35,6 +35,8 @@ def main():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--reps", type=int, default=5, help="timed repetitions (each on fresh batches)")
     p.add_argument("--failsafe", type=int, default=1, help="verified streamed calls (1, default) or not (0)")
+    p.add_argument("--same", action="store_true",
+                   help="every rep repeats the same call (bench.py's timed call: PlanPipeline's fast path)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -54,7 +56,7 @@ def main():
     torch.cuda.synchronize(dev)
     out = []
     for r in range(a.reps):
-        first = a.warmup + r * a.steps
+        first = a.warmup + (0 if a.same else r * a.steps)
         torch.cuda._sleep(1000)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
