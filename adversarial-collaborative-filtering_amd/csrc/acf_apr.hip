@@ -3897,6 +3897,7 @@ struct acf_apr_ctx {
   uint32_t last_tail_seq = 0;  // seq of the last launch with a tail (StepArgs.decide_prev)
   int32_t tail_on = 1;         // ACF_TAIL=0: write-back by k_stream_flush always (A/B)
   int32_t tail_flushers = 128; // ACF_TAIL_FLUSHERS: workgroups of the tail write-back
+  int32_t bplan_sort1024 = 0;   // ACF_BPLAN_SORT=1024: the batch plan's sort at 1,024 x 2 (A/B)
   unsigned long long* tail_diag = nullptr;  // ACF_TAIL_DIAG=1: tail stamps (acf_apr_diag_tail)
   unsigned long long* decide = nullptr;  // [0] decide word, [16, 16 + 288) the tail's arrival counters
   uint32_t tail_launches = 0;            // launches with a tail so far (StepArgs.tail_par)
@@ -4104,6 +4105,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   }
   if (const char* e = getenv("ACF_TAIL")) c->tail_on = atoi(e) != 0;
   if (const char* e = getenv("ACF_TAIL_FLUSHERS")) c->tail_flushers = std::max(1, atoi(e));
+  if (const char* e = getenv("ACF_BPLAN_SORT")) c->bplan_sort1024 = atoi(e) == 1024;
   if (const char* e = getenv("ACF_TAIL_DIAG"))
     if (atoi(e) && dalloc(c, &c->tail_diag, 8) == ACF_OK) (void)hipMemset(c->tail_diag, 0, 64);
   c->grp = new FailGroup();
@@ -4292,7 +4294,10 @@ static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, 
   // build: ~24 us for a 20-batch plan against ~32 us for 6 per thread / 256-thread
   // builds (per-thread loops serialise the build's dependent loads)
   if (B <= 512) {
-    k_bplan_sort<512, 3><<<nb, 512, 0, s>>>(p);
+    if (c->bplan_sort1024)  // ACF_BPLAN_SORT=1024 (A/B): 1,024 threads x 2 occurrences
+      k_bplan_sort<1024, 2><<<nb, 1024, 0, s>>>(p);
+    else
+      k_bplan_sort<512, 3><<<nb, 512, 0, s>>>(p);
     k_bplan_build<1024, 512><<<nb, 1024, 0, s>>>(p);
   } else {
     k_bplan_sort<1024, 3><<<nb, 1024, 0, s>>>(p);

@@ -47,13 +47,18 @@ chunk's steps are captured as hipGraphs once and replayed:
 
   * world 1: the exchanges are the identity (no collective), the whole chunk is
     ONE graph;
-  * world > 1 (r04): the fixed-size RCCL all_to_all / all_gather calls are
-    captured INSIDE the graph too (``capture_collectives``, default on; a
-    one-off capture + replay of an all_reduce checks that the RCCL in use can
-    be captured first, and ACF_SHARD_RCCL_GRAPH=0 turns it off), so a chunk is
-    again ONE graph with no host round trip per exchange; with it off, the local
-    work between two collectives is a captured segment and the collectives are
-    issued between the segment replays (r03).  ``force_collectives`` routes the
+  * world > 1 (r04): the fixed-size RCCL all_to_all / all_gather calls can be
+    captured INSIDE the graph too (``capture_collectives``, or
+    ACF_SHARD_RCCL_GRAPH=1; a one-off capture + replay of an all_reduce checks
+    at construction that the RCCL in use can be captured), so a chunk is again
+    ONE graph with no host round trip per exchange.  It is OFF by default: on
+    the one-GPU rehearsal (tools/rccl_capture_probe.py) a captured RCCL
+    all_to_all replays correctly but the process group then does not tear down
+    while the graph is alive, so ``close()`` drops the graphs first, and the
+    8-GPU behaviour is unmeasured.  Off, the steps run eagerly (r03 captured the
+    local work between two collectives as separate segments; rehearsed with
+    RCCL in r04 that met an allocator assertion, so it is gone).
+    ``force_collectives`` routes the
     exchanges through the process group even at world 1 (an RCCL self-exchange):
     the one-GPU rehearsal of the captured collectives
     (tests/test_gpu_distributed.py).
@@ -240,9 +245,10 @@ class ShardedAPR:
         if graph is None:  # ACF_SHARD_GRAPH=0: eager steps (A/B of the captured graphs)
             graph = os.environ.get("ACF_SHARD_GRAPH", "1") != "0"
         self.graph = bool(graph) and can_graph
-        if capture_collectives is None:
-            capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "1") != "0"
-        self._cap_coll = bool(capture_collectives) and self.graph and (self.G > 1 or self._force)
+        if capture_collectives is None:  # opt-in (see the module docstring)
+            capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "0") != "0"
+        multi = self.G > 1 or self._force  # exchanges that are collectives
+        self._cap_coll = bool(capture_collectives) and self.graph and multi
         self._C = 0   # per-peer block rows of the exchange buffers (only grows)
         self._T = 0   # steps the per-chunk maps hold
         self._buf = None
@@ -255,7 +261,12 @@ class ShardedAPR:
                       "graph_replays": 0}
         if self._cap_coll:  # here, where every rank is: the check is itself a collective
             self._cap_coll = self._collectives_capturable()
-
+        if multi and not self._cap_coll:
+            # steps with collectives are captured only with the collectives inside
+            # the graph; otherwise they run eagerly (capturing the local work between
+            # the collectives as separate segments met an allocator assertion in the
+            # RCCL rehearsal -- HIPCachingAllocator use_count -- and is not used)
+            self.graph = False
     # -- buffers -------------------------------------------------------------------
     def _ensure(self, T: int, C: int) -> None:
         if C <= self._C and T <= self._T:
@@ -329,14 +340,15 @@ class ShardedAPR:
             return bool(flag.item())
 
         x = torch.ones(64, device=self.device)
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph()  # its own memory pool: the step graphs' pool stays untouched
         ok = True
         try:
             torch.cuda.synchronize(self.device)
             self._cap_stream.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self._cap_stream):
-                g.capture_begin(pool=self._pool, capture_error_mode="thread_local")
+                g.capture_begin(capture_error_mode="thread_local")
                 try:
+                    x.mul_(1.0)  # a node besides the collective (a one-rank RCCL all_reduce may record none)
                     dist.all_reduce(x, group=self.group)
                 finally:
                     g.capture_end()
@@ -354,6 +366,7 @@ class ShardedAPR:
         except Exception as e:  # noqa: BLE001
             warnings.warn(f"ShardedAPR: a captured collective did not replay ({e!r}); collectives stay eager")
             ok = False
+        del g
         return agree(ok)
 
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
@@ -761,6 +774,13 @@ class ShardedAPR:
 
     def step_errors(self) -> int:
         return self.local.step_errors() if hasattr(self.local, "step_errors") else 0
+
+    def close(self) -> None:
+        """Drop the captured step graphs (call before destroying the process group:
+        a graph holding captured RCCL collectives keeps the communicator busy)."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self._graphs.clear()
 
     def full_tables(self):
         """The full tables on every rank (checkpoints, evaluation, tests)."""
