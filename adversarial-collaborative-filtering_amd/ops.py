@@ -8,6 +8,7 @@ index ranges are validated on device by the plan / sampler (``NativeIndexError``
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -411,6 +412,10 @@ class PlanPipeline:
         # default priority: a high-priority plan stream halved the configs[4] rate
         # (608M -> 313M triplets/s at d = 64, tools/large_prio.py, r03)
         self.side = torch.cuda.Stream(self.device)
+        # ACF_PIPE_STEP_PRIO=1: the steps of an overlapped run on a high-priority
+        # stream instead (the plan then fills what the step kernels leave idle)
+        self.step_priority = os.environ.get("ACF_PIPE_STEP_PRIO", "0") == "1"
+        self._hi = None
         self._free = [None, None]  # event: the last training on ctx[k] has been issued before it
         self._memo = None  # the last single-chunk call, validated (_repeat)
 
@@ -530,21 +535,28 @@ class PlanPipeline:
             if len(chunks) == 1 and not check and u is user and i is item_pos and j is item_neg:
                 self._remember(tables, hp, user, item_pos, item_neg, first_batch, n_batches, graph)
             return
-        if self._ov:
-            ready = torch.cuda.Event()
-            ready.record(main)  # triplets produced on the caller's stream
-            self.side.wait_event(ready)
+        ready = torch.cuda.Event()
+        ready.record(main)  # triplets produced on the caller's stream
+        self.side.wait_event(ready)
+        step = main
+        if self.step_priority:  # the steps on a high-priority stream, joined to the caller's
+            if self._hi is None:
+                self._hi = torch.cuda.Stream(self.device, priority=-1)
+            step = self._hi
+            step.wait_event(ready)
         planned = self._plan(0, u, i, j, *chunks[0], check)
-        for k, (b, n) in enumerate(chunks):
-            if planned is not None:
-                main.wait_event(planned)
-            self.ctx[k % 2].train_planned(tables, hp, 0, n, graph=graph)
-            if self._ov:
+        with torch.cuda.stream(step):
+            for k, (b, n) in enumerate(chunks):
+                if planned is not None:
+                    step.wait_event(planned)
+                self.ctx[k % 2].train_planned(tables, hp, 0, n, graph=graph)
                 done = torch.cuda.Event()
-                done.record(main)
+                done.record(step)
                 self._free[k % 2] = done
-            if k + 1 < len(chunks):
-                planned = self._plan(k + 1, u, i, j, *chunks[k + 1], check)
+                if k + 1 < len(chunks):
+                    planned = self._plan(k + 1, u, i, j, *chunks[k + 1], check)
+        if step is not main:
+            main.wait_stream(step)
         self._staged = (u, i, j)
 
 

@@ -5,6 +5,15 @@ OUT=gpurun_out/${OUT_TAG:-r04_c}
 mkdir -p $OUT
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_reference.py tests/test_gpu_torch_ops.py tests/test_gpu_e2e_video.py tests/test_gpu_neumf.py tests/test_gpu_distributed.py -m gpu > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_plan.py -m gpu > $OUT/pytest_plan.log 2>&1 || { tail -20 $OUT/pytest_plan.log; exit 1; }
+echo "plan tests: $(tail -1 $OUT/pytest_plan.log)"
+for v in radix count radix count; do
+  ACF_BPLAN_SORT=$v timeout -k 10 200 python3 tools/short_call.py --reps 40 --same > $OUT/sc_sort$v.json 2> $OUT/sc_sort$v.err
+  python3 -c "
+import json,statistics as st
+d=json.loads(open('$OUT/sc_sort$v.json').read().strip().splitlines()[-1]); r=[x['region_us'] for x in d['reps']][5:]
+print('sort $v region median', st.median(r), 'min', min(r))"
+done
 timeout -k 10 300 python3 -c "
 import sys, json, importlib, torch
 sys.path.insert(0, '.')
@@ -40,12 +49,3 @@ sh=b.get('sharded', {})
 for k,v in sh.items():
     if isinstance(v, dict): print('sharded', k, v.get('value'), v.get('ms_per_step'), v.get('config', {}).get('launch'))
     else: print('sharded', k, v)"
-ACF_BPLAN_SORT=1024 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_plan.py -m gpu > $OUT/pytest_sort1024.log 2>&1 || { tail -20 $OUT/pytest_sort1024.log; exit 1; }
-echo "sort1024 tests: $(tail -1 $OUT/pytest_sort1024.log)"
-for v in 0 1024 0 1024; do
-  ACF_BPLAN_SORT=$v timeout -k 10 200 python3 tools/short_call.py --reps 40 --same > $OUT/sc_sort$v.json 2> $OUT/sc_sort$v.err
-  python3 -c "
-import json,statistics as st
-d=json.loads(open('$OUT/sc_sort$v.json').read().strip().splitlines()[-1]); r=[x['region_us'] for x in d['reps']][5:]
-print('sort $v region median', st.median(r), 'min', min(r))"
-done

@@ -5,5 +5,7 @@ mkdir -p gpurun_out/rccl_probe
 for k in "all_to_all del_destroy" "all_to_all exit" "all_to_all del" "all_gather destroy"; do
   set -- $k
   timeout -k 10 60 python3 tools/rccl_capture_probe.py $1 $2 > gpurun_out/rccl_probe/$1_$2.log 2>&1
-  echo "$1 $2 rc=$?: $(grep -v amdgpu.ids gpurun_out/rccl_probe/$1_$2.log | tail -3 | tr '\n' ' ')"
+  rc=$?
+  echo "$1 $2 rc=$rc: $(grep -v amdgpu.ids gpurun_out/rccl_probe/$1_$2.log | tail -3 | tr '\n' ' ')"
+  [ $rc -ne 0 ] && exit $rc
 done
