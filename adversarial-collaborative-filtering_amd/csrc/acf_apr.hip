@@ -638,6 +638,325 @@ __global__ void k_task_list(const int32_t* __restrict__ flags, const int32_t* __
   if (y == stride - 1) cnt[t] = incl[x] - base;
 }
 
+// ---------------------------------------------------------------------------
+// Hash plan (r04): the plan of triplet-centric steps (one lane-group per slot,
+// fusion on, not shard mode; B >= 4,096) without a device-wide sort.  What such
+// a step reads of its plan: per triplet its rows, which of them occur once in the
+// batch ("single": stepped by the triplet itself) and, for the others ("shared"),
+// a slot id and the CSR position of the occurrence; per shared slot its row,
+// count and CSR range (the inline record), in which the combine adds the
+// occurrences' contributions IN OCCURRENCE ORDER (the slot path's bits); the
+// per-batch lists of shared slots and of hot slots with their pieces.  Slot ids
+// and CSR ranges may be numbered in any order; only the order inside a range is
+// fixed.  So (APR.py:183-195's Unique + UnsortedSegmentSum, restated):
+//  1. k_hplan_insert: each occurrence inserts its (side, row) key into its
+//     batch's open-addressing table (2^hs_log buckets >= 2 x 3B, linear probing;
+//     a bucket is {key, count}: one 64-bit CAS claims it, one 64-bit add counts)
+//     and keeps its bucket and its place in the bucket's (arbitrary) add order;
+//  2. k_hplan_claim: the occurrence that claimed a bucket of count > 1 allocates
+//     the slot id, the CSR range and the list places (one atomic per wave each)
+//     and writes the inline record;
+//  3. k_hplan_trip: per triplet, its record (single bits from the counts) and
+//     its shared occurrences' ids into their CSR ranges at the add-order place;
+//  4. k_hplan_rank_small / k_hplan_rank_hot: each range put in occurrence order
+//     -- <= 8 entries by one thread, <= 64 by a wave (all-pairs ranks), more by a
+//     workgroup (an LDS bitmap of the side's occurrences and its prefix
+//     popcounts) -- and every shared occurrence's CSR position written.
+// Only the tables are cleared (a fill per plan); 5 launches against the sort
+// plan's ~17, and no pass sorts the ~94% of rows that occur once.  The bits of a
+// step are the sort plan's (test_hash_plan_matches_sort_plan).
+// ---------------------------------------------------------------------------
+#define ACF_HPLAN_MAXB 65536  // the hot-rank bitmap: 2B bits of LDS per workgroup
+
+struct HPlanArgs {
+  const int32_t* user;
+  const int32_t* ipos;
+  const int32_t* ineg;
+  int64_t U1, I1;
+  int32_t B, S, nb, gen, hs_log, opad;  // opad: threads per batch (3B rounded up to a wave)
+  unsigned long long* H;  // [nb][2^hs_log] {key << 32 | count}, all ones = empty
+  int2* binfo;            // [nb][2^hs_log] {slot, CSR base} of a shared key (its claimer writes it)
+  int32_t* hb;            // [nb][3B] occurrence -> bucket
+  int32_t* rk;            // [nb][3B] occurrence -> place in its bucket's add order
+  int32_t* csr;           // [nb][3B] occurrence ids by CSR position: users [0, B), items B + [0, 2B)
+  int32_t* scnt;          // [nb] shared slots
+  int32_t* ucsr;          // [nb] user CSR positions taken
+  int32_t* icsr;          // [nb] item CSR positions taken
+  OccRec* inl;
+  OccRec* trec;
+  int32_t* tpos;          // [E][4] CSR positions of the triplet's occurrences
+  int32_t* slot_list;
+  int32_t* slot_cnt;
+  HotLists hl;
+  int32_t* err;
+  int32_t* gen_ptr;
+};
+
+__device__ __forceinline__ uint32_t hplan_hash(uint32_t key, int hs_log) {
+  return (key * 2654435761u) >> (32 - hs_log);  // Fibonacci hashing
+}
+
+// the (side, row) of occurrence o of batch t (users [0, B), items B + 2e + role)
+__device__ __forceinline__ uint32_t hplan_key(const HPlanArgs& p, int32_t t, int32_t o, int& err) {
+  const int B = p.B;
+  if (o < B) {
+    int32_t row = p.user[(int64_t)t * B + o];
+    if (row < 0 || row >= p.U1) { err |= 1; row = 0; }
+    return (uint32_t)row;
+  }
+  const int v = o - B;
+  int32_t row = ((v & 1) ? p.ineg : p.ipos)[(int64_t)t * B + (v >> 1)];
+  if (row < 0 || row >= p.I1) { err |= 2; row = 0; }
+  return 0x80000000u | (uint32_t)row;
+}
+
+__global__ void __launch_bounds__(256) k_hplan_insert(HPlanArgs p) {
+  const int64_t x = blockIdx.x * 256ll + threadIdx.x;
+  const int32_t t = (int32_t)(x / p.opad), o = (int32_t)(x - (int64_t)t * p.opad);
+  const int S3 = 3 * p.B;
+  if (t >= p.nb || o >= S3) return;
+  int err = 0;
+  const uint32_t key = hplan_key(p, t, o, err);
+  if (err) atomicOr(p.err, err);
+  const uint32_t mask = (1u << p.hs_log) - 1u;
+  unsigned long long* H = p.H + ((int64_t)t << p.hs_log);
+  const unsigned long long mine = ((unsigned long long)key << 32) | 1ull;
+  uint32_t h = hplan_hash(key, p.hs_log), rank = 0;
+  // the table holds at most 3B of its >= 6B buckets: the probe ends
+  for (;;) {
+    unsigned long long e = __hip_atomic_load(H + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e == ~0ull) {
+      const unsigned long long prev = atomicCAS(H + h, ~0ull, mine);
+      if (prev == ~0ull) break;  // claimed: first in add order
+      e = prev;
+    }
+    if ((uint32_t)(e >> 32) == key) {
+      rank = (uint32_t)atomicAdd(H + h, 1ull);  // the count before this occurrence
+      break;
+    }
+    h = (h + 1u) & mask;
+  }
+  p.hb[(int64_t)t * S3 + o] = (int32_t)h;
+  p.rk[(int64_t)t * S3 + o] = (int32_t)rank;
+}
+
+// exclusive prefix sum over the wave; total = the wave's sum
+__device__ __forceinline__ int32_t wave_excl_sum(int32_t v, int32_t& total) {
+  const int lane = threadIdx.x & 63;
+  int32_t incl = v;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const int32_t y = __shfl_up(incl, s);
+    if (lane >= s) incl += y;
+  }
+  total = __shfl(incl, 63);
+  return incl - v;
+}
+
+// one atomicAdd of the wave's total by lane 0; each lane's base = the old value + excl
+__device__ __forceinline__ int32_t wave_take(int32_t* ctr, int32_t v) {
+  int32_t total = 0;
+  const int32_t excl = wave_excl_sum(v, total);
+  int32_t base = 0;
+  if ((threadIdx.x & 63) == 0 && total > 0) base = atomicAdd(ctr, total);
+  return __shfl(base, 0) + excl;
+}
+
+__global__ void __launch_bounds__(256) k_hplan_claim(HPlanArgs p) {
+  const int64_t x = blockIdx.x * 256ll + threadIdx.x;
+  const int32_t t = (int32_t)(x / p.opad), o = (int32_t)(x - (int64_t)t * p.opad);
+  const int B = p.B, S3 = 3 * B;
+  if (t >= p.nb) return;  // whole waves (opad is a multiple of 64)
+  const bool live = o < S3;
+  int32_t h = 0, r = 1;
+  if (live) {
+    h = p.hb[(int64_t)t * S3 + o];
+    r = p.rk[(int64_t)t * S3 + o];
+  }
+  uint32_t cnt = 0, key = 0;
+  if (live && r == 0) {
+    const unsigned long long e = p.H[((int64_t)t << p.hs_log) + h];
+    cnt = (uint32_t)e;
+    key = (uint32_t)(e >> 32);
+  }
+  const bool claim = cnt > 1, item = o >= B, hot = claim && cnt > ACF_HOT_MIN;
+  const int32_t k = wave_take(p.scnt + t, claim ? 1 : 0);
+  const int32_t ub = wave_take(p.ucsr + t, claim && !item ? (int32_t)cnt : 0);
+  const int32_t ib = wave_take(p.icsr + t, claim && item ? (int32_t)cnt : 0);
+  const int32_t ls = wave_take(p.slot_cnt + t, claim && !hot ? 1 : 0);
+  const int32_t hx = wave_take(p.hl.cnt + t, hot ? 1 : 0);
+  const int32_t np = hot ? hot_pieces((int32_t)cnt) : 0;
+  const int32_t pb = wave_take(p.hl.pcnt + t, np);
+  if (!claim) return;
+  const int32_t base = item ? ib : ub;
+  p.binfo[((int64_t)t << p.hs_log) + h] = make_int2(k, base);
+  OccRec rec = {};
+  rec.own_row = (int32_t)(key & 0x7FFFFFFFu);
+  rec.own_src = rec.own_row;
+  rec.meta = (int32_t)cnt | (item ? ACF_ITEM_BIT : 0);
+  rec.ovf = (item ? t * 2 * B : t * B) + base;
+  rec.e_role = -1;
+  rec.gen = p.gen;
+  p.inl[(int64_t)t * p.S + k] = rec;
+  if (!hot) {
+    p.slot_list[(int64_t)t * p.S + ls] = k;
+  } else {
+    p.hl.list[(int64_t)t * p.hl.hot_stride + hx] = make_int4(k, np, pb, (int32_t)cnt);
+    int4* pc = p.hl.piece + (int64_t)t * p.hl.piece_stride + pb;
+    for (int32_t q = 0; q < np; ++q) pc[q] = make_int4(k, q, np, pb);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_hplan_trip(HPlanArgs p) {
+  const int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  const int B = p.B, S3 = 3 * B;
+  if (e == 0) *p.gen_ptr = p.gen;
+  if (e >= (int64_t)p.nb * B) return;
+  const int32_t t = (int32_t)(e / B), b = (int32_t)(e - (int64_t)t * B);
+  const int64_t ob = (int64_t)t * S3;
+  const int32_t oc[3] = {b, B + 2 * b, B + 2 * b + 1};
+  int32_t h[3], r[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    h[q] = p.hb[ob + oc[q]];
+    r[q] = p.rk[ob + oc[q]];
+  }
+  int err = 0;
+  const int32_t row[3] = {(int32_t)hplan_key(p, t, oc[0], err), (int32_t)(hplan_key(p, t, oc[1], err) & 0x7FFFFFFFu),
+                          (int32_t)(hplan_key(p, t, oc[2], err) & 0x7FFFFFFFu)};
+  const unsigned long long* H = p.H + ((int64_t)t << p.hs_log);
+  const int2* bi = p.binfo + ((int64_t)t << p.hs_log);
+  uint32_t cnt[3];
+  int2 sl[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    cnt[q] = (uint32_t)H[h[q]];
+    sl[q] = bi[h[q]];  // read whatever it holds; used only for shared keys
+  }
+  const bool su = cnt[0] == 1, si = cnt[1] == 1, sj = cnt[2] == 1;
+  if (!su) p.csr[ob + sl[0].y + r[0]] = b;
+  if (!si) p.csr[ob + B + sl[1].y + r[1]] = 2 * b;
+  if (!sj) p.csr[ob + B + sl[2].y + r[2]] = 2 * b + 1;
+  // fused-triplet record layout (see records_one): a = {u, i, j, slot u}, b = {slot i,
+  // slot j, src u, src i}, c = {src j, flags, e, gen}; in place: sources are the rows
+  OccRec q;
+  q.own_row = row[0]; q.own_src = row[1]; q.meta = row[2]; q.ovf = su ? 0 : sl[0].x;
+  q.e_role = si ? 0 : sl[1].x; q.pa_row = sj ? 0 : sl[2].x; q.pb_row = row[0]; q.pa_src = row[1];
+  q.pb_src = row[2];
+  q.pa_slot = ((su && si && sj) ? 1 : 0) | (su ? 2 + 16 : 0) | (si ? 4 + 32 : 0) | (sj ? 8 + 64 : 0);
+  q.pb_slot = (int32_t)e;
+  q.gen = p.gen;
+  p.trec[e] = q;
+}
+
+// CSR position of occurrence id v (users: b; items: 2b + role) of batch t at sorted place x
+__device__ __forceinline__ void hplan_put(const HPlanArgs& p, int32_t t, bool item, int32_t base, int32_t v,
+                                          int32_t x) {
+  const int B = p.B;
+  if (!item) p.tpos[((int64_t)t * B + v) * 4] = t * B + base + x;
+  else p.tpos[((int64_t)t * B + (v >> 1)) * 4 + 1 + (v & 1)] = t * 2 * B + base + x;
+}
+
+__device__ __forceinline__ void hplan_slot(const HPlanArgs& p, int32_t t, int32_t k, bool& item, int32_t& base,
+                                           int32_t& cnt) {
+  const OccRec r = p.inl[(int64_t)t * p.S + k];
+  item = (r.meta & ACF_ITEM_BIT) != 0;
+  cnt = r.meta & ACF_COUNT_MASK;
+  base = r.ovf - t * (item ? 2 : 1) * p.B;
+}
+
+// shared slots of <= ACF_HOT_MIN occurrences: one thread each, insertion sort
+__global__ void __launch_bounds__(256) k_hplan_rank_small(HPlanArgs p) {
+  const int64_t g = blockIdx.x * 256ll + threadIdx.x, G = (int64_t)gridDim.x * 256;
+  for (int32_t t = 0; t < p.nb; ++t) {
+    const int32_t n = p.slot_cnt[t];
+    for (int64_t x = g; x < n; x += G) {
+      const int32_t k = p.slot_list[(int64_t)t * p.S + x];
+      bool item;
+      int32_t base, cnt;
+      hplan_slot(p, t, k, item, base, cnt);
+      const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
+      int32_t v[ACF_HOT_MIN];
+#pragma unroll
+      for (int q = 0; q < ACF_HOT_MIN; ++q) v[q] = q < cnt ? seg[q] : 0x7fffffff;
+#pragma unroll
+      for (int q = 1; q < ACF_HOT_MIN; ++q) {  // fixed network: insertion by compare-exchange
+#pragma unroll
+        for (int w = q; w > 0; --w) {
+          const int32_t lo = min(v[w - 1], v[w]), hi = max(v[w - 1], v[w]);
+          v[w - 1] = lo;
+          v[w] = hi;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < ACF_HOT_MIN; ++q)
+        if (q < cnt) hplan_put(p, t, item, base, v[q], q);
+    }
+  }
+}
+
+// hot slots: <= 64 occurrences by one wave (all-pairs ranks), more by the
+// workgroup through an LDS bitmap of the side's occurrence ids (2B bits) and
+// its prefix popcounts.  Dynamic LDS: 2 x ceil(2B / 32) words.
+__global__ void __launch_bounds__(256) k_hplan_rank_hot(HPlanArgs p) {
+  using Scan = rocprim::block_scan<int32_t, 256>;
+  __shared__ typename Scan::storage_type scan_st;
+  extern __shared__ uint32_t hbits[];
+  const int nw = (2 * p.B + 31) >> 5;
+  uint32_t* pre = hbits + nw;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int nwaves = gridDim.x * 4;
+  for (int32_t t = 0; t < p.nb; ++t) {
+    const int32_t n = p.hl.cnt[t];
+    const int4* hl = p.hl.list + (int64_t)t * p.hl.hot_stride;
+    // slots of <= 64 occurrences: one wave each
+    for (int32_t x = blockIdx.x * 4 + wave; x < n; x += nwaves) {
+      const int4 he = hl[x];
+      if (he.w > 64) continue;
+      bool item;
+      int32_t base, cnt;
+      hplan_slot(p, t, he.x, item, base, cnt);
+      const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
+      const int32_t v = lane < cnt ? seg[lane] : 0x7fffffff;
+      int32_t rank = 0;
+      for (int j = 0; j < 64; ++j) rank += __shfl(v, j) < v ? 1 : 0;
+      if (lane < cnt) hplan_put(p, t, item, base, v, rank);
+    }
+    // larger ones: one workgroup each
+    for (int32_t x = blockIdx.x; x < n; x += gridDim.x) {
+      const int4 he = hl[x];
+      if (he.w <= 64) continue;  // uniform over the workgroup
+      bool item;
+      int32_t base, cnt;
+      hplan_slot(p, t, he.x, item, base, cnt);
+      const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
+      for (int w = tid; w < nw; w += 256) hbits[w] = 0u;
+      __syncthreads();
+      for (int32_t i = tid; i < cnt; i += 256) {
+        const int32_t v = seg[i];
+        atomicOr(&hbits[v >> 5], 1u << (v & 31));
+      }
+      __syncthreads();
+      const int wpt = (nw + 255) / 256, w0 = tid * wpt;
+      int32_t sum = 0;
+      for (int w = w0; w < min(w0 + wpt, nw); ++w) sum += __popc(hbits[w]);
+      int32_t excl = 0, tot = 0;
+      Scan().exclusive_scan(sum, excl, 0, tot, scan_st);
+      for (int w = w0; w < min(w0 + wpt, nw); ++w) {
+        pre[w] = (uint32_t)excl;
+        excl += __popc(hbits[w]);
+      }
+      __syncthreads();
+      for (int32_t i = tid; i < cnt; i += 256) {
+        const int32_t v = seg[i];
+        const int32_t rank = (int32_t)pre[v >> 5] + __popc(hbits[v >> 5] & ((1u << (v & 31)) - 1u));
+        hplan_put(p, t, item, base, v, rank);
+      }
+      __syncthreads();  // the bitmap is reused
+    }
+  }
+}
+
 // diagnostic build (-DACF_DIAG): s_memrealtime stamps of the plan and step kernels
 #ifdef ACF_DIAG
 __device__ uint64_t* g_stamps = nullptr;
@@ -4044,6 +4363,14 @@ struct acf_apr_ctx {
   int32_t task_lists = 0, task_stride = 0;
   // batch-local plan (k_bplan_sort / k_bplan_build)
   int32_t plan_mode = 0;     // 0 auto (batch-local plan where it applies), 1 always the sort plan
+  // hash plan of triplet-centric steps (k_hplan_*); ACF_HASH_PLAN=0 keeps the sort plan (A/B)
+  int32_t hash_on = 1;
+  int32_t plan_kind = -1;    // acf_apr_plan_kind
+  int32_t hplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
+  int32_t hplan_log = 0;     // buckets per batch = 2^hplan_log >= 6 maxB
+  unsigned long long* hplan_tab = nullptr;
+  int2* hplan_binfo = nullptr;
+  int32_t* hplan_cnt = nullptr;  // [3][maxNB] shared slots, user / item CSR positions
   int32_t bplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   unsigned long long* bmask[2] = {nullptr, nullptr};
   size_t bmask_words = 0;
@@ -4236,6 +4563,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   }
   if (const char* e = getenv("ACF_TAIL")) c->tail_on = atoi(e) != 0;
   if (const char* e = getenv("ACF_TAIL_FLUSHERS")) c->tail_flushers = std::max(1, atoi(e));
+  if (const char* e = getenv("ACF_HASH_PLAN")) c->hash_on = atoi(e) != 0;
   if (const char* e = getenv("ACF_BPLAN_SORT")) {  // radix | 1024 | count (A/B); unset: auto
     const std::string v(e);
     c->bplan_sort = v == "radix" ? 1 : v == "1024" ? 2 : v == "count" ? 3 : 0;
@@ -4397,6 +4725,83 @@ static bool bplan_ready(acf_apr_ctx* c) {
   return true;
 }
 
+static bool hplan_ready(acf_apr_ctx* c) {
+  if (c->hplan_ok >= 0) return c->hplan_ok == 1;
+  c->hplan_ok = 0;
+  if (c->maxB > ACF_HPLAN_MAXB) return false;
+  c->hplan_log = (int32_t)bits_for((uint64_t)6 * c->maxB - 1);
+  const size_t n = (size_t)c->maxNB << c->hplan_log;
+  std::vector<void*> got;
+  auto A = [&](auto** p, size_t m) -> bool {
+    if (dalloc(c, p, m) != ACF_OK) return false;
+    got.push_back(*p);
+    return true;
+  };
+  if (!(A(&c->hplan_tab, n) && A(&c->hplan_binfo, n) && A(&c->hplan_cnt, (size_t)3 * c->maxNB))) {
+    (void)hipGetLastError();
+    for (void* p : got) {
+      (void)hipFree(p);
+      c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), p));
+    }
+    c->hplan_tab = nullptr;
+    c->hplan_binfo = nullptr;
+    c->hplan_cnt = nullptr;
+    return false;
+  }
+  c->hplan_ok = 1;
+  return true;
+}
+
+// triplet-centric plans (see k_hplan_*): the same step inputs as the sort plan's
+// tri branch, slot ids and CSR ranges numbered in allocation order
+static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg, int32_t B,
+                     int32_t nb, int32_t gen, int32_t kb, int32_t check, hipStream_t s) {
+  const int64_t E = (int64_t)B * nb;
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  HIP_TRY(hipMemsetAsync(c->hplan_tab, 0xFF, ((size_t)nb << c->hplan_log) * 8, s));
+  HIP_TRY(hipMemsetAsync(c->hplan_cnt, 0, (size_t)3 * c->maxNB * sizeof(int32_t), s));
+  HIP_TRY(hipMemsetAsync(c->slot_cnt, 0, (size_t)c->maxNB * sizeof(int32_t), s));
+  HIP_TRY(hipMemsetAsync(c->flush_cnt, 0, (size_t)c->maxNB * sizeof(int32_t), s));
+  HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
+  HIP_TRY(hipMemsetAsync(c->hot.arrive, 0, (size_t)nb * c->hot.piece_stride * sizeof(int32_t), s));
+  HPlanArgs p;
+  p.user = user; p.ipos = ipos; p.ineg = ineg;
+  p.U1 = c->U1; p.I1 = c->I1;
+  p.B = B; p.S = 3 * B; p.nb = nb; p.gen = gen; p.hs_log = c->hplan_log;
+  p.opad = (3 * B + 63) & ~63;
+  p.H = c->hplan_tab; p.binfo = c->hplan_binfo;
+  p.hb = c->flag; p.rk = c->inc; p.csr = c->tsl;
+  p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
+  p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
+  p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt;
+  p.hl = c->hot;
+  p.err = c->err; p.gen_ptr = c->gen_dev;
+  const int64_t nocc = (int64_t)nb * p.opad;
+  k_hplan_insert<<<(unsigned)((nocc + 255) / 256), 256, 0, s>>>(p);
+  k_hplan_claim<<<(unsigned)((nocc + 255) / 256), 256, 0, s>>>(p);
+  k_hplan_trip<<<(unsigned)((E + 255) / 256), 256, 0, s>>>(p);
+  k_hplan_rank_small<<<1024, 256, 0, s>>>(p);
+  k_hplan_rank_hot<<<1024, 256, (size_t)2 * ((2 * B + 31) / 32) * sizeof(uint32_t), s>>>(p);
+  HIP_TRY(hipGetLastError());
+  c->plan_R = 1;
+  c->plan_kind2 = 0;
+  c->plan_kb = kb;
+  c->tri = 1;
+  c->plan_kind = 3;
+  c->task_lists = 0;
+  c->lists = 1;
+  if (check) {
+    int32_t herr = 0;
+    HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ACF_CHECK(herr == 0, ACF_E_RANGE, "triplet index out of range (%s%s)",
+              (herr & 1) ? "user >= num_user_rows " : "", (herr & 2) ? "item >= num_item_rows" : "");
+  }
+  c->B = B;
+  c->nb = nb;
+  return ACF_OK;
+}
+
 static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg,
                       int32_t B, int32_t nb, int32_t gen, int32_t kb, int32_t check, hipStream_t s) {
   const int cur = gen & 1, oth = cur ^ 1;
@@ -4454,6 +4859,8 @@ static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, 
   c->bmask_dirty[cur] = 1;
   c->bmask_dirty[oth] = 0;
   c->plan_R = c->R;
+  c->tri = 0;
+  c->plan_kind = 1;
   c->plan_kind2 = 1;
   c->plan_kb = kb;
   c->task_lists = 1;
@@ -4499,6 +4906,7 @@ static int shard_plan_small(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   c->plan_kind2 = 0;
   c->plan_kb = kb;
   c->tri = 0;
+  c->plan_kind = 2;
   c->task_lists = 0;
   c->lists = 1;
   if (check) {
@@ -4557,6 +4965,9 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   if (c->shard && nb == 1 && B <= 1024 && c->plan_mode == 0 &&
       bits_for((uint64_t)std::max(c->U1, c->I1)) <= 30)
     return shard_plan_small(c, user, ipos, ineg, B, gen, check, s);
+  if (is_packed(c, B) && !c->shard && c->fusion && c->plan_mode == 0 && c->hash_on && B <= ACF_HPLAN_MAXB &&
+      hplan_ready(c))
+    return hash_plan(c, user, ipos, ineg, B, nb, gen, (int32_t)bits_for((uint64_t)3 * B + 1), check, s);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
   // 32-bit keys (segment only, occurrence as the sort value) when they fit
   const uint32_t sb = std::max(bits_for((uint64_t)nb * (uint64_t)c->U1),
@@ -4626,6 +5037,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   }
   HIP_TRY(hipGetLastError());
   c->plan_R = packed ? 1 : c->R;
+  c->plan_kind = 0;
   c->plan_kind2 = all_dt;
   c->plan_kb = kb;
   c->tri = packed && !c->shard && c->fusion;
@@ -5317,6 +5729,8 @@ extern "C" int acf_apr_set_plan_mode(acf_apr_ctx* c, int32_t mode) {
   c->plan_mode = mode;
   return ACF_OK;
 }
+
+extern "C" int acf_apr_plan_kind(const acf_apr_ctx* c) { return c ? c->plan_kind : -1; }
 
 extern "C" int acf_apr_set_fusion(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");

@@ -241,6 +241,14 @@ class APRContext:
         m = {"auto": 0, "sort": 1}.get(mode, mode)
         call("acf_apr_set_plan_mode", self._ptr, int(m))
 
+    PLAN_KINDS = {-1: None, 0: "sort", 1: "batch", 2: "shard", 3: "hash"}
+
+    def plan_kind(self) -> str | None:
+        """The planner the last plan() used: 'sort' (device-wide radix sort),
+        'batch' (batch-local, B <= 1,024), 'shard' (one-workgroup shard plan) or
+        'hash' (triplet-centric plans); None before any plan."""
+        return self.PLAN_KINDS[_native.load().acf_apr_plan_kind(self._ptr)]
+
     def set_fusion(self, on: bool) -> None:
         """Fuse triplets whose three rows occur once in their batch (default on;
         identical results either way).  Applies to train_planned / time_kernels;

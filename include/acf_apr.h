@@ -168,11 +168,20 @@ int acf_apr_set_fusion(acf_apr_ctx* ctx, int32_t on);
 
 /* Which planner acf_apr_plan uses: 0 = auto (the default: the batch-local plan,
  * one workgroup per batch in two launches, for one-wavefront-per-slot plans of
- * batches up to 1,024 triplets on tables whose batch bitmaps fit 64 MB; the
- * device-wide sort plan otherwise), 1 = always the device-wide sort plan.  Both
- * write identical records, task lists and write-back tables.  Not part of the
- * reference surface (A/B and the planner-equivalence test). */
+ * batches up to 1,024 triplets on tables whose batch bitmaps fit 64 MB; the hash
+ * plan for triplet-centric plans -- one lane-group per slot, fusion on, not
+ * shard mode, batches up to 65,536 -- unless ACF_HASH_PLAN=0 was set when the
+ * context was made; the device-wide sort plan otherwise), 1 = always the
+ * device-wide sort plan.  Every planner gives the step identical bits (the hash
+ * plan numbers slots and CSR ranges in another order, and keeps the occurrence
+ * order inside each range).  Not part of the reference surface (A/B and the
+ * planner-equivalence tests). */
 int acf_apr_set_plan_mode(acf_apr_ctx* ctx, int32_t mode);
+
+/* The planner the last acf_apr_plan used: 0 device-wide sort plan, 1 batch-local
+ * plan, 2 one-workgroup shard plan, 3 hash plan; -1 before any plan.  Not part
+ * of the reference surface (tests and bench). */
+int acf_apr_plan_kind(const acf_apr_ctx* ctx);
 
 /* Overlapped APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
  * the setting is per context).  For plans with one

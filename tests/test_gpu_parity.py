@@ -571,6 +571,57 @@ def test_hot_slots_deterministic(ops, dev):
             assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("B,adver", [(32768, 1), (32768, 0), (4096, 1)])
+def test_hash_plan_matches_sort_plan(ops, dev, monkeypatch, B, adver):
+    """The hash plan (k_hplan_*: triplet-centric plans, the default) against the
+    device-wide sort plan: identical bits through the triplet-centric step, whole
+    range and piecewise, on Zipf positives whose top items have thousands of
+    occurrences per batch (the workgroup bitmap ranks), tens (the wave ranks) and
+    up to 8 (the per-thread network); ACF_HASH_PLAN=0 falls back to the sort plan."""
+    U1, I1, d, nb = 200_000, 100_000, 64, 3
+    P, Q, u, i, j = _zipf_large(11 + B + adver, U1, I1, d, B, nb)
+    cnt = np.bincount(np.concatenate([i[:B], j[:B]]))
+    assert cnt.max() > 64 and ((cnt > 8) & (cnt <= 64)).any() and ((cnt > 1) & (cnt <= 8)).any()
+    hp = ops.StepHParams(adver=adver, reg=0.01)
+    uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
+    runs = []
+    for mode, pieces, env in (("sort", [(0, nb)], "1"), ("auto", [(0, nb)], "1"),
+                              ("auto", [(0, 1), (1, nb - 1)], "1"), ("auto", [(0, nb)], "0")):
+        monkeypatch.setenv("ACF_HASH_PLAN", env)
+        ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+        ctx.set_plan_mode(mode)
+        ctx.plan(uu, ii, jj, B)
+        assert ctx.plan_kind() == ("hash" if mode == "auto" and env == "1" else "sort")
+        tabs = _gpu_tables(P, Q, dev)
+        for first, n in pieces:
+            ctx.train_planned(tabs, hp, first, n, graph=first == 0)
+        lc, la = ctx.losses()
+        assert ctx.step_errors() == 0
+        runs.append(tabs + [lc.clone(), la.clone()])
+    torch.cuda.synchronize()
+    names = ("P", "Q", "accP", "accQ", "loss_clean", "loss_adv")
+    for other in runs[1:]:
+        for x, y, n in zip(runs[0], other, names):
+            if n == "loss_adv" and not adver:
+                continue
+            assert torch.equal(x, y), n
+
+
+def test_hash_plan_range_check(ops, dev):
+    """A triplet index out of range raises from the hash plan too, and the next
+    clean plan works."""
+    from importlib import import_module
+    native = import_module("adversarial-collaborative-filtering_amd._native")
+    B = 4096
+    ctx = ops.APRContext(5000, 5000, 16, B, 2, dev)
+    ok = torch.arange(2 * B, dtype=torch.int32, device=dev) % 5000
+    bad = ok.clone()
+    bad[B + 7] = 5000
+    with pytest.raises(native.NativeIndexError):
+        ctx.plan(ok, bad, ok, B)
+    assert ctx.plan(ok, ok, ok, B) == 2 and ctx.plan_kind() == "hash"
+
+
 def _sparse_stream(seed, U1, I1, B, nb, hot=64, p_hot=0.05):
     """Mostly rows that occur once per batch (fused triplets), plus a small hot
     set that recurs across consecutive batches (pending / next-batch rows)."""
