@@ -687,6 +687,8 @@ struct HPlanArgs {
   int32_t* tpos;          // [E][4] CSR positions of the triplet's occurrences
   int32_t* slot_list;
   int32_t* slot_cnt;
+  int32_t* saux;          // [nb][S] beside slot_list: CSR base | count << 24 | item << 31
+  int32_t* haux;          // [nb][hot_stride] beside the hot list: CSR base | item << 31
   HotLists hl;
   int32_t* err;
   int32_t* gen_ptr;
@@ -753,20 +755,17 @@ __device__ __forceinline__ int32_t wave_excl_sum(int32_t v, int32_t& total) {
   return incl - v;
 }
 
-// one atomicAdd of the wave's total by lane 0; each lane's base = the old value + excl
-__device__ __forceinline__ int32_t wave_take(int32_t* ctr, int32_t v) {
-  int32_t total = 0;
-  const int32_t excl = wave_excl_sum(v, total);
-  int32_t base = 0;
-  if ((threadIdx.x & 63) == 0 && total > 0) base = atomicAdd(ctr, total);
-  return __shfl(base, 0) + excl;
-}
-
+// The claimers allocate six things at once (slot id, user / item CSR range, a
+// place in the shared-slot list, a hot-list entry, hot pieces): wave prefix
+// sums, then ONE atomicAdd per counter and workgroup, the six issued together
+// (a workgroup's 256 occurrences all belong to one batch: opad is a multiple
+// of 256).
 __global__ void __launch_bounds__(256) k_hplan_claim(HPlanArgs p) {
+  __shared__ int32_t s_at[4][6];
   const int64_t x = blockIdx.x * 256ll + threadIdx.x;
   const int32_t t = (int32_t)(x / p.opad), o = (int32_t)(x - (int64_t)t * p.opad);
-  const int B = p.B, S3 = 3 * B;
-  if (t >= p.nb) return;  // whole waves (opad is a multiple of 64)
+  const int B = p.B, S3 = 3 * B, wave = threadIdx.x >> 6;
+  if (t >= p.nb) return;  // whole workgroups
   const bool live = o < S3;
   int32_t h = 0, r = 1;
   if (live) {
@@ -780,15 +779,35 @@ __global__ void __launch_bounds__(256) k_hplan_claim(HPlanArgs p) {
     key = (uint32_t)(e >> 32);
   }
   const bool claim = cnt > 1, item = o >= B, hot = claim && cnt > ACF_HOT_MIN;
-  const int32_t k = wave_take(p.scnt + t, claim ? 1 : 0);
-  const int32_t ub = wave_take(p.ucsr + t, claim && !item ? (int32_t)cnt : 0);
-  const int32_t ib = wave_take(p.icsr + t, claim && item ? (int32_t)cnt : 0);
-  const int32_t ls = wave_take(p.slot_cnt + t, claim && !hot ? 1 : 0);
-  const int32_t hx = wave_take(p.hl.cnt + t, hot ? 1 : 0);
   const int32_t np = hot ? hot_pieces((int32_t)cnt) : 0;
-  const int32_t pb = wave_take(p.hl.pcnt + t, np);
+  const int32_t v[6] = {claim ? 1 : 0, claim && !item ? (int32_t)cnt : 0, claim && item ? (int32_t)cnt : 0,
+                        claim && !hot ? 1 : 0, hot ? 1 : 0, np};
+  int32_t ex[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    int32_t tot = 0;
+    ex[c] = wave_excl_sum(v[c], tot);
+    if ((threadIdx.x & 63) == 0) s_at[wave][c] = tot;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int c = threadIdx.x;
+    int32_t* ctr = c == 0 ? p.scnt : c == 1 ? p.ucsr : c == 2 ? p.icsr : c == 3 ? p.slot_cnt
+                 : c == 4 ? p.hl.cnt : p.hl.pcnt;
+    int32_t run[4], sum = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      run[w] = sum;
+      sum += s_at[w][c];
+    }
+    const int32_t base = sum > 0 ? atomicAdd(ctr + t, sum) : 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s_at[w][c] = base + run[w];
+  }
+  __syncthreads();
   if (!claim) return;
-  const int32_t base = item ? ib : ub;
+  const int32_t k = s_at[wave][0] + ex[0];
+  const int32_t base = item ? s_at[wave][2] + ex[2] : s_at[wave][1] + ex[1];
   p.binfo[((int64_t)t << p.hs_log) + h] = make_int2(k, base);
   OccRec rec = {};
   rec.own_row = (int32_t)(key & 0x7FFFFFFFu);
@@ -798,10 +817,16 @@ __global__ void __launch_bounds__(256) k_hplan_claim(HPlanArgs p) {
   rec.e_role = -1;
   rec.gen = p.gen;
   p.inl[(int64_t)t * p.S + k] = rec;
+  // the rank kernels' view of the slot: CSR base | count << 24 (<= 8) | item << 31
+  const int32_t aux = base | (item ? (int32_t)0x80000000 : 0);
   if (!hot) {
+    const int32_t ls = s_at[wave][3] + ex[3];
     p.slot_list[(int64_t)t * p.S + ls] = k;
+    p.saux[(int64_t)t * p.S + ls] = aux | ((int32_t)cnt << 24);
   } else {
+    const int32_t hx = s_at[wave][4] + ex[4], pb = s_at[wave][5] + ex[5];
     p.hl.list[(int64_t)t * p.hl.hot_stride + hx] = make_int4(k, np, pb, (int32_t)cnt);
+    p.haux[(int64_t)t * p.hl.hot_stride + hx] = aux;
     int4* pc = p.hl.piece + (int64_t)t * p.hl.piece_stride + pb;
     for (int32_t q = 0; q < np; ++q) pc[q] = make_int4(k, q, np, pb);
   }
@@ -857,47 +882,36 @@ __device__ __forceinline__ void hplan_put(const HPlanArgs& p, int32_t t, bool it
   else p.tpos[((int64_t)t * B + (v >> 1)) * 4 + 1 + (v & 1)] = t * 2 * B + base + x;
 }
 
-__device__ __forceinline__ void hplan_slot(const HPlanArgs& p, int32_t t, int32_t k, bool& item, int32_t& base,
-                                           int32_t& cnt) {
-  const OccRec r = p.inl[(int64_t)t * p.S + k];
-  item = (r.meta & ACF_ITEM_BIT) != 0;
-  cnt = r.meta & ACF_COUNT_MASK;
-  base = r.ovf - t * (item ? 2 : 1) * p.B;
-}
-
-// shared slots of <= ACF_HOT_MIN occurrences: one thread each, insertion sort
+// shared slots of <= ACF_HOT_MIN occurrences: one thread each, a fixed
+// compare-exchange network; blockIdx.y = the batch
 __global__ void __launch_bounds__(256) k_hplan_rank_small(HPlanArgs p) {
-  const int64_t g = blockIdx.x * 256ll + threadIdx.x, G = (int64_t)gridDim.x * 256;
-  for (int32_t t = 0; t < p.nb; ++t) {
-    const int32_t n = p.slot_cnt[t];
-    for (int64_t x = g; x < n; x += G) {
-      const int32_t k = p.slot_list[(int64_t)t * p.S + x];
-      bool item;
-      int32_t base, cnt;
-      hplan_slot(p, t, k, item, base, cnt);
-      const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
-      int32_t v[ACF_HOT_MIN];
+  const int32_t t = blockIdx.y, n = p.slot_cnt[t];
+  for (int32_t x = blockIdx.x * 256 + threadIdx.x; x < n; x += gridDim.x * 256) {
+    const int32_t aux = p.saux[(int64_t)t * p.S + x];
+    const bool item = aux < 0;
+    const int32_t base = aux & 0xFFFFFF, cnt = (aux >> 24) & 0x7F;
+    const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
+    int32_t v[ACF_HOT_MIN];
 #pragma unroll
-      for (int q = 0; q < ACF_HOT_MIN; ++q) v[q] = q < cnt ? seg[q] : 0x7fffffff;
+    for (int q = 0; q < ACF_HOT_MIN; ++q) v[q] = q < cnt ? seg[q] : 0x7fffffff;
 #pragma unroll
-      for (int q = 1; q < ACF_HOT_MIN; ++q) {  // fixed network: insertion by compare-exchange
+    for (int q = 1; q < ACF_HOT_MIN; ++q) {
 #pragma unroll
-        for (int w = q; w > 0; --w) {
-          const int32_t lo = min(v[w - 1], v[w]), hi = max(v[w - 1], v[w]);
-          v[w - 1] = lo;
-          v[w] = hi;
-        }
+      for (int w = q; w > 0; --w) {
+        const int32_t lo = min(v[w - 1], v[w]), hi = max(v[w - 1], v[w]);
+        v[w - 1] = lo;
+        v[w] = hi;
       }
-#pragma unroll
-      for (int q = 0; q < ACF_HOT_MIN; ++q)
-        if (q < cnt) hplan_put(p, t, item, base, v[q], q);
     }
+#pragma unroll
+    for (int q = 0; q < ACF_HOT_MIN; ++q)
+      if (q < cnt) hplan_put(p, t, item, base, v[q], q);
   }
 }
 
-// hot slots: <= 64 occurrences by one wave (all-pairs ranks), more by the
-// workgroup through an LDS bitmap of the side's occurrence ids (2B bits) and
-// its prefix popcounts.  Dynamic LDS: 2 x ceil(2B / 32) words.
+// hot slots of batch blockIdx.y: <= 64 occurrences by one wave (all-pairs
+// ranks), more by the workgroup through an LDS bitmap of the side's occurrence
+// ids (2B bits) and its prefix popcounts.  Dynamic LDS: 2 x ceil(2B / 32) words.
 __global__ void __launch_bounds__(256) k_hplan_rank_hot(HPlanArgs p) {
   using Scan = rocprim::block_scan<int32_t, 256>;
   __shared__ typename Scan::storage_type scan_st;
@@ -905,55 +919,51 @@ __global__ void __launch_bounds__(256) k_hplan_rank_hot(HPlanArgs p) {
   const int nw = (2 * p.B + 31) >> 5;
   uint32_t* pre = hbits + nw;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int nwaves = gridDim.x * 4;
-  for (int32_t t = 0; t < p.nb; ++t) {
-    const int32_t n = p.hl.cnt[t];
-    const int4* hl = p.hl.list + (int64_t)t * p.hl.hot_stride;
-    // slots of <= 64 occurrences: one wave each
-    for (int32_t x = blockIdx.x * 4 + wave; x < n; x += nwaves) {
-      const int4 he = hl[x];
-      if (he.w > 64) continue;
-      bool item;
-      int32_t base, cnt;
-      hplan_slot(p, t, he.x, item, base, cnt);
-      const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
-      const int32_t v = lane < cnt ? seg[lane] : 0x7fffffff;
-      int32_t rank = 0;
-      for (int j = 0; j < 64; ++j) rank += __shfl(v, j) < v ? 1 : 0;
-      if (lane < cnt) hplan_put(p, t, item, base, v, rank);
+  const int32_t t = blockIdx.y, n = p.hl.cnt[t];
+  const int4* hl = p.hl.list + (int64_t)t * p.hl.hot_stride;
+  const int32_t* ha = p.haux + (int64_t)t * p.hl.hot_stride;
+  for (int32_t x = blockIdx.x * 4 + wave; x < n; x += gridDim.x * 4) {
+    const int32_t cnt = hl[x].w;
+    if (cnt > 64) continue;  // wave-uniform
+    const int32_t aux = ha[x];
+    const bool item = aux < 0;
+    const int32_t base = aux & 0x7FFFFFFF;
+    const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
+    const int32_t v = lane < cnt ? seg[lane] : 0x7fffffff;
+    int32_t rank = 0;
+    for (int j = 0; j < 64; ++j) rank += __shfl(v, j) < v ? 1 : 0;
+    if (lane < cnt) hplan_put(p, t, item, base, v, rank);
+  }
+  for (int32_t x = blockIdx.x; x < n; x += gridDim.x) {
+    const int32_t cnt = hl[x].w;
+    if (cnt <= 64) continue;  // uniform over the workgroup
+    const int32_t aux = ha[x];
+    const bool item = aux < 0;
+    const int32_t base = aux & 0x7FFFFFFF;
+    const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
+    for (int w = tid; w < nw; w += 256) hbits[w] = 0u;
+    __syncthreads();
+    for (int32_t i = tid; i < cnt; i += 256) {
+      const int32_t v = seg[i];
+      atomicOr(&hbits[v >> 5], 1u << (v & 31));
     }
-    // larger ones: one workgroup each
-    for (int32_t x = blockIdx.x; x < n; x += gridDim.x) {
-      const int4 he = hl[x];
-      if (he.w <= 64) continue;  // uniform over the workgroup
-      bool item;
-      int32_t base, cnt;
-      hplan_slot(p, t, he.x, item, base, cnt);
-      const int32_t* seg = p.csr + (int64_t)t * 3 * p.B + (item ? p.B : 0) + base;
-      for (int w = tid; w < nw; w += 256) hbits[w] = 0u;
-      __syncthreads();
-      for (int32_t i = tid; i < cnt; i += 256) {
-        const int32_t v = seg[i];
-        atomicOr(&hbits[v >> 5], 1u << (v & 31));
-      }
-      __syncthreads();
-      const int wpt = (nw + 255) / 256, w0 = tid * wpt;
-      int32_t sum = 0;
-      for (int w = w0; w < min(w0 + wpt, nw); ++w) sum += __popc(hbits[w]);
-      int32_t excl = 0, tot = 0;
-      Scan().exclusive_scan(sum, excl, 0, tot, scan_st);
-      for (int w = w0; w < min(w0 + wpt, nw); ++w) {
-        pre[w] = (uint32_t)excl;
-        excl += __popc(hbits[w]);
-      }
-      __syncthreads();
-      for (int32_t i = tid; i < cnt; i += 256) {
-        const int32_t v = seg[i];
-        const int32_t rank = (int32_t)pre[v >> 5] + __popc(hbits[v >> 5] & ((1u << (v & 31)) - 1u));
-        hplan_put(p, t, item, base, v, rank);
-      }
-      __syncthreads();  // the bitmap is reused
+    __syncthreads();
+    const int wpt = (nw + 255) / 256, w0 = tid * wpt;
+    int32_t sum = 0;
+    for (int w = w0; w < min(w0 + wpt, nw); ++w) sum += __popc(hbits[w]);
+    int32_t excl = 0, tot = 0;
+    Scan().exclusive_scan(sum, excl, 0, tot, scan_st);
+    for (int w = w0; w < min(w0 + wpt, nw); ++w) {
+      pre[w] = (uint32_t)excl;
+      excl += __popc(hbits[w]);
     }
+    __syncthreads();
+    for (int32_t i = tid; i < cnt; i += 256) {
+      const int32_t v = seg[i];
+      const int32_t rank = (int32_t)pre[v >> 5] + __popc(hbits[v >> 5] & ((1u << (v & 31)) - 1u));
+      hplan_put(p, t, item, base, v, rank);
+    }
+    __syncthreads();  // the bitmap is reused
   }
 }
 
@@ -4371,6 +4381,7 @@ struct acf_apr_ctx {
   unsigned long long* hplan_tab = nullptr;
   int2* hplan_binfo = nullptr;
   int32_t* hplan_cnt = nullptr;  // [3][maxNB] shared slots, user / item CSR positions
+  int32_t* hplan_haux = nullptr;  // [maxNB][hot_stride] CSR base | item of each hot-list entry
   int32_t bplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   unsigned long long* bmask[2] = {nullptr, nullptr};
   size_t bmask_words = 0;
@@ -4737,7 +4748,8 @@ static bool hplan_ready(acf_apr_ctx* c) {
     got.push_back(*p);
     return true;
   };
-  if (!(A(&c->hplan_tab, n) && A(&c->hplan_binfo, n) && A(&c->hplan_cnt, (size_t)3 * c->maxNB))) {
+  if (!(A(&c->hplan_tab, n) && A(&c->hplan_binfo, n) && A(&c->hplan_cnt, (size_t)3 * c->maxNB) &&
+        A(&c->hplan_haux, (size_t)c->maxNB * c->hot.hot_stride))) {
     (void)hipGetLastError();
     for (void* p : got) {
       (void)hipFree(p);
@@ -4746,6 +4758,7 @@ static bool hplan_ready(acf_apr_ctx* c) {
     c->hplan_tab = nullptr;
     c->hplan_binfo = nullptr;
     c->hplan_cnt = nullptr;
+    c->hplan_haux = nullptr;
     return false;
   }
   c->hplan_ok = 1;
@@ -4768,20 +4781,22 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   p.user = user; p.ipos = ipos; p.ineg = ineg;
   p.U1 = c->U1; p.I1 = c->I1;
   p.B = B; p.S = 3 * B; p.nb = nb; p.gen = gen; p.hs_log = c->hplan_log;
-  p.opad = (3 * B + 63) & ~63;
+  p.opad = (3 * B + 255) & ~255;
   p.H = c->hplan_tab; p.binfo = c->hplan_binfo;
   p.hb = c->flag; p.rk = c->inc; p.csr = c->tsl;
   p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
   p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
   p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt;
+  p.saux = c->flush_list;  // unused by in-place plans
+  p.haux = c->hplan_haux;
   p.hl = c->hot;
   p.err = c->err; p.gen_ptr = c->gen_dev;
   const int64_t nocc = (int64_t)nb * p.opad;
   k_hplan_insert<<<(unsigned)((nocc + 255) / 256), 256, 0, s>>>(p);
   k_hplan_claim<<<(unsigned)((nocc + 255) / 256), 256, 0, s>>>(p);
   k_hplan_trip<<<(unsigned)((E + 255) / 256), 256, 0, s>>>(p);
-  k_hplan_rank_small<<<1024, 256, 0, s>>>(p);
-  k_hplan_rank_hot<<<1024, 256, (size_t)2 * ((2 * B + 31) / 32) * sizeof(uint32_t), s>>>(p);
+  k_hplan_rank_small<<<dim3(64, nb), 256, 0, s>>>(p);
+  k_hplan_rank_hot<<<dim3(64, nb), 256, (size_t)2 * ((2 * B + 31) / 32) * sizeof(uint32_t), s>>>(p);
   HIP_TRY(hipGetLastError());
   c->plan_R = 1;
   c->plan_kind2 = 0;
