@@ -640,63 +640,70 @@ __global__ void k_task_list(const int32_t* __restrict__ flags, const int32_t* __
 
 // ---------------------------------------------------------------------------
 // Hash plan (r04): the plan of triplet-centric steps (one lane-group per slot,
-// fusion on, not shard mode; B >= 4,096) without a device-wide sort.  What such
-// a step reads of its plan: per triplet its rows, which of them occur once in the
-// batch ("single": stepped by the triplet itself) and, for the others ("shared"),
-// a slot id and the CSR position of the occurrence; per shared slot its row,
-// count and CSR range (the inline record), in which the combine adds the
-// occurrences' contributions IN OCCURRENCE ORDER (the slot path's bits); the
-// per-batch lists of shared slots and of hot slots with their pieces.  Slot ids
-// and CSR ranges may be numbered in any order; only the order inside a range is
-// fixed.  So (APR.py:183-195's Unique + UnsortedSegmentSum, restated):
-//  1. k_hplan_insert: each occurrence inserts its (side, row) key into its
-//     batch's open-addressing table (2^hs_log buckets >= 2 x 3B, linear probing;
-//     a bucket is {key, count}: one 64-bit CAS claims it, one 64-bit add counts)
-//     and keeps its bucket and its place in the bucket's (arbitrary) add order;
-//  2. k_hplan_claim: the occurrence that claimed a bucket of count > 1 allocates
-//     the slot id, the CSR range and the list places (one atomic per wave each)
-//     and writes the inline record;
-//  3. k_hplan_trip: per triplet, its record (single bits from the counts) and
-//     its shared occurrences' ids into their CSR ranges at the add-order place;
-//  4. k_hplan_rank_small / k_hplan_rank_hot: each range put in occurrence order
-//     -- <= 8 entries by one thread, <= 64 by a wave (all-pairs ranks), more by a
-//     workgroup (an LDS bitmap of the side's occurrences and its prefix
+// fusion on, not shard mode; B >= 4,096) without the full-key radix sort.  What
+// such a step reads of its plan: per triplet its rows, which of them occur once
+// in the batch ("single": stepped by the triplet itself) and, for the others
+// ("shared"), a slot id and the CSR position of the occurrence; per shared slot
+// its row, count and CSR range (the inline record), in which the combine adds
+// the occurrences' contributions IN OCCURRENCE ORDER (the slot path's bits);
+// the per-batch lists of shared slots and of hot slots with their pieces.  Slot
+// ids and CSR ranges may be numbered in any order; only the order inside a range
+// is fixed.  So (APR.py:183-195's Unique + UnsortedSegmentSum, restated):
+//  1. k_hplan_keys + one rocPRIM radix sort of (batch, partition) -- the top PB
+//     bits of a Fibonacci hash of the (side, row) key, PB + log2(batches) bits
+//     (2 passes at configs[4] instead of the sort plan's 4 over 30-bit keys) --
+//     groups each batch's occurrences into 2^PB partitions of ~768, disjoint in
+//     keys; k_hplan_bounds finds each partition's range;
+//  2. k_hplan_dedup, one workgroup per partition: its keys counted in an LDS hash
+//     table (LDS atomics only); the shared keys claim slot ids, CSR ranges and
+//     list places (one global atomic per counter and workgroup) and write their
+//     inline records; every occurrence gets {slot or -1, CSR position} and the
+//     shared ones enter their CSR range (in LDS-atomic order).  A partition with
+//     more distinct keys than the table holds is split by further hash bits and
+//     done in rounds (terminates: the hash is a bijection of 32-bit keys);
+//  3. k_hplan_trip: per triplet its record (coalesced reads of step 2's output);
+//  4. k_hplan_rank_small / k_hplan_rank_hot: each CSR range put in occurrence
+//     order -- <= 8 entries by one thread, <= 64 by a wave (all-pairs ranks), more
+//     by a workgroup (an LDS bitmap of the side's occurrence ids and its prefix
 //     popcounts) -- and every shared occurrence's CSR position written.
-// Only the tables are cleared (a fill per plan); 5 launches against the sort
-// plan's ~17, and no pass sorts the ~94% of rows that occur once.  The bits of a
-// step are the sort plan's (test_hash_plan_matches_sort_plan).
+// The bits of a step are the sort plan's (test_hash_plan_matches_sort_plan).
+// (A first form inserted every occurrence into a device-wide open-addressing
+// table with 64-bit CAS / add: 1.3 ms per 32-batch chunk at configs[4], the
+// returning atomics serialising at the memory side on the Zipf-popular items;
+// tile-aggregated, still 0.48 ms: slower than the sort plan.)
 // ---------------------------------------------------------------------------
 #define ACF_HPLAN_MAXB 65536  // the hot-rank bitmap: 2B bits of LDS per workgroup
+#define ACF_HPLAN_TS 2048     // LDS buckets of a partition round (distinct keys <= 3/4 of them)
+#define ACF_HPLAN_PART 768    // occurrences per partition (mean)
 
 struct HPlanArgs {
   const int32_t* user;
   const int32_t* ipos;
   const int32_t* ineg;
   int64_t U1, I1;
-  int32_t B, S, nb, gen, hs_log, opad;  // opad: threads per batch (3B rounded up to a wave)
-  unsigned long long* H;  // [nb][2^hs_log] {key << 32 | count}, all ones = empty
-  int2* binfo;            // [nb][2^hs_log] {slot, CSR base} of a shared key (its claimer writes it)
-  int32_t* hb;            // [nb][3B] occurrence -> bucket
-  int32_t* rk;            // [nb][3B] occurrence -> place in its bucket's add order
-  int32_t* csr;           // [nb][3B] occurrence ids by CSR position: users [0, B), items B + [0, 2B)
-  int32_t* scnt;          // [nb] shared slots
-  int32_t* ucsr;          // [nb] user CSR positions taken
-  int32_t* icsr;          // [nb] item CSR positions taken
+  int32_t B, S, nb, gen, pb;  // pb: partition bits (2^pb partitions per batch)
+  uint32_t* pkey;             // [nb][3B] (batch << pb | partition), then sorted
+  unsigned long long* pval;   // [nb][3B] key << 32 | occurrence, sorted with pkey
+  int2* pseg;                 // [nb << pb] partition ranges in the sorted arrays
+  int2* occ;                  // [nb][3B] occurrence -> {slot or -1 (single), CSR position}
+  int32_t* csr;               // [nb][3B] occurrence ids by CSR position: users [0, B), items B + [0, 2B)
+  int32_t* scnt;              // [nb] shared slots
+  int32_t* ucsr;              // [nb] user CSR positions taken
+  int32_t* icsr;              // [nb] item CSR positions taken
   OccRec* inl;
   OccRec* trec;
-  int32_t* tpos;          // [E][4] CSR positions of the triplet's occurrences
+  int32_t* tpos;              // [E][4] CSR positions of the triplet's occurrences
   int32_t* slot_list;
   int32_t* slot_cnt;
-  int32_t* saux;          // [nb][S] beside slot_list: CSR base | count << 24 | item << 31
-  int32_t* haux;          // [nb][hot_stride] beside the hot list: CSR base | item << 31
+  int32_t* flush_cnt;
+  int32_t* saux;              // [nb][S] beside slot_list: CSR base | count << 24 | item << 31
+  int32_t* haux;              // [nb][hot_stride] beside the hot list: CSR base | item << 31
   HotLists hl;
   int32_t* err;
   int32_t* gen_ptr;
 };
 
-__device__ __forceinline__ uint32_t hplan_hash(uint32_t key, int hs_log) {
-  return (key * 2654435761u) >> (32 - hs_log);  // Fibonacci hashing
-}
+__device__ __forceinline__ uint32_t hplan_hash(uint32_t key) { return key * 2654435761u; }  // Fibonacci
 
 // the (side, row) of occurrence o of batch t (users [0, B), items B + 2e + role)
 __device__ __forceinline__ uint32_t hplan_key(const HPlanArgs& p, int32_t t, int32_t o, int& err) {
@@ -712,34 +719,35 @@ __device__ __forceinline__ uint32_t hplan_key(const HPlanArgs& p, int32_t t, int
   return 0x80000000u | (uint32_t)row;
 }
 
-__global__ void __launch_bounds__(256) k_hplan_insert(HPlanArgs p) {
+__global__ void __launch_bounds__(256) k_hplan_keys(HPlanArgs p) {
   const int64_t x = blockIdx.x * 256ll + threadIdx.x;
-  const int32_t t = (int32_t)(x / p.opad), o = (int32_t)(x - (int64_t)t * p.opad);
   const int S3 = 3 * p.B;
-  if (t >= p.nb || o >= S3) return;
+  // the plan's counters and partition ranges start at zero (instead of six fills:
+  // a fill launch costs ~9 us)
+  if (x < ((int64_t)p.nb << p.pb)) p.pseg[x] = make_int2(0, 0);
+  if (x < p.nb) {
+    p.scnt[x] = p.ucsr[x] = p.icsr[x] = 0;
+    p.slot_cnt[x] = p.flush_cnt[x] = 0;
+    p.hl.cnt[x] = p.hl.pcnt[x] = 0;
+  }
+  if (x < (int64_t)p.nb * p.hl.piece_stride) p.hl.arrive[x] = 0;
+  if (x >= (int64_t)p.nb * S3) return;
+  const int32_t t = (int32_t)(x / S3), o = (int32_t)(x - (int64_t)t * S3);
   int err = 0;
   const uint32_t key = hplan_key(p, t, o, err);
   if (err) atomicOr(p.err, err);
-  const uint32_t mask = (1u << p.hs_log) - 1u;
-  unsigned long long* H = p.H + ((int64_t)t << p.hs_log);
-  const unsigned long long mine = ((unsigned long long)key << 32) | 1ull;
-  uint32_t h = hplan_hash(key, p.hs_log), rank = 0;
-  // the table holds at most 3B of its >= 6B buckets: the probe ends
-  for (;;) {
-    unsigned long long e = __hip_atomic_load(H + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e == ~0ull) {
-      const unsigned long long prev = atomicCAS(H + h, ~0ull, mine);
-      if (prev == ~0ull) break;  // claimed: first in add order
-      e = prev;
-    }
-    if ((uint32_t)(e >> 32) == key) {
-      rank = (uint32_t)atomicAdd(H + h, 1ull);  // the count before this occurrence
-      break;
-    }
-    h = (h + 1u) & mask;
-  }
-  p.hb[(int64_t)t * S3 + o] = (int32_t)h;
-  p.rk[(int64_t)t * S3 + o] = (int32_t)rank;
+  const uint32_t part = p.pb ? hplan_hash(key) >> (32 - p.pb) : 0u;
+  p.pkey[x] = ((uint32_t)t << p.pb) | part;
+  p.pval[x] = ((unsigned long long)key << 32) | (uint32_t)o;
+}
+
+// partition ranges over the sorted (batch, partition) keys; absent partitions keep {0, 0}
+__global__ void __launch_bounds__(256) k_hplan_bounds(HPlanArgs p, const uint32_t* __restrict__ sk, int64_t n) {
+  const int64_t x = blockIdx.x * 256ll + threadIdx.x;
+  if (x >= n) return;
+  const uint32_t k = sk[x];
+  if (x == 0 || sk[x - 1] != k) p.pseg[k].x = (int32_t)x;
+  if (x == n - 1 || sk[x + 1] != k) p.pseg[k].y = (int32_t)(x + 1);
 }
 
 // exclusive prefix sum over the wave; total = the wave's sum
@@ -755,80 +763,155 @@ __device__ __forceinline__ int32_t wave_excl_sum(int32_t v, int32_t& total) {
   return incl - v;
 }
 
-// The claimers allocate six things at once (slot id, user / item CSR range, a
-// place in the shared-slot list, a hot-list entry, hot pieces): wave prefix
-// sums, then ONE atomicAdd per counter and workgroup, the six issued together
-// (a workgroup's 256 occurrences all belong to one batch: opad is a multiple
-// of 256).
-__global__ void __launch_bounds__(256) k_hplan_claim(HPlanArgs p) {
+#define ACF_HPLAN_EPT (ACF_HPLAN_TS / 256)  // LDS buckets per thread in the claims
+
+__global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
+  __shared__ uint32_t lkey[ACF_HPLAN_TS];
+  __shared__ int32_t lcnt[ACF_HPLAN_TS];  // count, then the CSR cursor
+  __shared__ int32_t lk[ACF_HPLAN_TS];    // slot (-1: the row occurs once)
+  __shared__ int32_t lb[ACF_HPLAN_TS];    // CSR base
   __shared__ int32_t s_at[4][6];
-  const int64_t x = blockIdx.x * 256ll + threadIdx.x;
-  const int32_t t = (int32_t)(x / p.opad), o = (int32_t)(x - (int64_t)t * p.opad);
-  const int B = p.B, S3 = 3 * B, wave = threadIdx.x >> 6;
-  if (t >= p.nb) return;  // whole workgroups
-  const bool live = o < S3;
-  int32_t h = 0, r = 1;
-  if (live) {
-    h = p.hb[(int64_t)t * S3 + o];
-    r = p.rk[(int64_t)t * S3 + o];
-  }
-  uint32_t cnt = 0, key = 0;
-  if (live && r == 0) {
-    const unsigned long long e = p.H[((int64_t)t << p.hs_log) + h];
-    cnt = (uint32_t)e;
-    key = (uint32_t)(e >> 32);
-  }
-  const bool claim = cnt > 1, item = o >= B, hot = claim && cnt > ACF_HOT_MIN;
-  const int32_t np = hot ? hot_pieces((int32_t)cnt) : 0;
-  const int32_t v[6] = {claim ? 1 : 0, claim && !item ? (int32_t)cnt : 0, claim && item ? (int32_t)cnt : 0,
-                        claim && !hot ? 1 : 0, hot ? 1 : 0, np};
-  int32_t ex[6];
-#pragma unroll
-  for (int c = 0; c < 6; ++c) {
-    int32_t tot = 0;
-    ex[c] = wave_excl_sum(v[c], tot);
-    if ((threadIdx.x & 63) == 0) s_at[wave][c] = tot;
-  }
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    const int c = threadIdx.x;
-    int32_t* ctr = c == 0 ? p.scnt : c == 1 ? p.ucsr : c == 2 ? p.icsr : c == 3 ? p.slot_cnt
-                 : c == 4 ? p.hl.cnt : p.hl.pcnt;
-    int32_t run[4], sum = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      run[w] = sum;
-      sum += s_at[w][c];
+  __shared__ int32_t s_distinct, s_over;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const int32_t t = blockIdx.x >> p.pb;
+  const int B = p.B, S3 = 3 * B;
+  const int2 seg = p.pseg[blockIdx.x];
+  if (seg.y <= seg.x) return;  // absent partition (uniform)
+  int rbits = 0;               // rounds: 2^rbits sub-partitions by the next hash bits
+  for (int r = 0; r < (1 << rbits);) {
+    for (int e = tid; e < ACF_HPLAN_TS; e += 256) {
+      lkey[e] = 0xFFFFFFFFu;
+      lcnt[e] = 0;
     }
-    const int32_t base = sum > 0 ? atomicAdd(ctr + t, sum) : 0;
+    if (tid == 0) { s_distinct = 0; s_over = 0; }
+    __syncthreads();
+    auto in_round = [&](uint32_t key) -> bool {
+      if (!rbits) return true;
+      return (int)((hplan_hash(key) << p.pb) >> (32 - rbits)) == r;
+    };
+    // count the round's keys
+    for (int32_t i = seg.x + tid; i < seg.y; i += 256) {
+      const uint32_t key = (uint32_t)(p.pval[i] >> 32);
+      if (!in_round(key)) continue;
+      uint32_t lh = (hplan_hash(key) >> 7) & (ACF_HPLAN_TS - 1);
+      for (;;) {
+        uint32_t cur = lkey[lh];
+        if (cur == 0xFFFFFFFFu) {
+          if (__hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+          cur = atomicCAS(&lkey[lh], 0xFFFFFFFFu, key);
+          if (cur == 0xFFFFFFFFu) {
+            cur = key;
+            if (atomicAdd(&s_distinct, 1) >= ACF_HPLAN_TS * 3 / 4) atomicOr(&s_over, 1);
+          }
+        }
+        if (cur == key) {
+          atomicAdd(&lcnt[lh], 1);
+          break;
+        }
+        lh = (lh + 1u) & (ACF_HPLAN_TS - 1);
+      }
+    }
+    __syncthreads();
+    if (s_over) {  // too many distinct keys: this round again as two halves
+      r <<= 1;
+      ++rbits;
+      __syncthreads();
+      continue;
+    }
+    // claims of the shared keys (count > 1), aggregated over the workgroup
+    int32_t v[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int w = 0; w < 4; ++w) s_at[w][c] = base + run[w];
-  }
-  __syncthreads();
-  if (!claim) return;
-  const int32_t k = s_at[wave][0] + ex[0];
-  const int32_t base = item ? s_at[wave][2] + ex[2] : s_at[wave][1] + ex[1];
-  p.binfo[((int64_t)t << p.hs_log) + h] = make_int2(k, base);
-  OccRec rec = {};
-  rec.own_row = (int32_t)(key & 0x7FFFFFFFu);
-  rec.own_src = rec.own_row;
-  rec.meta = (int32_t)cnt | (item ? ACF_ITEM_BIT : 0);
-  rec.ovf = (item ? t * 2 * B : t * B) + base;
-  rec.e_role = -1;
-  rec.gen = p.gen;
-  p.inl[(int64_t)t * p.S + k] = rec;
-  // the rank kernels' view of the slot: CSR base | count << 24 (<= 8) | item << 31
-  const int32_t aux = base | (item ? (int32_t)0x80000000 : 0);
-  if (!hot) {
-    const int32_t ls = s_at[wave][3] + ex[3];
-    p.slot_list[(int64_t)t * p.S + ls] = k;
-    p.saux[(int64_t)t * p.S + ls] = aux | ((int32_t)cnt << 24);
-  } else {
-    const int32_t hx = s_at[wave][4] + ex[4], pb = s_at[wave][5] + ex[5];
-    p.hl.list[(int64_t)t * p.hl.hot_stride + hx] = make_int4(k, np, pb, (int32_t)cnt);
-    p.haux[(int64_t)t * p.hl.hot_stride + hx] = aux;
-    int4* pc = p.hl.piece + (int64_t)t * p.hl.piece_stride + pb;
-    for (int32_t q = 0; q < np; ++q) pc[q] = make_int4(k, q, np, pb);
+    for (int q = 0; q < ACF_HPLAN_EPT; ++q) {
+      const int e = tid * ACF_HPLAN_EPT + q;
+      const int32_t c = lkey[e] == 0xFFFFFFFFu ? 0 : lcnt[e];
+      if (c < 2) continue;
+      const bool item = (lkey[e] & 0x80000000u) != 0, hot = c > ACF_HOT_MIN;
+      v[0] += 1;
+      v[item ? 2 : 1] += c;
+      v[hot ? 4 : 3] += 1;
+      if (hot) v[5] += hot_pieces(c);
+    }
+    int32_t ex[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      int32_t tot = 0;
+      ex[c] = wave_excl_sum(v[c], tot);
+      if ((tid & 63) == 0) s_at[wave][c] = tot;
+    }
+    __syncthreads();
+    if (tid < 6) {
+      int32_t* ctr = tid == 0 ? p.scnt : tid == 1 ? p.ucsr : tid == 2 ? p.icsr : tid == 3 ? p.slot_cnt
+                   : tid == 4 ? p.hl.cnt : p.hl.pcnt;
+      int32_t run[4], sum = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        run[w] = sum;
+        sum += s_at[w][tid];
+      }
+      const int32_t base = sum > 0 ? atomicAdd(ctr + t, sum) : 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) s_at[w][tid] = base + run[w];
+    }
+    __syncthreads();
+    int32_t nx[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) nx[c] = s_at[wave][c] + ex[c];
+#pragma unroll
+    for (int q = 0; q < ACF_HPLAN_EPT; ++q) {
+      const int e = tid * ACF_HPLAN_EPT + q;
+      const uint32_t key = lkey[e];
+      const int32_t c = key == 0xFFFFFFFFu ? 0 : lcnt[e];
+      lk[e] = -1;
+      lcnt[e] = 0;  // the CSR cursor from here on
+      if (c < 2) continue;
+      const bool item = (key & 0x80000000u) != 0, hot = c > ACF_HOT_MIN;
+      const int32_t k = nx[0]++;
+      const int32_t base = item ? nx[2] : nx[1];
+      nx[item ? 2 : 1] += c;
+      lk[e] = k;
+      lb[e] = base;
+      OccRec rec = {};
+      rec.own_row = (int32_t)(key & 0x7FFFFFFFu);
+      rec.own_src = rec.own_row;
+      rec.meta = c | (item ? ACF_ITEM_BIT : 0);
+      rec.ovf = (item ? t * 2 * B : t * B) + base;
+      rec.e_role = -1;
+      rec.gen = p.gen;
+      p.inl[(int64_t)t * p.S + k] = rec;
+      const int32_t aux = base | (item ? (int32_t)0x80000000 : 0);
+      if (!hot) {
+        const int32_t ls = nx[3]++;
+        p.slot_list[(int64_t)t * p.S + ls] = k;
+        p.saux[(int64_t)t * p.S + ls] = aux | (c << 24);
+      } else {
+        const int32_t hx = nx[4]++, np = hot_pieces(c), pb0 = nx[5];
+        nx[5] += np;
+        p.hl.list[(int64_t)t * p.hl.hot_stride + hx] = make_int4(k, np, pb0, c);
+        p.haux[(int64_t)t * p.hl.hot_stride + hx] = aux;
+        int4* pc = p.hl.piece + (int64_t)t * p.hl.piece_stride + pb0;
+        for (int32_t w = 0; w < np; ++w) pc[w] = make_int4(k, w, np, pb0);
+      }
+    }
+    __syncthreads();
+    // every occurrence of the round: {slot, CSR position}, and its CSR entry
+    for (int32_t i = seg.x + tid; i < seg.y; i += 256) {
+      const unsigned long long pv = p.pval[i];
+      const uint32_t key = (uint32_t)(pv >> 32);
+      if (!in_round(key)) continue;
+      const int32_t o = (int32_t)(uint32_t)pv;
+      uint32_t lh = (hplan_hash(key) >> 7) & (ACF_HPLAN_TS - 1);
+      while (lkey[lh] != key) lh = (lh + 1u) & (ACF_HPLAN_TS - 1);
+      int2 out = make_int2(-1, 0);
+      if (lk[lh] >= 0) {
+        const int32_t pos = lb[lh] + atomicAdd(&lcnt[lh], 1);
+        out = make_int2(lk[lh], pos);
+        const bool item = o >= B;
+        p.csr[(int64_t)t * S3 + (item ? B : 0) + pos] = item ? o - B : o;
+      }
+      p.occ[(int64_t)t * S3 + o] = out;
+    }
+    __syncthreads();
+    ++r;
   }
 }
 
@@ -839,35 +922,17 @@ __global__ void __launch_bounds__(256) k_hplan_trip(HPlanArgs p) {
   if (e >= (int64_t)p.nb * B) return;
   const int32_t t = (int32_t)(e / B), b = (int32_t)(e - (int64_t)t * B);
   const int64_t ob = (int64_t)t * S3;
-  const int32_t oc[3] = {b, B + 2 * b, B + 2 * b + 1};
-  int32_t h[3], r[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    h[q] = p.hb[ob + oc[q]];
-    r[q] = p.rk[ob + oc[q]];
-  }
+  const int2 su_ = p.occ[ob + b], si_ = p.occ[ob + B + 2 * b], sj_ = p.occ[ob + B + 2 * b + 1];
   int err = 0;
-  const int32_t row[3] = {(int32_t)hplan_key(p, t, oc[0], err), (int32_t)(hplan_key(p, t, oc[1], err) & 0x7FFFFFFFu),
-                          (int32_t)(hplan_key(p, t, oc[2], err) & 0x7FFFFFFFu)};
-  const unsigned long long* H = p.H + ((int64_t)t << p.hs_log);
-  const int2* bi = p.binfo + ((int64_t)t << p.hs_log);
-  uint32_t cnt[3];
-  int2 sl[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    cnt[q] = (uint32_t)H[h[q]];
-    sl[q] = bi[h[q]];  // read whatever it holds; used only for shared keys
-  }
-  const bool su = cnt[0] == 1, si = cnt[1] == 1, sj = cnt[2] == 1;
-  if (!su) p.csr[ob + sl[0].y + r[0]] = b;
-  if (!si) p.csr[ob + B + sl[1].y + r[1]] = 2 * b;
-  if (!sj) p.csr[ob + B + sl[2].y + r[2]] = 2 * b + 1;
+  const int32_t u = (int32_t)hplan_key(p, t, b, err), i = (int32_t)(hplan_key(p, t, B + 2 * b, err) & 0x7FFFFFFFu),
+                j = (int32_t)(hplan_key(p, t, B + 2 * b + 1, err) & 0x7FFFFFFFu);
+  const bool su = su_.x < 0, si = si_.x < 0, sj = sj_.x < 0;
   // fused-triplet record layout (see records_one): a = {u, i, j, slot u}, b = {slot i,
   // slot j, src u, src i}, c = {src j, flags, e, gen}; in place: sources are the rows
   OccRec q;
-  q.own_row = row[0]; q.own_src = row[1]; q.meta = row[2]; q.ovf = su ? 0 : sl[0].x;
-  q.e_role = si ? 0 : sl[1].x; q.pa_row = sj ? 0 : sl[2].x; q.pb_row = row[0]; q.pa_src = row[1];
-  q.pb_src = row[2];
+  q.own_row = u; q.own_src = i; q.meta = j; q.ovf = su ? 0 : su_.x;
+  q.e_role = si ? 0 : si_.x; q.pa_row = sj ? 0 : sj_.x; q.pb_row = u; q.pa_src = i;
+  q.pb_src = j;
   q.pa_slot = ((su && si && sj) ? 1 : 0) | (su ? 2 + 16 : 0) | (si ? 4 + 32 : 0) | (sj ? 8 + 64 : 0);
   q.pb_slot = (int32_t)e;
   q.gen = p.gen;
@@ -4377,9 +4442,10 @@ struct acf_apr_ctx {
   int32_t hash_on = 1;
   int32_t plan_kind = -1;    // acf_apr_plan_kind
   int32_t hplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
-  int32_t hplan_log = 0;     // buckets per batch = 2^hplan_log >= 6 maxB
-  unsigned long long* hplan_tab = nullptr;
-  int2* hplan_binfo = nullptr;
+  int2* hplan_occ = nullptr;   // [3 maxE] occurrence -> {slot or -1, CSR position}
+  int2* hplan_seg = nullptr;   // [maxNB << pb] partition ranges
+  void* hplan_tmp = nullptr;   // rocPRIM temporary storage when c->tmp is too small
+  size_t hplan_tmp_bytes = 0;
   int32_t* hplan_cnt = nullptr;  // [3][maxNB] shared slots, user / item CSR positions
   int32_t* hplan_haux = nullptr;  // [maxNB][hot_stride] CSR base | item of each hot-list entry
   int32_t bplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
@@ -4736,29 +4802,44 @@ static bool bplan_ready(acf_apr_ctx* c) {
   return true;
 }
 
+// partition bits of a batch of B triplets: 2^pb partitions of <= ACF_HPLAN_PART occurrences on average
+static int32_t hplan_pbits(int32_t B) {
+  const uint64_t parts = ((uint64_t)3 * B + ACF_HPLAN_PART - 1) / ACF_HPLAN_PART;
+  return parts <= 1 ? 0 : (int32_t)bits_for(parts - 1);
+}
+
 static bool hplan_ready(acf_apr_ctx* c) {
   if (c->hplan_ok >= 0) return c->hplan_ok == 1;
   c->hplan_ok = 0;
   if (c->maxB > ACF_HPLAN_MAXB) return false;
-  c->hplan_log = (int32_t)bits_for((uint64_t)6 * c->maxB - 1);
-  const size_t n = (size_t)c->maxNB << c->hplan_log;
+  const int32_t pb = hplan_pbits(c->maxB);
+  if (pb + (int32_t)bits_for((uint64_t)c->maxNB) > 32) return false;
+  const size_t n3 = (size_t)3 * c->maxE;
+  size_t tb = 0;
+  if (rocprim::radix_sort_pairs(nullptr, tb, reinterpret_cast<uint32_t*>(c->flag), reinterpret_cast<uint32_t*>(c->inc),
+                                c->key_in, c->key_out, n3, 0, 32) != hipSuccess)
+    return false;
   std::vector<void*> got;
   auto A = [&](auto** p, size_t m) -> bool {
     if (dalloc(c, p, m) != ACF_OK) return false;
     got.push_back(*p);
     return true;
   };
-  if (!(A(&c->hplan_tab, n) && A(&c->hplan_binfo, n) && A(&c->hplan_cnt, (size_t)3 * c->maxNB) &&
-        A(&c->hplan_haux, (size_t)c->maxNB * c->hot.hot_stride))) {
+  bool ok = A(&c->hplan_occ, n3) && A(&c->hplan_seg, (size_t)c->maxNB << pb) &&
+            A(&c->hplan_cnt, (size_t)3 * c->maxNB) && A(&c->hplan_haux, (size_t)c->maxNB * c->hot.hot_stride);
+  c->hplan_tmp_bytes = tb;
+  if (ok && tb > c->tmp_bytes) ok = A(reinterpret_cast<char**>(&c->hplan_tmp), tb);
+  if (!ok) {
     (void)hipGetLastError();
     for (void* p : got) {
       (void)hipFree(p);
       c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), p));
     }
-    c->hplan_tab = nullptr;
-    c->hplan_binfo = nullptr;
+    c->hplan_occ = nullptr;
+    c->hplan_seg = nullptr;
     c->hplan_cnt = nullptr;
     c->hplan_haux = nullptr;
+    c->hplan_tmp = nullptr;
     return false;
   }
   c->hplan_ok = 1;
@@ -4769,31 +4850,37 @@ static bool hplan_ready(acf_apr_ctx* c) {
 // tri branch, slot ids and CSR ranges numbered in allocation order
 static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg, int32_t B,
                      int32_t nb, int32_t gen, int32_t kb, int32_t check, hipStream_t s) {
-  const int64_t E = (int64_t)B * nb;
-  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
-  HIP_TRY(hipMemsetAsync(c->hplan_tab, 0xFF, ((size_t)nb << c->hplan_log) * 8, s));
-  HIP_TRY(hipMemsetAsync(c->hplan_cnt, 0, (size_t)3 * c->maxNB * sizeof(int32_t), s));
-  HIP_TRY(hipMemsetAsync(c->slot_cnt, 0, (size_t)c->maxNB * sizeof(int32_t), s));
-  HIP_TRY(hipMemsetAsync(c->flush_cnt, 0, (size_t)c->maxNB * sizeof(int32_t), s));
-  HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
-  HIP_TRY(hipMemsetAsync(c->hot.arrive, 0, (size_t)nb * c->hot.piece_stride * sizeof(int32_t), s));
+  const int64_t E = (int64_t)B * nb, n3 = 3 * E;
+  const int32_t pb = hplan_pbits(B);
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));  // the other counters: k_hplan_keys
   HPlanArgs p;
   p.user = user; p.ipos = ipos; p.ineg = ineg;
   p.U1 = c->U1; p.I1 = c->I1;
-  p.B = B; p.S = 3 * B; p.nb = nb; p.gen = gen; p.hs_log = c->hplan_log;
-  p.opad = (3 * B + 255) & ~255;
-  p.H = c->hplan_tab; p.binfo = c->hplan_binfo;
-  p.hb = c->flag; p.rk = c->inc; p.csr = c->tsl;
+  p.B = B; p.S = 3 * B; p.nb = nb; p.gen = gen; p.pb = pb;
+  p.pkey = reinterpret_cast<uint32_t*>(c->flag);
+  p.pval = reinterpret_cast<unsigned long long*>(c->key_in);
+  p.pseg = c->hplan_seg; p.occ = c->hplan_occ; p.csr = c->tsl;
   p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
   p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
-  p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt;
+  p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt; p.flush_cnt = c->flush_cnt;
   p.saux = c->flush_list;  // unused by in-place plans
   p.haux = c->hplan_haux;
   p.hl = c->hot;
   p.err = c->err; p.gen_ptr = c->gen_dev;
-  const int64_t nocc = (int64_t)nb * p.opad;
-  k_hplan_insert<<<(unsigned)((nocc + 255) / 256), 256, 0, s>>>(p);
-  k_hplan_claim<<<(unsigned)((nocc + 255) / 256), 256, 0, s>>>(p);
+  const int64_t nclear = std::max<int64_t>({n3, (int64_t)nb << pb, (int64_t)nb * c->hot.piece_stride});
+  k_hplan_keys<<<(unsigned)((nclear + 255) / 256), 256, 0, s>>>(p);
+  HIP_TRY(hipGetLastError());
+  uint32_t* sk = reinterpret_cast<uint32_t*>(c->inc);
+  {
+    void* tmp = c->hplan_tmp ? c->hplan_tmp : c->tmp;
+    size_t tb = c->hplan_tmp ? c->hplan_tmp_bytes : c->tmp_bytes;
+    HIP_TRY(rocprim::radix_sort_pairs(tmp, tb, p.pkey, sk, c->key_in, c->key_out, (size_t)n3, 0,
+                                      pb + (int32_t)bits_for((uint64_t)nb), s));
+  }
+  p.pkey = sk;
+  p.pval = reinterpret_cast<unsigned long long*>(c->key_out);
+  k_hplan_bounds<<<(unsigned)((n3 + 255) / 256), 256, 0, s>>>(p, sk, n3);
+  k_hplan_dedup<<<(unsigned)(nb << pb), 256, 0, s>>>(p);
   k_hplan_trip<<<(unsigned)((E + 255) / 256), 256, 0, s>>>(p);
   k_hplan_rank_small<<<dim3(64, nb), 256, 0, s>>>(p);
   k_hplan_rank_hot<<<dim3(64, nb), 256, (size_t)2 * ((2 * B + 31) / 32) * sizeof(uint32_t), s>>>(p);

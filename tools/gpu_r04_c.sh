@@ -26,7 +26,7 @@ import json; d=json.load(open('$OUT/eval.json'))
 for k,v in d.items(): print(k, v['ms_per_eval'], v['mfma_ms_per_eval'], v['valu_ms_per_eval'], v['positions_equal_valu'], v['roofline']['frac'])"
 timeout -k 10 200 python3 tools/neumf_rate.py > $OUT/nmf.log 2>&1
 echo "nmf default: $(tail -1 $OUT/nmf.log)"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/large_prof -o lg -- python3 -c "
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/large_prof -o lg -- python3 -c "
 import sys, json, importlib, torch
 sys.path.insert(0, '.')
 import bench
