@@ -1224,137 +1224,6 @@ __global__ void __launch_bounds__(BS) k_bplan_sort(BPlanArgs p) {
   STAMP(t, tid >> 6, 4);
 }
 
-// k_bplan_sort for small key spaces (2^(rb+1) <= ACF_BPLAN_COUNT_KEYS keys:
-// ml-1m's 6,041 users and 3,707 items): a counting sort in LDS instead of the
-// block radix sort's 2 x (rb + 1) / 4 passes.  One 16-bit counter per key (two
-// per LDS word), one LDS atomic per occurrence, ONE block scan over the
-// counters (each thread owns KPT consecutive keys: slots and CSR starts in key
-// order), then each occurrence's rank among equal keys in occurrence order
-// (the atomics' order is arbitrary: an occurrence counts the smaller
-// occurrence indices in its key's segment).  Same outputs bit for bit as
-// k_bplan_sort (test_batch_plan_counting_sort_matches_radix).
-#define ACF_BPLAN_COUNT_KEYS 16384
-
-template <int BS, int IPT>
-__global__ void __launch_bounds__(BS) k_bplan_count(BPlanArgs p, int32_t keys_n) {
-  constexpr int N = BS * IPT;
-  using Scan = rocprim::block_scan<int32_t, BS>;
-  extern __shared__ uint32_t dyn[];
-  uint32_t* cw = dyn;                                        // [keys_n / 2] counts, then slots
-  int32_t* sst = reinterpret_cast<int32_t*>(dyn + keys_n / 2);  // [N + 1] slot -> CSR start
-  int32_t* seg = sst + N + 1;                                // [N] occurrences by slot
-  __shared__ typename Scan::storage_type scan_st;
-  __shared__ int32_t s_err, s_nu;
-  const int t = blockIdx.x, tid = threadIdx.x, B = p.B, S3 = 3 * B;
-  const int KPT = keys_n / BS;  // even: keys_n >= 2 BS
-  if (tid == 0) { s_err = 0; s_nu = 0; }
-  if (t == 0 && tid == 0) *p.final_cnt = 0;  // k_bplan_build appends to it
-  for (int w = tid; w < keys_n / 2; w += BS) cw[w] = 0u;
-  const uint32_t side_bit = 1u << p.rb;
-  int32_t raw[IPT];
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int o = tid * IPT + k;  // occurrence: users [0, B), items B + 2e + role
-    raw[k] = 0;
-    if (o < B) {
-      raw[k] = p.user[(int64_t)t * B + o];
-    } else if (o < S3) {
-      const int v = o - B;
-      raw[k] = ((v & 1) ? p.ineg : p.ipos)[(int64_t)t * B + (v >> 1)];
-    }
-  }
-  uint32_t keys[IPT];
-  int err = 0;
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int o = tid * IPT + k;
-    int32_t x = raw[k];
-    keys[k] = 0u;
-    if (o < B) {
-      if (x < 0 || x >= p.U1) { err |= 1; x = 0; }
-      keys[k] = (uint32_t)x;
-    } else if (o < S3) {
-      if (x < 0 || x >= p.I1) { err |= 2; x = 0; }
-      keys[k] = side_bit | (uint32_t)x;
-    }
-  }
-  __syncthreads();  // counters zeroed
-  if (err) atomicOr(&s_err, err);
-  uint32_t rk[IPT];  // place among the key's occurrences in atomic order
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    rk[k] = 0u;
-    if (tid * IPT + k < S3) {
-      const uint32_t sh = (keys[k] & 1u) * 16u;
-      rk[k] = (atomicAdd(&cw[keys[k] >> 1], 1u << sh) >> sh) & 0xFFFFu;
-    }
-  }
-  __syncthreads();
-  // this thread's keys [k0, k0 + KPT): unique rows and occurrences (both < 2^16)
-  const int k0 = tid * KPT;
-  int32_t np = 0, no = 0;
-  for (int x = 0; x < KPT / 2; ++x) {
-    const uint32_t w = cw[k0 / 2 + x];
-    const int32_t c0 = (int32_t)(w & 0xFFFFu), c1 = (int32_t)(w >> 16);
-    np += (c0 > 0) + (c1 > 0);
-    no += c0 + c1;
-  }
-  int32_t excl = 0, total = 0;
-  Scan().exclusive_scan(np | (no << 16), excl, 0, total, scan_st);
-  const int32_t nuniq = total & 0xFFFF;
-  int32_t s = excl & 0xFFFF, q = excl >> 16;
-  if (k0 == (int)side_bit) s_nu = s;  // slots before the first item key: the user rows
-  const int64_t rbase = (int64_t)t * p.S;
-  for (int x = 0; x < KPT / 2; ++x) {
-    const uint32_t w = cw[k0 / 2 + x];
-    uint32_t slots = 0u;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int32_t c = (int32_t)((w >> (16 * h)) & 0xFFFFu);
-      if (!c) continue;
-      const uint32_t key = (uint32_t)(k0 + 2 * x + h);
-      const int64_t row = (int64_t)(key & (side_bit - 1));
-      const int64_t rid = (key & side_bit) ? p.U1 + row : row;
-      sst[s] = q;
-      p.bkey[rbase + s] = key;
-      p.bstart[(int64_t)t * (p.S + 1) + s] = q;
-      p.slot_of[rid * p.nbs + t] = (uint16_t)s;
-      atomicOr(p.mask + rid * p.W + (t >> 6), 1ull << (t & 63));
-      slots |= (uint32_t)s << (16 * h);
-      ++s;
-      q += c;
-    }
-    cw[k0 / 2 + x] = slots;  // this thread's own words: no other thread reads them yet
-  }
-  if (tid == 0) sst[nuniq] = S3;
-  lds_barrier();  // slots and starts (LDS); the row writes above stay in flight
-  int32_t sl[IPT];
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    sl[k] = -1;
-    const int o = tid * IPT + k;
-    if (o >= S3) continue;
-    const uint32_t sh = (keys[k] & 1u) * 16u;
-    sl[k] = (int32_t)((cw[keys[k] >> 1] >> sh) & 0xFFFFu);
-    seg[sst[sl[k]] + (int32_t)rk[k]] = o;
-  }
-  lds_barrier();
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int o = tid * IPT + k;
-    if (o >= S3) continue;
-    const int32_t a0 = sst[sl[k]], a1 = sst[sl[k] + 1];
-    int32_t r = 0;
-    for (int32_t x = a0; x < a1; ++x) r += seg[x] < o ? 1 : 0;
-    p.bocc[rbase + o] = sl[k] | (r << 16);
-  }
-  if (tid == 0) {
-    p.bstart[(int64_t)t * (p.S + 1) + nuniq] = S3;
-    p.bn[t] = make_int2(nuniq, s_nu);
-    p.berr[t] = s_err;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // One-workgroup shard plan (shard mode, one batch of B <= 1,024 triplets:
 // distributed.ShardedAPR's per-step plan).  It writes what the device-wide sort
@@ -4422,7 +4291,7 @@ struct acf_apr_ctx {
   uint32_t last_tail_seq = 0;  // seq of the last launch with a tail (StepArgs.decide_prev)
   int32_t tail_on = 1;         // ACF_TAIL=0: write-back by k_stream_flush always (A/B)
   int32_t tail_flushers = 128; // ACF_TAIL_FLUSHERS: workgroups of the tail write-back
-  int32_t bplan_sort = 0;  // batch plan's sort: 0 auto, 1 radix, 2 radix 1,024 x 2, 3 counting (ACF_BPLAN_SORT)
+  int32_t bplan_sort = 0;  // batch plan's sort: 0 default (512 x 3), 2 1,024 x 2 (ACF_BPLAN_SORT=1024, A/B)
   unsigned long long* tail_diag = nullptr;  // ACF_TAIL_DIAG=1: tail stamps (acf_apr_diag_tail)
   unsigned long long* decide = nullptr;  // [0] decide word, [16, 16 + 288) the tail's arrival counters
   uint32_t tail_launches = 0;            // launches with a tail so far (StepArgs.tail_par)
@@ -4641,10 +4510,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (const char* e = getenv("ACF_TAIL")) c->tail_on = atoi(e) != 0;
   if (const char* e = getenv("ACF_TAIL_FLUSHERS")) c->tail_flushers = std::max(1, atoi(e));
   if (const char* e = getenv("ACF_HASH_PLAN")) c->hash_on = atoi(e) != 0;
-  if (const char* e = getenv("ACF_BPLAN_SORT")) {  // radix | 1024 | count (A/B); unset: auto
-    const std::string v(e);
-    c->bplan_sort = v == "radix" ? 1 : v == "1024" ? 2 : v == "count" ? 3 : 0;
-  }
+  if (const char* e = getenv("ACF_BPLAN_SORT")) c->bplan_sort = atoi(e) == 1024 ? 2 : 0;
   if (const char* e = getenv("ACF_TAIL_DIAG"))
     if (atoi(e) && dalloc(c, &c->tail_diag, 8) == ACF_OK) (void)hipMemset(c->tail_diag, 0, 64);
   c->grp = new FailGroup();
@@ -4934,27 +4800,14 @@ static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, 
   // 3 occurrences per thread in the sort, one thread per slot / triplet in the
   // build: ~24 us for a 20-batch plan against ~32 us for 6 per thread / 256-thread
   // builds (per-thread loops serialise the build's dependent loads)
-  // the counting sort when the key space is small (c->bplan_sort 0 auto / 3),
-  // else the block radix sort (1; 2: 1,024 threads x 2 occurrences, A/B)
-  const int32_t key_bits = p.rb + 1;
-  const bool count = (c->bplan_sort == 0 || c->bplan_sort == 3) && (1 << key_bits) <= ACF_BPLAN_COUNT_KEYS;
   if (B <= 512) {
-    if (count) {
-      const int32_t keys_n = std::max(1 << key_bits, 2 * 512);
-      k_bplan_count<512, 3><<<nb, 512, (size_t)(keys_n / 2 + 2 * 1536 + 1) * 4, s>>>(p, keys_n);
-    } else if (c->bplan_sort == 2) {
+    if (c->bplan_sort == 2)  // ACF_BPLAN_SORT=1024 (A/B): 1,024 threads x 2 occurrences
       k_bplan_sort<1024, 2><<<nb, 1024, 0, s>>>(p);
-    } else {
+    else
       k_bplan_sort<512, 3><<<nb, 512, 0, s>>>(p);
-    }
     k_bplan_build<1024, 512><<<nb, 1024, 0, s>>>(p);
   } else {
-    if (count) {
-      const int32_t keys_n = std::max(1 << key_bits, 2 * 1024);
-      k_bplan_count<1024, 3><<<nb, 1024, (size_t)(keys_n / 2 + 2 * 3072 + 1) * 4, s>>>(p, keys_n);
-    } else {
-      k_bplan_sort<1024, 3><<<nb, 1024, 0, s>>>(p);
-    }
+    k_bplan_sort<1024, 3><<<nb, 1024, 0, s>>>(p);
     k_bplan_build<1024, 1024><<<nb, 1024, 0, s>>>(p);
   }
   HIP_TRY(hipGetLastError());

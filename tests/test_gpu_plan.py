@@ -87,29 +87,6 @@ def test_batch_plan_matches_sort_plan(ops, acf, dev, shape, B, nb, d, adver):
                 assert torch.equal(x, y), (ovl, stream, pieces, n)
 
 
-@pytest.mark.parametrize("shape,B,nb", [("hot", 1024, 3), ("sparse", 64, 150), ("ml1m", 512, 24)])
-def test_batch_plan_counting_sort_matches_radix(ops, acf, dev, monkeypatch, shape, B, nb):
-    """The batch plan's two sorts (ACF_BPLAN_SORT, read when a context is made):
-    the LDS counting sort that small key spaces take by default and the block
-    radix sort give the same records, hence the same bits through the streamed
-    step, whole-range and piecewise."""
-    d = 64
-    U1, I1, u, i, j = _stream(shape, acf, dev, B, nb, seed=5 + B)
-    rng = np.random.default_rng(5)
-    P = (rng.standard_normal((U1, d)) * 0.2).astype(np.float32)
-    Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
-    hp = ops.StepHParams(adver=1, reg=0.01)
-    split = [(0, 1), (1, 2), (3, nb - 3)] if nb > 3 else [(0, 1), (1, nb - 1)]
-    for pieces in ([(0, nb)], split):
-        outs = []
-        for mode in ("radix", "count"):
-            monkeypatch.setenv("ACF_BPLAN_SORT", mode)
-            outs.append(_train(ops, dev, U1, I1, d, B, nb, u, i, j, P, Q, hp, "auto", False, True, pieces))
-        torch.cuda.synchronize()
-        for x, y, n in zip(*outs, ("P", "Q", "accP", "accQ", "loss_clean", "loss_adv")):
-            assert torch.equal(x, y), (pieces, n)
-
-
 def test_batch_plan_replans_and_bitmap_reuse(ops, oracle, dev):
     """Consecutive plans on one context alternate the two row bitmaps (each plan
     clears the one the previous plan set); a sort plan in between leaves the
