@@ -3674,36 +3674,25 @@ __global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
   for (int x = gid; x < n; x += ngroups) flush_slot(a, a.t - 1, a.wnew_prev, lst[x], l, LPR);
 }
 
-// shared slots with <= ACF_HOT_MIN occurrences: one lane-group each, in order;
-// hot slots: piece waves [slot_waves, slot_waves + hot_waves) into hot_part, then
-// hot_blocks workgroups (waves from slot_waves + hot_waves on) that each combine
-// hot slots as k_hot_combine does once all their pieces are stored.  A piece is
-// stored write-through, the wave drains its stores, and one lane adds 1 to the
-// slot's arrival count; a combining workgroup polls that count (device scope),
-// and every load of the pieces is a device-scope load (Guideline 16, row 1).
-// The combining workgroups come after every piece wave in dispatch order, so
-// the pieces they wait for are already running: the launch always drains.
+// Hot slots first in dispatch order, so their chain (pieces -> arrival count ->
+// combining workgroup) starts at once: piece waves [0, hot_waves) into hot_part,
+// then hot_blocks workgroups that each combine hot slots as k_hot_combine does
+// once all their pieces are stored, then slot waves [.., + slot_waves): shared
+// slots with <= ACF_HOT_MIN occurrences, one lane-group each, in order.  A piece
+// is stored write-through, the wave drains its stores, and one lane adds 1 to
+// the slot's arrival count; a combining workgroup polls that count (device
+// scope), and every load of the pieces is a device-scope load (Guideline 16,
+// row 1).  The combining workgroups come after every piece wave in dispatch
+// order, so the pieces they wait for are already running: the launch always
+// drains.  (hot_waves is a multiple of 4: whole workgroups.)
 template <int LPR, int NV, int MODE>
 __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
   __shared__ float4 red[NV * 256];
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
-  if (wave < a.slot_waves) {
-    const int ngroups = a.slot_waves * (64 / LPR), gid = wave * (64 / LPR) + g;
-    const int n = a.slot_cnt[a.t];
-    const int32_t* lst = a.slot_list + (int64_t)a.t * a.S;
-    for (int x = gid; x < n; x += ngroups) {
-      const int k = lst[x];
-      const TriSlot h = tri_slot(a, k);
-      RowV<NV> G = zero_row<NV>();
-      tri_add<LPR, NV>(a, h, 0, h.count, 1, l, G);
-      tri_finish<LPR, NV, MODE>(a, k, h, G, l);
-    }
-    return;
-  }
   int32_t* arrive = a.hot.arrive + (int64_t)a.t * a.hot.piece_stride;
-  const int hw = wave - a.slot_waves;
-  if (hw < a.hot_waves) {
+  if (wave < a.hot_waves) {
+    const int hw = wave;
     constexpr int TEAM = 64 / LPR;
     const int n = a.hot.pcnt[a.t];
     const int4* pl = a.hot.piece + (int64_t)a.t * a.hot.piece_stride;
@@ -3724,27 +3713,40 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
     }
     return;
   }
-  // hot-slot combining workgroups (whole workgroups: slot_waves + hot_waves is a multiple of 4)
-  const int hb = (wave - a.slot_waves - a.hot_waves) >> 2;
-  if (hb >= a.hot_blocks) return;
-  const int n = a.hot.cnt[a.t];
-  const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
-  for (int hx = hb; hx < n; hx += a.hot_blocks) {
-    const int4 e = hl[hx];  // {slot, pieces, piece base, count}
-    if (threadIdx.x == 0) {
-      int it = 0;
-      while (__hip_atomic_load(arrive + e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.y) {
-        if (++it > ACF_SPIN_LIMIT) {
-          atomicOr(a.step_err, 1);
-          break;
+  const int hb = (wave - a.hot_waves) >> 2;
+  if (hb < a.hot_blocks) {  // hot-slot combining workgroups (whole workgroups)
+    const int n = a.hot.cnt[a.t];
+    const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
+    for (int hx = hb; hx < n; hx += a.hot_blocks) {
+      const int4 e = hl[hx];  // {slot, pieces, piece base, count}
+      if (threadIdx.x == 0) {
+        int it = 0;
+        while (__hip_atomic_load(arrive + e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.y) {
+          if (++it > ACF_SPIN_LIMIT) {
+            atomicOr(a.step_err, 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_s_sleep(2);
+        // every piece of this pass is in: ready for the next pass over the batch
+        __hip_atomic_store(arrive + e.z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      // every piece of this pass is in: ready for the next pass over the batch
-      __hip_atomic_store(arrive + e.z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      hot_combine_slot<LPR, NV, MODE, true>(a, e, red);
     }
-    __syncthreads();
-    hot_combine_slot<LPR, NV, MODE, true>(a, e, red);
+    return;
+  }
+  const int sw = wave - a.hot_waves - 4 * a.hot_blocks;
+  if (sw >= a.slot_waves) return;
+  const int ngroups = a.slot_waves * (64 / LPR), gid = sw * (64 / LPR) + g;
+  const int n = a.slot_cnt[a.t];
+  const int32_t* lst = a.slot_list + (int64_t)a.t * a.S;
+  for (int x = gid; x < n; x += ngroups) {
+    const int k = lst[x];
+    const TriSlot h = tri_slot(a, k);
+    RowV<NV> G = zero_row<NV>();
+    tri_add<LPR, NV>(a, h, 0, h.count, 1, l, G);
+    tri_finish<LPR, NV, MODE>(a, k, h, G, l);
   }
 }
 
@@ -4309,6 +4311,7 @@ struct acf_apr_ctx {
   int32_t plan_mode = 0;     // 0 auto (batch-local plan where it applies), 1 always the sort plan
   // hash plan of triplet-centric steps (k_hplan_*); ACF_HASH_PLAN=0 keeps the sort plan (A/B)
   int32_t hash_on = 1;
+  int32_t tri_comb_waves = 4096;  // slot waves of k_tri_combine (ACF_TRI_COMB_WAVES)
   int32_t plan_kind = -1;    // acf_apr_plan_kind
   int32_t hplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   int2* hplan_occ = nullptr;   // [3 maxE] occurrence -> {slot or -1, CSR position}
@@ -4510,6 +4513,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (const char* e = getenv("ACF_TAIL")) c->tail_on = atoi(e) != 0;
   if (const char* e = getenv("ACF_TAIL_FLUSHERS")) c->tail_flushers = std::max(1, atoi(e));
   if (const char* e = getenv("ACF_HASH_PLAN")) c->hash_on = atoi(e) != 0;
+  if (const char* e = getenv("ACF_TRI_COMB_WAVES")) c->tri_comb_waves = std::max(4, atoi(e));
   if (const char* e = getenv("ACF_BPLAN_SORT")) c->bplan_sort = atoi(e) == 1024 ? 2 : 0;
   if (const char* e = getenv("ACF_TAIL_DIAG"))
     if (atoi(e) && dalloc(c, &c->tail_diag, 8) == ACF_OK) (void)hipMemset(c->tail_diag, 0, 64);
@@ -5465,7 +5469,8 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   if (K.tri) {  // triplet-centric list step (see k_tri_*)
     // k_tri_combine with its hot-slot combining workgroups after the piece waves
     // (whole workgroups: the two wave ranges rounded up to multiples of 4)
-    const int SW4 = (SW + 3) & ~3, HW4 = (HW + 3) & ~3, HBT = std::min(HB, ACF_TRI_HOT_BLOCKS);
+    const int SWT = std::min(SW, c->tri_comb_waves);  // ACF_TRI_COMB_WAVES
+    const int SW4 = (SWT + 3) & ~3, HW4 = (HW + 3) & ~3, HBT = std::min(HB, ACF_TRI_HOT_BLOCKS);
     const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);  // one lane-group per triplet
     for (int32_t t = first; t < first + n; ++t) {
       // every row is updated in its table (StepArgs.inplace): nothing pending from t-1
