@@ -649,11 +649,10 @@ __global__ void k_task_list(const int32_t* __restrict__ flags, const int32_t* __
 // the per-batch lists of shared slots and of hot slots with their pieces.  Slot
 // ids and CSR ranges may be numbered in any order; only the order inside a range
 // is fixed.  So (APR.py:183-195's Unique + UnsortedSegmentSum, restated):
-//  1. k_hplan_keys + one rocPRIM radix sort of (batch, partition) -- the top PB
-//     bits of a Fibonacci hash of the (side, row) key, PB + log2(batches) bits
-//     (2 passes at configs[4] instead of the sort plan's 4 over 30-bit keys) --
-//     groups each batch's occurrences into 2^PB partitions of ~768, disjoint in
-//     keys; k_hplan_bounds finds each partition's range;
+//  1. k_hplan_keys / k_hplan_scatter: a one-pass partition of each batch's
+//     occurrences by the top pb bits of a Fibonacci hash of the (side, row) key
+//     (2^pb partitions of ~768 occurrences, disjoint in keys): per-tile counts,
+//     their exclusive scan, a scatter -- in place of the sort plan's radix sort;
 //  2. k_hplan_dedup, one workgroup per partition: its keys counted in an LDS hash
 //     table (LDS atomics only); the shared keys claim slot ids, CSR ranges and
 //     list places (one global atomic per counter and workgroup) and write their
@@ -682,10 +681,16 @@ struct HPlanArgs {
   const int32_t* ineg;
   int64_t U1, I1;
   int32_t B, S, nb, gen, pb;  // pb: partition bits (2^pb partitions per batch)
-  uint32_t* pkey;             // [nb][3B] (batch << pb | partition), then sorted
-  unsigned long long* pval;   // [nb][3B] key << 32 | occurrence, sorted with pkey
-  int2* pseg;                 // [nb << pb] partition ranges in the sorted arrays
+  int32_t tpb;                // tiles of ACF_HPLAN_PTILE occurrences per batch
+  uint32_t* ppr;              // [nb][3B] partition << 16 | place in the tile's share of it
+  unsigned long long* pstage; // [nb][3B] key << 32 | occurrence, occurrence order
+  unsigned long long* pval;   // [nb][3B] the same, partition order
+  int32_t* pcnt;              // [nb][2^pb][tpb] occurrences per (partition, tile)
+  int32_t* poff;              // its exclusive scan: where each (partition, tile) share starts
   int2* occ;                  // [nb][3B] occurrence -> {slot or -1 (single), CSR position}
+  int4* claims;               // [nb][3B / 2] HClaim: a partition's shared keys from x0 / 2
+  int32_t* ptot;              // [nb << pb][6] partition totals
+  int32_t* pbase;             // [nb << pb][6] their exclusive scans over the batch
   int32_t* csr;               // [nb][3B] occurrence ids by CSR position: users [0, B), items B + [0, 2B)
   int32_t* scnt;              // [nb] shared slots
   int32_t* ucsr;              // [nb] user CSR positions taken
@@ -719,35 +724,78 @@ __device__ __forceinline__ uint32_t hplan_key(const HPlanArgs& p, int32_t t, int
   return 0x80000000u | (uint32_t)row;
 }
 
+// One workgroup per tile of ACF_HPLAN_PTILE occurrences of a batch: keys,
+// partitions, each occurrence's place among the tile's occurrences of its
+// partition (LDS atomics) and the tile's per-partition counts; after their
+// exclusive scan (partition-major inside each batch) k_hplan_scatter moves
+// every occurrence to its partition's range -- a one-pass partition, instead of
+// a radix sort.  The plan's counters start at zero here too (instead of six
+// fills: a fill launch costs ~9 us).
+#define ACF_HPLAN_PIPT 8
+#define ACF_HPLAN_PTILE (256 * ACF_HPLAN_PIPT)
+
 __global__ void __launch_bounds__(256) k_hplan_keys(HPlanArgs p) {
-  const int64_t x = blockIdx.x * 256ll + threadIdx.x;
-  const int S3 = 3 * p.B;
-  // the plan's counters and partition ranges start at zero (instead of six fills:
-  // a fill launch costs ~9 us)
-  if (x < ((int64_t)p.nb << p.pb)) p.pseg[x] = make_int2(0, 0);
-  if (x < p.nb) {
-    p.scnt[x] = p.ucsr[x] = p.icsr[x] = 0;
-    p.slot_cnt[x] = p.flush_cnt[x] = 0;
-    p.hl.cnt[x] = p.hl.pcnt[x] = 0;
+  __shared__ int32_t hist[256];
+  const int S3 = 3 * p.B, P = 1 << p.pb, tid = threadIdx.x;
+  const int32_t t = blockIdx.x / p.tpb, tile = blockIdx.x - t * p.tpb;
+  const int64_t gx = blockIdx.x * 256ll + tid, G = (int64_t)gridDim.x * 256;
+  for (int64_t x = gx; x < (int64_t)p.nb * p.hl.piece_stride; x += G) p.hl.arrive[x] = 0;
+  if (gx < p.nb) {
+    p.scnt[gx] = p.ucsr[gx] = p.icsr[gx] = 0;
+    p.slot_cnt[gx] = p.flush_cnt[gx] = 0;
+    p.hl.cnt[gx] = p.hl.pcnt[gx] = 0;
   }
-  if (x < (int64_t)p.nb * p.hl.piece_stride) p.hl.arrive[x] = 0;
-  if (x >= (int64_t)p.nb * S3) return;
-  const int32_t t = (int32_t)(x / S3), o = (int32_t)(x - (int64_t)t * S3);
+  for (int q = tid; q < P; q += 256) hist[q] = 0;
+  __syncthreads();
+  // every key's loads first, then the LDS counts, then the stores
   int err = 0;
-  const uint32_t key = hplan_key(p, t, o, err);
+  uint32_t key[ACF_HPLAN_PIPT];
+#pragma unroll
+  for (int q = 0; q < ACF_HPLAN_PIPT; ++q) {
+    const int32_t o = tile * ACF_HPLAN_PTILE + q * 256 + tid;
+    key[q] = o < S3 ? hplan_key(p, t, o, err) : 0u;
+  }
   if (err) atomicOr(p.err, err);
-  const uint32_t part = p.pb ? hplan_hash(key) >> (32 - p.pb) : 0u;
-  p.pkey[x] = ((uint32_t)t << p.pb) | part;
-  p.pval[x] = ((unsigned long long)key << 32) | (uint32_t)o;
+  uint32_t pr[ACF_HPLAN_PIPT];
+#pragma unroll
+  for (int q = 0; q < ACF_HPLAN_PIPT; ++q) {
+    const int32_t o = tile * ACF_HPLAN_PTILE + q * 256 + tid;
+    const uint32_t part = p.pb ? hplan_hash(key[q]) >> (32 - p.pb) : 0u;
+    pr[q] = o < S3 ? (part << 16) | (uint32_t)atomicAdd(&hist[part], 1) : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < ACF_HPLAN_PIPT; ++q) {
+    const int32_t o = tile * ACF_HPLAN_PTILE + q * 256 + tid;
+    if (o >= S3) continue;
+    p.ppr[(int64_t)t * S3 + o] = pr[q];
+    p.pstage[(int64_t)t * S3 + o] = ((unsigned long long)key[q] << 32) | (uint32_t)o;
+    p.occ[(int64_t)t * S3 + o] = make_int2(-1, 0);  // single until k_hplan_emit says otherwise
+  }
+  __syncthreads();
+  for (int q = tid; q < P; q += 256) p.pcnt[((int64_t)t * P + q) * p.tpb + tile] = hist[q];
 }
 
-// partition ranges over the sorted (batch, partition) keys; absent partitions keep {0, 0}
-__global__ void __launch_bounds__(256) k_hplan_bounds(HPlanArgs p, const uint32_t* __restrict__ sk, int64_t n) {
-  const int64_t x = blockIdx.x * 256ll + threadIdx.x;
-  if (x >= n) return;
-  const uint32_t k = sk[x];
-  if (x == 0 || sk[x - 1] != k) p.pseg[k].x = (int32_t)x;
-  if (x == n - 1 || sk[x + 1] != k) p.pseg[k].y = (int32_t)(x + 1);
+__global__ void __launch_bounds__(256) k_hplan_scatter(HPlanArgs p) {
+  const int S3 = 3 * p.B, P = 1 << p.pb, tid = threadIdx.x;
+  const int32_t t = blockIdx.x / p.tpb, tile = blockIdx.x - t * p.tpb;
+  // loads in three rounds, each with all of the thread's occurrences in flight
+  uint32_t pr[ACF_HPLAN_PIPT];
+  unsigned long long pv[ACF_HPLAN_PIPT];
+  int32_t pos[ACF_HPLAN_PIPT];
+#pragma unroll
+  for (int q = 0; q < ACF_HPLAN_PIPT; ++q) {
+    const int32_t o = tile * ACF_HPLAN_PTILE + q * 256 + tid;
+    pr[q] = o < S3 ? p.ppr[(int64_t)t * S3 + o] : 0u;
+    pv[q] = o < S3 ? p.pstage[(int64_t)t * S3 + o] : 0ull;
+  }
+#pragma unroll
+  for (int q = 0; q < ACF_HPLAN_PIPT; ++q)
+    pos[q] = p.poff[((int64_t)t * P + (pr[q] >> 16)) * p.tpb + tile] + (int32_t)(pr[q] & 0xFFFFu);
+#pragma unroll
+  for (int q = 0; q < ACF_HPLAN_PIPT; ++q) {
+    const int32_t o = tile * ACF_HPLAN_PTILE + q * 256 + tid;
+    if (o < S3) p.pval[pos[q]] = pv[q];
+  }
 }
 
 // exclusive prefix sum over the wave; total = the wave's sum
@@ -765,20 +813,65 @@ __device__ __forceinline__ int32_t wave_excl_sum(int32_t v, int32_t& total) {
 
 #define ACF_HPLAN_EPT (ACF_HPLAN_TS / 256)  // LDS buckets per thread in the claims
 
+// Partition dedup, in three launches so that no global counter is contended
+// (one workgroup per partition claiming from per-batch counters queued ~256
+// same-address atomics per counter):
+//  k_hplan_dedup (one workgroup per partition): the keys counted in an LDS hash
+//    table, the shared ones numbered partition-locally (slot j, user / item CSR
+//    offset, list / hot-list / piece places) into claims[x0 / 2 + j] (a
+//    partition of n occurrences has <= n / 2 shared keys), the shared
+//    occurrences as {occurrence, local CSR position, j} from x0, seven totals;
+//  k_hplan_bases (one workgroup per batch): exclusive scans of the totals over
+//    the batch's partitions, and the batch's list lengths;
+//  k_hplan_emit (one workgroup per partition): local -> batch numbering, the
+//    inline records, lists and pieces, the shared occurrences' {slot, CSR
+//    position} and CSR entries (k_hplan_keys preset every occurrence to single).
+// Equal LDS buckets inside a wave are counted with one atomic (the wave's first
+// active lane's bucket: a Zipf-popular item fills most of its partition).
+struct HClaim {
+  uint32_t key;
+  int32_t count;
+  int32_t csr;    // CSR offset inside the partition's user or item share
+  int32_t place;  // place in the partition's shared-slot list, or hot-list place | first piece << 16
+};
+#define ACF_HPLAN_DQ 4   // occurrences per thread loaded together in k_hplan_dedup
+#define ACF_HPLAN_TOT 8  // partition totals: slots, user CSR, item CSR, list, hot, pieces, shared occurrences
+
+// lanes with act add 1 to cnt[lh]; returns each lane's count before its add.
+// The first active lane's bucket is added once for all lanes that share it.
+__device__ __forceinline__ int32_t wave_lds_count(int32_t* cnt, uint32_t lh, bool act) {
+  const unsigned long long m = __ballot(act);
+  int32_t before = 0;
+  if (!m) return 0;
+  const int lane = threadIdx.x & 63, lead = __ffsll((long long)m) - 1;
+  const uint32_t L = __shfl(lh, lead);
+  const bool mine = act && lh == L;
+  const unsigned long long same = __ballot(mine);
+  int32_t b = 0;
+  if (lane == lead) b = atomicAdd(&cnt[L], __popcll(same));
+  b = __shfl(b, lead);
+  if (mine) before = b + __popcll(same & ((1ull << lane) - 1ull));
+  else if (act) before = atomicAdd(&cnt[lh], 1);
+  return before;
+}
+
 __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
   __shared__ uint32_t lkey[ACF_HPLAN_TS];
   __shared__ int32_t lcnt[ACF_HPLAN_TS];  // count, then the CSR cursor
-  __shared__ int32_t lk[ACF_HPLAN_TS];    // slot (-1: the row occurs once)
-  __shared__ int32_t lb[ACF_HPLAN_TS];    // CSR base
+  __shared__ int32_t lk[ACF_HPLAN_TS];    // local slot (-1: the row occurs once)
+  __shared__ int32_t lb[ACF_HPLAN_TS];    // local CSR offset
   __shared__ int32_t s_at[4][6];
+  __shared__ int32_t s_run[ACF_HPLAN_TOT];
   __shared__ int32_t s_distinct, s_over;
-  const int tid = threadIdx.x, wave = tid >> 6;
-  const int32_t t = blockIdx.x >> p.pb;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int B = p.B, S3 = 3 * B;
-  const int2 seg = p.pseg[blockIdx.x];
-  if (seg.y <= seg.x) return;  // absent partition (uniform)
-  int rbits = 0;               // rounds: 2^rbits sub-partitions by the next hash bits
-  for (int r = 0; r < (1 << rbits);) {
+  const int64_t nparts = (int64_t)p.nb << p.pb;
+  const int2 seg = make_int2(p.poff[(int64_t)blockIdx.x * p.tpb],
+                             blockIdx.x + 1 < nparts ? p.poff[(int64_t)(blockIdx.x + 1) * p.tpb] : p.nb * S3);
+  if (tid < ACF_HPLAN_TOT) s_run[tid] = 0;
+  unsigned long long* shl = p.pstage + seg.x;  // shared occurrences (k_hplan_scatter consumed pstage)
+  int rbits = 0;  // rounds: 2^rbits sub-partitions by the next hash bits
+  for (int r = 0; r < (1 << rbits) && seg.y > seg.x;) {
     for (int e = tid; e < ACF_HPLAN_TS; e += 256) {
       lkey[e] = 0xFFFFFFFFu;
       lcnt[e] = 0;
@@ -789,27 +882,39 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
       if (!rbits) return true;
       return (int)((hplan_hash(key) << p.pb) >> (32 - rbits)) == r;
     };
-    // count the round's keys
-    for (int32_t i = seg.x + tid; i < seg.y; i += 256) {
-      const uint32_t key = (uint32_t)(p.pval[i] >> 32);
-      if (!in_round(key)) continue;
-      uint32_t lh = (hplan_hash(key) >> 7) & (ACF_HPLAN_TS - 1);
-      for (;;) {
-        uint32_t cur = lkey[lh];
-        if (cur == 0xFFFFFFFFu) {
-          if (__hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-          cur = atomicCAS(&lkey[lh], 0xFFFFFFFFu, key);
-          if (cur == 0xFFFFFFFFu) {
-            cur = key;
-            if (atomicAdd(&s_distinct, 1) >= ACF_HPLAN_TS * 3 / 4) atomicOr(&s_over, 1);
-          }
-        }
-        if (cur == key) {
-          atomicAdd(&lcnt[lh], 1);
-          break;
-        }
-        lh = (lh + 1u) & (ACF_HPLAN_TS - 1);
+    for (int32_t i00 = seg.x; i00 < seg.y; i00 += 256 * ACF_HPLAN_DQ) {  // wave-uniform trip counts
+      unsigned long long pvq[ACF_HPLAN_DQ];  // loads issued together: one round trip per 256 x DQ
+#pragma unroll
+      for (int q = 0; q < ACF_HPLAN_DQ; ++q) {
+        const int32_t i = i00 + q * 256 + tid;
+        pvq[q] = i < seg.y ? p.pval[i] : 0ull;
       }
+#pragma unroll
+    for (int q = 0; q < ACF_HPLAN_DQ; ++q) {
+      const int32_t i = i00 + q * 256 + tid;
+      const uint32_t key = (uint32_t)(pvq[q] >> 32);
+      bool act = i < seg.y && in_round(key);
+      uint32_t lh = (hplan_hash(key) >> 7) & (ACF_HPLAN_TS - 1);
+      if (act) {
+        for (;;) {
+          uint32_t cur = lkey[lh];
+          if (cur == 0xFFFFFFFFu) {
+            if (__hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+              act = false;
+              break;
+            }
+            cur = atomicCAS(&lkey[lh], 0xFFFFFFFFu, key);
+            if (cur == 0xFFFFFFFFu) {
+              cur = key;
+              if (atomicAdd(&s_distinct, 1) >= ACF_HPLAN_TS * 3 / 4) atomicOr(&s_over, 1);
+            }
+          }
+          if (cur == key) break;
+          lh = (lh + 1u) & (ACF_HPLAN_TS - 1);
+        }
+      }
+      (void)wave_lds_count(lcnt, lh, act);
+    }
     }
     __syncthreads();
     if (s_over) {  // too many distinct keys: this round again as two halves
@@ -818,7 +923,7 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
       __syncthreads();
       continue;
     }
-    // claims of the shared keys (count > 1), aggregated over the workgroup
+    // local numbering of the round's shared keys (count > 1), after the earlier rounds'
     int32_t v[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < ACF_HPLAN_EPT; ++q) {
@@ -836,26 +941,24 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
     for (int c = 0; c < 6; ++c) {
       int32_t tot = 0;
       ex[c] = wave_excl_sum(v[c], tot);
-      if ((tid & 63) == 0) s_at[wave][c] = tot;
+      if (lane == 0) s_at[wave][c] = tot;
     }
     __syncthreads();
     if (tid < 6) {
-      int32_t* ctr = tid == 0 ? p.scnt : tid == 1 ? p.ucsr : tid == 2 ? p.icsr : tid == 3 ? p.slot_cnt
-                   : tid == 4 ? p.hl.cnt : p.hl.pcnt;
-      int32_t run[4], sum = 0;
+      int32_t sum = s_run[tid];
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        run[w] = sum;
-        sum += s_at[w][tid];
+        const int32_t x = s_at[w][tid];
+        s_at[w][tid] = sum;
+        sum += x;
       }
-      const int32_t base = sum > 0 ? atomicAdd(ctr + t, sum) : 0;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) s_at[w][tid] = base + run[w];
+      s_run[tid] = sum;
     }
     __syncthreads();
     int32_t nx[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) nx[c] = s_at[wave][c] + ex[c];
+    HClaim* claims = reinterpret_cast<HClaim*>(p.claims) + seg.x / 2;
 #pragma unroll
     for (int q = 0; q < ACF_HPLAN_EPT; ++q) {
       const int e = tid * ACF_HPLAN_EPT + q;
@@ -865,53 +968,129 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
       lcnt[e] = 0;  // the CSR cursor from here on
       if (c < 2) continue;
       const bool item = (key & 0x80000000u) != 0, hot = c > ACF_HOT_MIN;
-      const int32_t k = nx[0]++;
-      const int32_t base = item ? nx[2] : nx[1];
+      const int32_t j = nx[0]++;
+      const int32_t off = nx[item ? 2 : 1];
       nx[item ? 2 : 1] += c;
-      lk[e] = k;
-      lb[e] = base;
-      OccRec rec = {};
-      rec.own_row = (int32_t)(key & 0x7FFFFFFFu);
-      rec.own_src = rec.own_row;
-      rec.meta = c | (item ? ACF_ITEM_BIT : 0);
-      rec.ovf = (item ? t * 2 * B : t * B) + base;
-      rec.e_role = -1;
-      rec.gen = p.gen;
-      p.inl[(int64_t)t * p.S + k] = rec;
-      const int32_t aux = base | (item ? (int32_t)0x80000000 : 0);
-      if (!hot) {
-        const int32_t ls = nx[3]++;
-        p.slot_list[(int64_t)t * p.S + ls] = k;
-        p.saux[(int64_t)t * p.S + ls] = aux | (c << 24);
+      lk[e] = j;
+      lb[e] = off;
+      HClaim h;
+      h.key = key;
+      h.count = c;
+      h.csr = off;
+      if (hot) {
+        h.place = nx[4]++ | (nx[5] << 16);
+        nx[5] += hot_pieces(c);
       } else {
-        const int32_t hx = nx[4]++, np = hot_pieces(c), pb0 = nx[5];
-        nx[5] += np;
-        p.hl.list[(int64_t)t * p.hl.hot_stride + hx] = make_int4(k, np, pb0, c);
-        p.haux[(int64_t)t * p.hl.hot_stride + hx] = aux;
-        int4* pc = p.hl.piece + (int64_t)t * p.hl.piece_stride + pb0;
-        for (int32_t w = 0; w < np; ++w) pc[w] = make_int4(k, w, np, pb0);
+        h.place = nx[3]++;
       }
+      claims[j] = h;
     }
     __syncthreads();
-    // every occurrence of the round: {slot, CSR position}, and its CSR entry
-    for (int32_t i = seg.x + tid; i < seg.y; i += 256) {
-      const unsigned long long pv = p.pval[i];
-      const uint32_t key = (uint32_t)(pv >> 32);
-      if (!in_round(key)) continue;
-      const int32_t o = (int32_t)(uint32_t)pv;
-      uint32_t lh = (hplan_hash(key) >> 7) & (ACF_HPLAN_TS - 1);
-      while (lkey[lh] != key) lh = (lh + 1u) & (ACF_HPLAN_TS - 1);
-      int2 out = make_int2(-1, 0);
-      if (lk[lh] >= 0) {
-        const int32_t pos = lb[lh] + atomicAdd(&lcnt[lh], 1);
-        out = make_int2(lk[lh], pos);
-        const bool item = o >= B;
-        p.csr[(int64_t)t * S3 + (item ? B : 0) + pos] = item ? o - B : o;
+    // the round's shared occurrences: {occurrence, local CSR position, local slot}
+    for (int32_t i00 = seg.x; i00 < seg.y; i00 += 256 * ACF_HPLAN_DQ) {
+      unsigned long long pvq[ACF_HPLAN_DQ];
+#pragma unroll
+      for (int q = 0; q < ACF_HPLAN_DQ; ++q) {
+        const int32_t i = i00 + q * 256 + tid;
+        pvq[q] = i < seg.y ? p.pval[i] : 0ull;
       }
-      p.occ[(int64_t)t * S3 + o] = out;
+#pragma unroll
+    for (int q = 0; q < ACF_HPLAN_DQ; ++q) {
+      const int32_t i = i00 + q * 256 + tid;
+      const unsigned long long pv = pvq[q];
+      const uint32_t key = (uint32_t)(pv >> 32);
+      bool act = i < seg.y && in_round(key);
+      uint32_t lh = (hplan_hash(key) >> 7) & (ACF_HPLAN_TS - 1);
+      if (act) {
+        while (lkey[lh] != key) lh = (lh + 1u) & (ACF_HPLAN_TS - 1);
+        act = lk[lh] >= 0;
+      }
+      const int32_t rank = wave_lds_count(lcnt, lh, act);
+      // append (one LDS atomic per wave)
+      const unsigned long long m = __ballot(act);
+      int32_t at = 0;
+      if (m) {
+        const int lead = __ffsll((long long)m) - 1;
+        if (lane == lead) at = atomicAdd(&s_run[6], __popcll(m));
+        at = __shfl(at, lead) + __popcll(m & ((1ull << lane) - 1ull));
+      }
+      if (act)
+        shl[at] = (unsigned long long)(uint32_t)pv | ((unsigned long long)(lb[lh] + rank) << 18) |
+                  ((unsigned long long)lk[lh] << 36);
+    }
     }
     __syncthreads();
     ++r;
+  }
+  if (tid < ACF_HPLAN_TOT) p.ptot[(int64_t)blockIdx.x * ACF_HPLAN_TOT + tid] = s_run[tid];
+}
+
+// one workgroup per batch: partition bases (exclusive scans of the totals over
+// the batch's partitions, <= 256 of them) and the batch's list lengths
+__global__ void __launch_bounds__(256) k_hplan_bases(HPlanArgs p) {
+  using Scan = rocprim::block_scan<int32_t, 256>;
+  __shared__ typename Scan::storage_type st;
+  const int32_t t = blockIdx.x, P = 1 << p.pb, tid = threadIdx.x;
+  const int64_t at = ((int64_t)t * P + tid) * ACF_HPLAN_TOT;
+  for (int c = 0; c < 6; ++c) {
+    const int32_t v = tid < P ? p.ptot[at + c] : 0;
+    int32_t ex = 0, tot = 0;
+    Scan().exclusive_scan(v, ex, 0, tot, st);
+    if (tid < P) p.pbase[at + c] = ex;
+    if (tid == 0) {
+      if (c == 3) p.slot_cnt[t] = tot;
+      if (c == 4) p.hl.cnt[t] = tot;
+      if (c == 5) p.hl.pcnt[t] = tot;
+    }
+    __syncthreads();  // the scan storage is reused
+  }
+}
+
+__global__ void __launch_bounds__(256) k_hplan_emit(HPlanArgs p) {
+  __shared__ int32_t base[6];
+  const int tid = threadIdx.x;
+  const int B = p.B, S3 = 3 * B;
+  const int32_t t = blockIdx.x >> p.pb;
+  const int64_t x0 = p.poff[(int64_t)blockIdx.x * p.tpb];
+  if (tid < 6) base[tid] = p.pbase[(int64_t)blockIdx.x * ACF_HPLAN_TOT + tid];
+  const int32_t nclaims = p.ptot[(int64_t)blockIdx.x * ACF_HPLAN_TOT];
+  const int32_t nsh = p.ptot[(int64_t)blockIdx.x * ACF_HPLAN_TOT + 6];
+  if (nclaims == 0) return;  // uniform
+  __syncthreads();
+  const HClaim* claims = reinterpret_cast<const HClaim*>(p.claims) + x0 / 2;
+  for (int32_t j = tid; j < nclaims; j += 256) {
+    const HClaim h = claims[j];
+    const bool item = (h.key & 0x80000000u) != 0, hot = h.count > ACF_HOT_MIN;
+    const int32_t k = base[0] + j, csr = (item ? base[2] : base[1]) + h.csr;
+    OccRec rec = {};
+    rec.own_row = (int32_t)(h.key & 0x7FFFFFFFu);
+    rec.own_src = rec.own_row;
+    rec.meta = h.count | (item ? ACF_ITEM_BIT : 0);
+    rec.ovf = (item ? t * 2 * B : t * B) + csr;
+    rec.e_role = -1;
+    rec.gen = p.gen;
+    p.inl[(int64_t)t * p.S + k] = rec;
+    const int32_t aux = csr | (item ? (int32_t)0x80000000 : 0);  // the rank kernels' view
+    if (!hot) {
+      const int32_t ls = base[3] + h.place;
+      p.slot_list[(int64_t)t * p.S + ls] = k;
+      p.saux[(int64_t)t * p.S + ls] = aux | (h.count << 24);
+    } else {
+      const int32_t hx = base[4] + (h.place & 0xFFFF), pb0 = base[5] + (h.place >> 16), np = hot_pieces(h.count);
+      p.hl.list[(int64_t)t * p.hl.hot_stride + hx] = make_int4(k, np, pb0, h.count);
+      p.haux[(int64_t)t * p.hl.hot_stride + hx] = aux;
+      int4* pc = p.hl.piece + (int64_t)t * p.hl.piece_stride + pb0;
+      for (int32_t w = 0; w < np; ++w) pc[w] = make_int4(k, w, np, pb0);
+    }
+  }
+  const unsigned long long* shl = p.pstage + x0;
+  for (int32_t x = tid; x < nsh; x += 256) {
+    const unsigned long long v = shl[x];
+    const int32_t o = (int32_t)(v & 0x3FFFFull), lpos = (int32_t)((v >> 18) & 0x3FFFFull), j = (int32_t)(v >> 36);
+    const bool item = o >= B;
+    const int32_t pos = (item ? base[2] : base[1]) + lpos;
+    p.occ[(int64_t)t * S3 + o] = make_int2(base[0] + j, pos);
+    p.csr[(int64_t)t * S3 + (item ? B : 0) + pos] = item ? o - B : o;
   }
 }
 
@@ -4315,7 +4494,9 @@ struct acf_apr_ctx {
   int32_t plan_kind = -1;    // acf_apr_plan_kind
   int32_t hplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   int2* hplan_occ = nullptr;   // [3 maxE] occurrence -> {slot or -1, CSR position}
-  int2* hplan_seg = nullptr;   // [maxNB << pb] partition ranges
+  int32_t* hplan_pcnt = nullptr;  // [2][maxNB << pb][tiles] partition counts, their scan
+  int4* hplan_claims = nullptr;   // [3 maxE / 2] shared keys, partition-local numbering
+  int32_t* hplan_ptot = nullptr;  // [2][maxNB << pb][6] partition totals, their scan
   void* hplan_tmp = nullptr;   // rocPRIM temporary storage when c->tmp is too small
   size_t hplan_tmp_bytes = 0;
   int32_t* hplan_cnt = nullptr;  // [3][maxNB] shared slots, user / item CSR positions
@@ -4685,9 +4866,9 @@ static bool hplan_ready(acf_apr_ctx* c) {
   const int32_t pb = hplan_pbits(c->maxB);
   if (pb + (int32_t)bits_for((uint64_t)c->maxNB) > 32) return false;
   const size_t n3 = (size_t)3 * c->maxE;
+  const size_t ncnt = ((size_t)c->maxNB << pb) * (((size_t)3 * c->maxB + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE);
   size_t tb = 0;
-  if (rocprim::radix_sort_pairs(nullptr, tb, reinterpret_cast<uint32_t*>(c->flag), reinterpret_cast<uint32_t*>(c->inc),
-                                c->key_in, c->key_out, n3, 0, 32) != hipSuccess)
+  if (rocprim::exclusive_scan(nullptr, tb, c->flag, c->inc, 0, ncnt, rocprim::plus<int32_t>()) != hipSuccess)
     return false;
   std::vector<void*> got;
   auto A = [&](auto** p, size_t m) -> bool {
@@ -4695,7 +4876,8 @@ static bool hplan_ready(acf_apr_ctx* c) {
     got.push_back(*p);
     return true;
   };
-  bool ok = A(&c->hplan_occ, n3) && A(&c->hplan_seg, (size_t)c->maxNB << pb) &&
+  bool ok = A(&c->hplan_occ, n3) && A(&c->hplan_pcnt, 2 * ncnt) && A(&c->hplan_claims, n3 / 2 + 1) &&
+            A(&c->hplan_ptot, ((size_t)c->maxNB << pb) * 2 * ACF_HPLAN_TOT) &&
             A(&c->hplan_cnt, (size_t)3 * c->maxNB) && A(&c->hplan_haux, (size_t)c->maxNB * c->hot.hot_stride);
   c->hplan_tmp_bytes = tb;
   if (ok && tb > c->tmp_bytes) ok = A(reinterpret_cast<char**>(&c->hplan_tmp), tb);
@@ -4706,7 +4888,9 @@ static bool hplan_ready(acf_apr_ctx* c) {
       c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), p));
     }
     c->hplan_occ = nullptr;
-    c->hplan_seg = nullptr;
+    c->hplan_pcnt = nullptr;
+    c->hplan_claims = nullptr;
+    c->hplan_ptot = nullptr;
     c->hplan_cnt = nullptr;
     c->hplan_haux = nullptr;
     c->hplan_tmp = nullptr;
@@ -4720,16 +4904,25 @@ static bool hplan_ready(acf_apr_ctx* c) {
 // tri branch, slot ids and CSR ranges numbered in allocation order
 static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg, int32_t B,
                      int32_t nb, int32_t gen, int32_t kb, int32_t check, hipStream_t s) {
-  const int64_t E = (int64_t)B * nb, n3 = 3 * E;
+  const int64_t E = (int64_t)B * nb;
   const int32_t pb = hplan_pbits(B);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));  // the other counters: k_hplan_keys
   HPlanArgs p;
   p.user = user; p.ipos = ipos; p.ineg = ineg;
   p.U1 = c->U1; p.I1 = c->I1;
   p.B = B; p.S = 3 * B; p.nb = nb; p.gen = gen; p.pb = pb;
-  p.pkey = reinterpret_cast<uint32_t*>(c->flag);
-  p.pval = reinterpret_cast<unsigned long long*>(c->key_in);
-  p.pseg = c->hplan_seg; p.occ = c->hplan_occ; p.csr = c->tsl;
+  p.tpb = (3 * B + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE;
+  p.ppr = reinterpret_cast<uint32_t*>(c->flag);
+  p.pstage = reinterpret_cast<unsigned long long*>(c->key_in);
+  p.pval = reinterpret_cast<unsigned long long*>(c->key_out);
+  const int64_t ncnt = ((int64_t)nb << pb) * p.tpb;
+  p.pcnt = c->hplan_pcnt;
+  p.poff = c->hplan_pcnt + ((size_t)c->maxNB << hplan_pbits(c->maxB)) *
+                               (((size_t)3 * c->maxB + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE);
+  p.occ = c->hplan_occ; p.csr = c->tsl;
+  p.claims = c->hplan_claims;
+  p.ptot = c->hplan_ptot;
+  p.pbase = c->hplan_ptot + ((size_t)c->maxNB << hplan_pbits(c->maxB)) * ACF_HPLAN_TOT;
   p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
   p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
   p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt; p.flush_cnt = c->flush_cnt;
@@ -4737,20 +4930,18 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   p.haux = c->hplan_haux;
   p.hl = c->hot;
   p.err = c->err; p.gen_ptr = c->gen_dev;
-  const int64_t nclear = std::max<int64_t>({n3, (int64_t)nb << pb, (int64_t)nb * c->hot.piece_stride});
-  k_hplan_keys<<<(unsigned)((nclear + 255) / 256), 256, 0, s>>>(p);
+  const unsigned tiles = (unsigned)(nb * p.tpb);
+  k_hplan_keys<<<tiles, 256, 0, s>>>(p);
   HIP_TRY(hipGetLastError());
-  uint32_t* sk = reinterpret_cast<uint32_t*>(c->inc);
   {
     void* tmp = c->hplan_tmp ? c->hplan_tmp : c->tmp;
     size_t tb = c->hplan_tmp ? c->hplan_tmp_bytes : c->tmp_bytes;
-    HIP_TRY(rocprim::radix_sort_pairs(tmp, tb, p.pkey, sk, c->key_in, c->key_out, (size_t)n3, 0,
-                                      pb + (int32_t)bits_for((uint64_t)nb), s));
+    HIP_TRY(rocprim::exclusive_scan(tmp, tb, p.pcnt, p.poff, 0, (size_t)ncnt, rocprim::plus<int32_t>(), s));
   }
-  p.pkey = sk;
-  p.pval = reinterpret_cast<unsigned long long*>(c->key_out);
-  k_hplan_bounds<<<(unsigned)((n3 + 255) / 256), 256, 0, s>>>(p, sk, n3);
+  k_hplan_scatter<<<tiles, 256, 0, s>>>(p);
   k_hplan_dedup<<<(unsigned)(nb << pb), 256, 0, s>>>(p);
+  k_hplan_bases<<<(unsigned)nb, 256, 0, s>>>(p);
+  k_hplan_emit<<<(unsigned)(nb << pb), 256, 0, s>>>(p);
   k_hplan_trip<<<(unsigned)((E + 255) / 256), 256, 0, s>>>(p);
   k_hplan_rank_small<<<dim3(64, nb), 256, 0, s>>>(p);
   k_hplan_rank_hot<<<dim3(64, nb), 256, (size_t)2 * ((2 * B + 31) / 32) * sizeof(uint32_t), s>>>(p);
