@@ -479,14 +479,16 @@ struct HotLists {
   int32_t* pcnt;    // [nb] pieces of the batch
   int32_t* arrive;  // [nb][piece_stride] at a hot slot's piece base: its pieces stored so far
                     // (triplet-centric combine: the slot's combine waits for all of them)
+  int2* paux;       // [nb][piece_stride] beside each piece: {slot count, local CSR base | item << 31}
   int32_t hot_stride, piece_stride;
 };
 
 // Per-slot flags of packed plans (non-fused and not hot << 32 | row stays in W
 // scratch), written by k_records for the slot's first occurrence (the hot
 // lists likewise); scanned into the per-batch slot and write-back lists.
+// csr: the slot's local CSR base | item << 31 (the triplet-centric combine's piece waves read it beside the piece)
 __device__ __forceinline__ void slot_flag(uint64_t* __restrict__ sflags, const HotLists& hl, int64_t t, int32_t S,
-                                          int32_t k, int32_t count, bool single, bool inplace) {
+                                          int32_t k, int32_t count, bool single, bool inplace, int32_t csr) {
   const bool hot = !single && count > ACF_HOT_MIN;
   sflags[t * S + k] = ((uint64_t)(!single && !hot) << 32) | (uint64_t)(!inplace);
   if (hot) {
@@ -494,7 +496,10 @@ __device__ __forceinline__ void slot_flag(uint64_t* __restrict__ sflags, const H
     const int32_t h = atomicAdd(hl.cnt + t, 1);
     const int32_t base = atomicAdd(hl.pcnt + t, np);
     hl.list[t * hl.hot_stride + h] = make_int4(k, np, base, count);
-    for (int32_t p = 0; p < np; ++p) hl.piece[t * hl.piece_stride + base + p] = make_int4(k, p, np, base);
+    for (int32_t p = 0; p < np; ++p) {
+      hl.piece[t * hl.piece_stride + base + p] = make_int4(k, p, np, base);
+      hl.paux[t * hl.piece_stride + base + p] = make_int2(count, csr);
+    }
   }
 }
 
@@ -553,9 +558,13 @@ __device__ __forceinline__ void records_one(int64_t e, int32_t t, int32_t ub0, i
   if (rr < R) { if (!(tri && sj)) inl[(base + kj) * R + rr] = rj; }
   else if (!tri) irec[ps.z] = rj;
   if (sflags) {  // packed plans: the slot flags and hot lists, from each slot's first occurrence
-    if (ps.x == U.w && !(tri && su)) slot_flag(sflags, hl, t, S, k, info_count(U), xu, f.in_u);
-    if (ps.y == I.w && !(tri && si)) slot_flag(sflags, hl, t, S, ki, info_count(I), xi, f.in_i);
-    if (ps.z == J.w && !(tri && sj)) slot_flag(sflags, hl, t, S, kj, info_count(J), xj, f.in_j);
+    // local CSR bases (users: t * B + x, items: t * 2B + x; t is 0 in the shard plan's batch)
+    const int32_t Bt = S / 3;
+    if (ps.x == U.w && !(tri && su)) slot_flag(sflags, hl, t, S, k, info_count(U), xu, f.in_u, U.w - (int32_t)t * Bt);
+    if (ps.y == I.w && !(tri && si))
+      slot_flag(sflags, hl, t, S, ki, info_count(I), xi, f.in_i, (I.w - (int32_t)t * 2 * Bt) | (int32_t)0x80000000);
+    if (ps.z == J.w && !(tri && sj))
+      slot_flag(sflags, hl, t, S, kj, info_count(J), xj, f.in_j, (J.w - (int32_t)t * 2 * Bt) | (int32_t)0x80000000);
   }
   if (f.fused || tri) {  // other triplets' records read as absent (older generation)
     OccRec q;
@@ -1080,7 +1089,11 @@ __global__ void __launch_bounds__(256) k_hplan_emit(HPlanArgs p) {
       p.hl.list[(int64_t)t * p.hl.hot_stride + hx] = make_int4(k, np, pb0, h.count);
       p.haux[(int64_t)t * p.hl.hot_stride + hx] = aux;
       int4* pc = p.hl.piece + (int64_t)t * p.hl.piece_stride + pb0;
-      for (int32_t w = 0; w < np; ++w) pc[w] = make_int4(k, w, np, pb0);
+      int2* pa = p.hl.paux + (int64_t)t * p.hl.piece_stride + pb0;
+      for (int32_t w = 0; w < np; ++w) {
+        pc[w] = make_int4(k, w, np, pb0);
+        pa[w] = make_int2(h.count, aux);
+      }
     }
   }
   const unsigned long long* shl = p.pstage + x0;
@@ -3477,8 +3490,15 @@ __device__ __forceinline__ void hot_combine_slot(const StepArgs& a, const int4 e
   constexpr int NG = 256 / LPR;
   const int g = threadIdx.x / LPR, l = threadIdx.x & (LPR - 1), d = a.d;
   RowV<NV> G = zero_row<NV>();
-#pragma unroll 4
-  for (int p = g; p < e.y; p += NG) G = add_row(G, load_piece<LPR, NV, SC1>(a.hot_part, (int64_t)e.z + p, d, l));
+  for (int p0 = g; p0 < e.y; p0 += 8 * NG) {  // 8 pieces' loads in flight per lane-group; the adds in order
+    RowV<NV> x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (p0 + q * NG < e.y) x[q] = load_piece<LPR, NV, SC1>(a.hot_part, (int64_t)e.z + p0 + q * NG, d, l);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (p0 + q * NG < e.y) G = add_row(G, x[q]);
+  }
 #pragma unroll
   for (int v = 0; v < NV; ++v) red[v * 256 + threadIdx.x] = G.v[v];
   __syncthreads();
@@ -3810,6 +3830,44 @@ __device__ __forceinline__ void tri_add(const StepArgs& a, const TriSlot& h, int
   }
 }
 
+// tri_add with a lane-group's loads issued together, Q occurrences at a time;
+// the additions keep tri_add's order (same bits)
+template <int LPR, int NV>
+__device__ __forceinline__ void tri_add_q(const StepArgs& a, const TriSlot& h, int o0, int o1, int step, int l,
+                                          RowV<NV>& G) {
+  constexpr int Q = 4;
+  const int d = a.d;
+  for (int ob = o0; ob < o1; ob += Q * step) {
+    if (h.is_item) {
+      const float* c = tri_ci(a);
+      RowV<NV> x[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (ob + q * step < o1) x[q] = load_row<LPR, NV>(c, h.base + ob + q * step, d, l);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (ob + q * step < o1) G = add_row(G, x[q]);
+    } else {
+      const float* c = tri_cu(a);
+      RowV<NV> x[2 * Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (ob + q * step < o1) {
+          x[2 * q] = load_row<LPR, NV>(c, 2 * (h.base + ob + q * step), d, l);
+          x[2 * q + 1] = load_row<LPR, NV>(c, 2 * (h.base + ob + q * step) + 1, d, l);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (ob + q * step < o1) {
+          G = add_row(G, x[2 * q]);
+          G = add_row(G, x[2 * q + 1]);
+        }
+      }
+    }
+  }
+}
+
 // finish a shared row from its summed G (as the slot kernels' team leader and
 // k_hot_combine do): MODE 0 g0 + delta, 1 BPR Adagrad, 2 APR Adagrad
 template <int LPR, int NV, int MODE>
@@ -3875,12 +3933,18 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
     constexpr int TEAM = 64 / LPR;
     const int n = a.hot.pcnt[a.t];
     const int4* pl = a.hot.piece + (int64_t)a.t * a.hot.piece_stride;
+    const int2* pxa = a.hot.paux + (int64_t)a.t * a.hot.piece_stride;
     for (int x = hw; x < n; x += a.hot_waves) {
       const int4 pc = pl[x];  // {slot, piece, pieces, piece base}
-      const TriSlot h = tri_slot(a, pc.x);
+      const int2 px = pxa[x];  // {count, CSR base | item << 31}: no dependent slot-record load
+      TriSlot h;
+      h.count = px.x;
+      h.is_item = px.y < 0;
+      h.base = px.y & 0x7FFFFFFF;
+      h.row = h.src = 0;  // not read here
       const int o0 = (int)((int64_t)pc.y * h.count / pc.z), o1 = (int)((int64_t)(pc.y + 1) * h.count / pc.z);
       RowV<NV> G = zero_row<NV>();
-      tri_add<LPR, NV>(a, h, o0 + g, o1, TEAM, l, G);
+      tri_add_q<LPR, NV>(a, h, o0 + g, o1, TEAM, l, G);
       team_allreduce<LPR, TEAM, NV>(G);
       if (a.hot_blocks == 0) {  // combined by k_hot_combine (the next launch)
         if (g == 0) store_row<LPR, NV>(a.hot_part, (int64_t)pc.w + pc.y, a.d, l, G);
@@ -3924,7 +3988,7 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
     const int k = lst[x];
     const TriSlot h = tri_slot(a, k);
     RowV<NV> G = zero_row<NV>();
-    tri_add<LPR, NV>(a, h, 0, h.count, 1, l, G);
+    tri_add_q<LPR, NV>(a, h, 0, h.count, 1, l, G);
     tri_finish<LPR, NV, MODE>(a, k, h, G, l);
   }
 }
@@ -4643,6 +4707,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->hot.list, (size_t)maxNB * c->hot.hot_stride); A(&c->hot.piece, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot.cnt, 2 * (size_t)maxNB);
   A(&c->hot.arrive, (size_t)maxNB * c->hot.piece_stride);
+  A(&c->hot.paux, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot_part, (size_t)c->hot.piece_stride * d);
   A(&c->contrib, (size_t)4 * maxB * d);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
