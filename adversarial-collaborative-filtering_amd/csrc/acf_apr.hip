@@ -681,8 +681,8 @@ __global__ void k_task_list(const int32_t* __restrict__ flags, const int32_t* __
 // tile-aggregated, still 0.48 ms: slower than the sort plan.)
 // ---------------------------------------------------------------------------
 #define ACF_HPLAN_MAXB 65536  // the hot-rank bitmap: 2B bits of LDS per workgroup
-#define ACF_HPLAN_TS 2048     // LDS buckets of a partition round (distinct keys <= 3/4 of them)
-#define ACF_HPLAN_PART 768    // occurrences per partition (mean)
+// partitions of ~768 occurrences (2,048 LDS buckets) by default, ~384 (1,024) with
+// ACF_HPLAN_PART=384 (A/B); a round takes at most 3/4 of the buckets
 
 struct HPlanArgs {
   const int32_t* user;
@@ -744,7 +744,7 @@ __device__ __forceinline__ uint32_t hplan_key(const HPlanArgs& p, int32_t t, int
 #define ACF_HPLAN_PTILE (256 * ACF_HPLAN_PIPT)
 
 __global__ void __launch_bounds__(256) k_hplan_keys(HPlanArgs p) {
-  __shared__ int32_t hist[256];
+  __shared__ int32_t hist[512];
   const int S3 = 3 * p.B, P = 1 << p.pb, tid = threadIdx.x;
   const int32_t t = blockIdx.x / p.tpb, tile = blockIdx.x - t * p.tpb;
   const int64_t gx = blockIdx.x * 256ll + tid, G = (int64_t)gridDim.x * 256;
@@ -820,7 +820,6 @@ __device__ __forceinline__ int32_t wave_excl_sum(int32_t v, int32_t& total) {
   return incl - v;
 }
 
-#define ACF_HPLAN_EPT (ACF_HPLAN_TS / 256)  // LDS buckets per thread in the claims
 
 // Partition dedup, in three launches so that no global counter is contended
 // (one workgroup per partition claiming from per-batch counters queued ~256
@@ -864,11 +863,13 @@ __device__ __forceinline__ int32_t wave_lds_count(int32_t* cnt, uint32_t lh, boo
   return before;
 }
 
+template <int TS>
 __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
-  __shared__ uint32_t lkey[ACF_HPLAN_TS];
-  __shared__ int32_t lcnt[ACF_HPLAN_TS];  // count, then the CSR cursor
-  __shared__ int32_t lk[ACF_HPLAN_TS];    // local slot (-1: the row occurs once)
-  __shared__ int32_t lb[ACF_HPLAN_TS];    // local CSR offset
+  constexpr int EPT = TS / 256;  // LDS buckets per thread in the claims
+  __shared__ uint32_t lkey[TS];
+  __shared__ int32_t lcnt[TS];  // count, then the CSR cursor
+  __shared__ int32_t lk[TS];    // local slot (-1: the row occurs once)
+  __shared__ int32_t lb[TS];    // local CSR offset
   __shared__ int32_t s_at[4][6];
   __shared__ int32_t s_run[ACF_HPLAN_TOT];
   __shared__ int32_t s_distinct, s_over;
@@ -881,7 +882,7 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
   unsigned long long* shl = p.pstage + seg.x;  // shared occurrences (k_hplan_scatter consumed pstage)
   int rbits = 0;  // rounds: 2^rbits sub-partitions by the next hash bits
   for (int r = 0; r < (1 << rbits) && seg.y > seg.x;) {
-    for (int e = tid; e < ACF_HPLAN_TS; e += 256) {
+    for (int e = tid; e < TS; e += 256) {
       lkey[e] = 0xFFFFFFFFu;
       lcnt[e] = 0;
     }
@@ -903,7 +904,7 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
       const int32_t i = i00 + q * 256 + tid;
       const uint32_t key = (uint32_t)(pvq[q] >> 32);
       bool act = i < seg.y && in_round(key);
-      uint32_t lh = (hplan_hash(key) >> 7) & (ACF_HPLAN_TS - 1);
+      uint32_t lh = (hplan_hash(key) >> 7) & (TS - 1);
       if (act) {
         for (;;) {
           uint32_t cur = lkey[lh];
@@ -915,11 +916,11 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
             cur = atomicCAS(&lkey[lh], 0xFFFFFFFFu, key);
             if (cur == 0xFFFFFFFFu) {
               cur = key;
-              if (atomicAdd(&s_distinct, 1) >= ACF_HPLAN_TS * 3 / 4) atomicOr(&s_over, 1);
+              if (atomicAdd(&s_distinct, 1) >= TS * 3 / 4) atomicOr(&s_over, 1);
             }
           }
           if (cur == key) break;
-          lh = (lh + 1u) & (ACF_HPLAN_TS - 1);
+          lh = (lh + 1u) & (TS - 1);
         }
       }
       (void)wave_lds_count(lcnt, lh, act);
@@ -935,8 +936,8 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
     // local numbering of the round's shared keys (count > 1), after the earlier rounds'
     int32_t v[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int q = 0; q < ACF_HPLAN_EPT; ++q) {
-      const int e = tid * ACF_HPLAN_EPT + q;
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid * EPT + q;
       const int32_t c = lkey[e] == 0xFFFFFFFFu ? 0 : lcnt[e];
       if (c < 2) continue;
       const bool item = (lkey[e] & 0x80000000u) != 0, hot = c > ACF_HOT_MIN;
@@ -969,8 +970,8 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
     for (int c = 0; c < 6; ++c) nx[c] = s_at[wave][c] + ex[c];
     HClaim* claims = reinterpret_cast<HClaim*>(p.claims) + seg.x / 2;
 #pragma unroll
-    for (int q = 0; q < ACF_HPLAN_EPT; ++q) {
-      const int e = tid * ACF_HPLAN_EPT + q;
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid * EPT + q;
       const uint32_t key = lkey[e];
       const int32_t c = key == 0xFFFFFFFFu ? 0 : lcnt[e];
       lk[e] = -1;
@@ -1009,9 +1010,9 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
       const unsigned long long pv = pvq[q];
       const uint32_t key = (uint32_t)(pv >> 32);
       bool act = i < seg.y && in_round(key);
-      uint32_t lh = (hplan_hash(key) >> 7) & (ACF_HPLAN_TS - 1);
+      uint32_t lh = (hplan_hash(key) >> 7) & (TS - 1);
       if (act) {
-        while (lkey[lh] != key) lh = (lh + 1u) & (ACF_HPLAN_TS - 1);
+        while (lkey[lh] != key) lh = (lh + 1u) & (TS - 1);
         act = lk[lh] >= 0;
       }
       const int32_t rank = wave_lds_count(lcnt, lh, act);
@@ -1035,9 +1036,9 @@ __global__ void __launch_bounds__(256) k_hplan_dedup(HPlanArgs p) {
 }
 
 // one workgroup per batch: partition bases (exclusive scans of the totals over
-// the batch's partitions, <= 256 of them) and the batch's list lengths
-__global__ void __launch_bounds__(256) k_hplan_bases(HPlanArgs p) {
-  using Scan = rocprim::block_scan<int32_t, 256>;
+// the batch's partitions, <= 1,024 of them) and the batch's list lengths
+__global__ void __launch_bounds__(1024) k_hplan_bases(HPlanArgs p) {
+  using Scan = rocprim::block_scan<int32_t, 1024>;
   __shared__ typename Scan::storage_type st;
   const int32_t t = blockIdx.x, P = 1 << p.pb, tid = threadIdx.x;
   const int64_t at = ((int64_t)t * P + tid) * ACF_HPLAN_TOT;
@@ -3911,6 +3912,88 @@ __global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
   for (int x = gid; x < n; x += ngroups) flush_slot(a, a.t - 1, a.wnew_prev, lst[x], l, LPR);
 }
 
+// The triplet-centric combine's hot slot, as hot_combine_slot<LPR, NV, MODE,
+// true> computes it (the same additions in the same order), except that the
+// finish runs on lane-group FG = the first of wave 1, which loads what the
+// finish reads besides the pieces -- the slot record, then the Adagrad slot, g0
+// and the row (MODE 2), or the Adagrad slot and the row (MODE 1) -- BEFORE the
+// workgroup waits for the pieces: none of it depends on them (in place: the
+// tables are current; g0 came from the previous launch).  It has to be another
+// wave than the polling thread's: a wave's load counter is shared, and the poll
+// would wait for the prefetch (tried on lane-group 0: slower).
+template <int LPR, int NV>
+struct TriHotPre {
+  int32_t row, src, is_item;
+  RowV<NV> acc, own, g0;
+};
+
+template <int LPR, int NV, int MODE>
+__device__ __forceinline__ TriHotPre<LPR, NV> tri_hot_prefetch(const StepArgs& a, const int4 e) {
+  TriHotPre<LPR, NV> f;
+  const int l = threadIdx.x & (LPR - 1), d = a.d;
+  const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + e.x) * a.R);
+  f.is_item = (r.meta() & ACF_ITEM_BIT) != 0;
+  f.row = r.own_row();
+  f.src = r.own_src();
+  if (MODE != 0) {
+    f.acc = load_row<LPR, NV>(f.is_item ? a.accQ : a.accP, f.row, d, l);
+    if (MODE == 1) f.own = load_at<LPR, NV>(row_src(a, f.is_item ? a.Q : a.P, f.row, f.src), d, l);
+    else f.own = load_row<LPR, NV>(f.is_item ? a.Q : a.P, f.row, d, l);
+  }
+  if (MODE == 2) f.g0 = load_row<LPR, NV>(a.g0, e.x, d, l);
+  return f;
+}
+
+template <int LPR, int NV, int MODE>
+__device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, float4* __restrict__ red,
+                                               TriHotPre<LPR, NV>& f) {
+  constexpr int NG = 256 / LPR, FG = 64 / LPR;
+  const int g = threadIdx.x / LPR, l = threadIdx.x & (LPR - 1), d = a.d;
+  RowV<NV> G = zero_row<NV>();
+  for (int p0 = g; p0 < e.y; p0 += 8 * NG) {
+    RowV<NV> x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (p0 + q * NG < e.y) x[q] = load_piece<LPR, NV, true>(a.hot_part, (int64_t)e.z + p0 + q * NG, d, l);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (p0 + q * NG < e.y) G = add_row(G, x[q]);
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) red[v * 256 + threadIdx.x] = G.v[v];
+  __syncthreads();
+  if (g == FG) {
+    // group 0's sum, then groups 1, 2, ... in order: hot_combine_slot's additions
+    RowV<NV> T;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) T.v[v] = red[v * 256 + l];
+    for (int gg = 1; gg < NG; ++gg) {
+      RowV<NV> o;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) o.v[v] = red[v * 256 + gg * LPR + l];
+      T = add_row(T, o);
+    }
+    const int k = e.x;
+    if (MODE == 0) {
+      const RowV<NV> dl = make_delta<LPR, NV>(a, T, f.is_item, f.row, l);
+      store_row<LPR, NV>(a.g0, k, d, l, T);
+      store_row<LPR, NV>(a.delta, k, d, l, dl);
+    } else {
+      RowV<NV> wout;
+      if (MODE == 1) {
+        adagrad_row(a, T, f.own, f.acc, e.w, wout);
+      } else {
+        RowV<NV> G0 = f.g0;
+        axpy_row(G0, a.reg_adv, T);
+        adagrad_row(a, G0, f.own, f.acc, e.w, wout);
+      }
+      store_row<LPR, NV>(f.is_item ? a.accQ : a.accP, f.row, d, l, f.acc);
+      store_row<LPR, NV>(f.is_item ? a.Q : a.P, f.row, d, l, wout);  // in place (tri plans)
+    }
+  }
+  __syncthreads();
+}
+
 // Hot slots first in dispatch order, so their chain (pieces -> arrival count ->
 // combining workgroup) starts at once: piece waves [0, hot_waves) into hot_part,
 // then hot_blocks workgroups that each combine hot slots as k_hot_combine does
@@ -3962,6 +4045,8 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
     const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
     for (int hx = hb; hx < n; hx += a.hot_blocks) {
       const int4 e = hl[hx];  // {slot, pieces, piece base, count}
+      TriHotPre<LPR, NV> pre;
+      if (threadIdx.x / LPR == 64 / LPR) pre = tri_hot_prefetch<LPR, NV, MODE>(a, e);  // the finishing group
       if (threadIdx.x == 0) {
         int it = 0;
         while (__hip_atomic_load(arrive + e.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.y) {
@@ -3975,7 +4060,7 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
         __hip_atomic_store(arrive + e.z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
-      hot_combine_slot<LPR, NV, MODE, true>(a, e, red);
+      tri_hot_finish<LPR, NV, MODE>(a, e, red, pre);
     }
     return;
   }
@@ -4556,6 +4641,7 @@ struct acf_apr_ctx {
   int32_t hash_on = 1;
   int32_t tri_comb_waves = 4096;  // slot waves of k_tri_combine (ACF_TRI_COMB_WAVES)
   int32_t plan_kind = -1;    // acf_apr_plan_kind
+  int32_t hplan_part = 768;  // hash plan: occurrences per partition (ACF_HPLAN_PART=384, A/B)
   int32_t hplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   int2* hplan_occ = nullptr;   // [3 maxE] occurrence -> {slot or -1, CSR position}
   int32_t* hplan_pcnt = nullptr;  // [2][maxNB << pb][tiles] partition counts, their scan
@@ -4759,6 +4845,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (const char* e = getenv("ACF_TAIL")) c->tail_on = atoi(e) != 0;
   if (const char* e = getenv("ACF_TAIL_FLUSHERS")) c->tail_flushers = std::max(1, atoi(e));
   if (const char* e = getenv("ACF_HASH_PLAN")) c->hash_on = atoi(e) != 0;
+  if (const char* e = getenv("ACF_HPLAN_PART")) c->hplan_part = atoi(e) == 384 ? 384 : 768;
   if (const char* e = getenv("ACF_TRI_COMB_WAVES")) c->tri_comb_waves = std::max(4, atoi(e));
   if (const char* e = getenv("ACF_BPLAN_SORT")) c->bplan_sort = atoi(e) == 1024 ? 2 : 0;
   if (const char* e = getenv("ACF_TAIL_DIAG"))
@@ -4919,8 +5006,8 @@ static bool bplan_ready(acf_apr_ctx* c) {
 }
 
 // partition bits of a batch of B triplets: 2^pb partitions of <= ACF_HPLAN_PART occurrences on average
-static int32_t hplan_pbits(int32_t B) {
-  const uint64_t parts = ((uint64_t)3 * B + ACF_HPLAN_PART - 1) / ACF_HPLAN_PART;
+static int32_t hplan_pbits(int32_t B, int32_t part) {
+  const uint64_t parts = ((uint64_t)3 * B + part - 1) / part;
   return parts <= 1 ? 0 : (int32_t)bits_for(parts - 1);
 }
 
@@ -4928,7 +5015,7 @@ static bool hplan_ready(acf_apr_ctx* c) {
   if (c->hplan_ok >= 0) return c->hplan_ok == 1;
   c->hplan_ok = 0;
   if (c->maxB > ACF_HPLAN_MAXB) return false;
-  const int32_t pb = hplan_pbits(c->maxB);
+  const int32_t pb = hplan_pbits(c->maxB, 384);  // room for either partition size
   if (pb + (int32_t)bits_for((uint64_t)c->maxNB) > 32) return false;
   const size_t n3 = (size_t)3 * c->maxE;
   const size_t ncnt = ((size_t)c->maxNB << pb) * (((size_t)3 * c->maxB + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE);
@@ -4970,7 +5057,7 @@ static bool hplan_ready(acf_apr_ctx* c) {
 static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg, int32_t B,
                      int32_t nb, int32_t gen, int32_t kb, int32_t check, hipStream_t s) {
   const int64_t E = (int64_t)B * nb;
-  const int32_t pb = hplan_pbits(B);
+  const int32_t pb = hplan_pbits(B, c->hplan_part);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));  // the other counters: k_hplan_keys
   HPlanArgs p;
   p.user = user; p.ipos = ipos; p.ineg = ineg;
@@ -4982,12 +5069,12 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   p.pval = reinterpret_cast<unsigned long long*>(c->key_out);
   const int64_t ncnt = ((int64_t)nb << pb) * p.tpb;
   p.pcnt = c->hplan_pcnt;
-  p.poff = c->hplan_pcnt + ((size_t)c->maxNB << hplan_pbits(c->maxB)) *
+  p.poff = c->hplan_pcnt + ((size_t)c->maxNB << hplan_pbits(c->maxB, 384)) *
                                (((size_t)3 * c->maxB + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE);
   p.occ = c->hplan_occ; p.csr = c->tsl;
   p.claims = c->hplan_claims;
   p.ptot = c->hplan_ptot;
-  p.pbase = c->hplan_ptot + ((size_t)c->maxNB << hplan_pbits(c->maxB)) * ACF_HPLAN_TOT;
+  p.pbase = c->hplan_ptot + ((size_t)c->maxNB << hplan_pbits(c->maxB, 384)) * ACF_HPLAN_TOT;
   p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
   p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
   p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt; p.flush_cnt = c->flush_cnt;
@@ -5004,8 +5091,11 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
     HIP_TRY(rocprim::exclusive_scan(tmp, tb, p.pcnt, p.poff, 0, (size_t)ncnt, rocprim::plus<int32_t>(), s));
   }
   k_hplan_scatter<<<tiles, 256, 0, s>>>(p);
-  k_hplan_dedup<<<(unsigned)(nb << pb), 256, 0, s>>>(p);
-  k_hplan_bases<<<(unsigned)nb, 256, 0, s>>>(p);
+  if (c->hplan_part == 384)
+    k_hplan_dedup<1024><<<(unsigned)(nb << pb), 256, 0, s>>>(p);
+  else
+    k_hplan_dedup<2048><<<(unsigned)(nb << pb), 256, 0, s>>>(p);
+  k_hplan_bases<<<(unsigned)nb, 1024, 0, s>>>(p);
   k_hplan_emit<<<(unsigned)(nb << pb), 256, 0, s>>>(p);
   k_hplan_trip<<<(unsigned)((E + 255) / 256), 256, 0, s>>>(p);
   k_hplan_rank_small<<<dim3(64, nb), 256, 0, s>>>(p);

@@ -565,10 +565,11 @@ class ShardedAPR:
 
     # -- one step ------------------------------------------------------------------
     def _pipelined(self) -> bool:
-        """The next step's plan beside this step: the local passes support it, and
-        no graph segment is cut between here and the next step (eager steps, or a
-        capture that holds its collectives)."""
-        return getattr(self.local, "pipelined", False) and (self._rec is None or self._cap_coll)
+        """The next step's plan beside this step: the local passes support it.  A
+        capture never cuts the chunk into segments any more (its collectives are
+        inside the graph, or there are none: world 1), so the side-stream plan is
+        a branch of the captured graph, forked and joined by events."""
+        return getattr(self.local, "pipelined", False)
 
     def _plan_step(self, m, t: int, nb: list, pipe: bool) -> None:
         """The plan of step t (nb[t] local triplets): in line, or -- pipelined -- the
