@@ -30,7 +30,8 @@ PKG = os.path.basename(PKG_DIR)
 LIBS = {
     "apr": {"lib": f"{PKG}/lib/libacf_apr.so",
             "srcs": [f"{PKG}/csrc/acf_apr.hip", f"{PKG}/csrc/acf_ops.hip"],
-            "headers": ["include/acf_apr.h", f"{PKG}/csrc/acf_rows.h"]},
+            "headers": ["include/acf_apr.h", f"{PKG}/csrc/acf_rows.h", f"{PKG}/csrc/acf_hplan.h",
+                        f"{PKG}/csrc/acf_eval.h"]},
     "neumf": {"lib": f"{PKG}/lib/libacf_neumf.so",
               "srcs": [f"{PKG}/csrc/acf_neumf.hip"],
               "headers": ["include/acf_apr.h", "include/acf_neumf.h"]},
