@@ -3785,7 +3785,7 @@ struct acf_apr_ctx {
   int32_t hash_on = 1;
   int32_t tri_comb_waves = 4096;  // slot waves of k_tri_combine (ACF_TRI_COMB_WAVES)
   int32_t plan_kind = -1;    // acf_apr_plan_kind
-  int32_t hplan_part = 768;  // hash plan: occurrences per partition (ACF_HPLAN_PART=384, A/B)
+  int32_t hplan_part = 384;  // hash plan: occurrences per partition (ACF_HPLAN_PART=768, A/B)
   int32_t hplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   int2* hplan_occ = nullptr;   // [3 maxE] occurrence -> {slot or -1, CSR position}
   int32_t* hplan_pcnt = nullptr;  // [2][maxNB << pb][tiles] partition counts, their scan
@@ -3989,7 +3989,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (const char* e = getenv("ACF_TAIL")) c->tail_on = atoi(e) != 0;
   if (const char* e = getenv("ACF_TAIL_FLUSHERS")) c->tail_flushers = std::max(1, atoi(e));
   if (const char* e = getenv("ACF_HASH_PLAN")) c->hash_on = atoi(e) != 0;
-  if (const char* e = getenv("ACF_HPLAN_PART")) c->hplan_part = atoi(e) == 384 ? 384 : 768;
+  if (const char* e = getenv("ACF_HPLAN_PART")) c->hplan_part = atoi(e) == 768 ? 768 : 384;
   if (const char* e = getenv("ACF_TRI_COMB_WAVES")) c->tri_comb_waves = std::max(4, atoi(e));
   if (const char* e = getenv("ACF_BPLAN_SORT")) c->bplan_sort = atoi(e) == 1024 ? 2 : 0;
   if (const char* e = getenv("ACF_TAIL_DIAG"))

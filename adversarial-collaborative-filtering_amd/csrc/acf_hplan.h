@@ -36,8 +36,8 @@
 // tile-aggregated, still 0.48 ms: slower than the sort plan.)
 // ---------------------------------------------------------------------------
 #define ACF_HPLAN_MAXB 65536  // the hot-rank bitmap: 2B bits of LDS per workgroup
-// partitions of ~768 occurrences (2,048 LDS buckets) by default, ~384 (1,024) with
-// ACF_HPLAN_PART=384 (A/B); a round takes at most 3/4 of the buckets
+// partitions of ~384 occurrences (1,024 LDS buckets) by default, ~768 (2,048) with
+// ACF_HPLAN_PART=768 (A/B: 0.5% slower at configs[4]); a round takes at most 3/4 of the buckets
 
 struct HPlanArgs {
   const int32_t* user;
