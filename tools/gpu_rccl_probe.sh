@@ -7,5 +7,5 @@ for k in "all_to_all del_destroy" "all_to_all exit" "all_to_all del" "all_gather
   timeout -k 10 60 python3 tools/rccl_capture_probe.py $1 $2 > gpurun_out/rccl_probe/$1_$2.log 2>&1
   rc=$?
   echo "$1 $2 rc=$rc: $(grep -v amdgpu.ids gpurun_out/rccl_probe/$1_$2.log | tail -3 | tr '\n' ' ')"
-  [ $rc -ne 0 ] && exit $rc
+  if [ $rc -ne 0 ]; then exit $rc; fi
 done
