@@ -132,10 +132,7 @@ def test_sharded_collectives_captured_in_graph_world1(ops, dev, exchange, routed
     outs, segs = [], []
     try:
         uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
-        cases = [(False, False), (True, False)]
-        if os.environ.get("ACF_TEST_RCCL_GRAPH") == "1":  # opt-in, as capture_collectives is
-            cases.append((True, True))
-        for graph, cap in cases:
+        for graph, cap in ((False, False), (True, False), (True, True)):
             sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, item_exchange=exchange, graph=graph,
                                local_batch=B if routed else None, force_collectives=True, capture_collectives=cap)
             assert sh._cap_coll == cap and sh.graph == (graph and cap)
@@ -150,9 +147,7 @@ def test_sharded_collectives_captured_in_graph_world1(ops, dev, exchange, routed
             del sh
     finally:
         dist.destroy_process_group()
-    assert segs[1] == [], segs
-    if len(segs) > 2:
-        assert segs[2] and segs[2] == [1] * len(segs[2]), segs  # one graph per chunk
+    assert segs[1] == [] and segs[2] and segs[2] == [1] * len(segs[2]), segs  # one graph per chunk
     for o in outs[1:]:
         for g, e, n in zip(o, outs[0], ("P", "Q", "accP", "accQ")):
             assert torch.equal(g, e), n
