@@ -8,7 +8,6 @@ index ranges are validated on device by the plan / sampler (``NativeIndexError``
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 
 import torch
@@ -419,11 +418,9 @@ class PlanPipeline:
         self.ctx[1].share_failsafe(self.ctx[0])  # one verification queue for both (acf_apr.h)
         # default priority: a high-priority plan stream halved the configs[4] rate
         # (608M -> 313M triplets/s at d = 64, tools/large_prio.py, r03)
+        # (the steps on a high-priority stream instead, the plan filling what they
+        # leave idle, was 1.8x slower at configs[4]: 775M -> 424M triplets/s, r04)
         self.side = torch.cuda.Stream(self.device)
-        # ACF_PIPE_STEP_PRIO=1: the steps of an overlapped run on a high-priority
-        # stream instead (the plan then fills what the step kernels leave idle)
-        self.step_priority = os.environ.get("ACF_PIPE_STEP_PRIO", "0") == "1"
-        self._hi = None
         self._free = [None, None]  # event: the last training on ctx[k] has been issued before it
         self._memo = None  # the last single-chunk call, validated (_repeat)
 
@@ -546,25 +543,16 @@ class PlanPipeline:
         ready = torch.cuda.Event()
         ready.record(main)  # triplets produced on the caller's stream
         self.side.wait_event(ready)
-        step = main
-        if self.step_priority:  # the steps on a high-priority stream, joined to the caller's
-            if self._hi is None:
-                self._hi = torch.cuda.Stream(self.device, priority=-1)
-            step = self._hi
-            step.wait_event(ready)
         planned = self._plan(0, u, i, j, *chunks[0], check)
-        with torch.cuda.stream(step):
-            for k, (b, n) in enumerate(chunks):
-                if planned is not None:
-                    step.wait_event(planned)
-                self.ctx[k % 2].train_planned(tables, hp, 0, n, graph=graph)
-                done = torch.cuda.Event()
-                done.record(step)
-                self._free[k % 2] = done
-                if k + 1 < len(chunks):
-                    planned = self._plan(k + 1, u, i, j, *chunks[k + 1], check)
-        if step is not main:
-            main.wait_stream(step)
+        for k, (b, n) in enumerate(chunks):
+            if planned is not None:
+                main.wait_event(planned)
+            self.ctx[k % 2].train_planned(tables, hp, 0, n, graph=graph)
+            done = torch.cuda.Event()
+            done.record(main)
+            self._free[k % 2] = done
+            if k + 1 < len(chunks):
+                planned = self._plan(k + 1, u, i, j, *chunks[k + 1], check)
         self._staged = (u, i, j)
 
 
