@@ -607,6 +607,41 @@ def test_hash_plan_matches_sort_plan(ops, dev, monkeypatch, B, adver):
             assert torch.equal(x, y), n
 
 
+def test_hash_plan_crowded_partition_rounds(ops, dev):
+    """A batch whose users all hash into ONE partition of the hash plan (the top
+    partition bits of k_hplan's Fibonacci hash equal): ~2,000 distinct users there,
+    more than a partition round holds (3/4 of its LDS buckets), so the partition
+    is split into rounds by further hash bits.  The bits equal the sort plan's."""
+    U1, I1, d, B, nb = 300_000, 50_000, 32, 4096, 2
+    pb = 5  # hplan_pbits(4096, 384): 12,288 occurrences / 384 -> 32 partitions
+    rows = np.arange(U1, dtype=np.uint64)
+    part = ((rows * 2654435761) & 0xFFFFFFFF) >> (32 - pb)
+    crowd = rows[part == part[12345]].astype(np.int32)
+    assert len(crowd) > 4000
+    rng = np.random.default_rng(21)
+    u = rng.choice(crowd[:2000], nb * B).astype(np.int32)  # ~2,000 distinct users, ~2 occurrences each
+    i = rng.integers(0, I1, nb * B).astype(np.int32)
+    j = rng.integers(0, I1, nb * B).astype(np.int32)
+    P = (rng.standard_normal((U1, d)) * 0.1).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.1).astype(np.float32)
+    hp = ops.StepHParams(adver=1, reg=0.01)
+    uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
+    runs = []
+    for mode in ("sort", "auto"):
+        ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+        ctx.set_plan_mode(mode)
+        ctx.plan(uu, ii, jj, B)
+        assert ctx.plan_kind() == ("hash" if mode == "auto" else "sort")
+        tabs = _gpu_tables(P, Q, dev)
+        ctx.train_planned(tabs, hp)
+        lc, la = ctx.losses()
+        assert ctx.step_errors() == 0
+        runs.append(tabs + [lc.clone(), la.clone()])
+    torch.cuda.synchronize()
+    for x, y, n in zip(*runs, ("P", "Q", "accP", "accQ", "loss_clean", "loss_adv")):
+        assert torch.equal(x, y), n
+
+
 def test_hash_plan_range_check(ops, dev):
     """A triplet index out of range raises from the hash plan too, and the next
     clean plan works."""
