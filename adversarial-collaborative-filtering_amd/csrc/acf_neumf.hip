@@ -1036,8 +1036,8 @@ constexpr int LAZY_W = 32;  // lr_t window (> the catch-up period)
 // workgroups of a step's catch-up slice, beside the step's kernels (r03, period
 // 8: 32 WGs 3.9M instances/s (the slice outlasts the step), 64 5.6M, 96 7.55M,
 // 128 7.3M, 192 7.45M, 256 7.35M; r04, period 16: 48 5.1M, 64 5.8-6.0M, 96 7.10M,
-// 128 7.15M); ACF_NMF_CATCHUP_WG for A/B
-constexpr int64_t CATCHUP_WG = 128;
+// 128 7.10-7.15M, 192 7.16-7.18M, 256 7.13M); ACF_NMF_CATCHUP_WG for A/B
+constexpr int64_t CATCHUP_WG = 192;
 static_assert(LAZY_W > LAZY_S, "lr window");
 
 struct AdamLazy {
