@@ -37,7 +37,15 @@ def main():
     p.add_argument("--failsafe", type=int, default=1, help="verified streamed calls (1, default) or not (0)")
     p.add_argument("--same", action="store_true",
                    help="every rep repeats the same call (bench.py's timed call: PlanPipeline's fast path)")
+    p.add_argument("--sched", default="", choices=["", "auto", "spin", "yield", "blocking"],
+                   help="hipSetDeviceFlags schedule before the device is used (A/B of the host wait)")
     a = p.parse_args()
+    if a.sched:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        flag = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}[a.sched]
+        rc = hip.hipSetDeviceFlags(ctypes.c_uint(flag))
+        print(f"hipSetDeviceFlags({flag}) -> {rc}", file=sys.stderr)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     acf = importlib.import_module(PKG)
