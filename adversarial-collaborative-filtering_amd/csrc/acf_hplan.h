@@ -15,7 +15,7 @@
 // is fixed.  So (APR.py:183-195's Unique + UnsortedSegmentSum, restated):
 //  1. k_hplan_keys / k_hplan_scatter: a one-pass partition of each batch's
 //     occurrences by the top pb bits of a Fibonacci hash of the (side, row) key
-//     (2^pb partitions of ~768 occurrences, disjoint in keys): per-tile counts,
+//     (2^pb partitions of ~384 occurrences, disjoint in keys): per-tile counts,
 //     their exclusive scan, a scatter -- in place of the sort plan's radix sort;
 //  2. k_hplan_dedup, one workgroup per partition: its keys counted in an LDS hash
 //     table (LDS atomics only); the shared keys claim slot ids, CSR ranges and
