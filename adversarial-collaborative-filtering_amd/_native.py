@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libacf_apr.so")
 
 ACF_OK, ACF_E_INVALID, ACF_E_RANGE, ACF_E_HIP, ACF_E_NOMEM, ACF_E_STATE = range(6)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
@@ -65,6 +65,7 @@ SIGNATURES = {
     "acf_apr_set_spin_limit": (ctypes.c_int, [_P, _I32]),
     "acf_apr_stream_recoveries": (ctypes.c_int, [_P, ctypes.POINTER(_I64)]),
     "acf_apr_resolve": (ctypes.c_int, [_P]),
+    "acf_apr_resolve_all": (ctypes.c_int, []),
     "acf_apr_share_failsafe": (ctypes.c_int, [_P, _P]),
     "acf_apr_copy_losses": (ctypes.c_int, [_P, _P, _P, _P]),
     "acf_apr_delta_scatter": (ctypes.c_int, [_P, _P, _P, _P]),

@@ -47,6 +47,7 @@
 #include <deque>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "acf_apr.h"
@@ -3710,6 +3711,20 @@ struct FailGroup {
   std::deque<Pending> q;
   int refs = 0;
 };
+// every live group, for acf_apr_resolve_all (readers outside a group: evaluation,
+// forward, checkpoints)
+static std::vector<FailGroup*> g_groups;
+static FailGroup* new_group() {
+  FailGroup* g = new FailGroup();
+  g->refs = 1;
+  g_groups.push_back(g);
+  return g;
+}
+static void drop_group(FailGroup* g) {
+  if (g->gate) (void)hipFree(g->gate);
+  g_groups.erase(std::find(g_groups.begin(), g_groups.end(), g));
+  delete g;
+}
 
 struct acf_apr_ctx {
   int64_t U1 = 0, I1 = 0;
@@ -3994,8 +4009,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (const char* e = getenv("ACF_BPLAN_SORT")) c->bplan_sort = atoi(e) == 1024 ? 2 : 0;
   if (const char* e = getenv("ACF_TAIL_DIAG"))
     if (atoi(e) && dalloc(c, &c->tail_diag, 8) == ACF_OK) (void)hipMemset(c->tail_diag, 0, 64);
-  c->grp = new FailGroup();
-  c->grp->refs = 1;
+  c->grp = new_group();
   if (hipMalloc(&c->grp->gate, 16) != hipSuccess || hipMemset(c->grp->gate, 0, 16) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     (void)hipGetLastError();
@@ -4012,10 +4026,7 @@ static void leave_group(acf_apr_ctx* c) {
   if (!g) return;
   for (auto it = g->q.begin(); it != g->q.end();)
     it = it->c == c ? g->q.erase(it) : it + 1;
-  if (--g->refs == 0) {
-    if (g->gate) (void)hipFree(g->gate);
-    delete g;
-  }
+  if (--g->refs == 0) drop_group(g);
 }
 
 static bool decided(const Pending& p, bool* failed) {
@@ -4027,6 +4038,23 @@ static bool decided(const Pending& p, bool* failed) {
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                     int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds,
                     int allow_overlap, int tri_phases);
+
+// Block until queued call p has reported its outcome: poll its word of the
+// host-mapped status ring, not the stream (a stream sync also waited
+// for every call enqueued after p, e.g. the other context's chunk of a
+// PlanPipeline).  A stream that has gone idle without an outcome is an error.
+static int wait_decided(const Pending& p, bool* failed) {
+  for (;;) {
+    if (decided(p, failed)) return ACF_OK;
+    const hipError_t q = hipStreamQuery(p.s);
+    if (q == hipSuccess) {
+      if (decided(p, failed)) return ACF_OK;
+      return set_error(ACF_E_STATE, "streamed call %u reported no outcome", p.seq);
+    }
+    if (q != hipErrorNotReady) return set_error(ACF_E_HIP, "hipStreamQuery: %s", hipGetErrorString(q));
+    std::this_thread::yield();
+  }
+}
 
 // Settle the queued verified streamed calls of c's group (see FailGroup), front
 // to back.  mode 0: only calls that have already reported; 1: block until every
@@ -4041,9 +4069,7 @@ static int resolve(acf_apr_ctx* c, int mode) {
       bool need = mode == 2;
       for (const auto& x : g->q) need = need || (mode == 1 && x.c == c);
       if (!need) return ACF_OK;
-      HIP_TRY(hipStreamSynchronize(p.s));
-      if (!decided(p, &failed))
-        return set_error(ACF_E_STATE, "streamed call %u reported no outcome", p.seq);
+      ACF_RET(wait_decided(p, &failed));
     }
     if (!failed) {
       g->q.pop_front();
@@ -4053,10 +4079,7 @@ static int resolve(acf_apr_ctx* c, int mode) {
     // clear the gate and replay them all, in order
     for (const auto& x : g->q) {
       bool f2 = false;
-      if (!decided(x, &f2)) {
-        HIP_TRY(hipStreamSynchronize(x.s));
-        if (!decided(x, &f2)) return set_error(ACF_E_STATE, "streamed call %u reported no outcome", x.seq);
-      }
+      ACF_RET(wait_decided(x, &f2));
     }
     std::deque<Pending> todo;
     todo.swap(g->q);
@@ -4099,10 +4122,13 @@ extern "C" int acf_apr_share_failsafe(acf_apr_ctx* c, acf_apr_ctx* peer) {
   FailGroup* g = c->grp;
   c->grp = peer->grp;
   ++c->grp->refs;
-  if (--g->refs == 0) {
-    (void)hipFree(g->gate);
-    delete g;
-  }
+  if (--g->refs == 0) drop_group(g);
+  return ACF_OK;
+}
+
+extern "C" int acf_apr_resolve_all(void) {
+  for (size_t k = 0; k < g_groups.size(); ++k)
+    if (!g_groups[k]->q.empty()) ACF_RET(resolve(g_groups[k]->q.front().c, 2));
   return ACF_OK;
 }
 
@@ -4874,6 +4900,10 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     // the write-back in k_stream's tail: the whole plan in one launch (the final-
     // slot list is the plan's), and a launch the host counts (not captured)
     const bool tail = c->tail_on && c->final_ok && first == 0 && n == c->nb && cap == 0;
+    // an unverified launch behind queued verified calls would run gated if one of
+    // them failed (dropped for good): settle the group first (not
+    // possible while capturing: a captured call is documented as unverified)
+    if (!verify && cap == 0 && !c->grp->q.empty()) ACF_RET(resolve(c, 2));
     if (verify) {  // at most 8 queued calls per context (its status ring)
       int mine = 0;
       for (const auto& x : c->grp->q) mine += x.c == c;

@@ -47,17 +47,18 @@ chunk's steps are captured as hipGraphs once and replayed:
 
   * world 1: the exchanges are the identity (no collective), the whole chunk is
     ONE graph;
-  * world > 1 (r04): the fixed-size RCCL all_to_all / all_gather calls can be
-    captured INSIDE the graph too (``capture_collectives``, or
-    ACF_SHARD_RCCL_GRAPH=1; a one-off capture + replay of an all_reduce checks
-    at construction that the RCCL in use can be captured), so a chunk is again
-    ONE graph with no host round trip per exchange.  It is OFF by default: on
-    the one-GPU rehearsal (tools/rccl_capture_probe.py) a captured RCCL
-    all_to_all replays correctly but the process group then does not tear down
-    while the graph is alive, so ``close()`` drops the graphs first, and the
-    8-GPU behaviour is unmeasured.  Off, the steps run eagerly (r03 captured the
-    local work between two collectives as separate segments; rehearsed with
-    RCCL in r04 that met an allocator assertion, so it is gone).
+  * world > 1: the fixed-size RCCL all_to_all / all_gather calls are captured
+    INSIDE the graph too (``capture_collectives``, default on since r05;
+    ACF_SHARD_RCCL_GRAPH=0 turns it off), after a one-off capture + replay of an
+    all_reduce at construction that every rank must pass (else every rank runs
+    the steps eagerly), so a chunk is again ONE graph with no host round trip
+    per exchange.  A graph holding captured RCCL work keeps the communicator
+    busy, so the graphs are dropped before the process group goes: ``close()``,
+    the with-block, the object's collection or, failing all three, the
+    interpreter's exit (a weakref.finalize; tools/rccl_capture_probe.py checks
+    the orders).  Without captured collectives the steps run eagerly (r03
+    captured the local work between two collectives as separate segments;
+    that path is gone).
     ``force_collectives`` routes the
     exchanges through the process group even at world 1 (an RCCL self-exchange):
     the one-GPU rehearsal of the captured collectives
@@ -77,10 +78,19 @@ from __future__ import annotations
 import os
 import time
 import warnings
+import weakref
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+
+def _drop_graphs(graphs: dict, device) -> None:
+    """ShardedAPR's finalizer: wait for the device, then release the captured step
+    graphs (it holds no reference to the ShardedAPR itself)."""
+    if device is not None and graphs:
+        torch.cuda.synchronize(device)
+    graphs.clear()
 
 
 class HipLocal:
@@ -245,8 +255,8 @@ class ShardedAPR:
         if graph is None:  # ACF_SHARD_GRAPH=0: eager steps (A/B of the captured graphs)
             graph = os.environ.get("ACF_SHARD_GRAPH", "1") != "0"
         self.graph = bool(graph) and can_graph
-        if capture_collectives is None:  # opt-in (see the module docstring)
-            capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "0") != "0"
+        if capture_collectives is None:  # default on (r05); ACF_SHARD_RCCL_GRAPH=0 keeps the steps eager
+            capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "1") != "0"
         multi = self.G > 1 or self._force  # exchanges that are collectives
         self._cap_coll = bool(capture_collectives) and self.graph and multi
         self._C = 0   # per-peer block rows of the exchange buffers (only grows)
@@ -254,6 +264,12 @@ class ShardedAPR:
         self._buf = None
         self._maps = None
         self._graphs = {}
+        # the captured graphs (which may hold RCCL work) are dropped before the
+        # process group goes: by close() / the with-block, else when this object is
+        # collected, else at interpreter exit (weakref.finalize runs its atexit hook
+        # before torch's process-group destructors)
+        self._finalizer = weakref.finalize(self, _drop_graphs, self._graphs,
+                                           self.device if self.device.type == "cuda" else None)
         self._pool = None
         self._cap_stream = None
         self._rec = None  # the segment recorder while capturing
@@ -777,11 +793,16 @@ class ShardedAPR:
         return self.local.step_errors() if hasattr(self.local, "step_errors") else 0
 
     def close(self) -> None:
-        """Drop the captured step graphs (call before destroying the process group:
-        a graph holding captured RCCL collectives keeps the communicator busy)."""
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
-        self._graphs.clear()
+        """Drop the captured step graphs (before the process group is destroyed: a
+        graph holding captured RCCL collectives keeps the communicator busy).  Also
+        run by the with-block, when the object is collected, and at exit."""
+        self._finalizer()
+
+    def __enter__(self) -> "ShardedAPR":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
 
     def full_tables(self):
         """The full tables on every rank (checkpoints, evaluation, tests)."""

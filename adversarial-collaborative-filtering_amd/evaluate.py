@@ -100,7 +100,7 @@ def positions(P, Q, plan: EvalPlan, kernel: str = "auto"):
     dev = P.device
     u, t, o, c = plan.device_arrays(dev)
     if plan.mode == "all":
-        return ops.eval_positions_all(P, Q, u, t, plan.num_candidates, o, c, kernel=kernel)
+        return ops.eval_positions_all(P, Q, u, t, plan.num_candidates, o, c, kernel=kernel, unique_lists=True)
     return ops.eval_positions_list(P, Q, u, t, o, c)
 
 

@@ -109,6 +109,7 @@ class MF:
     # -- state ----------------------------------------------------------------
     @property
     def tables(self):
+        ops.settle_tables()
         return (self.embedding_P, self.embedding_Q, self.accumulator_P, self.accumulator_Q)
 
     def hparams(self, adver=None) -> ops.StepHParams:
@@ -224,6 +225,8 @@ class Session:
             out["output_neg"] = on.cpu().numpy().reshape(-1, 1)
         elif "output" in names:
             out["output"] = m.scores(u, i)
+        if "embedding_P" in names or "embedding_Q" in names:
+            ops.settle_tables()
         if "embedding_P" in names:
             out["embedding_P"] = m.embedding_P.cpu().numpy()
         if "embedding_Q" in names:

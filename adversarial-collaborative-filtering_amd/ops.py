@@ -8,6 +8,7 @@ index ranges are validated on device by the plan / sampler (``NativeIndexError``
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -464,14 +465,14 @@ class PlanPipeline:
         for c in self.ctx:
             c.set_plan_mode(mode)
 
-    def _remember(self, tables, hp, user, item_pos, item_neg, first_batch, n_batches, graph) -> None:
+    def _remember(self, tables, hp, user, item_pos, item_neg, first_batch, n_arg, n_batches, graph) -> None:
         c = self.ctx[0]
         P, Q, aP, aQ = tables
         tb, h = c._tables(P, Q, aP, aQ), hp.to_c()
         off = first_batch * self.batch_size * 4
         args = (c._ptr, ctypes.byref(tb), ctypes.byref(h), user.data_ptr() + off, item_pos.data_ptr() + off,
                 item_neg.data_ptr() + off, self.batch_size, n_batches, 0, int(bool(graph)))
-        self._memo = (user, item_pos, item_neg, hp, first_batch, n_batches, graph, P, Q, aP, aQ, dict(hp.__dict__),
+        self._memo = (user, item_pos, item_neg, hp, first_batch, n_arg, graph, P, Q, aP, aQ, dict(hp.__dict__),
                       (P.data_ptr(), Q.data_ptr(), aP.data_ptr(), aQ.data_ptr(), user.data_ptr(),
                        item_pos.data_ptr(), item_neg.data_ptr()),
                       _native.load().acf_apr_train, args, c, tb, h)
@@ -521,6 +522,7 @@ class PlanPipeline:
                                                                  n_batches, graph):
             return
         self._memo = None
+        n_arg = n_batches  # the memo compares the caller's own argument (None or a count)
         B = self.batch_size
         u, i, j = (_idx(x, n, self.device) for x, n in ((user, "user"), (item_pos, "item_pos"),
                                                        (item_neg, "item_neg")))
@@ -538,7 +540,7 @@ class PlanPipeline:
                 self.ctx[k % 2].train_range(tables, hp, u, i, j, B, b, n, graph=graph, check=check, _checked=True)
             self._staged = (u, i, j)
             if len(chunks) == 1 and not check and u is user and i is item_pos and j is item_neg:
-                self._remember(tables, hp, user, item_pos, item_neg, first_batch, n_batches, graph)
+                self._remember(tables, hp, user, item_pos, item_neg, first_batch, n_arg, n_batches, graph)
             return
         ready = torch.cuda.Event()
         ready.record(main)  # triplets produced on the caller's stream
@@ -556,9 +558,18 @@ class PlanPipeline:
         self._staged = (u, i, j)
 
 
+def settle_tables() -> None:
+    """Settle every queued (lazily verified) streamed call of the process
+    (acf_apr_resolve_all): a failed one is replayed before anything reads the
+    tables.  The readers outside a context's group call it first: the forward,
+    evaluation, dns selection, Session fetches of the tables and checkpoints."""
+    call("acf_apr_resolve_all")
+
+
 def bpr_forward(P, Q, user, item_pos, item_neg, batch_size: int, clip_lo=CLIP_LO, clip_hi=CLIP_HI,
                 want_scores: bool = False):
     """training_loss_acc's forward (utils.py:159-175): per-batch loss sum and #correct."""
+    settle_tables()
     dev = P.device
     _require(P, "embedding_P", torch.float32, None, 2)
     _require(Q, "embedding_Q", torch.float32, dev, 2)
@@ -570,7 +581,8 @@ def bpr_forward(P, Q, user, item_pos, item_neg, batch_size: int, clip_lo=CLIP_LO
         raise ValueError("triplets must be equal-length multiples of batch_size")
     nb = n // batch_size
     _check_range(u, P.shape[0], "user")
-    _check_range(torch.cat([i, j]), Q.shape[0], "item")
+    _check_range(i, Q.shape[0], "item")
+    _check_range(j, Q.shape[0], "item")
     bl = torch.empty(nb, dtype=torch.float32, device=dev)
     bc = torch.empty(nb, dtype=torch.int32, device=dev)
     op = torch.empty(n, dtype=torch.float32, device=dev) if want_scores else None
@@ -583,31 +595,60 @@ def bpr_forward(P, Q, user, item_pos, item_neg, batch_size: int, clip_lo=CLIP_LO
     return bl, bc, op, on
 
 
-_RANGE_OK: dict = {}  # index tensors already range-checked, by (storage, version, bound)
+_RANGE_OK: dict = {}  # (address, length, version, bound, device) -> weakref of the checked tensor
 
 
 def _check_range(idx: torch.Tensor, rows: int, name: str) -> None:
     """IndexError unless every index lies in [0, rows).  The check reads the
     extremes back to the host (a device sync), so a tensor that passed is
     remembered by (address, length, in-place version, bound): an evaluation plan
-    re-uses the same user / test tensors every epoch and pays the check once."""
+    re-uses the same user / test tensors every epoch and pays the check once.
+    The cache holds weak references only: an entry never extends a
+    tensor's lifetime and leaves the cache when the tensor is freed."""
     key = (idx.data_ptr(), idx.numel(), idx._version, rows, idx.device)
-    if _RANGE_OK.get(key) is idx:
+    ref = _RANGE_OK.get(key)
+    if ref is not None and ref() is idx:
         return
     if idx.numel() and (int(idx.min()) < 0 or int(idx.max()) >= rows):
         raise _native.NativeIndexError(_native.ACF_E_RANGE, "range check",
                                        f"{name} index outside [0, {rows})")
-    if len(_RANGE_OK) > 64:
-        _RANGE_OK.clear()
-    _RANGE_OK[key] = idx
+
+    def _evict(r, k=key):
+        if _RANGE_OK.get(k) is r:
+            del _RANGE_OK[k]
+    _RANGE_OK[key] = weakref.ref(idx, _evict)
 
 
 EVAL_KERNELS = {"auto": 0, "mfma": 1, "valu": 2}
 
 
-def eval_positions_all(P, Q, users, test_items, num_candidates: int, excl_off, excl_items, kernel: str = "auto"):
+def _unique_exclusions(off: torch.Tensor, ex: torch.Tensor, n_users: int) -> torch.Tensor:
+    """Each user's exclusion list as a SET (the reference's set(trainList[u]),
+    utils.py:188-195): a repeated entry of a list is replaced by -1, which every
+    sweep ignores (never a candidate).  The MFMA sweep applies a list as a bitmap
+    (set semantics) and the VALU sweep subtracts once per entry, so without this a
+    duplicate made them disagree.  Sort + compare on the device, no
+    host sync; the lengths stay as given."""
+    if ex.numel() < 2:
+        return ex
+    seg = torch.repeat_interleave(torch.arange(n_users, device=ex.device), off[1:] - off[:-1],
+                                  output_size=ex.numel())
+    wide = int(2 ** 31)
+    key = seg * wide + ex.long().clamp(-1, wide - 2) + 1
+    skey, perm = torch.sort(key)
+    dup = torch.zeros(ex.numel(), dtype=torch.bool, device=ex.device)
+    dup[perm[1:]] = skey[1:] == skey[:-1]
+    return torch.where(dup, torch.full_like(ex, -1), ex)
+
+
+def eval_positions_all(P, Q, users, test_items, num_candidates: int, excl_off, excl_items, kernel: str = "auto",
+                       unique_lists: bool = False):
     """_eval_by_user positions over all items minus the exclusion lists.  kernel:
-    'auto' | 'mfma' | 'valu' (acf_eval_positions_all_kernel; same positions)."""
+    'auto' | 'mfma' | 'valu' (acf_eval_positions_all_kernel; same positions).
+    A list may repeat an item: it is excluded once (set semantics); callers whose
+    lists are already duplicate-free (EvalPlan: np.union1d) pass unique_lists=True
+    to skip the device-side dedup."""
+    settle_tables()
     dev = P.device
     _require(P, "embedding_P", torch.float32, None, 2)
     _require(Q, "embedding_Q", torch.float32, dev, 2)
@@ -622,6 +663,8 @@ def eval_positions_all(P, Q, users, test_items, num_candidates: int, excl_off, e
     _check_range(t, Q.shape[0], "test item")
     if num_candidates > Q.shape[0]:
         raise ValueError("num_candidates exceeds item rows")
+    if not unique_lists and len(excl_items):
+        ex = _unique_exclusions(off, ex, u.numel())
     pos = torch.empty(u.numel(), dtype=torch.int32, device=dev)
     with _on(dev):
         call("acf_eval_positions_all_kernel", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
@@ -632,6 +675,7 @@ def eval_positions_all(P, Q, users, test_items, num_candidates: int, excl_off, e
 
 def eval_positions_list(P, Q, users, test_items, cand_off, cand_items):
     """_eval_by_user positions over explicit candidate lists ("sample" mode)."""
+    settle_tables()
     dev = P.device
     _require(P, "embedding_P", torch.float32, None, 2)
     _require(Q, "embedding_Q", torch.float32, dev, 2)
@@ -639,7 +683,8 @@ def eval_positions_list(P, Q, users, test_items, cand_off, cand_items):
     off = torch.as_tensor(cand_off).to(device=dev, dtype=torch.int64).contiguous()
     c = _idx(cand_items, "cand_items", dev) if len(cand_items) else torch.zeros(1, dtype=torch.int32, device=dev)
     _check_range(u, P.shape[0], "user")
-    _check_range(torch.cat([t, c]), Q.shape[0], "item")
+    _check_range(t, Q.shape[0], "item")
+    _check_range(c, Q.shape[0], "item")
     pos = torch.empty(u.numel(), dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
         call("acf_eval_positions_list", P.data_ptr(), Q.data_ptr(), P.shape[0], Q.shape[0], P.shape[1],
@@ -693,6 +738,7 @@ def sample_epoch(pos_user, pos_item, batch_size: int, num_items: int, list_off, 
 
 def dns_select(P, Q, user, cand, dns: int):
     """utils.py:121-133: argmax-score negative among dns candidates per triplet."""
+    settle_tables()
     dev = P.device
     _require(P, "embedding_P", torch.float32, None, 2)
     _require(Q, "embedding_Q", torch.float32, dev, 2)

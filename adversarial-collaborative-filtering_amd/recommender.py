@@ -14,6 +14,7 @@ from types import SimpleNamespace
 
 import numpy as np
 
+from . import ops
 from .model import MF
 from .sampler import EpochTriplets
 
@@ -83,6 +84,7 @@ class APR(Recommender):
 
     def save(self, path):
         self._ensure()
+        ops.settle_tables()
         np.savez(path if path.endswith(".npz") else path + ".npz",
                  embedding_P=self.model.embedding_P.cpu().numpy(),
                  embedding_Q=self.model.embedding_Q.cpu().numpy())

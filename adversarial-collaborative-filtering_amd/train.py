@@ -155,6 +155,7 @@ def ckpt_dirs(args, time_stamp):
 
 def save_checkpoint(model, directory, step):
     os.makedirs(directory, exist_ok=True)
+    ops.settle_tables()
     name = "weights-%d" % step
     np.savez(os.path.join(directory, name + ".npz"),
              embedding_P=model.embedding_P.cpu().numpy(), embedding_Q=model.embedding_Q.cpu().numpy())

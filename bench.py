@@ -388,6 +388,7 @@ def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
             "route_ms_rank0": round(1e3 * (sh.stats["route_s"] - st0["route_s"]), 3),
             "launch": "hipGraph" if sh.stats["graph_replays"] > st0["graph_replays"] else "eager",
             "step_errors": sh.step_errors()}
+        sh.close()
         del sh, u, i, j
         torch.cuda.empty_cache()
 
@@ -426,6 +427,7 @@ def sharded_lines(acf, ops, dev, dist, world, rank, big, steps):
                            "parallelism": f"user/item row shards x{world}, E1 by {exchange}, all_to_all x3"},
                 "launch": "hipGraph" if sh.stats["graph_replays"] > r0 else "eager",
                 "step_errors": sh.step_errors()}
+            sh.close()
             del sh
             torch.cuda.empty_cache()
     finally:

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define ACF_APR_ABI_VERSION 1
+#define ACF_APR_ABI_VERSION 2
 
 enum {
   ACF_OK = 0,
@@ -218,7 +218,9 @@ int acf_apr_set_stream(acf_apr_ctx* ctx, int32_t on);
  * two-kernel schedule (exact: same result as acf_apr_set_stream 0).
  * failsafe = 0 (and timed or graph-captured calls): a give-up is reported by
  * acf_apr_step_errors (bit 0, sticky until read) and that call's rows are not
- * applied; later calls are applied normally.
+ * applied; later calls are applied normally.  Such an unverified call settles
+ * the group's queue before it launches (except inside a capture), so it never
+ * runs behind the gate of an earlier failed verified call.
  * acf_apr_set_spin_limit: version polls before a give-up (default 65,536; 0
  * gives up at the first unready poll -- tests force the replay with it).
  * acf_apr_stream_recoveries: streamed calls replayed so far. */
@@ -228,6 +230,10 @@ int acf_apr_stream_recoveries(acf_apr_ctx* ctx, int64_t* out);
 /* Settle every queued verified streamed call of the context's group (blocks
  * until they have all reported; replays failed ones, see above). */
 int acf_apr_resolve(acf_apr_ctx* ctx);
+/* acf_apr_resolve for every group of the process with a queued call: what a
+ * reader of the tables outside the group calls first (evaluation, forward,
+ * checkpoints; the Python layer does so in ops.settle_tables). */
+int acf_apr_resolve_all(void);
 /* ctx joins peer's verification group: contexts that train the same tables on
  * one stream (a PlanPipeline's contexts) must share one, so that a failed call
  * of either gates the later calls of both.  Settles both groups first. */

@@ -313,6 +313,30 @@ def test_eval_exclusions_unsorted_and_out_of_range(ops, oracle, dev):
         ops.eval_positions_all(*args, kernel="gemm")
 
 
+def test_eval_exclusions_duplicated_entries(ops, oracle, dev):
+    """A list that repeats an item (and the test item) excludes it once, as the
+    reference's set(trainList[u]) does (utils.py:188-195): the MFMA and VALU
+    sweeps give the positions of the duplicate-free lists."""
+    rng = np.random.default_rng(22)
+    U1, I1, d, num_cand = 200, 600, 64, 600
+    P = rng.standard_normal((U1, d)).astype(np.float32)
+    Q = rng.standard_normal((I1, d)).astype(np.float32)
+    users = rng.permutation(U1)[:150].astype(np.int32)
+    tests = rng.integers(0, num_cand, len(users)).astype(np.int32)
+    lists = [np.unique(np.append(rng.integers(0, num_cand, 30), t)).astype(np.int32) for t in tests]
+    off = np.zeros(len(users) + 1, np.int64)
+    np.cumsum([len(x) for x in lists], out=off[1:])
+    want = oracle.eval_positions_all(P, Q, users, tests, num_cand, off, np.concatenate(lists))
+    dup = [rng.permutation(np.concatenate([x, x[: 1 + k % len(x)], [t, t]])).astype(np.int32)
+           for k, (x, t) in enumerate(zip(lists, tests))]
+    off2 = np.zeros(len(users) + 1, np.int64)
+    np.cumsum([len(x) for x in dup], out=off2[1:])
+    args = (torch.tensor(P, device=dev), torch.tensor(Q, device=dev), torch.tensor(users, device=dev),
+            torch.tensor(tests, device=dev), num_cand, off2, np.concatenate(dup))
+    for kernel in ("auto", "mfma", "valu"):
+        np.testing.assert_array_equal(ops.eval_positions_all(*args, kernel=kernel).cpu().numpy(), want)
+
+
 def test_sampler_properties(ops, acf, dev):
     ds = acf.synthetic_dataset(500, 300, 20000, seed=3)
     s = acf.DeviceSampler(ds, 128, dev, seed=1)

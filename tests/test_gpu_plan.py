@@ -227,3 +227,43 @@ def test_concurrent_plan_beside_stream_no_step_errors(ops, acf, dev):
     torch.cuda.synchronize()
     for x, y in zip(*runs):
         assert torch.equal(x, y)
+
+
+def test_pipeline_repeat_memo_matches_validated_path(ops, acf, dev):
+    """PlanPipeline._repeat (the validated single-chunk call re-issued straight to
+    the C-ABI) gives the bits of the validated path, also with n_batches=None,
+    and is invalidated when the hyper-parameters, a table or an index tensor
+    change."""
+    B, d, nb = 512, 64, 6
+    U1, I1, u, i, j = _stream("ml1m", acf, dev, B, 3 * nb, seed=4)
+    rng = np.random.default_rng(5)
+    P = (rng.standard_normal((U1, d)) * 0.01).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.01).astype(np.float32)
+    ut, it, jt = (torch.tensor(x[: nb * B], device=dev) for x in (u, i, j))
+    u2, i2, j2 = (torch.tensor(x[nb * B: 2 * nb * B], device=dev) for x in (u, i, j))
+
+    def run(calls, n_arg):
+        tabs = _tables(P, Q, dev)
+        pipe = ops.PlanPipeline(U1, I1, d, B, nb, dev)
+        hp = ops.StepHParams(adver=1)
+        hits = 0
+        for k, what in enumerate(calls):
+            if what == "hp":
+                hp = ops.StepHParams(adver=1, eps=0.25)
+            trip = (u2, i2, j2) if what == "idx" else (ut, it, jt)
+            if what == "table":
+                tabs[0] = tabs[0].clone()
+            before = pipe._memo
+            pipe.run(tabs, hp, *trip, 0, n_arg, check=(what == "check"))
+            hits += before is not None and pipe._memo is before
+        assert pipe.step_errors() == 0
+        torch.cuda.synchronize()
+        return tabs, hits
+
+    calls = ["first", "same", "same", "hp", "same", "table", "same", "idx", "same"]
+    for n_arg in (nb, None):
+        memo, hits = run(calls, n_arg)
+        assert hits == 4, (n_arg, hits)  # each "same" call that repeats the call before it
+        ref, _ = run(["check" if c == "same" else c for c in calls], n_arg)
+        for x, y, n in zip(memo, ref, ("P", "Q", "accP", "accQ")):
+            assert torch.equal(x, y), (n_arg, n)
