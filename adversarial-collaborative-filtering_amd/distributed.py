@@ -250,7 +250,10 @@ class ShardedAPR:
         gq = item_exchange == "allgather" and (G > 1 or self._force)
         self._qpad = torch.zeros(self._qcap, dim, **f) if gq else None
         self._qall = torch.empty(G * self._qcap, dim, **f) if gq else None
-        self.local = local(self) if local is not None else HipLocal(self)
+        # the local passes see this object through a weak proxy: no reference cycle,
+        # so dropping the last reference runs the finalizer at once (see close)
+        me = weakref.proxy(self)
+        self.local = local(me) if local is not None else HipLocal(me)
         can_graph = (self.device.type == "cuda" and not self._stage and getattr(self.local, "graphable", False))
         if graph is None:  # ACF_SHARD_GRAPH=0: eager steps (A/B of the captured graphs)
             graph = os.environ.get("ACF_SHARD_GRAPH", "1") != "0"
