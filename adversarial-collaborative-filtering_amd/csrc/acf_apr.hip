@@ -199,8 +199,6 @@ __global__ void k_compact(KT key, const int32_t* __restrict__ inc, const int32_t
 //  - the two-kernel step reads dt = 1 rows from W scratch of batch t-1 (the
 //    flush to the table happens inside batch t's first kernel) and every other
 //    row from the table (pend1);
-//  - the overlapped step (k_ovl) also reads dt = 2 rows from W(t-2), while
-//    W(t-1) is being flushed beside it;
 //  - the streamed step (k_stream) reads any dt from that batch's row version.
 // Plans with one lane-group per slot (packed) encode dt = 1 only (binary
 // search of batch t-1); one-wave-per-slot plans encode every dt (k_prev_next).
@@ -1266,14 +1264,7 @@ struct StepArgs {
   const int32_t* slot_cnt;    // [nb]
   const int32_t* flush_cnt;   // [nb]
   int32_t slot_waves;  // waves [0, slot_waves) are slot waves, the rest fused-triplet waves
-  // overlapped step (k_ovl): adv(t) publishes flags[t][slot] once W(t)[slot] is
-  // stored; clean(t+1) in the same launch waits for the rows it reads from W(t)
-  int32_t* flags;       // [nb][S]
-  int32_t* step_err;    // bit 0: a wait gave up (ACF_SPIN_LIMIT)
-  float* wnew_prev2;    // [S, d] updated rows of batch t-2 (clean half of k_ovl)
-  int32_t prev2_valid;  // 1: batch t-2 ran in this call (its W scratch is live)
-  int32_t ovl_flush;    // adv half writes back W(t-1) (the launch has no clean half)
-  int32_t ovl_delay;    // clean half: s_sleep(8) rounds before starting (ACF_OVL_DELAY, tuning)
+  int32_t* step_err;    // bit 0: a wait gave up (acf_apr_set_spin_limit), sticky until read
   // streamed step (k_stream): one launch runs batches [first, t_end); every row a
   // batch updates becomes a VERSION at [batch][slot] (weights ver_w, Adagrad slot
   // ver_a) and every delta too (ver_d), as tagged granules (tag = *epoch)
@@ -1387,83 +1378,7 @@ __device__ __forceinline__ const float* row_src(const StepArgs& a, const float* 
                                             : table + (int64_t)row * a.d;
 }
 
-// --- overlapped step: sources, waits and publication ------------------------
-// The clean half of k_ovl (batch t) runs beside adv(t-1): a row batch t-1
-// updates comes from W(t-1) once adv(t-1) has published it, a row last updated
-// by batch t-2 from W(t-2) (its flush to the table is running in this launch).
-#define ACF_SPIN_LIMIT (1 << 16)
-
-__device__ __forceinline__ const float* row_src_ovl(const StepArgs& a, const float* table, int32_t row,
-                                                    int32_t src) {
-  if (src < 0 && a.prev_valid) {
-    const int32_t dt = src_dt(src, a.kb);
-    if (dt == 1) return a.wnew_prev + (int64_t)src_slot(src, a.kb) * a.d;
-    if (dt == 2 && a.prev2_valid) return a.wnew_prev2 + (int64_t)src_slot(src, a.kb) * a.d;
-  }
-  return table + (int64_t)row * a.d;
-}
-
-__device__ __forceinline__ bool src_waits(const StepArgs& a, int32_t src) {
-  return a.prev_valid && pend1(src, a.kb);
-}
-
-
-// Wave-wide: wait until every listed source row (0 = none) that batch t-1
-// updates is published.  Bounded: after ACF_SPIN_LIMIT polls the wave records
-// bit 0 in step_err and goes on (the call then reports an error).
-// No L2 invalidate is needed after the flag: the flag load is device-coherent
-// (sc1), the rows were stored write-through before it (publish), and no L2 can
-// hold a stale copy of them — every launch starts with invalidated L2s and a W(t)
-// row is read in this launch only after its flag.  The compiler barrier keeps
-// the row loads behind the wait.
-// Lane x of each lane-group polls the group's x-th source (x < 5, LPR >= 8;
-// narrower groups poll their sources in turn), so one poll is one round trip.
-template <int LPR>
-__device__ __forceinline__ void wait_srcs(const StepArgs& a, int32_t s0, int32_t s1, int32_t s2, int32_t s3,
-                                          int32_t s4) {
-  const int l = (int)(threadIdx.x & (LPR - 1));
-  const int32_t* fl = a.flags + (int64_t)(a.t - 1) * a.S;
-  const int32_t src[5] = {s0, s1, s2, s3, s4};
-  constexpr int PER = LPR >= 8 ? 1 : (5 + LPR - 1) / LPR;  // sources per lane
-  int32_t mine[PER];
-  bool need = false;
-#pragma unroll
-  for (int p = 0; p < PER; ++p) {
-    const int x = l + p * LPR;
-    int32_t v = 0;
-#pragma unroll
-    for (int y = 0; y < 5; ++y) v = x == y ? src[y] : v;
-    mine[p] = src_waits(a, v) ? src_slot(v, a.kb) : -1;  // flag index, or -1
-    need = need || mine[p] >= 0;
-  }
-  if (!__any(need)) return;
-  for (int it = 0;; ++it) {
-    bool ok = true;
-#pragma unroll
-    for (int p = 0; p < PER; ++p)
-      if (mine[p] >= 0)
-        ok = ok && __hip_atomic_load(fl + mine[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    if (__all(ok)) break;
-    if (it >= ACF_SPIN_LIMIT) {
-      atomicOr(a.step_err, 1);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(4);
-  }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-// after this wave stored W(t)[k] (and k2, k3) with store_row_wt: wait for the
-// stores to complete at device scope, then set the flags
-__device__ __forceinline__ void publish(const StepArgs& a, bool leader, int k, int k2 = -1, int k3 = -1) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (leader) {
-    int32_t* f = a.flags + (int64_t)a.t * a.S;
-    __hip_atomic_store(f + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k2 >= 0) __hip_atomic_store(f + k2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k3 >= 0) __hip_atomic_store(f + k3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
+#define ACF_SPIN_LIMIT (1 << 16)  // default version polls before a k_stream wait gives up
 
 template <int LPR, int NV>
 __device__ __forceinline__ RowV<NV> load_at(const float* __restrict__ p, int d, int l) {
@@ -1767,10 +1682,7 @@ __device__ __forceinline__ RowV<NV> make_delta(const StepArgs& a, const RowV<NV>
 // the row goes clean -> delta -> adversarial -> Adagrad; otherwise (BPR graph,
 // inside k_clean<FUSE_APPLY>) rows are read through their batch-start source and
 // the clean gradient is applied.
-// OVL (inside k_ovl): rows are read through their batch-start source (W(t-1)
-// is being flushed beside it) and every row also goes to W(t), where clean(t+2)
-// finds a row batch t+1 does not touch; its flags are published.
-template <int LPR, int NV, bool ADV, bool OVL = false>
+template <int LPR, int NV, bool ADV>
 __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
   if (b >= a.B) return;
   const int64_t e = (int64_t)a.t * a.B + b;
@@ -1779,7 +1691,7 @@ __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
   const int d = a.d;
   const int32_t u = r.a.x, i = r.a.y, j = r.a.z, flags = r.c.y;
   RowV<NV> p, qi, qj;
-  if (ADV && !OVL) {
+  if (ADV) {
     p = load_row<LPR, NV>(a.P, u, d, l);
     qi = load_row<LPR, NV>(a.Q, i, d, l);
     qj = load_row<LPR, NV>(a.Q, j, d, l);
@@ -1819,19 +1731,9 @@ __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
   adagrad_row(a, Gu, p, cu, 1, wu);
   adagrad_row(a, Gi, qi, ci, 1, wi);
   adagrad_row(a, Gj, qj, cj, 1, wj);
-  if (OVL) {  // publish first: the flags wait only for the W rows
-    store_row_wt<LPR, NV>(a.wnew_cur, r.a.w, d, l, wu);
-    store_row_wt<LPR, NV>(a.wnew_cur, r.b.x, d, l, wi);
-    store_row_wt<LPR, NV>(a.wnew_cur, r.b.y, d, l, wj);
-    publish(a, l == 0, r.a.w, r.b.x, r.b.y);
-    if (flags & 2) store_row<LPR, NV>(a.P, u, d, l, wu);
-    if (flags & 4) store_row<LPR, NV>(a.Q, i, d, l, wi);
-    if (flags & 8) store_row<LPR, NV>(a.Q, j, d, l, wj);
-  }
   store_row<LPR, NV>(a.accP, u, d, l, cu);
   store_row<LPR, NV>(a.accQ, i, d, l, ci);
   store_row<LPR, NV>(a.accQ, j, d, l, cj);
-  if (OVL) return;
   // in place unless the row is pending from batch t-1 or read by batch t+1
   store_row<LPR, NV>((flags & 2) ? a.P : a.wnew_cur, (flags & 2) ? u : r.a.w, d, l, wu);
   store_row<LPR, NV>((flags & 4) ? a.Q : a.wnew_cur, (flags & 4) ? i : r.b.x, d, l, wi);
@@ -1843,20 +1745,16 @@ __device__ __forceinline__ void k_single(const StepArgs& a, int b, int l) {
 // over its occurrences, its delta (APR graph), or — BPR graph, FUSE_APPLY — the
 // Adagrad update straight away.  Slot k, team member m, lane l of the row-group,
 // the team leader's lane.
-// OVL: the clean half of k_ovl (one wave per slot, APR graph): sources via
-// row_src_ovl, waiting for rows adv(t-1) is still producing.
-template <int LPR, int NV, bool FUSE_APPLY, int TEAM, bool FLUSH = false, bool OVL = false>
+template <int LPR, int NV, bool FUSE_APPLY, int TEAM, bool FLUSH = false>
 __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int l, int leader, int wave,
                                            int tl = 0) {
-  static_assert(!OVL || (!FUSE_APPLY && TEAM * LPR == 64), "k_ovl: one wave per slot, APR");
-  // write-back of slot k of batch t-1 (OVL: of t-2, whose adv half runs beside
-  // us): its record is loaded next to our header
+  // write-back of slot k of batch t-1: its record is loaded next to our header
   RecV frec;
-  if (FLUSH) frec = flush_rec(a, OVL ? a.t - 2 : a.t - 1, k);
+  if (FLUSH) frec = flush_rec(a, a.t - 1, k);
   const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
   FlushOp fo;
-  if (FLUSH) fo = flush_load(a, frec, OVL ? a.wnew_prev2 : a.wnew_prev, k, tl, TEAM * LPR);
+  if (FLUSH) fo = flush_load(a, frec, a.wnew_prev, k, tl, TEAM * LPR);
   STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
     if (FLUSH) flush_store(fo);
@@ -1864,8 +1762,7 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
   }
   const int d = a.d;
   const float* own_tab = h.is_item ? a.Q : a.P;
-  RowV<NV> own;
-  if (!OVL) own = load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l);
+  const RowV<NV> own = load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l);
   RowV<NV> acc;
   if (FUSE_APPLY && m == 0)
     acc = load_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l);
@@ -1879,20 +1776,6 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
     RecV r0, r1;
     if (a0) r0 = occ_rec<TEAM>(a, sr, i0, m);
     if (a1) r1 = occ_rec<TEAM>(a, sr, i1, m);
-    if (OVL) {  // the pass is wave-uniform (one team per wave)
-      wait_srcs<LPR>(a, base == 0 ? h.own_src : 0, a0 ? r0.pa_src() : 0, a0 ? r0.pb_src() : 0,
-                a1 ? r1.pa_src() : 0, a1 ? r1.pb_src() : 0);
-      if (base == 0) STAMP(a.diag_launch, wave, 5);
-      if (base == 0) own = load_at<LPR, NV>(row_src_ovl(a, own_tab, h.own_row, h.own_src), d, l);
-      if (a0) {
-        ra0 = load_at<LPR, NV>(row_src_ovl(a, h.is_item ? a.P : a.Q, r0.pa_row(), r0.pa_src()), d, l);
-        rb0 = load_at<LPR, NV>(row_src_ovl(a, a.Q, r0.pb_row(), r0.pb_src()), d, l);
-      }
-      if (a1) {
-        ra1 = load_at<LPR, NV>(row_src_ovl(a, h.is_item ? a.P : a.Q, r1.pa_row(), r1.pa_src()), d, l);
-        rb1 = load_at<LPR, NV>(row_src_ovl(a, a.Q, r1.pb_row(), r1.pb_src()), d, l);
-      }
-    } else {
     // user slot: ra = Q[i], rb = Q[j];  item slot: ra = P[u], rb = Q[other]
     if (a0) {
       ra0 = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r0.pa_row(), r0.pa_src()), d, l);
@@ -1901,7 +1784,6 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
     if (a1) {
       ra1 = load_at<LPR, NV>(row_src(a, h.is_item ? a.P : a.Q, r1.pa_row(), r1.pa_src()), d, l);
       rb1 = load_at<LPR, NV>(row_src(a, a.Q, r1.pb_row(), r1.pb_src()), d, l);
-    }
     }
     occ_term<LPR, NV>(a, h.is_item, own, r0, ra0, rb0, a0, l, a.loss_clean, G);
     if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, own, r1, ra1, rb1, a1, l, a.loss_clean, G);
@@ -1931,20 +1813,8 @@ __device__ __forceinline__ void clean_slot(const StepArgs& a, int k, int m, int 
 // Phase 2 = adversarial half of sess.run(optimizer) (APR.py:130-141,156-165)
 // and SparseApplyAdagrad: loss on p+dP[u], q+dQ[i]; G = G_clean + reg_adv*G_adv;
 // Adagrad into wnew_cur.  The tables are current (flushed by phase 1).
-// OVL (adv half of k_ovl): batch t-1's rows were not flushed by a phase 1, so
-// this wave writes back slot k of W(t-1) (its loads overlap the slot's own) and
-// reads rows through their batch-start source; W(t)[k] is then published.
-template <int LPR, int NV, int TEAM, bool OVL = false>
-__device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l, int leader, int wave,
-                                         int tl = 0) {
-  constexpr bool OFL = OVL && TEAM * LPR >= 64;  // write-back overlapped with the loads (d <= 256)
-  RecV frec;
-  FlushOp fo;
-  fo.dst = nullptr;
-  if (OVL && a.prev_valid && a.ovl_flush) {
-    if (OFL && a.d <= 4 * TEAM * LPR) frec = flush_rec(a, a.t - 1, k);
-    else flush_slot(a, a.t - 1, a.wnew_prev, k, tl, TEAM * LPR);
-  }
+template <int LPR, int NV, int TEAM>
+__device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l, int leader, int wave) {
   // read (not copy) batch t+1's record of this slot: phase 1 of the next batch
   // then finds it in the Infinity Cache instead of HBM
   int4 nxt = make_int4(0, 0, 0, 0), nxt1 = nxt;
@@ -1955,18 +1825,14 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
   }
   const SlotRec sr = slot_header<LPR, TEAM>(a, k, m, leader);
   const SlotHdr& h = sr.h;
-  if (OFL && a.prev_valid && a.ovl_flush && a.d <= 4 * TEAM * LPR)
-    fo = flush_load(a, frec, a.wnew_prev, k, tl, TEAM * LPR);
   STAMP(a.diag_launch, wave, 1);
   if (h.count == 0) {
-    if (OFL) flush_store(fo);
     if (nxt.x == -0x7fffffff && nxt1.y == 0x7fffffff) a.loss_adv[0] = 0.f;
     return;
   }
   const int d = a.d;
   const float* own_tab = h.is_item ? a.Q : a.P;
-  const RowV<NV> own = OVL ? load_at<LPR, NV>(row_src(a, own_tab, h.own_row, h.own_src), d, l)
-                           : load_row<LPR, NV>(own_tab, h.own_row, d, l);
+  const RowV<NV> own = load_row<LPR, NV>(own_tab, h.own_row, d, l);
   const RowV<NV> ownp = add_row(own, load_row<LPR, NV>(a.delta, k, d, l));
   RowV<NV> acc, G0;
   if (m == 0) {
@@ -1983,41 +1849,26 @@ __device__ __forceinline__ void adv_slot(const StepArgs& a, int k, int m, int l,
     if (a1) r1 = occ_rec<TEAM>(a, sr, i1, m);
     const float* ptab = h.is_item ? a.P : a.Q;
     if (a0) {
-      ra0 = add_row(OVL ? load_at<LPR, NV>(row_src(a, ptab, r0.pa_row(), r0.pa_src()), d, l)
-                        : load_row<LPR, NV>(ptab, r0.pa_row(), d, l),
-                    load_row<LPR, NV>(a.delta, r0.pa_slot(), d, l));
-      rb0 = add_row(OVL ? load_at<LPR, NV>(row_src(a, a.Q, r0.pb_row(), r0.pb_src()), d, l)
-                        : load_row<LPR, NV>(a.Q, r0.pb_row(), d, l),
-                    load_row<LPR, NV>(a.delta, r0.pb_slot(), d, l));
+      ra0 = add_row(load_row<LPR, NV>(ptab, r0.pa_row(), d, l), load_row<LPR, NV>(a.delta, r0.pa_slot(), d, l));
+      rb0 = add_row(load_row<LPR, NV>(a.Q, r0.pb_row(), d, l), load_row<LPR, NV>(a.delta, r0.pb_slot(), d, l));
     }
     if (a1) {
-      ra1 = add_row(OVL ? load_at<LPR, NV>(row_src(a, ptab, r1.pa_row(), r1.pa_src()), d, l)
-                        : load_row<LPR, NV>(ptab, r1.pa_row(), d, l),
-                    load_row<LPR, NV>(a.delta, r1.pa_slot(), d, l));
-      rb1 = add_row(OVL ? load_at<LPR, NV>(row_src(a, a.Q, r1.pb_row(), r1.pb_src()), d, l)
-                        : load_row<LPR, NV>(a.Q, r1.pb_row(), d, l),
-                    load_row<LPR, NV>(a.delta, r1.pb_slot(), d, l));
+      ra1 = add_row(load_row<LPR, NV>(ptab, r1.pa_row(), d, l), load_row<LPR, NV>(a.delta, r1.pa_slot(), d, l));
+      rb1 = add_row(load_row<LPR, NV>(a.Q, r1.pb_row(), d, l), load_row<LPR, NV>(a.delta, r1.pb_slot(), d, l));
     }
     occ_term<LPR, NV>(a, h.is_item, ownp, r0, ra0, rb0, a0, l, a.loss_adv, G);
     if (__any(a1)) occ_term<LPR, NV>(a, h.is_item, ownp, r1, ra1, rb1, a1, l, a.loss_adv, G);
   }
   STAMP(a.diag_launch, wave, 2);
   team_allreduce<LPR, TEAM, NV>(G);
-  if (OFL) flush_store(fo);
   if (m == 0 && a.shard && h.is_item) {  // partial adversarial item sum for the owner
     store_row<LPR, NV>(a.g0, k, d, l, G);
   } else if (m == 0) {
     axpy_row(G0, a.reg_adv, G);
     RowV<NV> wout;
     adagrad_row(a, G0, own, acc, h.count, wout);
-    if (OVL) {  // publish first: the flag waits only for the W row
-      store_row_wt<LPR, NV>(a.wnew_cur, k, d, l, wout);
-      publish(a, l == 0, k);
-      store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
-    } else {
-      store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
-      store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
-    }
+    store_row<LPR, NV>(h.is_item ? a.accQ : a.accP, h.own_row, d, l, acc);
+    store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
   }
   if (nxt.x == -0x7fffffff && nxt1.y == 0x7fffffff) a.loss_adv[0] = 0.f;  // keeps the reads alive; never true
 }
@@ -2056,40 +1907,6 @@ __global__ void __launch_bounds__(256) k_adv(StepArgs a) {
   STAMP(a.diag_launch, q.wave, 0);
   adv_slot<LPR, NV, TEAM>(a, q.k, q.m, q.l, q.leader, q.wave);
   STAMP(a.diag_launch, q.wave, 4);
-}
-
-// Overlapped APR step (small batches, one wave per slot): adv(t) of `aa` on
-// waves [0, adv_waves) — slot waves, then fused-triplet waves — and clean(t+1)
-// of `ac` on the waves after them.  A clean wave only waits for flags of adv
-// waves; those come first in dispatch order and never wait, so the launch
-// always drains.  Saves one kernel boundary and the slowest waves' tail per
-// batch against k_clean + k_adv, with identical arithmetic.
-template <int LPR, int NV, int TEAM>
-__global__ void __launch_bounds__(256) k_ovl(StepArgs aa, StepArgs ac, int32_t adv_waves) {
-  static_assert(TEAM * LPR == 64, "k_ovl: one wave per slot");
-  const Geo<LPR, TEAM> q;
-  STAMP(aa.diag_launch, q.wave, 0);
-  if (q.wave < adv_waves) {
-    if (q.wave >= aa.slot_waves) {
-      if (aa.use_single)
-        k_single<LPR, NV, true, true>(aa, (q.wave - aa.slot_waves) * (64 / LPR) + (int)(threadIdx.x & 63) / LPR,
-                                      q.l);
-    } else {
-      adv_slot<LPR, NV, TEAM, true>(aa, q.k, q.m, q.l, q.leader, q.wave, q.tl);
-    }
-  } else {
-    const int w = q.wave - adv_waves;  // slot of batch t+1
-    for (int x = 0; x < ac.ovl_delay; ++x) __builtin_amdgcn_s_sleep(8);
-    // the clean half writes back W(t-1) (= W(t+1-2)): nothing in this launch
-    // reads those rows from the tables
-    if (ac.prev2_valid && ac.d <= 4 * TEAM * LPR) {
-      clean_slot<LPR, NV, false, TEAM, true, true>(ac, w, q.m, q.l, q.leader, q.wave, q.tl);
-    } else {
-      if (ac.prev2_valid) flush_slot(ac, ac.t - 2, ac.wnew_prev2, w, q.tl, TEAM * LPR);
-      clean_slot<LPR, NV, false, TEAM, false, true>(ac, w, q.m, q.l, q.leader, q.wave, q.tl);
-    }
-  }
-  STAMP(aa.diag_launch, q.wave, 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -3761,12 +3578,9 @@ struct acf_apr_ctx {
   int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
-  int32_t overlap = 1;  // k_ovl for APR runs of one-wave-per-slot plans (ACF_STEP_OVERLAP=0 disables)
   int32_t plan_kind2 = 0;  // the plan encodes sources at every distance (k_prev_next)
   int32_t plan_kb = 1;     // slot bits of the plan's src encoding
   int32_t* nextt = nullptr;  // [maxNB][S] next batch touching each slot's row (k_prev_next)
-  int32_t ovl_delay = 0;   // ACF_OVL_DELAY (tuning only)
-  int32_t* flags = nullptr;  // [maxNB][S] k_ovl publication flags
   // streamed step (k_stream): row versions of every batch of a launch
   int32_t stream = 1;        // ACF_STREAM=0 disables
   int32_t stream_depth = 2;  // ACF_STREAM_DEPTH: max waves per position (batches in flight)
@@ -3778,10 +3592,7 @@ struct acf_apr_ctx {
   int64_t recoveries = 0;    // streamed calls replayed on the two-kernel schedule
   uint32_t seq = 0;          // streamed launches so far (StepArgs.seq)
   uint32_t last_tail_seq = 0;  // seq of the last launch with a tail (StepArgs.decide_prev)
-  int32_t tail_on = 1;         // ACF_TAIL=0: write-back by k_stream_flush always (A/B)
-  int32_t tail_flushers = 128; // ACF_TAIL_FLUSHERS: workgroups of the tail write-back
-  int32_t bplan_sort = 0;  // batch plan's sort: 0 default (512 x 3), 2 1,024 x 2 (ACF_BPLAN_SORT=1024, A/B)
-  unsigned long long* tail_diag = nullptr;  // ACF_TAIL_DIAG=1: tail stamps (acf_apr_diag_tail)
+  unsigned long long* tail_diag = nullptr;  // diagnostic builds, ACF_TAIL_DIAG=1: tail stamps (acf_apr_diag_tail)
   unsigned long long* decide = nullptr;  // [0] decide word, [16, 16 + 288) the tail's arrival counters
   uint32_t tail_launches = 0;            // launches with a tail so far (StepArgs.tail_par)
   FailGroup* grp = nullptr;  // contexts whose streamed calls are verified together (PlanPipeline)
@@ -3797,10 +3608,7 @@ struct acf_apr_ctx {
   // batch-local plan (k_bplan_sort / k_bplan_build)
   int32_t plan_mode = 0;     // 0 auto (batch-local plan where it applies), 1 always the sort plan
   // hash plan of triplet-centric steps (k_hplan_*); ACF_HASH_PLAN=0 keeps the sort plan (A/B)
-  int32_t hash_on = 1;
-  int32_t tri_comb_waves = 4096;  // slot waves of k_tri_combine (ACF_TRI_COMB_WAVES)
   int32_t plan_kind = -1;    // acf_apr_plan_kind
-  int32_t hplan_part = 384;  // hash plan: occurrences per partition (ACF_HPLAN_PART=768, A/B)
   int32_t hplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   int2* hplan_occ = nullptr;   // [3 maxE] occurrence -> {slot or -1, CSR position}
   int32_t* hplan_pcnt = nullptr;  // [2][maxNB << pb][tiles] partition counts, their scan
@@ -3960,8 +3768,8 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
   A(&c->err, 4); A(&c->gen_dev, 4); A(&c->epoch, 4); A(&c->decide, 16 + 2 * 144);
-  A(&c->g0, 2 * S * d); A(&c->delta, 2 * S * d);  // by batch parity (k_ovl: clean(t+1) beside adv(t))
-  A(&c->flags, 3 * maxE);
+  A(&c->g0, 2 * S * d); A(&c->delta, 2 * S * d);  // by batch parity
+
   A(&c->nextt, 3 * maxE);
   A(&c->task_list, 4 * maxE); A(&c->task_cnt, maxNB);
   A(&c->wnew[0], S * d); A(&c->wnew[1], S * d);
@@ -4001,14 +3809,10 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
     acf_apr_destroy(c);
     return set_error(ACF_E_HIP, "hipMemset failed");
   }
-  if (const char* e = getenv("ACF_TAIL")) c->tail_on = atoi(e) != 0;
-  if (const char* e = getenv("ACF_TAIL_FLUSHERS")) c->tail_flushers = std::max(1, atoi(e));
-  if (const char* e = getenv("ACF_HASH_PLAN")) c->hash_on = atoi(e) != 0;
-  if (const char* e = getenv("ACF_HPLAN_PART")) c->hplan_part = atoi(e) == 768 ? 768 : 384;
-  if (const char* e = getenv("ACF_TRI_COMB_WAVES")) c->tri_comb_waves = std::max(4, atoi(e));
-  if (const char* e = getenv("ACF_BPLAN_SORT")) c->bplan_sort = atoi(e) == 1024 ? 2 : 0;
+#ifdef ACF_DIAG  // the tail's stamps (tools/tail_diag.py): diagnostic builds only
   if (const char* e = getenv("ACF_TAIL_DIAG"))
     if (atoi(e) && dalloc(c, &c->tail_diag, 8) == ACF_OK) (void)hipMemset(c->tail_diag, 0, 64);
+#endif
   c->grp = new_group();
   if (hipMalloc(&c->grp->gate, 16) != hipSuccess || hipMemset(c->grp->gate, 0, 16) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
@@ -4037,7 +3841,7 @@ static bool decided(const Pending& p, bool* failed) {
 
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                     int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds,
-                    int allow_overlap, int tri_phases);
+                    int allow_stream, int tri_phases);
 
 // Block until queued call p has reported its outcome: poll its word of the
 // host-mapped status ring, not the stream (a stream sync also waited
@@ -4185,7 +3989,7 @@ static bool hplan_ready(acf_apr_ctx* c) {
   if (c->hplan_ok >= 0) return c->hplan_ok == 1;
   c->hplan_ok = 0;
   if (c->maxB > ACF_HPLAN_MAXB) return false;
-  const int32_t pb = hplan_pbits(c->maxB, 384);  // room for either partition size
+  const int32_t pb = hplan_pbits(c->maxB, ACF_HPLAN_PART);
   if (pb + (int32_t)bits_for((uint64_t)c->maxNB) > 32) return false;
   const size_t n3 = (size_t)3 * c->maxE;
   const size_t ncnt = ((size_t)c->maxNB << pb) * (((size_t)3 * c->maxB + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE);
@@ -4227,7 +4031,7 @@ static bool hplan_ready(acf_apr_ctx* c) {
 static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg, int32_t B,
                      int32_t nb, int32_t gen, int32_t kb, int32_t check, hipStream_t s) {
   const int64_t E = (int64_t)B * nb;
-  const int32_t pb = hplan_pbits(B, c->hplan_part);
+  const int32_t pb = hplan_pbits(B, ACF_HPLAN_PART);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));  // the other counters: k_hplan_keys
   HPlanArgs p;
   p.user = user; p.ipos = ipos; p.ineg = ineg;
@@ -4239,12 +4043,12 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   p.pval = reinterpret_cast<unsigned long long*>(c->key_out);
   const int64_t ncnt = ((int64_t)nb << pb) * p.tpb;
   p.pcnt = c->hplan_pcnt;
-  p.poff = c->hplan_pcnt + ((size_t)c->maxNB << hplan_pbits(c->maxB, 384)) *
+  p.poff = c->hplan_pcnt + ((size_t)c->maxNB << hplan_pbits(c->maxB, ACF_HPLAN_PART)) *
                                (((size_t)3 * c->maxB + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE);
   p.occ = c->hplan_occ; p.csr = c->tsl;
   p.claims = c->hplan_claims;
   p.ptot = c->hplan_ptot;
-  p.pbase = c->hplan_ptot + ((size_t)c->maxNB << hplan_pbits(c->maxB, 384)) * ACF_HPLAN_TOT;
+  p.pbase = c->hplan_ptot + ((size_t)c->maxNB << hplan_pbits(c->maxB, ACF_HPLAN_PART)) * ACF_HPLAN_TOT;
   p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
   p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
   p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt; p.flush_cnt = c->flush_cnt;
@@ -4261,10 +4065,7 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
     HIP_TRY(rocprim::exclusive_scan(tmp, tb, p.pcnt, p.poff, 0, (size_t)ncnt, rocprim::plus<int32_t>(), s));
   }
   k_hplan_scatter<<<tiles, 256, 0, s>>>(p);
-  if (c->hplan_part == 384)
-    k_hplan_dedup<1024><<<(unsigned)(nb << pb), 256, 0, s>>>(p);
-  else
-    k_hplan_dedup<2048><<<(unsigned)(nb << pb), 256, 0, s>>>(p);
+  k_hplan_dedup<ACF_HPLAN_BUCKETS><<<(unsigned)(nb << pb), 256, 0, s>>>(p);
   k_hplan_bases<<<(unsigned)nb, 1024, 0, s>>>(p);
   k_hplan_emit<<<(unsigned)(nb << pb), 256, 0, s>>>(p);
   k_hplan_trip<<<(unsigned)((E + 255) / 256), 256, 0, s>>>(p);
@@ -4321,10 +4122,7 @@ static int batch_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, 
   // build: ~24 us for a 20-batch plan against ~32 us for 6 per thread / 256-thread
   // builds (per-thread loops serialise the build's dependent loads)
   if (B <= 512) {
-    if (c->bplan_sort == 2)  // ACF_BPLAN_SORT=1024 (A/B): 1,024 threads x 2 occurrences
-      k_bplan_sort<1024, 2><<<nb, 1024, 0, s>>>(p);
-    else
-      k_bplan_sort<512, 3><<<nb, 512, 0, s>>>(p);
+    k_bplan_sort<512, 3><<<nb, 512, 0, s>>>(p);
     k_bplan_build<1024, 512><<<nb, 1024, 0, s>>>(p);
   } else {
     k_bplan_sort<1024, 3><<<nb, 1024, 0, s>>>(p);
@@ -4440,7 +4238,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   if (c->shard && nb == 1 && B <= 1024 && c->plan_mode == 0 &&
       bits_for((uint64_t)std::max(c->U1, c->I1)) <= 30)
     return shard_plan_small(c, user, ipos, ineg, B, gen, check, s);
-  if (is_packed(c, B) && !c->shard && c->fusion && c->plan_mode == 0 && c->hash_on && B <= ACF_HPLAN_MAXB &&
+  if (is_packed(c, B) && !c->shard && c->fusion && c->plan_mode == 0 && B <= ACF_HPLAN_MAXB &&
       hplan_ready(c))
     return hash_plan(c, user, ipos, ineg, B, nb, gen, (int32_t)bits_for((uint64_t)3 * B + 1), check, s);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
@@ -4472,7 +4270,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   }
   // where each unique row's value lives at batch start, then the records; one
   // lane-group per slot (large batches) reads only a slot's first record inline
-  // and never runs k_ovl, so only one-wave-per-slot plans encode t-2 sources
+  // (one-wave-per-slot plans encode every earlier batch, below)
   const int packed = is_packed(c, B);
   const int32_t kb = (int32_t)bits_for((uint64_t)3 * B + 1);
   // one-wave-per-slot plans encode every earlier batch (dt < nb must fit the src)
@@ -4585,11 +4383,6 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.g0 = c->g0 + par; a.delta = c->delta + par;
   a.wnew_cur = c->wnew[t & 1];
   a.wnew_prev = c->wnew[(t + 1) & 1];
-  a.wnew_prev2 = c->wnew[t & 1];  // W(t-2) shares W(t)'s buffer (read only by k_ovl's clean half)
-  a.prev2_valid = 0;
-  a.ovl_flush = 0;
-  a.ovl_delay = c->ovl_delay;
-  a.flags = c->flags;
   a.step_err = c->err + 1;
   a.loss_clean = c->loss_clean; a.loss_adv = c->loss_adv;
   a.gen_ptr = c->gen_dev;
@@ -4630,7 +4423,6 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
 // kernel kinds for timing: 0 = phase-1 (clean, or fused BPR), 1 = adversarial, 2 = flush
 struct Kernels {
   void *clean_apr = nullptr, *clean_bpr = nullptr, *adv = nullptr, *flush = nullptr;
-  void* ovl = nullptr;  // k_ovl (one wave per slot only)
   void* stream = nullptr;  // k_stream (one wave per slot, d <= 256)
   void* stream_flush = nullptr;  // its write-back, k_stream_flush<LPR>
   void *hot_clean = nullptr, *hot_bpr = nullptr, *hot_adv = nullptr;  // k_hot_combine (list kernels)
@@ -4643,6 +4435,8 @@ struct Kernels {
 };
 
 #define ACF_LIST_WAVES 4096  // slot waves of a list kernel
+#define ACF_TRI_COMB_WAVES 4096  // small-slot waves of k_tri_combine (512 / 1,024 slower: r04 A/B)
+#define ACF_TAIL_FLUSHERS 128    // workgroups of k_stream's tail write-back
 #define ACF_HOT_WAVES 2048   // piece waves of a list kernel (hot slots)
 #define ACF_HOT_BLOCKS 1024  // workgroups of k_hot_combine
 #define ACF_TRI_HOT_BLOCKS 512  // hot-slot combining workgroups of k_tri_combine
@@ -4696,7 +4490,6 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists, int tri) {
     k->slots_per_wave = OPW;
   } else {
     kernel_ptrs_team<LPR, NV, OPW>(k, fused);
-    k->ovl = reinterpret_cast<void*>(&k_ovl<LPR, NV, OPW>);
     if constexpr (NV == 1) {
       k->stream = reinterpret_cast<void*>(&k_stream<LPR, NV, OPW>);
       k->stream_flush = reinterpret_cast<void*>(&k_stream_flush<LPR>);
@@ -4730,22 +4523,6 @@ static int launch(void* fn, const StepArgs& a, int waves, hipStream_t s, hipEven
   return ACF_OK;
 }
 
-typedef void (*OvlKernel)(StepArgs, StepArgs, int32_t);
-
-static int launch_ovl(void* fn, const StepArgs& aa, const StepArgs& ac, int adv_waves, int clean_waves,
-                      hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
-  if (aa.slot_waves > adv_waves || clean_waves < 0 || (clean_waves > 0 && clean_waves != ac.S))
-    return set_error(ACF_E_STATE, "bad overlapped step geometry");
-  const int waves = adv_waves + clean_waves;
-  const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
-  if (e0)
-    hipExtLaunchKernelGGL(reinterpret_cast<OvlKernel>(fn), grid, block, 0, s, e0, e1, 0, aa, ac, adv_waves);
-  else
-    hipLaunchKernelGGL(reinterpret_cast<OvlKernel>(fn), grid, block, 0, s, aa, ac, adv_waves);
-  HIP_TRY(hipGetLastError());
-  return ACF_OK;
-}
-
 static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                       int32_t t) {
   ACF_CHECK(c && tb && hp, ACF_E_INVALID, "NULL ctx/tables/hparams");
@@ -4758,17 +4535,9 @@ static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hp
 // training_batch over planned batches [first, first+n): per batch phase 1
 // (+ flush of the previous batch) and, for APR, phase 2; a final flush.
 // events != nullptr: timing mode, 2 events per launch, kinds[] per launch.
-// The APR graph of a one-wave-per-slot plan runs overlapped: clean(first),
-// then k_ovl = adv(t) + clean(t+1) for t < last, k_ovl = adv(last) alone, flush.
-// Only for rows made of whole 128-B cache lines (d % 32 == 0): k_ovl's clean half reads
-// a published W(t) row with plain loads, and two rows sharing a line let the
-// first read cache the line before the second row was published (an untagged
-// stale read; seen at d = 16 in test_batch_plan_matches_sort_plan).  The
-// streamed step's version rows carry a tag in every granule, so a stale line
-// there only delays the reader.
-static bool use_overlap(const acf_apr_ctx* c, const Kernels& K, const acf_apr_hparams* hp) {
-  return c->overlap && hp->adver && K.ovl && !K.lists && K.slots_per_wave == 1 && c->plan_kind2 && c->d % 32 == 0;
-}
+// (r05: the overlapped schedule k_ovl -- adv(t) + clean(t+1) per launch -- is
+// gone; k_stream replaced it for d <= 256, the two-kernel schedule serves the
+// rest and the failsafe replay.)
 
 // Streamed step: version buffers (allocated at first use: 3 x maxNB x S x d
 // granules) and the resident-wave budget of k_stream.
@@ -4860,14 +4629,14 @@ static void prepare_stream(acf_apr_ctx* c, const acf_apr_hparams* hp) {
   if (c->stream && hp->adver && c->stream_ok < 0 && get_kernels(c, &K, c->fusion) == ACF_OK) (void)stream_ready(c, K);
 }
 
-// kinds: 0 phase 1 / fused BPR, 1 phase 2, 2 flush, 3 k_ovl with both halves, 4 k_stream,
+// kinds: 0 phase 1 / fused BPR, 1 phase 2, 2 flush, 3 (unused since r05: k_ovl), 4 k_stream,
 // 5 hot-slot combine (list kernels)
 // tri_phases (triplet-centric plans, one batch through the two-phase API): bit 0
 // the clean phase (delta_update), bit 1 the adversarial / BPR phase + the
 // call-counter bump (optimizer_step); train_planned runs both.
 static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
                     int32_t first, int32_t n, hipStream_t s, hipEvent_t* events, int* kinds,
-                    int allow_overlap = 2, int tri_phases = 3) {
+                    int allow_stream = 2, int tri_phases = 3) {
   ACF_CHECK(!(c->tri && !c->fusion), ACF_E_STATE,
             "fusion was switched off after a triplet-centric plan (rows are updated in place): plan again");
   Kernels K;
@@ -4886,7 +4655,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     ++li;
     return launch(fn, b, waves, s, e0, e1);
   };
-  if (allow_overlap >= 2 && use_stream(c, K, hp)) {
+  if (allow_stream >= 2 && use_stream(c, K, hp)) {
     const int P = stream_positions(c, K, fuse);  // upper bound of the tasks of a batch
     const int lists = fuse && c->task_lists;
     // with task lists the kernel sizes its positions from the plan: give it the
@@ -4899,7 +4668,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     const bool verify = c->failsafe && !events && cap == 0;
     // the write-back in k_stream's tail: the whole plan in one launch (the final-
     // slot list is the plan's), and a launch the host counts (not captured)
-    const bool tail = c->tail_on && c->final_ok && first == 0 && n == c->nb && cap == 0;
+    const bool tail = c->final_ok && first == 0 && n == c->nb && cap == 0;
     // an unverified launch behind queued verified calls would run gated if one of
     // them failed (dropped for good): settle the group first (not
     // possible while capturing: a captured call is documented as unverified)
@@ -4925,7 +4694,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     if (tail) {
       a.tail_par = (int32_t)(c->tail_launches++ & 1);
       a.tail = 1;
-      a.flushers = c->tail_flushers;
+      a.flushers = ACF_TAIL_FLUSHERS;
       a.decide_prev = (unsigned long long)c->last_tail_seq << 1;
       c->last_tail_seq = a.seq;
     }
@@ -4958,30 +4727,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     }
     return ACF_OK;
   }
-  if (allow_overlap && use_overlap(c, K, hp)) {
-    HIP_TRY(hipMemsetAsync(c->flags + (size_t)first * S, 0, (size_t)n * S * sizeof(int32_t), s));
-    auto args = [&](int32_t t, int pv) {
-      StepArgs a = make_args(c, tb, hp, t, pv);
-      a.use_single = fuse;
-      a.slot_waves = SW;
-      a.touch_next = 0;
-      a.prev2_valid = t - 2 >= first ? 1 : 0;
-      return a;
-    };
-    ACF_RET(L(K.clean_apr, args(first, 0), SW, 0));
-    for (int32_t t = first; t < first + n; ++t) {
-      const bool both = t + 1 < first + n;
-      StepArgs aa = args(t, t > first ? 1 : 0);
-      aa.ovl_flush = both ? 0 : 1;  // otherwise the clean half writes W(t-1) back
-      const StepArgs ac = both ? args(t + 1, 1) : aa;
-      hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
-      if (kinds) kinds[li] = both ? 3 : 1;
-      StepArgs xa = aa, xc = ac;
-      xa.diag_launch = xc.diag_launch = li;
-      ++li;
-      ACF_RET(launch_ovl(K.ovl, xa, xc, SW + TW, both ? SW : 0, s, e0, e1));
-    }
-  } else {
+  {
   // list kernels: piece waves of the hot slots after the slot waves, and a
   // combine launch (kind 5) after each pass
   const int HW = K.lists ? std::min(c->hot.piece_stride, ACF_HOT_WAVES) : 0;
@@ -4989,7 +4735,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
   if (K.tri) {  // triplet-centric list step (see k_tri_*)
     // k_tri_combine with its hot-slot combining workgroups after the piece waves
     // (whole workgroups: the two wave ranges rounded up to multiples of 4)
-    const int SWT = std::min(SW, c->tri_comb_waves);  // ACF_TRI_COMB_WAVES
+    const int SWT = std::min(SW, ACF_TRI_COMB_WAVES);
     const int SW4 = (SWT + 3) & ~3, HW4 = (HW + 3) & ~3, HBT = std::min(HB, ACF_TRI_HOT_BLOCKS);
     const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);  // one lane-group per triplet
     for (int32_t t = first; t < first + n; ++t) {
@@ -5125,7 +4871,7 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   key.hp = *hp;
   key.first = first; key.n = n; key.B = c->B; key.d = c->d; key.mapping = c->mapping;
   key.fusion = c->fusion;
-  key.ovl = c->overlap | (c->stream << 1);
+  key.ovl = c->stream;
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -5224,14 +4970,6 @@ extern "C" int acf_apr_set_stream(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   c->stream = on != 0;
-  return ACF_OK;
-}
-
-extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
-  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
-  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
-  ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);
-  c->overlap = on;
   return ACF_OK;
 }
 

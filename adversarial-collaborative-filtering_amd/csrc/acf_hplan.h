@@ -36,8 +36,10 @@
 // tile-aggregated, still 0.48 ms: slower than the sort plan.)
 // ---------------------------------------------------------------------------
 #define ACF_HPLAN_MAXB 65536  // the hot-rank bitmap: 2B bits of LDS per workgroup
-// partitions of ~384 occurrences (1,024 LDS buckets) by default, ~768 (2,048) with
-// ACF_HPLAN_PART=768 (A/B: 0.5% slower at configs[4]); a round takes at most 3/4 of the buckets
+// partitions of ~384 occurrences, 1,024 LDS buckets (~768 / 2,048 was 0.5% slower at
+// configs[4], r04 A/B); a round takes at most 3/4 of the buckets
+#define ACF_HPLAN_PART 384
+#define ACF_HPLAN_BUCKETS 1024
 
 struct HPlanArgs {
   const int32_t* user;

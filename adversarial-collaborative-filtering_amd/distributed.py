@@ -255,9 +255,7 @@ class ShardedAPR:
         me = weakref.proxy(self)
         self.local = local(me) if local is not None else HipLocal(me)
         can_graph = (self.device.type == "cuda" and not self._stage and getattr(self.local, "graphable", False))
-        if graph is None:  # ACF_SHARD_GRAPH=0: eager steps (A/B of the captured graphs)
-            graph = os.environ.get("ACF_SHARD_GRAPH", "1") != "0"
-        self.graph = bool(graph) and can_graph
+        self.graph = (True if graph is None else bool(graph)) and can_graph
         if capture_collectives is None:  # default on (r05); ACF_SHARD_RCCL_GRAPH=0 keeps the steps eager
             capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "1") != "0"
         multi = self.G > 1 or self._force  # exchanges that are collectives

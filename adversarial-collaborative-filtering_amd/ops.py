@@ -80,7 +80,7 @@ def _idx(t, name, device) -> torch.Tensor:
 
 
 class StepWaitError(RuntimeError):
-    """A streamed / overlapped step gave up waiting for a row (ACF_SPIN_LIMIT
+    """A streamed step gave up waiting for a row (ACF_SPIN_LIMIT
     polls): the tables of that call hold stale rows and must not be trusted."""
 
     def __init__(self, bits: int):
@@ -262,9 +262,8 @@ class APRContext:
         measured with start/stop events attached to each launch of the sequence
         train_planned runs (tables are trained exactly as by it).  Kinds: clean
         (phase 1, or the fused BPR step), adv (phase 2 + Adagrad), flush
-        (end-of-call write-back), ovl (overlapped adv(t) + clean(t+1), k_ovl),
-        stream (the whole range in one launch, k_stream), hot (the hot-slot
-        combine of large-batch plans, k_hot_combine)."""
+        (end-of-call write-back), stream (the whole range in one launch,
+        k_stream), hot (the hot-slot combine of large-batch plans)."""
         n = self.n_batches - first if n is None else n
         tb, h = self._tables(*tables), hp.to_c()
         ms = (ctypes.c_double * 6)()
@@ -272,17 +271,13 @@ class APRContext:
         with torch.cuda.device(self.device):
             call("acf_apr_time_kernels", self._ptr, ctypes.byref(tb), ctypes.byref(h), first, n, ms, cnt,
                  _stream_ptr(self.device))
-        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush", "ovl", "stream", "hot"))}
+        # (slot 3 was the overlapped step k_ovl, removed in r05)
+        return {k: (ms[x], cnt[x]) for x, k in enumerate(("clean", "adv", "flush", None, "stream", "hot")) if k}
 
     def set_stream(self, on: bool) -> None:
         """Streamed APR steps (default on; identical results either way): one
         launch runs the whole batch range through tagged row versions."""
         call("acf_apr_set_stream", self._ptr, int(bool(on)))
-
-    def set_step_overlap(self, on: bool) -> None:
-        """Overlapped APR steps (default on; identical results either way): the
-        adversarial pass of batch t and the clean pass of batch t+1 in one launch."""
-        call("acf_apr_set_step_overlap", self._ptr, int(bool(on)))
 
     def set_failsafe(self, on: bool) -> None:
         """Verified streamed steps (default on): a streamed call stays asynchronous
@@ -428,10 +423,6 @@ class PlanPipeline:
     def set_fusion(self, on: bool) -> None:
         for c in self.ctx:
             c.set_fusion(on)
-
-    def set_step_overlap(self, on: bool) -> None:
-        for c in self.ctx:
-            c.set_step_overlap(on)
 
     def set_stream(self, on: bool) -> None:
         for c in self.ctx:

@@ -65,10 +65,8 @@ def parse():
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="N > 1 code path on a one-GPU box: every rank on cuda:0, gloo (host-staged) "
                         "instead of RCCL; a rehearsal of the launch, not a measurement")
-    p.add_argument("--no-step-overlap", action="store_true",
-                   help="two kernels per APR step instead of the overlapped k_ovl (A/B)")
     p.add_argument("--no-stream", action="store_true",
-                   help="per-batch launches (k_ovl) instead of the streamed step k_stream (A/B)")
+                   help="per-batch launches (two kernels per step) instead of the streamed step k_stream (A/B)")
     p.add_argument("--mapping", default="auto", choices=["auto", "wave", "group"],
                    help="slot mapping of the step kernels (auto: by batch size)")
     return p.parse_args()
@@ -98,12 +96,11 @@ def bytes_per_launch(kind: int, d: int, B: int, st: dict, nb: int = 1) -> float:
     clean (phase 1): P[u], Q[i], Q[j] + indices per triplet that is not fused;
     flush: read the scratch row + write the table row, per unique row (upper bound:
       rows a fused triplet wrote in place are not flushed);
-    ovl (k_ovl = adv of batch t + clean of batch t+1 in one launch): adv + clean;
     stream (k_stream = the whole APR step of all nb batches of a call in one launch):
       the official figure per triplet x every triplet of the launch."""
     rows = st["unique_user_rows"] + st["unique_item_rows"]
     clean, adv = (3 * d * 4 + 12) * (B - st["fused_triplets"]), (6 * d * 4 + 12) * B
-    return {0: clean, 1: adv, 2: 2 * d * 4 * rows, 3: adv + clean, 4: adv * nb}[kind]
+    return {0: clean, 1: adv, 2: 2 * d * 4 * rows, 4: adv * nb}[kind]
 
 
 def unique_rw_bytes(d: int, B: int, st: dict) -> float:
@@ -151,8 +148,6 @@ def step_kernel_name(kind: str, d: int, B: int) -> str:
         return f"k_stream<{lpr}, {nv}, {team}>"
     if kind == "stream_flush":
         return "k_stream_flush"
-    if kind == "ovl":
-        return f"k_ovl<{lpr}, {nv}, {team}>"
     if kind == "adv":
         return f"k_adv<{lpr}, {nv}, {team}, true>"
     if kind == "clean":
@@ -182,15 +177,15 @@ def kernel_roofline(ops, ctx, tabs, hp, u, i, j, B, d, nb, st):
     s = slice(0, nb * B)
     ctx.plan(u[s], i[s], j[s], B, check=False)
     t = ctx.time_kernels(tabs, hp, 0, nb)
-    kinds = ["clean", "adv", "flush", "ovl", "stream", "hot"]
+    kinds = ["clean", "adv", "flush", "stream", "hot"]
     tot = {k: t[k][0] for k in kinds}
-    dom = max(kinds[:5], key=lambda k: tot[k])  # the step kernels (hot = their hot-slot combine)
-    kid = kinds.index(dom)
+    dom = max(kinds[:4], key=lambda k: tot[k])  # the step kernels (hot = their hot-slot combine)
+    kid = {"clean": 0, "adv": 1, "flush": 2, "stream": 4}[dom]  # bytes_per_launch's kinds
     avg_ms = t[dom][0] / max(t[dom][1], 1)
     alg_bytes = bytes_per_launch(kid, d, B, st, nb)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     rw = None
-    if kid in (1, 3):
+    if kid == 1:
         rw = unique_rw_bytes(d, B, st) / (avg_ms * 1e-3) / 1e9
     elif kid == 4:
         rw = unique_rw_bytes(d, B, st) * nb / (avg_ms * 1e-3) / 1e9
@@ -594,7 +589,6 @@ def main():
     # chunk c+1 is planned on a side stream beside chunk c's streamed step
     pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev, overlap=False if a.no_plan_overlap else None)
     pipe.set_slot_mapping(a.mapping)
-    pipe.set_step_overlap(not a.no_step_overlap)
     pipe.set_stream(not a.no_stream)
     hp = ops.StepHParams(lr=0.05, eps=0.5, reg=0.0, reg_adv=1.0, adver=1)
     graph = not a.eager
@@ -631,7 +625,6 @@ def main():
     # roofline of the dominant kernel (separate eager pass with per-launch events)
     tctx = ops.APRContext(U1, I1, d, B, a.time_batches, dev)
     tctx.set_slot_mapping(a.mapping)
-    tctx.set_step_overlap(not a.no_step_overlap)
     tctx.set_stream(not a.no_stream)
     st = batch_stats(u, i, j, B, a.time_batches, U1, I1)
     roof = kernel_roofline(ops, tctx, tabs, hp, u, i, j, B, d, a.time_batches, st)
@@ -660,7 +653,6 @@ def main():
         "tables_finite": finite,
         "step_errors": step_errors,
         "stream_recoveries": recoveries,
-        "step_overlap": not a.no_step_overlap,
         "step_stream": roof["kernel"].startswith("k_stream"),
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

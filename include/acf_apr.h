@@ -135,8 +135,8 @@ int acf_apr_train(acf_apr_ctx* ctx, const acf_apr_tables* tables, const acf_apr_
  * (eager, same stream, same kernels, tables updated) but brackets every kernel
  * with hipExtLaunchKernelGGL start/stop events.  Writes, per kernel kind
  * k = 0 (clean pass, or the fused BPR step), 1 (adversarial pass + Adagrad),
- * 2 (write-back: k_flush / k_stream_flush), 3 (overlapped step k_ovl),
- * 4 (streamed step k_stream), 5 (hot-slot combine of large-batch plans), the
+ * 2 (write-back: k_flush / k_stream_flush), 3 (unused since r05: the
+ * overlapped step k_ovl is gone), 4 (streamed step k_stream), 5 (hot-slot combine of large-batch plans), the
  * summed kernel time in ms to ms_out[k] and the launch count to
  * launches_out[k] (arrays of 6).  Synchronous.  Not part of the reference
  * surface. */
@@ -170,8 +170,7 @@ int acf_apr_set_fusion(acf_apr_ctx* ctx, int32_t on);
  * one workgroup per batch in two launches, for one-wavefront-per-slot plans of
  * batches up to 1,024 triplets on tables whose batch bitmaps fit 64 MB; the hash
  * plan for triplet-centric plans -- one lane-group per slot, fusion on, not
- * shard mode, batches up to 65,536 -- unless ACF_HASH_PLAN=0 was set when the
- * context was made; the device-wide sort plan otherwise), 1 = always the
+ * shard mode, batches up to 65,536; the device-wide sort plan otherwise), 1 = always the
  * device-wide sort plan.  Every planner gives the step identical bits (the hash
  * plan numbers slots and CSR ranges in another order, and keeps the occurrence
  * order inside each range).  Not part of the reference surface (A/B and the
@@ -182,15 +181,6 @@ int acf_apr_set_plan_mode(acf_apr_ctx* ctx, int32_t mode);
  * plan, 2 one-workgroup shard plan, 3 hash plan; -1 before any plan.  Not part
  * of the reference surface (tests and bench). */
 int acf_apr_plan_kind(const acf_apr_ctx* ctx);
-
-/* Overlapped APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
- * the setting is per context).  For plans with one
- * wavefront per slot, the adversarial pass of batch t and the clean pass of
- * batch t+1 run in one launch: a t+1 row waits (bounded spin on a per-row flag)
- * only for the rows batch t is still updating.  Arithmetic and order of every
- * sum are unchanged, so on and off give identical bits.  Not part of the
- * reference surface. */
-int acf_apr_set_step_overlap(acf_apr_ctx* ctx, int32_t on);
 
 /* Streamed APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
  * the setting is per context).  For plans with one wavefront

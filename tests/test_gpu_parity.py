@@ -596,12 +596,12 @@ def test_hot_slots_deterministic(ops, dev):
 
 
 @pytest.mark.parametrize("B,adver", [(32768, 1), (32768, 0), (4096, 1)])
-def test_hash_plan_matches_sort_plan(ops, dev, monkeypatch, B, adver):
+def test_hash_plan_matches_sort_plan(ops, dev, B, adver):
     """The hash plan (k_hplan_*: triplet-centric plans, the default) against the
     device-wide sort plan: identical bits through the triplet-centric step, whole
-    range and piecewise, on Zipf positives whose top items have thousands of
-    occurrences per batch (the workgroup bitmap ranks), tens (the wave ranks) and
-    up to 8 (the per-thread network); ACF_HASH_PLAN=0 falls back to the sort plan."""
+    range and piecewise (both planners), on Zipf positives whose top items have
+    thousands of occurrences per batch (the workgroup bitmap ranks), tens (the
+    wave ranks) and up to 8 (the per-thread network)."""
     U1, I1, d, nb = 200_000, 100_000, 64, 3
     P, Q, u, i, j = _zipf_large(11 + B + adver, U1, I1, d, B, nb)
     cnt = np.bincount(np.concatenate([i[:B], j[:B]]))
@@ -609,13 +609,12 @@ def test_hash_plan_matches_sort_plan(ops, dev, monkeypatch, B, adver):
     hp = ops.StepHParams(adver=adver, reg=0.01)
     uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
     runs = []
-    for mode, pieces, env in (("sort", [(0, nb)], "1"), ("auto", [(0, nb)], "1"),
-                              ("auto", [(0, 1), (1, nb - 1)], "1"), ("auto", [(0, nb)], "0")):
-        monkeypatch.setenv("ACF_HASH_PLAN", env)
+    for mode, pieces in (("sort", [(0, nb)]), ("auto", [(0, nb)]), ("auto", [(0, 1), (1, nb - 1)]),
+                         ("sort", [(0, 1), (1, nb - 1)])):
         ctx = ops.APRContext(U1, I1, d, B, nb, dev)
         ctx.set_plan_mode(mode)
         ctx.plan(uu, ii, jj, B)
-        assert ctx.plan_kind() == ("hash" if mode == "auto" and env == "1" else "sort")
+        assert ctx.plan_kind() == ("hash" if mode == "auto" else "sort")
         tabs = _gpu_tables(P, Q, dev)
         for first, n in pieces:
             ctx.train_planned(tabs, hp, first, n, graph=first == 0)
@@ -815,12 +814,12 @@ def _overlap_stream(shape, acf, dev, B, nb, seed):
 @pytest.mark.parametrize("d", [8, 32, 64, 128, 256, 512])
 @pytest.mark.parametrize("shape", ["hot", "sparse", "ml1m"])
 @pytest.mark.parametrize("fuse", [False, True])
-def test_step_overlap_bit_identical(ops, acf, dev, d, shape, fuse):
-    """Overlapped APR steps (k_ovl: adv(t) + clean(t+1) in one launch, clean
-    rows waiting on adv(t)'s flags) and streamed steps (k_stream: the whole range
-    in one launch through tagged row versions) vs two kernels per step:
+def test_stream_bit_identical_to_two_kernels(ops, acf, dev, d, shape, fuse):
+    """Streamed steps (k_stream: the whole range in one launch through tagged row
+    versions; d > 256 falls back to two kernels) vs two kernels per step:
     identical bits for tables, accumulators and both losses, over one call
-    (graph and eager) and over piecewise calls; no wait gave up."""
+    (graph and eager) and over piecewise calls; no wait gave up.  (r04 also ran
+    the overlapped step k_ovl here; it was removed in r05.)"""
     if shape == "ml1m" and d not in (32, 64):
         pytest.skip("ml1m shape at the headline dims only")
     B, nb = {"hot": (64, 12), "sparse": (256, 8), "ml1m": (512, 24)}[shape]
@@ -834,11 +833,9 @@ def test_step_overlap_bit_identical(ops, acf, dev, d, shape, fuse):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     runs = []
     split = [(0, 1), (1, 2), (3, 4), (7, nb - 7)]
-    for ovl, stream, pieces, graph in ((False, False, [(0, nb)], True), (True, False, [(0, nb)], True),
-                                       (True, False, [(0, nb)], False), (True, False, split, True),
-                                       (False, True, [(0, nb)], True), (False, True, [(0, nb)], False),
-                                       (False, True, split, True), (False, True, split, False)):
-        ctx.set_step_overlap(ovl)
+    for stream, pieces, graph in ((False, [(0, nb)], True), (False, [(0, nb)], False), (False, split, True),
+                                  (True, [(0, nb)], True), (True, [(0, nb)], False), (True, split, True),
+                                  (True, split, False)):
         ctx.set_stream(stream)
         tabs = _gpu_tables(P, Q, dev)
         for first, n in pieces:
@@ -853,9 +850,10 @@ def test_step_overlap_bit_identical(ops, acf, dev, d, shape, fuse):
             assert torch.equal(x, y), (k, n)
 
 
-def test_step_overlap_kernel_timing_kinds(ops, dev):
-    """time_kernels reports the launch sequence train_planned runs: one clean,
-    nb-1 overlapped, one adv and one flush launch (and matches training)."""
+def test_two_kernel_timing_kinds(ops, dev):
+    """time_kernels reports the launch sequence train_planned runs with streamed
+    steps off: a clean and an adv launch per batch and one flush launch (and
+    matches training)."""
     U1, I1, d, B, nb = 300, 200, 64, 128, 9
     u, i, j = _sparse_stream(5, U1, I1, B, nb, hot=16, p_hot=0.3)
     rng = np.random.default_rng(1)
@@ -867,7 +865,7 @@ def test_step_overlap_kernel_timing_kinds(ops, dev):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ta, tb = _gpu_tables(P, Q, dev), _gpu_tables(P, Q, dev)
     t = ctx.time_kernels(ta, hp)
-    assert {k: v[1] for k, v in t.items()} == {"clean": 1, "ovl": nb - 1, "adv": 1, "flush": 1, "stream": 0, "hot": 0}
+    assert {k: v[1] for k, v in t.items()} == {"clean": nb, "adv": nb, "flush": 1, "stream": 0, "hot": 0}
     ctx.train_planned(tb, hp)
     for x, y in zip(ta, tb):
         assert torch.equal(x, y)
@@ -890,12 +888,12 @@ def test_stream_kernel_timing_kinds(ops, dev, d):
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     ta, tb = _gpu_tables(P, Q, dev), _gpu_tables(P, Q, dev)
     t = ctx.time_kernels(ta, hp)
-    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "ovl": 0, "adv": 0, "flush": 0, "stream": 1, "hot": 0}
+    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "adv": 0, "flush": 0, "stream": 1, "hot": 0}
     ctx.train_planned(tb, hp)
     for x, y in zip(ta, tb):
         assert torch.equal(x, y)
     t = ctx.time_kernels(ta, hp, 2, nb - 2)
-    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "ovl": 0, "adv": 0, "flush": 1, "stream": 1, "hot": 0}
+    assert {k: v[1] for k, v in t.items()} == {"clean": 0, "adv": 0, "flush": 1, "stream": 1, "hot": 0}
     ctx.train_planned(tb, hp, 2, nb - 2)
     for x, y in zip(ta, tb):
         assert torch.equal(x, y)

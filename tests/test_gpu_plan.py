@@ -3,7 +3,7 @@ and the headline-shape parity of the default path (batch plan + k_stream).
 
 The two planners must write identical records, task lists and write-back tables,
 so training through either gives identical bits, whichever step schedule runs
-(two kernels, k_ovl, k_stream; BPR or APR) and however the range is split.
+(two kernels or k_stream; BPR or APR) and however the range is split.
 """
 import numpy as np
 import pytest
@@ -45,10 +45,9 @@ def _stream(shape, acf, dev, B, nb, seed):
     return (ds.num_users + 1, ds.num_items + 1) + tuple(np.concatenate(x)[:n] for x in (u, i, j))
 
 
-def _train(ops, dev, U1, I1, d, B, nb, u, i, j, P, Q, hp, plan_mode, ovl, stream, pieces, graph=True):
+def _train(ops, dev, U1, I1, d, B, nb, u, i, j, P, Q, hp, plan_mode, stream, pieces, graph=True):
     ctx = ops.APRContext(U1, I1, d, B, nb, dev)
     ctx.set_plan_mode(plan_mode)
-    ctx.set_step_overlap(ovl)
     ctx.set_stream(stream)
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     tabs = _tables(P, Q, dev)
@@ -74,17 +73,17 @@ def test_batch_plan_matches_sort_plan(ops, acf, dev, shape, B, nb, d, adver):
     Q = (rng.standard_normal((I1, d)) * 0.2).astype(np.float32)
     hp = ops.StepHParams(adver=adver, reg=0.01)
     split = [(0, 1), (1, 2), (3, nb - 3)] if nb > 3 else [(0, 1), (1, nb - 1)]
-    schedules = [(False, False)] + ([(True, False), (False, True)] if adver else [])
+    schedules = [False] + ([True] if adver else [])  # streamed steps: APR only
     names = ("P", "Q", "accP", "accQ", "loss_clean", "loss_adv")
-    for ovl, stream in schedules:
+    for stream in schedules:
         for pieces in ([(0, nb)], split):
-            want = _train(ops, dev, U1, I1, d, B, nb, u, i, j, P, Q, hp, "sort", ovl, stream, pieces)
-            got = _train(ops, dev, U1, I1, d, B, nb, u, i, j, P, Q, hp, "auto", ovl, stream, pieces)
+            want = _train(ops, dev, U1, I1, d, B, nb, u, i, j, P, Q, hp, "sort", stream, pieces)
+            got = _train(ops, dev, U1, I1, d, B, nb, u, i, j, P, Q, hp, "auto", stream, pieces)
             torch.cuda.synchronize()
             for x, y, n in zip(want, got, names):
                 if n == "loss_adv" and not adver:
                     continue
-                assert torch.equal(x, y), (ovl, stream, pieces, n)
+                assert torch.equal(x, y), (stream, pieces, n)
 
 
 def test_batch_plan_replans_and_bitmap_reuse(ops, oracle, dev):

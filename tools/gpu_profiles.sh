@@ -1,8 +1,8 @@
-# r04 closing pass, part 2: profiles (short-call trace, configs[4] d=64 step
+# closing pass, part 2: profiles (short-call trace, configs[4] d=64 step
 # timeline, bench rocprofv3 stats + PMC passes)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/${OUT_TAG:-r04_prof}
+OUT=gpurun_out/${OUT_TAG:-profiles}
 mkdir -p $OUT
 timeout -k 10 200 rocprofv3 --kernel-trace -f csv -d $OUT/sc_trace -o sc -- python3 tools/short_call.py --reps 10 --same > $OUT/sc_trace.log 2>&1
 python3 tools/trace_region.py $(find $OUT/sc_trace -name '*kernel_trace.csv' | head -1) > $OUT/short_call_trace_breakdown.json 2>&1 || true

@@ -1,5 +1,5 @@
 # split step with captured hipGraphs: GPU distributed tests, then the split-step bench lines
-# (world 1) with and without the graphs.  A test failure still runs the lines; a fault,
+# (world 1).  A test failure still runs the lines; a fault,
 # abort or time limit stops the script.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${OUT_TAG:-shard_graph}
@@ -10,8 +10,6 @@ tail -3 $OUT/dist.log
 [ $rc -le 1 ] || { echo "pytest rc $rc: stopping"; exit $rc; }
 timeout -k 10 300 python3 tools/shard_profile.py ${STEPS:-24} > $OUT/shard.json 2> $OUT/shard.err || { echo "shard lines failed"; tail -20 $OUT/shard.err; exit 1; }
 python3 -c "import json;d=json.loads(open('$OUT/shard.json').read().strip().splitlines()[-1]);[print(k, v['ms_per_step'], v['value'], v.get('launch')) for k, v in d.items()]"
-ACF_SHARD_GRAPH=0 timeout -k 10 300 python3 tools/shard_profile.py ${STEPS:-24} > $OUT/shard_eager.json 2> $OUT/shard_eager.err || { echo "eager shard lines failed"; tail -20 $OUT/shard_eager.err; exit 1; }
-python3 -c "import json;d=json.loads(open('$OUT/shard_eager.json').read().strip().splitlines()[-1]);[print('eager', k, v['ms_per_step'], v['value'], v.get('launch')) for k, v in d.items()]"
 if [ -n "$WITH_PROF" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o shard -- python3 tools/shard_profile.py ${STEPS:-24} > $OUT/shard_prof.json 2> $OUT/shard_prof.err || exit 1
 fi

@@ -1,7 +1,9 @@
 #!/usr/bin/env python
 """Where the end of a streamed call goes (r04 A/B aid): runs the driver-shaped
-20-batch call with ACF_TAIL_DIAG=1 and prints k_stream's tail stamps (us after
-the kernel's start), see acf_apr_diag_tail in csrc/acf_apr.hip."""
+20-batch call with ACF_TAIL_DIAG=1 through the diagnostic library
+(tools/libacf_apr_diag.so, tools/build_diag.sh: the tail stamps exist only in
+-DACF_DIAG builds since r05) and prints k_stream's tail stamps (us after the
+kernel's start), see acf_apr_diag_tail in csrc/acf_apr.hip."""
 from __future__ import annotations
 
 import ctypes
@@ -24,7 +26,12 @@ def main():
     acf = importlib.import_module("adversarial-collaborative-filtering_amd")
     ops = importlib.import_module("adversarial-collaborative-filtering_amd.ops")
     nat = importlib.import_module("adversarial-collaborative-filtering_amd._native")
-    lib = nat.load()
+    # the diagnostic library, without the product library's build-hash check
+    lib = ctypes.CDLL(os.path.join(REPO, "tools", "libacf_apr_diag.so"))
+    for fname, (res, args) in nat.SIGNATURES.items():
+        fn = getattr(lib, fname)
+        fn.restype, fn.argtypes = res, args
+    nat._lib = lib
     lib.acf_apr_diag_tail.restype = ctypes.c_int
     lib.acf_apr_diag_tail.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
     B, d, steps = 512, 64, 20
@@ -44,7 +51,7 @@ def main():
     names = ["last_wg_done", "last_arrival", "decided", "actions", "flusher_saw", "flush_done"]
     med = {n: st.median([x[k] for x in rows[2:] if x[k] is not None]) for k, n in enumerate(names)
            if any(x[k] is not None for x in rows[2:])}
-    print(json.dumps({"env": {k: os.environ.get(k) for k in ("ACF_TAIL", "ACF_TAIL_FLUSHERS")},
+    print(json.dumps({
                       "us_after_start_median": med, "reps": rows[-3:]}))
 
 
