@@ -181,3 +181,45 @@ def test_split_step_skewed_ranks_share_block_size(tmp_path, oracle, fp32_parity)
     oracle.apr_train(P, Q, aP, aQ, u, i, j, SK_B, HParams(adver=1))
     for k, (want, n) in enumerate(zip((P, Q, aP, aQ), ("P", "Q", "accP", "accQ"))):
         fp32_parity(got[f"arr_{k}"], want, n)
+
+
+def _lifetime_worker(rank, world, port, out_dir):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import gc
+    import weakref
+    from apr_oracle import HParams
+    from shard_oracle import OracleShardLocal
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D_ = importlib.import_module(PKG + ".distributed")
+    P, Q, u, i, j = _problem()
+    res = []
+    # with-block: close() runs at its end
+    with D_.ShardedAPR(U1, I1, D, B, init_P=P, init_Q=Q, local=OracleShardLocal) as sh:
+        sh.train(u, i, j, HParams(adver=1), chunk=CHUNK)
+        fin = sh._finalizer
+    res.append(not fin.alive)
+    # the local passes see the object through a weak proxy: no cycle, so dropping
+    # the last reference runs the finalizer at once (no gc pass needed)
+    gc.disable()
+    sh = D_.ShardedAPR(U1, I1, D, B, init_P=P, init_Q=Q, local=OracleShardLocal)
+    sh.train(u, i, j, HParams(adver=1), chunk=CHUNK)
+    fin, ref = sh._finalizer, weakref.ref(sh)
+    del sh
+    res.append(not fin.alive and ref() is None)
+    gc.enable()
+    np.save(os.path.join(out_dir, f"life{rank}.npy"), np.array(res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_lifetime_close_with_and_drop():
+    """ShardedAPR releases its captured graphs (and anything else its finalizer
+    holds) at close(), at the end of a with-block, or as soon as the last
+    reference goes: the local passes hold only a weak proxy (world 2, gloo)."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_lifetime_worker, args=(2, _free_port(), tmp), nprocs=2, join=True)
+        for r in range(2):
+            assert np.load(os.path.join(tmp, f"life{r}.npy")).all()
