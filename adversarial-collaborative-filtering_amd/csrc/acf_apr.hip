@@ -577,6 +577,37 @@ __device__ __forceinline__ void records_one(int64_t e, int32_t t, int32_t ub0, i
   }
 }
 
+// Per-batch triplet lists of triplet-centric plans (riders, StepArgs.tsel):
+// batch t's non-fused triplets from the front of tlist[t][0, B), its fused ones
+// (all three rows single) from the back, counted in tcnt[2t] / tcnt[2t + 1]
+// (zeroed by the plan).  Wave-aggregated appends: one atomic per list per wave
+// when the wave's triplets share a batch (B % 64 == 0 always does).  The order
+// in a list varies from run to run; no triplet's step depends on it.
+__device__ __forceinline__ void tri_list_put(int32_t* tlist, int32_t* tcnt, int32_t B, int32_t t, int32_t b,
+                                             bool fused) {
+  const int lane = (int)__lane_id();
+  const int lead = __ffsll((unsigned long long)__ballot(1)) - 1;
+  const int32_t tl = __shfl(t, lead);
+  int32_t* row = tlist + (int64_t)t * B;
+  if (__all(t == tl)) {
+    const uint64_t mf = __ballot(fused), mn = __ballot(!fused);
+    int32_t bf = 0, bn = 0;
+    if (lane == lead) {
+      if (mf) bf = atomicAdd(tcnt + 2 * t + 1, (int32_t)__popcll(mf));
+      if (mn) bn = atomicAdd(tcnt + 2 * t, (int32_t)__popcll(mn));
+    }
+    bf = __shfl(bf, lead);
+    bn = __shfl(bn, lead);
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    if (fused) row[B - 1 - (bf + (int32_t)__popcll(mf & below))] = b;
+    else row[bn + (int32_t)__popcll(mn & below)] = b;
+  } else if (fused) {
+    row[B - 1 - atomicAdd(tcnt + 2 * t + 1, 1)] = b;
+  } else {
+    row[atomicAdd(tcnt + 2 * t, 1)] = b;
+  }
+}
+
 __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb, int32_t no_fuse,
                           int32_t tri,
                           const int4* __restrict__ tsl, const int4* __restrict__ tpos,
@@ -584,13 +615,19 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
                           const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
                           OccRec* __restrict__ urec, OccRec* __restrict__ irec,
                           OccRec* __restrict__ inl, OccRec* __restrict__ trec,
-                          int32_t* __restrict__ gen_ptr, uint64_t* __restrict__ sflags, HotLists hl) {
+                          int32_t* __restrict__ gen_ptr, uint64_t* __restrict__ sflags, HotLists hl,
+                          int32_t* __restrict__ tlist, int32_t* __restrict__ tcnt) {
   const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (e == 0) *gen_ptr = gen;
   if (e >= E) return;
   const int32_t t = (int32_t)(e / B);
   records_one(e, t, ubs[t], ubs[t + 1] - ubs[t], ibs[t], S, R, gen, kb, no_fuse, tri, tsl, tpos, uinfo, iinfo,
               urec, irec, inl, trec, sflags, hl);
+  if (tlist) {  // triplet-centric plans: fused = all three rows single (trec's flag 1)
+    const int4 sl = tsl[e];
+    const bool fused = info_count(uinfo[sl.x]) == 1 && info_count(iinfo[sl.y]) == 1 && info_count(iinfo[sl.z]) == 1;
+    tri_list_put(tlist, tcnt, B, t, (int32_t)(e - (int64_t)t * B), fused);
+  }
 }
 
 __global__ void k_slot_lists(const uint64_t* __restrict__ flags, const uint64_t* __restrict__ incl,
@@ -1335,19 +1372,15 @@ struct StepArgs {
   int32_t xflush;
   // triplet-centric list step (k_tri_*): per-occurrence contributions of shared rows
   const int4* tpos;    // [E] CSR positions of a triplet's three occurrences
-  float* contrib;      // users [B][2][d] (positive, negative branch), then items [2B][d]; by batch parity
+  float* contrib;      // users [B][2][d] (positive, negative branch), then items [2B][d]
+  // (r05) riders: APR steps of triplet-centric plans over the plan's per-batch
+  // triplet lists (tlist / tcnt, tri_list_put): k_tri_clean and k_tri_adv run
+  // the non-fused triplets (tsel 1), the fused ones ride in the combine
+  // launches (tsel 2 / 3, tri_riders); tsel 0: every triplet in batch order
+  const int32_t* tlist;  // [nb][B]
+  const int32_t* tcnt;   // [nb][2]: non-fused, fused
+  int32_t tsel, rider_waves;
   int32_t inplace;     // triplet-centric plans: every row is updated in its table (no W scratch)
-  // triplet-centric overlap (r05): batch t's final combine (k_tri_combine<2>) and
-  // batch t+1's clean pass run in ONE launch (k_tri_c2c).  A row the combine
-  // updates is handed to the clean pass per row: k_tri_combine<0> of batch t marks
-  // each shared row with t's id (mark) and clears its done word; the final combine
-  // stores the row write-through, drains and sets done = id; a clean-pass triplet
-  // whose row carries mark == pend_bid polls done and reloads the row device-scope
-  // (MI355X guide, Guideline 16 row 1).  nullptr / 0: no overlap.
-  int32_t *markP, *markQ;  // [U1] / [I1]
-  int32_t *doneP, *doneQ;  // [U1] / [I1]
-  int32_t bid;             // this batch's id (> 0; repeats only across replays of one graph)
-  int32_t pend_bid;        // k_tri_clean: rows marked with this id may still be being combined
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
   uint64_t seed;
@@ -2908,34 +2941,6 @@ __global__ void __launch_bounds__(256) k_adv_list(StepArgs a) {
 __device__ __forceinline__ float* tri_cu(const StepArgs& a) { return a.contrib; }
 __device__ __forceinline__ float* tri_ci(const StepArgs& a) { return a.contrib + (int64_t)2 * a.B * a.d; }
 
-// Overlapped clean pass (StepArgs.pend_bid): a row the final combine beside it
-// is still updating (mark == pend_bid) is polled until its done word says so,
-// then reloaded with device-scope loads (the combine stored it write-through).
-// The marks were written by an earlier launch (plain loads); every lane polls
-// its group's flags (same addresses: one fetch per group).  Bounded: a give-up
-// sets step_err bit 0.
-template <int LPR, int NV>
-__device__ __forceinline__ void tri_wait_pending(const StepArgs& a, int32_t u, int32_t i, int32_t j, int l,
-                                                 RowV<NV>& p, RowV<NV>& qi, RowV<NV>& qj) {
-  const bool wu = a.markP[u] == a.pend_bid, wi = a.markQ[i] == a.pend_bid, wj = a.markQ[j] == a.pend_bid;
-  if (!__any(wu || wi || wj)) return;
-  for (int it = 0;; ++it) {
-    bool ok = true;
-    if (wu) ok = ok && __hip_atomic_load(a.doneP + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.pend_bid;
-    if (wi) ok = ok && __hip_atomic_load(a.doneQ + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.pend_bid;
-    if (wj) ok = ok && __hip_atomic_load(a.doneQ + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.pend_bid;
-    if (__all(ok)) break;
-    if (it >= ACF_SPIN_LIMIT) {
-      atomicOr(a.step_err, 1);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  if (wu) p = load_piece<LPR, NV, true>(a.P, u, a.d, l);
-  if (wi) qi = load_piece<LPR, NV, true>(a.Q, i, a.d, l);
-  if (wj) qj = load_piece<LPR, NV, true>(a.Q, j, a.d, l);
-}
-
 // PASS 0: APR clean (shared rows: clean contributions; single rows: nothing,
 // k_tri_adv recomputes their term); 1: BPR (single rows: Adagrad; shared:
 // contributions); 2: APR adversarial.
@@ -2962,7 +2967,6 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
     p = load_at<LPR, NV>(row_src(a, a.P, u, r.b.z), d, l);
     qi = load_at<LPR, NV>(row_src(a, a.Q, i, r.b.w), d, l);
     qj = load_at<LPR, NV>(row_src(a, a.Q, j, r.c.x), d, l);
-    if (PASS == 0 && a.pend_bid) tri_wait_pending<LPR, NV>(a, u, i, j, l, p, qi, qj);
   }
   RowV<NV> cu, ci, cj, du, di, dj;  // Adagrad slots of the single rows, deltas of the shared ones
   if (PASS != 0) {
@@ -3066,16 +3070,59 @@ __device__ __forceinline__ void tri_rec(const StepArgs& a, int b, RecV& r, int4&
 // many wave rounds
 __host__ __device__ constexpr int tri_gpw(int nv) { return nv == 1 ? 2 : 1; }
 
+// list positions x0, x0 + 64/LPR, ... (< hi) of batch a.t's triplet list (back:
+// the fused end, position x at [B - 1 - x]; see tri_list_put): the groups of
+// tri_triplets (GPW of them per wave), with one dependent load (the list) in
+// front of the records
+template <int LPR, int NV, int PASS, int GPW>
+__device__ __forceinline__ void tri_list_group(const StepArgs& a, int x0, int hi, bool back, int lane) {
+  constexpr int OPW = 64 / LPR;
+  const int32_t* lst = a.tlist + (int64_t)a.t * a.B;
+  int bb[GPW];
+#pragma unroll
+  for (int x = 0; x < GPW; ++x) {
+    const int pos = x0 + x * OPW;
+    bb[x] = pos < hi ? lst[back ? a.B - 1 - pos : pos] : a.B;
+  }
+  RecV r[GPW];
+  int4 ps[GPW];
+#pragma unroll
+  for (int x = 0; x < GPW; ++x) tri_rec(a, bb[x], r[x], ps[x]);
+#pragma unroll
+  for (int x = 0; x < GPW; ++x) tri_triplet_r<LPR, NV, PASS>(a, bb[x], lane & (LPR - 1), r[x], ps[x]);
+}
+
 template <int LPR, int NV, int PASS>
 __device__ __forceinline__ void tri_triplets(const StepArgs& a, int tw, int lane) {
   constexpr int OPW = 64 / LPR, GPW = tri_gpw(NV);
   const int b0 = tw * GPW * OPW + lane / LPR;
+  if (a.tsel) {  // the non-fused triplets only (the fused ones ride in the combines)
+    tri_list_group<LPR, NV, PASS, GPW>(a, b0, a.tcnt[2 * a.t], false, lane);
+    return;
+  }
   RecV r[GPW];
   int4 ps[GPW];
 #pragma unroll
   for (int x = 0; x < GPW; ++x) tri_rec(a, b0 + x * OPW, r[x], ps[x]);
 #pragma unroll
   for (int x = 0; x < GPW; ++x) tri_triplet_r<LPR, NV, PASS>(a, b0 + x * OPW, lane & (LPR - 1), r[x], ps[x]);
+}
+
+// Riders (StepArgs.tsel 2 / 3): waves after a combine's own run the batch's
+// fused triplets -- their whole APR step (PASS 2), which needs nothing any
+// combine produces and touches no row a combine reads or writes (all three
+// rows occur once in the batch) -- while the combine's hot chain leaves the
+// chip idle.  tsel 2 (in k_tri_combine<0>): fused positions [0, half); 3
+// (k_tri_combine<2>): the rest; rider_waves waves stride over the groups, one
+// group at a time (two, as k_tri_adv, took the combine launch from 94 / 116 to
+// 145 VGPRs).
+template <int LPR, int NV>
+__device__ __forceinline__ void tri_riders(const StepArgs& a, int rw, int lane) {
+  constexpr int PER = 64 / LPR;
+  const int nf = a.tcnt[2 * a.t + 1], half = (nf + 1) >> 1;
+  const int lo = a.tsel == 2 ? 0 : half, hi = a.tsel == 2 ? half : nf;
+  for (int g0 = lo + rw * PER; g0 < hi; g0 += a.rider_waves * PER)
+    tri_list_group<LPR, NV, 2, 1>(a, g0 + lane / LPR, hi, true, lane);
 }
 
 // header of shared slot k: count, side, own row, source, local CSR base
@@ -3151,21 +3198,6 @@ __device__ __forceinline__ void tri_add_q(const StepArgs& a, const TriSlot& h, i
   }
 }
 
-// overlap marks (StepArgs.markP): k_tri_combine<0> marks a shared row of batch
-// a.bid (its final combine is the one that will update it) and clears its done
-// word; plain stores, read by later launches
-__device__ __forceinline__ void tri_mark_row(const StepArgs& a, int is_item, int32_t row) {
-  (is_item ? a.markQ : a.markP)[row] = a.bid;
-  (is_item ? a.doneQ : a.doneP)[row] = 0;
-}
-
-// k_tri_combine<2> in an overlapped launch: after this wave's write-through row
-// stores have drained, the done word (device scope) tells the clean pass beside it
-__device__ __forceinline__ void tri_done_row(const StepArgs& a, int is_item, int32_t row, bool lead) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lead) __hip_atomic_store((is_item ? a.doneQ : a.doneP) + row, a.bid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // finish a shared row from its summed G (as the slot kernels' team leader and
 // k_hot_combine do): MODE 0 g0 + delta, 1 BPR Adagrad, 2 APR Adagrad
 template <int LPR, int NV, int MODE>
@@ -3175,7 +3207,6 @@ __device__ __forceinline__ void tri_finish(const StepArgs& a, int k, const TriSl
     const RowV<NV> dl = make_delta<LPR, NV>(a, G, h.is_item, h.row, l);
     store_row<LPR, NV>(a.g0, k, d, l, G);
     store_row<LPR, NV>(a.delta, k, d, l, dl);
-    if (a.markP && l == 0) tri_mark_row(a, h.is_item, h.row);
     return;
   }
   float* acc_tab = h.is_item ? a.accQ : a.accP;
@@ -3191,14 +3222,8 @@ __device__ __forceinline__ void tri_finish(const StepArgs& a, int k, const TriSl
     adagrad_row(a, G0, own, acc, h.count, wout);
   }
   store_row<LPR, NV>(acc_tab, h.row, d, l, acc);
-  if (MODE == 2 && a.markP) {  // handed to the clean pass beside this launch (in place)
-    store_row_wt<LPR, NV>(h.is_item ? a.Q : a.P, h.row, d, l, wout);
-    tri_done_row(a, h.is_item, h.row, l == 0);
-  } else if (a.inplace) {
-    store_row<LPR, NV>(h.is_item ? a.Q : a.P, h.row, d, l, wout);
-  } else {
-    store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
-  }
+  if (a.inplace) store_row<LPR, NV>(h.is_item ? a.Q : a.P, h.row, d, l, wout);
+  else store_row<LPR, NV>(a.wnew_cur, k, d, l, wout);
 }
 
 template <int LPR, int NV, bool BPR>
@@ -3282,7 +3307,6 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
       const RowV<NV> dl = make_delta<LPR, NV>(a, T, f.is_item, f.row, l);
       store_row<LPR, NV>(a.g0, k, d, l, T);
       store_row<LPR, NV>(a.delta, k, d, l, dl);
-      if (a.markP && l == 0) tri_mark_row(a, f.is_item, f.row);
     } else {
       RowV<NV> wout;
       if (MODE == 1) {
@@ -3293,12 +3317,7 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
         adagrad_row(a, G0, f.own, f.acc, e.w, wout);
       }
       store_row<LPR, NV>(f.is_item ? a.accQ : a.accP, f.row, d, l, f.acc);
-      if (MODE == 2 && a.markP) {  // handed to the clean pass beside this launch
-        store_row_wt<LPR, NV>(f.is_item ? a.Q : a.P, f.row, d, l, wout);
-        tri_done_row(a, f.is_item, f.row, l == 0);
-      } else {
-        store_row<LPR, NV>(f.is_item ? a.Q : a.P, f.row, d, l, wout);  // in place (tri plans)
-      }
+      store_row<LPR, NV>(f.is_item ? a.Q : a.P, f.row, d, l, wout);  // in place (tri plans)
     }
   }
   __syncthreads();
@@ -3316,7 +3335,9 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
 // order, so the pieces they wait for are already running: the launch always
 // drains.  (hot_waves is a multiple of 4: whole workgroups.)
 template <int LPR, int NV, int MODE>
-__device__ __forceinline__ void tri_combine_body(const StepArgs& a, float4* __restrict__ red, int wave) {
+__global__ void __launch_bounds__(256, (NV == 1 && MODE != 1) ? 4 : 1) k_tri_combine(StepArgs a) {
+  __shared__ float4 red[NV * 256];
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
   int32_t* arrive = a.hot.arrive + (int64_t)a.t * a.hot.piece_stride;
   if (wave < a.hot_waves) {
@@ -3373,7 +3394,10 @@ __device__ __forceinline__ void tri_combine_body(const StepArgs& a, float4* __re
     return;
   }
   const int sw = wave - a.hot_waves - 4 * a.hot_blocks;
-  if (sw >= a.slot_waves) return;
+  if (sw >= a.slot_waves) {
+    if (MODE != 1 && a.tsel >= 2) tri_riders<LPR, NV>(a, sw - a.slot_waves, lane);
+    return;
+  }
   const int ngroups = a.slot_waves * (64 / LPR), gid = sw * (64 / LPR) + g;
   const int n = a.slot_cnt[a.t];
   const int32_t* lst = a.slot_list + (int64_t)a.t * a.S;
@@ -3384,32 +3408,6 @@ __device__ __forceinline__ void tri_combine_body(const StepArgs& a, float4* __re
     tri_add_q<LPR, NV>(a, h, 0, h.count, 1, l, G);
     tri_finish<LPR, NV, MODE>(a, k, h, G, l);
   }
-}
-
-template <int LPR, int NV, int MODE>
-__global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
-  __shared__ float4 red[NV * 256];
-  tri_combine_body<LPR, NV, MODE>(a, red, (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6));
-}
-
-// Overlapped APR step of triplet-centric plans (r05): batch t's final combine
-// (k_tri_combine<2>, `ac`: waves [0, comb_waves), whole workgroups) and batch
-// t+1's clean pass (k_tri_clean's triplet waves, `an`: the waves after them) in
-// ONE launch.  The clean pass reads rows the combine is updating only after
-// their hand-off (tri_wait_pending: per-row done words; the combine's waves come
-// first in every XCD's in-order dispatch and never wait for the clean pass, so
-// the launch always drains).  Everything else of the two is disjoint: contrib
-// and g0 / delta by batch parity, hot_part only in the combine.  Same arithmetic
-// as the two launches, so the same bits.
-template <int LPR, int NV>
-__global__ void __launch_bounds__(256) k_tri_c2c(StepArgs ac, StepArgs an, int32_t comb_waves) {
-  __shared__ float4 red[NV * 256];
-  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
-  if (wave < comb_waves) {
-    tri_combine_body<LPR, NV, 2>(ac, red, wave);
-    return;
-  }
-  tri_triplets<LPR, NV, 0>(an, wave - comb_waves, threadIdx.x & 63);
 }
 
 // k_tri_adv: 4 blocks (16 waves) per CU asked of the register allocator (d <= 256)
@@ -3648,6 +3646,8 @@ struct acf_apr_ctx {
   int4 *uinfo = nullptr, *iinfo = nullptr;   // per unique row, see k_slot_info
   int32_t *iuniq = nullptr, *ioff = nullptr, *ibs = nullptr;
   OccRec* trec = nullptr;
+  int32_t* tlist = nullptr;  // [maxE] per-batch triplet lists of triplet-centric plans (tri_list_put)
+  int32_t* tcnt = nullptr;   // [2 maxNB] their counts: non-fused, fused
   OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr;
   int32_t *err = nullptr, *gen_dev = nullptr;
   void* tmp = nullptr;
@@ -3666,13 +3666,11 @@ struct acf_apr_ctx {
   HotLists hot = {};            // hot slots of list plans (k_records)
   int32_t shard = 0;            // shard mode (acf_apr_set_shard_mode): item rows are partial sums
   int32_t tri = 0;              // the plan is triplet-centric (packed, not shard: k_tri_*)
-  float* contrib = nullptr;     // [2][4 maxB, d] per-occurrence contributions of shared rows (k_tri_*), by batch parity
-  int32_t* tri_marks = nullptr;  // [2][U1 + I1]: overlap marks and done words (StepArgs.markP), at first use
-  int32_t tri_ovl = 1;           // overlapped triplet-centric steps (acf_apr_set_step_overlap)
-  int32_t tri_bid = 0;           // the last batch id handed out (StepArgs.bid)
+  float* contrib = nullptr;     // [4 maxB, d] per-occurrence contributions of shared rows (k_tri_*)
   int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
+  int32_t riders = 1;   // fused triplets ride in the combine launches (acf_apr_set_step_overlap)
   int32_t plan_kind2 = 0;  // the plan encodes sources at every distance (k_prev_next)
   int32_t plan_kb = 1;     // slot bits of the plan's src encoding
   int32_t* nextt = nullptr;  // [maxNB][S] next batch touching each slot's row (k_prev_next)
@@ -3857,10 +3855,10 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->hot.arrive, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot.paux, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot_part, (size_t)c->hot.piece_stride * d);
-  A(&c->contrib, (size_t)8 * maxB * d);
+  A(&c->contrib, (size_t)4 * maxB * d);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
   A(&c->iinfo, 2 * maxE);
-  A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
+  A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE); A(&c->tlist, maxE); A(&c->tcnt, 2 * maxNB);
   A(&c->inl, (size_t)maxNB * S * c->R);
   A(&c->err, 4); A(&c->gen_dev, 4); A(&c->epoch, 4); A(&c->decide, 16 + 2 * 144);
   A(&c->g0, 2 * S * d); A(&c->delta, 2 * S * d);  // by batch parity
@@ -4128,6 +4126,7 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   const int64_t E = (int64_t)B * nb;
   const int32_t pb = hplan_pbits(B, ACF_HPLAN_PART);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));  // the other counters: k_hplan_keys
+  HIP_TRY(hipMemsetAsync(c->tcnt, 0, 2 * (size_t)nb * sizeof(int32_t), s));
   HPlanArgs p;
   p.user = user; p.ipos = ipos; p.ineg = ineg;
   p.U1 = c->U1; p.I1 = c->I1;
@@ -4146,6 +4145,7 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   p.pbase = c->hplan_ptot + ((size_t)c->maxNB << hplan_pbits(c->maxB, ACF_HPLAN_PART)) * ACF_HPLAN_TOT;
   p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
   p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
+  p.tlist = c->tlist; p.tcnt = c->tcnt;
   p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt; p.flush_cnt = c->flush_cnt;
   p.saux = c->flush_list;  // unused by in-place plans
   p.haux = c->hplan_haux;
@@ -4416,6 +4416,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
     // current (k_flush scans every slot of the batch).
     HIP_TRY(hipMemsetAsync(c->inl, 0, (size_t)nb * 3 * B * sizeof(OccRec), s));
   }
+  if (c->tri) HIP_TRY(hipMemsetAsync(c->tcnt, 0, 2 * (size_t)nb * sizeof(int32_t), s));
   if (packed) {  // k_records writes the slot flags of the slots it finds; the rest read 0
     HIP_TRY(hipMemsetAsync(c->key_in, 0, (size_t)3 * E * sizeof(uint64_t), s));
     HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
@@ -4425,7 +4426,8 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
                                         reinterpret_cast<const int4*>(c->tsl),
                                         reinterpret_cast<const int4*>(c->tpos), c->uinfo, c->iinfo,
                                         c->ubs, c->ibs, c->urec, c->irec, c->inl, c->trec, c->gen_dev,
-                                        packed ? c->key_in : nullptr, c->hot);
+                                        packed ? c->key_in : nullptr, c->hot, c->tri ? c->tlist : nullptr,
+                                        c->tcnt);
   HIP_TRY(hipGetLastError());
   c->task_lists = 0;
   if (all_dt) {  // streamed-step task lists
@@ -4507,10 +4509,10 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.xn = a.xblocks = a.xflush = 0;
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
-  a.contrib = c->contrib + (size_t)(t & 1) * 4 * c->maxB * c->d;
+  a.contrib = c->contrib;
   a.inplace = c->tri;
-  a.markP = a.markQ = a.doneP = a.doneQ = nullptr;
-  a.bid = a.pend_bid = 0;
+  a.tlist = c->tlist; a.tcnt = c->tcnt;
+  a.tsel = a.rider_waves = 0;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -4526,13 +4528,13 @@ struct Kernels {
   // triplet-centric list step (tri plans with fusion): clean (APR / BPR), combine (MODE 0/1/2), adversarial
   void *tri_clean = nullptr, *tri_clean_bpr = nullptr, *tri_adv = nullptr;
   void* tri_comb[3] = {nullptr, nullptr, nullptr};
-  void* tri_c2c = nullptr;  // batch t's final combine + batch t+1's clean pass in one launch
   int tri = 0;
   int slots_per_wave = 1;
   int lists = 0;  // list kernels: slot waves stride over the plan's per-batch lists
 };
 
 #define ACF_LIST_WAVES 4096  // slot waves of a list kernel
+#define ACF_TRI_RIDER_WAVES 2048  // rider waves after each combine's (tri_riders)
 #define ACF_TRI_COMB_WAVES 4096  // small-slot waves of k_tri_combine (512 / 1,024 slower: r04 A/B)
 #define ACF_TAIL_FLUSHERS 128    // workgroups of k_stream's tail write-back
 #define ACF_HOT_WAVES 2048   // piece waves of a list kernel (hot slots)
@@ -4564,7 +4566,6 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists, int tri) {
     k->tri_comb[0] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 0>);
     k->tri_comb[1] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 1>);
     k->tri_comb[2] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 2>);
-    k->tri_c2c = reinterpret_cast<void*>(&k_tri_c2c<LPR, NV>);
     k->hot_clean = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 0>);
     k->hot_bpr = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 1>);
     k->hot_adv = reinterpret_cast<void*>(&k_hot_combine<LPR, NV, 2>);
@@ -4620,37 +4621,6 @@ static int launch(void* fn, const StepArgs& a, int waves, hipStream_t s, hipEven
     hipLaunchKernelGGL(reinterpret_cast<StepKernel>(fn), grid, block, 0, s, a);
   HIP_TRY(hipGetLastError());
   return ACF_OK;
-}
-
-typedef void (*C2CKernel)(StepArgs, StepArgs, int32_t);
-
-static int launch_c2c(void* fn, const StepArgs& ac, const StepArgs& an, int comb_waves, int clean_waves,
-                      hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  if (comb_waves % 4) return set_error(ACF_E_STATE, "k_tri_c2c: the combine takes whole workgroups");
-  const dim3 grid((unsigned)((comb_waves + clean_waves + 3) / 4)), block(256);
-  if (e0)
-    hipExtLaunchKernelGGL(reinterpret_cast<C2CKernel>(fn), grid, block, 0, s, e0, e1, 0, ac, an, comb_waves);
-  else
-    hipLaunchKernelGGL(reinterpret_cast<C2CKernel>(fn), grid, block, 0, s, ac, an, comb_waves);
-  HIP_TRY(hipGetLastError());
-  return ACF_OK;
-}
-
-static void free_alloc(acf_apr_ctx* c, void* p);
-
-// Overlap marks of triplet-centric steps (StepArgs.markP), at first use and
-// outside any capture: 2 x (U1 + I1) words, zero (no batch id is 0)
-static void prepare_tri(acf_apr_ctx* c) {
-  if (c->tri_marks || !c->tri_ovl || !c->tri) return;
-  int32_t* m = nullptr;
-  const size_t n = (size_t)2 * (c->U1 + c->I1);
-  if (dalloc(c, &m, n) != ACF_OK) return;  // no overlap: the four launches per batch
-  if (hipMemset(m, 0, n * sizeof(int32_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-    (void)hipGetLastError();
-    free_alloc(c, m);
-    return;
-  }
-  c->tri_marks = m;
 }
 
 static int check_step(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hparams* hp,
@@ -4868,65 +4838,40 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     const int SWT = std::min(SW, ACF_TRI_COMB_WAVES);
     const int SW4 = (SWT + 3) & ~3, HW4 = (HW + 3) & ~3, HBT = std::min(HB, ACF_TRI_HOT_BLOCKS);
     const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);  // one lane-group per triplet
-    // overlapped (APR, whole calls of >= 2 batches): clean(first), then per batch
-    // combine<0>(t), adv(t) and ONE launch of combine<2>(t) + clean(t+1)
-    // (k_tri_c2c; the last batch's combine<2> alone)
-    const bool ovl = hp->adver && tri_phases == 3 && n > 1 && c->tri_ovl && c->tri_marks && K.tri_c2c;
-    const int32_t bid0 = c->tri_bid;
-    if (ovl) c->tri_bid += n;
-    auto targs = [&](int32_t t) {
+    const int TW = (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv);
+    // riders (whole APR steps; see tri_riders): clean and adversarial passes over
+    // the non-fused triplets, the fused ones in RW waves after each combine's
+    const bool riders = hp->adver && tri_phases == 3 && c->riders;
+    const int RW = riders ? std::min(TW, ACF_TRI_RIDER_WAVES) : 0;
+    for (int32_t t = first; t < first + n; ++t) {
       // every row is updated in its table (StepArgs.inplace): nothing pending from t-1
       StepArgs a = make_args(c, tb, hp, t, 0);
       a.use_single = 1;
       a.slot_waves = SW;
       a.hot_waves = HW;
-      if (ovl) {
-        a.markP = c->tri_marks;
-        a.markQ = c->tri_marks + c->U1;
-        a.doneP = c->tri_marks + c->U1 + c->I1;
-        a.doneQ = a.doneP + c->U1;
-        a.bid = bid0 + (t - first) + 1;
-      }
-      return a;
-    };
-    auto tclean = [&](const StepArgs& a) {
+      StepArgs ah = a;
+      ah.slot_waves = 4 * HB;
       StepArgs at = a;
       at.slot_waves = 0;  // k_tri_clean: triplet waves only (no write-back of t-1)
-      return at;
-    };
-    auto tcomb = [&](const StepArgs& a) {
       StepArgs ac = a;
       ac.slot_waves = SW4;
       ac.hot_waves = HW4;
       ac.hot_blocks = HBT;
-      return ac;
-    };
-    const int CW = SW4 + HW4 + 4 * HBT;
-    const int TW = (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv);
-    for (int32_t t = first; t < first + n; ++t) {
-      const StepArgs a = targs(t);
-      const StepArgs ac = tcomb(a);
-      if (ovl) {
-        if (t == first) ACF_RET(L(K.tri_clean, tclean(a), TW, 0));  // later ones ran beside combine<2>(t-1)
-        ACF_RET(L(K.tri_comb[0], ac, CW, 5));
+      const int CW = SW4 + HW4 + 4 * HBT;
+      (void)ah;
+      if (riders) {
+        a.tsel = at.tsel = 1;
+        StepArgs ar = ac;
+        ar.rider_waves = RW;
+        ar.tsel = 2;
+        ACF_RET(L(K.tri_clean, at, TW, 0));
+        ACF_RET(L(K.tri_comb[0], ar, CW + RW, 5));
         ACF_RET(L(K.tri_adv, a, TW, 1));
-        if (t + 1 < first + n) {
-          StepArgs an = tclean(targs(t + 1));
-          an.pend_bid = a.bid;
-          hipEvent_t e0 = events ? events[2 * li] : nullptr, e1 = events ? events[2 * li + 1] : nullptr;
-          if (kinds) kinds[li] = 5;
-          StepArgs xc = ac;
-          xc.diag_launch = an.diag_launch = li;
-          ++li;
-          ACF_RET(launch_c2c(K.tri_c2c, xc, an, CW, TW, s, e0, e1));
-        } else {
-          StepArgs al = ac;
-          al.markP = al.markQ = al.doneP = al.doneQ = nullptr;  // nothing beside it: plain stores
-          ACF_RET(L(K.tri_comb[2], al, CW, 5));
-        }
+        ar.tsel = 3;
+        ACF_RET(L(K.tri_comb[2], ar, CW + RW, 5));
       } else if (hp->adver) {
         if (tri_phases & 1) {
-          ACF_RET(L(K.tri_clean, tclean(a), TW, 0));
+          ACF_RET(L(K.tri_clean, at, TW, 0));
           ACF_RET(L(K.tri_comb[0], ac, CW, 5));
         }
         if (tri_phases & 2) {
@@ -4934,7 +4879,7 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
           ACF_RET(L(K.tri_comb[2], ac, CW, 5));
         }
       } else if (tri_phases & 2) {
-        ACF_RET(L(K.tri_clean_bpr, tclean(a), TW, 0));
+        ACF_RET(L(K.tri_clean_bpr, at, TW, 0));
         ACF_RET(L(K.tri_comb[1], ac, CW, 5));
       }
     }
@@ -5028,7 +4973,6 @@ extern "C" int acf_apr_train_planned(acf_apr_ctx* c, const acf_apr_tables* tb,
   hipStream_t s = static_cast<hipStream_t>(stream_);
   c->last_delta_batch = -1;
   prepare_stream(c, hp);
-  prepare_tri(c);
   Kernels K;
   const bool streamed = get_kernels(c, &K, c->fusion) == ACF_OK && use_stream(c, K, hp);
   // a streamed call runs gated behind a queued call of the group that may have
@@ -5081,7 +5025,6 @@ static int time_kernels(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_
   ACF_RET(check_step(c, tb, hp, first));
   hipStream_t s = static_cast<hipStream_t>(stream_);
   prepare_stream(c, hp);
-  prepare_tri(c);
   const int nl = 6 * n + 2;
   std::vector<hipEvent_t> ev((size_t)2 * nl, nullptr);
   std::vector<int> kinds(nl, -1);
@@ -5138,18 +5081,17 @@ extern "C" int acf_apr_set_fusion(acf_apr_ctx* c, int32_t on) {
   return ACF_OK;
 }
 
+extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
+  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);
+  c->riders = on;
+  return ACF_OK;
+}
+
 extern "C" int acf_apr_set_stream(acf_apr_ctx* c, int32_t on) {
   ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
   ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   c->stream = on != 0;
-  return ACF_OK;
-}
-
-extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
-  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
-  ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
-  ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);
-  c->tri_ovl = on;
   return ACF_OK;
 }
 

@@ -1027,16 +1027,18 @@ __global__ void __launch_bounds__(256) k_nmf_adam(float4* __restrict__ p, float4
 //                     of the rows brought to iteration t, so no row is more than
 //                     LAZY_S iterations behind; after the call's last step, every
 //                     row (caller's stream).
-// catch-up period (acf_neumf_ctx::lazy_s, default LAZY_S; ACF_NMF_LAZY_S for A/B):
+// catch-up period (acf_neumf_ctx::lazy_s = LAZY_S):
 // a row is at most lazy_s iterations behind; a step's slice is 1/lazy_s of the
 // rows, so a longer period is a smaller slice beside each step (r04, yelp shape,
-// d 64, B 512, one box: period 8 6.47M instances/s, 16 7.10-7.15M, 24 6.91M, 31 6.74M)
+// d 64, B 512, one box: period 8 6.47M instances/s, 16 7.10-7.15M, 24 6.91M, 31 6.74M;
+// r05, same-box A/B with the workgroups below: 16 x 192 7.24M, 24 x 128 6.96-7.06M,
+// 31 x 192 6.84-6.86M, 31 x 96 6.75-6.88M -- the env knobs of those A/Bs are gone)
 constexpr int LAZY_S = 16;
 constexpr int LAZY_W = 32;  // lr_t window (> the catch-up period)
 // workgroups of a step's catch-up slice, beside the step's kernels (r03, period
 // 8: 32 WGs 3.9M instances/s (the slice outlasts the step), 64 5.6M, 96 7.55M,
 // 128 7.3M, 192 7.45M, 256 7.35M; r04, period 16: 48 5.1M, 64 5.8-6.0M, 96 7.10M,
-// 128 7.10-7.15M, 192 7.16-7.18M, 256 7.13M); ACF_NMF_CATCHUP_WG for A/B
+// 128 7.10-7.15M, 192 7.16-7.18M, 256 7.13M)
 constexpr int64_t CATCHUP_WG = 192;
 static_assert(LAZY_W > LAZY_S, "lr window");
 
@@ -1293,8 +1295,6 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
   if (r != ACF_OK) return r;
   ACF_CHECK(maxB > 0 && maxB <= (1 << 24), ACF_E_INVALID, "max_batch must be in (0, 2^24], got %d", maxB);
   acf_neumf_ctx* c = new acf_neumf_ctx();
-  if (const char* e = getenv("ACF_NMF_LAZY_S")) c->lazy_s = std::min(std::max(1, atoi(e)), LAZY_W - 1);
-  if (const char* e = getenv("ACF_NMF_CATCHUP_WG")) c->catchup_wg = std::max(1, atoi(e));
   c->U1 = U1; c->I1 = I1; c->d = d; c->maxB = maxB;
   c->L = make_layout(U1, I1, d);
   const size_t B = (size_t)maxB, dd = (size_t)d;

@@ -50,15 +50,17 @@ chunk's steps are captured as hipGraphs once and replayed:
   * world > 1: the fixed-size RCCL all_to_all / all_gather calls are captured
     INSIDE the graph too (``capture_collectives``, default on since r05;
     ACF_SHARD_RCCL_GRAPH=0 turns it off), after a one-off capture + replay of an
-    all_reduce at construction that every rank must pass (else every rank runs
-    the steps eagerly), so a chunk is again ONE graph with no host round trip
+    all_reduce at construction that every rank must pass, so a chunk is again
+    ONE graph with no host round trip
     per exchange.  A graph holding captured RCCL work keeps the communicator
     busy, so the graphs are dropped before the process group goes: ``close()``,
     the with-block, the object's collection or, failing all three, the
     interpreter's exit (a weakref.finalize; tools/rccl_capture_probe.py checks
-    the orders).  Without captured collectives the steps run eagerly (r03
-    captured the local work between two collectives as separate segments;
-    that path is gone).
+    the orders).  Without captured collectives (the check failed on some rank,
+    or ACF_SHARD_RCCL_GRAPH=0) a chunk is captured as SEGMENTS cut at every
+    collective, the collectives host-issued between the segment replays, with
+    the plans in line while capturing (r04's pipelined plan straddled the cuts:
+    the capture failed -- the "allocator assertion" of r04).
     ``force_collectives`` routes the
     exchanges through the process group even at world 1 (an RCCL self-exchange):
     the one-GPU rehearsal of the captured collectives
@@ -278,12 +280,13 @@ class ShardedAPR:
                       "graph_replays": 0}
         if self._cap_coll:  # here, where every rank is: the check is itself a collective
             self._cap_coll = self._collectives_capturable()
-        if multi and not self._cap_coll:
-            # steps with collectives are captured only with the collectives inside
-            # the graph; otherwise they run eagerly (capturing the local work between
-            # the collectives as separate segments met an allocator assertion in the
-            # RCCL rehearsal -- HIPCachingAllocator use_count -- and is not used)
-            self.graph = False
+        # without the collectives inside (the check failed, or capture_collectives
+        # off), a chunk's steps are captured as SEGMENTS cut at every collective,
+        # which runs host-issued between the segment replays (_SegmentRecorder); the
+        # segments are captured with the plans in line (_run_steps): r04's pipelined
+        # plan forked a side stream across a cut -- unjoined work in the segment,
+        # the capture failed and the RCCL call after it met a broken capture state
+        # (tools/segment_capture_probe.py)
     # -- buffers -------------------------------------------------------------------
     def _ensure(self, T: int, C: int) -> None:
         if C <= self._C and T <= self._T:
@@ -582,10 +585,10 @@ class ShardedAPR:
 
     # -- one step ------------------------------------------------------------------
     def _pipelined(self) -> bool:
-        """The next step's plan beside this step: the local passes support it.  A
-        capture never cuts the chunk into segments any more (its collectives are
-        inside the graph, or there are none: world 1), so the side-stream plan is
-        a branch of the captured graph, forked and joined by events."""
+        """The next step's plan beside this step: the local passes support it.  In
+        a whole-chunk capture (collectives inside the graph, or none: world 1) the
+        side-stream plan is a branch of the captured graph, forked and joined by
+        events; a segment capture plans in line instead (_run_steps)."""
         return getattr(self.local, "pipelined", False)
 
     def _plan_step(self, m, t: int, nb: list, pipe: bool) -> None:
@@ -685,7 +688,10 @@ class ShardedAPR:
     def _run_steps(self, m, nb: list, hp, count: bool) -> None:
         """The steps of a chunk, each step's plan beside the previous step where
         the local passes allow it (_pipelined)."""
-        pipe = self.device.type == "cuda" and self._pipelined()
+        # never across a segment cut (see the constructor): plans in line while
+        # capturing segments; eager runs and whole-step graphs keep the pipeline
+        segments = self._rec is not None and not self._cap_coll
+        pipe = self.device.type == "cuda" and self._pipelined() and not segments
         if pipe and getattr(self, "_plan_stream", None) is None:
             self._plan_stream = torch.cuda.Stream(self.device)
         self._planned, self._free = [None, None], [None, None]

@@ -281,7 +281,8 @@ class APRContext:
 
     def set_step_overlap(self, on: bool) -> None:
         """Overlapped steps of large batches (default on; identical results either
-        way): batch t's final combine and batch t+1's clean pass in one launch."""
+        way): the fused triplets' steps run beside the two combines, in their
+        launches, instead of in the adversarial pass."""
         call("acf_apr_set_step_overlap", self._ptr, int(bool(on)))
 
     def set_failsafe(self, on: bool) -> None:

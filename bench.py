@@ -302,7 +302,7 @@ def large_batch_roofline(acf, ops, dev, ds, d=128, nb=256, chunk=32, step_overla
     tabs = [torch.randn(U1, d, device=dev, generator=g) * 0.01, torch.randn(I1, d, device=dev, generator=g) * 0.01,
             torch.full((U1, d), 0.1, device=dev), torch.full((I1, d), 0.1, device=dev)]
     pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev)
-    pipe.set_step_overlap(step_overlap)  # batch t's final combine beside batch t+1's clean pass (A/B)
+    pipe.set_step_overlap(step_overlap)  # the fused triplets ride in the combine launches (A/B)
     hp = ops.StepHParams(adver=1)
     pipe.run(tabs, hp, u, i, j, 0, nb)  # warm (graph capture)
     torch.cuda.synchronize(dev)

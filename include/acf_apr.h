@@ -184,13 +184,16 @@ int acf_apr_plan_kind(const acf_apr_ctx* ctx);
 
 /* Overlapped APR steps of triplet-centric plans (one lane-group per slot with
  * fusion: batches of 4,096 triplets and more) in acf_apr_train_planned (1 = on,
- * the default; 0 = off; per context).  Batch t's final combine (shared rows'
- * Adagrad) and batch t+1's clean pass run in ONE launch: a t+1 triplet whose row
- * batch t is still updating waits for that row alone (bounded spin on a per-row
- * word).  Arithmetic and order of every sum are unchanged, so on and off give
- * identical bits.  Uses 8 x (num_user_rows + num_item_rows) bytes of device
- * memory, allocated at first use.  Not part of the reference surface.  (r04's
- * overlapped schedule of small batches, k_ovl, is gone: k_stream replaced it.) */
+ * the default; 0 = off; per context).  The batch's fused triplets (all three
+ * rows occurring once in the batch) run their whole step beside the two
+ * combines of the shared rows, in the same launches, instead of in the
+ * adversarial pass; the clean and adversarial passes take the other triplets.
+ * Every triplet's arithmetic is unchanged, so on and off give identical bits.
+ * The two-phase API (acf_apr_delta_update / acf_apr_apply) always runs the
+ * fused triplets in its adversarial pass.  Not part of the reference surface.
+ * (r04's overlapped schedule of small batches, k_ovl, is gone: k_stream
+ * replaced it; r05's k_tri_c2c, batch t's final combine beside batch t+1's
+ * clean pass, was slower and is gone too.) */
 int acf_apr_set_step_overlap(acf_apr_ctx* ctx, int32_t on);
 
 /* Streamed APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;

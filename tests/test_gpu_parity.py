@@ -552,13 +552,13 @@ def _zipf_large(seed, U1, I1, d, B, nb, s=1.1):
 
 @pytest.mark.parametrize("d", [64, 128])
 def test_tri_overlap_bit_identical(ops, dev, d):
-    """The overlapped triplet-centric step (r05, k_tri_c2c: batch t's final
-    combine and batch t+1's clean pass in one launch, the rows batch t is still
-    updating handed over row by row) against four launches per batch: identical
-    bits for tables, accumulators and both losses over 5 Zipf batches of 32,768
-    (hot items shared by consecutive batches), whole range and piecewise, graph
-    and eager; no wait gave up; time_kernels sees the overlapped launch sequence
-    (one clean pass, then per batch combine<0>, adv, combine<2> + next clean)."""
+    """The overlapped triplet-centric step (r05 riders: the fused triplets' whole
+    steps run in the two combine launches, the clean and adversarial passes take
+    the others from the plan's per-batch lists) against the batch-order passes:
+    identical bits for tables, accumulators and both losses over 5 Zipf batches
+    of 32,768 (hot items shared by consecutive batches), whole range and
+    piecewise, graph and eager; no wait gave up; time_kernels sees four launches
+    per batch (clean, combine<0>, adv, combine<2>) and the closing flush."""
     U1, I1, B, nb = 200_000, 100_000, 32768, 5
     P, Q, u, i, j = _zipf_large(41 + d, U1, I1, d, B, nb)
     j[::11] = i[::11]  # i == j occurrences (the trainList quirk)
@@ -585,7 +585,7 @@ def test_tri_overlap_bit_identical(ops, dev, d):
     ctx = ops.APRContext(U1, I1, d, B, nb, dev)
     ctx.plan(uu, ii, jj, B)
     t = ctx.time_kernels(_gpu_tables(P, Q, dev), hp)
-    assert {k: v[1] for k, v in t.items()} == {"clean": 1, "adv": nb, "flush": 1, "stream": 0, "hot": 2 * nb}
+    assert {k: v[1] for k, v in t.items()} == {"clean": nb, "adv": nb, "flush": 1, "stream": 0, "hot": 2 * nb}
     assert ctx.step_errors() == 0
 
 

@@ -1,5 +1,6 @@
-# r05: the overlapped triplet-centric step (k_tri_c2c) -- its parity tests, then
-# the configs[4] d = 64 / 128 lines with the overlap on and off, interleaved.
+# r05: the overlapped triplet-centric step (riders: the fused triplets beside the
+# combines) -- its parity tests, the segment-capture fix, then the configs[4]
+# d = 64 / 128 lines with the overlap on and off, interleaved.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${OUT_TAG:-tri_overlap}
 mkdir -p $OUT
@@ -12,5 +13,11 @@ timeout -k 10 300 python3 -u -m pytest -x -q --timeout 300 --timeout-method thre
 rc=$?
 tail -2 $OUT/config5.log
 [ $rc -eq 0 ] || { echo "config5 rc $rc: stopping"; exit $rc; }
+if [ -n "$WITH_SHARD" ]; then
+  timeout -k 10 300 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_distributed.py -k captured > $OUT/captured.log 2>&1
+  rc=$?
+  grep -E "PASSED|FAILED|ERROR|passed|failed" $OUT/captured.log | tail -4
+  [ $rc -eq 0 ] || { echo "captured rc $rc: stopping"; exit $rc; }
+fi
 timeout -k 10 500 python3 tools/large_line.py ${LINES:-64 64:noovl 64 64:noovl 128 128:noovl} > $OUT/lines.json 2> $OUT/lines.err || { tail -20 $OUT/lines.err; exit 1; }
-cat $OUT/lines.json | cut -c1-400
+cut -c1-400 $OUT/lines.json

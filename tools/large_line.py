@@ -1,6 +1,7 @@
 """configs[4] line(s) alone (bench.large_batch_roofline) for same-box A/B runs:
 python3 tools/large_line.py [d[:noovl] ...] -> one JSON line per entry
-(":noovl": the overlapped step off, acf_apr_set_step_overlap 0)."""
+(":noovl": the overlapped step off -- the fused triplets in the adversarial pass
+instead of beside the combines, acf_apr_set_step_overlap 0)."""
 import importlib
 import json
 import os
