@@ -59,7 +59,6 @@ SIGNATURES = {
     "acf_apr_set_plan_mode": (ctypes.c_int, [_P, _I32]),
     "acf_apr_plan_kind": (ctypes.c_int, [_P]),
     "acf_apr_set_stream": (ctypes.c_int, [_P, _I32]),
-    "acf_apr_set_step_overlap": (ctypes.c_int, [_P, _I32]),
     "acf_apr_step_errors": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), _P]),
     "acf_apr_set_failsafe": (ctypes.c_int, [_P, _I32]),
     "acf_apr_set_spin_limit": (ctypes.c_int, [_P, _I32]),

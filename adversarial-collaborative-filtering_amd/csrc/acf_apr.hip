@@ -577,37 +577,6 @@ __device__ __forceinline__ void records_one(int64_t e, int32_t t, int32_t ub0, i
   }
 }
 
-// Per-batch triplet lists of triplet-centric plans (riders, StepArgs.tsel):
-// batch t's non-fused triplets from the front of tlist[t][0, B), its fused ones
-// (all three rows single) from the back, counted in tcnt[2t] / tcnt[2t + 1]
-// (zeroed by the plan).  Wave-aggregated appends: one atomic per list per wave
-// when the wave's triplets share a batch (B % 64 == 0 always does).  The order
-// in a list varies from run to run; no triplet's step depends on it.
-__device__ __forceinline__ void tri_list_put(int32_t* tlist, int32_t* tcnt, int32_t B, int32_t t, int32_t b,
-                                             bool fused) {
-  const int lane = (int)__lane_id();
-  const int lead = __ffsll((unsigned long long)__ballot(1)) - 1;
-  const int32_t tl = __shfl(t, lead);
-  int32_t* row = tlist + (int64_t)t * B;
-  if (__all(t == tl)) {
-    const uint64_t mf = __ballot(fused), mn = __ballot(!fused);
-    int32_t bf = 0, bn = 0;
-    if (lane == lead) {
-      if (mf) bf = atomicAdd(tcnt + 2 * t + 1, (int32_t)__popcll(mf));
-      if (mn) bn = atomicAdd(tcnt + 2 * t, (int32_t)__popcll(mn));
-    }
-    bf = __shfl(bf, lead);
-    bn = __shfl(bn, lead);
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    if (fused) row[B - 1 - (bf + (int32_t)__popcll(mf & below))] = b;
-    else row[bn + (int32_t)__popcll(mn & below)] = b;
-  } else if (fused) {
-    row[B - 1 - atomicAdd(tcnt + 2 * t + 1, 1)] = b;
-  } else {
-    row[atomicAdd(tcnt + 2 * t, 1)] = b;
-  }
-}
-
 __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t gen, int32_t kb, int32_t no_fuse,
                           int32_t tri,
                           const int4* __restrict__ tsl, const int4* __restrict__ tpos,
@@ -615,19 +584,13 @@ __global__ void k_records(int64_t E, int32_t B, int32_t S, int32_t R, int32_t ge
                           const int32_t* __restrict__ ubs, const int32_t* __restrict__ ibs,
                           OccRec* __restrict__ urec, OccRec* __restrict__ irec,
                           OccRec* __restrict__ inl, OccRec* __restrict__ trec,
-                          int32_t* __restrict__ gen_ptr, uint64_t* __restrict__ sflags, HotLists hl,
-                          int32_t* __restrict__ tlist, int32_t* __restrict__ tcnt) {
+                          int32_t* __restrict__ gen_ptr, uint64_t* __restrict__ sflags, HotLists hl) {
   const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (e == 0) *gen_ptr = gen;
   if (e >= E) return;
   const int32_t t = (int32_t)(e / B);
   records_one(e, t, ubs[t], ubs[t + 1] - ubs[t], ibs[t], S, R, gen, kb, no_fuse, tri, tsl, tpos, uinfo, iinfo,
               urec, irec, inl, trec, sflags, hl);
-  if (tlist) {  // triplet-centric plans: fused = all three rows single (trec's flag 1)
-    const int4 sl = tsl[e];
-    const bool fused = info_count(uinfo[sl.x]) == 1 && info_count(iinfo[sl.y]) == 1 && info_count(iinfo[sl.z]) == 1;
-    tri_list_put(tlist, tcnt, B, t, (int32_t)(e - (int64_t)t * B), fused);
-  }
 }
 
 __global__ void k_slot_lists(const uint64_t* __restrict__ flags, const uint64_t* __restrict__ incl,
@@ -1373,13 +1336,6 @@ struct StepArgs {
   // triplet-centric list step (k_tri_*): per-occurrence contributions of shared rows
   const int4* tpos;    // [E] CSR positions of a triplet's three occurrences
   float* contrib;      // users [B][2][d] (positive, negative branch), then items [2B][d]
-  // (r05) riders: APR steps of triplet-centric plans over the plan's per-batch
-  // triplet lists (tlist / tcnt, tri_list_put): k_tri_clean and k_tri_adv run
-  // the non-fused triplets (tsel 1), the fused ones ride in the combine
-  // launches (tsel 2 / 3, tri_riders); tsel 0: every triplet in batch order
-  const int32_t* tlist;  // [nb][B]
-  const int32_t* tcnt;   // [nb][2]: non-fused, fused
-  int32_t tsel, rider_waves;
   int32_t inplace;     // triplet-centric plans: every row is updated in its table (no W scratch)
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
   int32_t adver, adv_mode, zero_delta;
@@ -3070,59 +3026,16 @@ __device__ __forceinline__ void tri_rec(const StepArgs& a, int b, RecV& r, int4&
 // many wave rounds
 __host__ __device__ constexpr int tri_gpw(int nv) { return nv == 1 ? 2 : 1; }
 
-// list positions x0, x0 + 64/LPR, ... (< hi) of batch a.t's triplet list (back:
-// the fused end, position x at [B - 1 - x]; see tri_list_put): the groups of
-// tri_triplets (GPW of them per wave), with one dependent load (the list) in
-// front of the records
-template <int LPR, int NV, int PASS, int GPW>
-__device__ __forceinline__ void tri_list_group(const StepArgs& a, int x0, int hi, bool back, int lane) {
-  constexpr int OPW = 64 / LPR;
-  const int32_t* lst = a.tlist + (int64_t)a.t * a.B;
-  int bb[GPW];
-#pragma unroll
-  for (int x = 0; x < GPW; ++x) {
-    const int pos = x0 + x * OPW;
-    bb[x] = pos < hi ? lst[back ? a.B - 1 - pos : pos] : a.B;
-  }
-  RecV r[GPW];
-  int4 ps[GPW];
-#pragma unroll
-  for (int x = 0; x < GPW; ++x) tri_rec(a, bb[x], r[x], ps[x]);
-#pragma unroll
-  for (int x = 0; x < GPW; ++x) tri_triplet_r<LPR, NV, PASS>(a, bb[x], lane & (LPR - 1), r[x], ps[x]);
-}
-
 template <int LPR, int NV, int PASS>
 __device__ __forceinline__ void tri_triplets(const StepArgs& a, int tw, int lane) {
   constexpr int OPW = 64 / LPR, GPW = tri_gpw(NV);
   const int b0 = tw * GPW * OPW + lane / LPR;
-  if (a.tsel) {  // the non-fused triplets only (the fused ones ride in the combines)
-    tri_list_group<LPR, NV, PASS, GPW>(a, b0, a.tcnt[2 * a.t], false, lane);
-    return;
-  }
   RecV r[GPW];
   int4 ps[GPW];
 #pragma unroll
   for (int x = 0; x < GPW; ++x) tri_rec(a, b0 + x * OPW, r[x], ps[x]);
 #pragma unroll
   for (int x = 0; x < GPW; ++x) tri_triplet_r<LPR, NV, PASS>(a, b0 + x * OPW, lane & (LPR - 1), r[x], ps[x]);
-}
-
-// Riders (StepArgs.tsel 2 / 3): waves after a combine's own run the batch's
-// fused triplets -- their whole APR step (PASS 2), which needs nothing any
-// combine produces and touches no row a combine reads or writes (all three
-// rows occur once in the batch) -- while the combine's hot chain leaves the
-// chip idle.  tsel 2 (in k_tri_combine<0>): fused positions [0, half); 3
-// (k_tri_combine<2>): the rest; rider_waves waves stride over the groups, one
-// group at a time (two, as k_tri_adv, took the combine launch from 94 / 116 to
-// 145 VGPRs).
-template <int LPR, int NV>
-__device__ __forceinline__ void tri_riders(const StepArgs& a, int rw, int lane) {
-  constexpr int PER = 64 / LPR;
-  const int nf = a.tcnt[2 * a.t + 1], half = (nf + 1) >> 1;
-  const int lo = a.tsel == 2 ? 0 : half, hi = a.tsel == 2 ? half : nf;
-  for (int g0 = lo + rw * PER; g0 < hi; g0 += a.rider_waves * PER)
-    tri_list_group<LPR, NV, 2, 1>(a, g0 + lane / LPR, hi, true, lane);
 }
 
 // header of shared slot k: count, side, own row, source, local CSR base
@@ -3231,7 +3144,9 @@ __global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
   if (wave >= a.slot_waves) {
+    STAMP(a.diag_launch, wave, 0);
     tri_triplets<LPR, NV, BPR ? 1 : 0>(a, wave - a.slot_waves, lane);
+    STAMP(a.diag_launch, wave, 5);
     return;
   }
   if (!a.prev_valid) return;  // write-back of the rows batch t-1 left in W scratch
@@ -3323,11 +3238,13 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
   __syncthreads();
 }
 
-// Hot slots first in dispatch order, so their chain (pieces -> arrival count ->
+// Hot pieces first in dispatch order, so their chain (pieces -> arrival count ->
 // combining workgroup) starts at once: piece waves [0, hot_waves) into hot_part,
-// then hot_blocks workgroups that each combine hot slots as k_hot_combine does
-// once all their pieces are stored, then slot waves [.., + slot_waves): shared
-// slots with <= ACF_HOT_MIN occurrences, one lane-group each, in order.  A piece
+// then slot waves [.., + slot_waves): shared slots with <= ACF_HOT_MIN
+// occurrences, one lane-group each, in order, then hot_blocks workgroups that
+// each combine hot slots as k_hot_combine does once all their pieces are stored
+// (r05: before the slot waves they held the CUs while they waited, and the slot
+// waves, the launch's tail in the diag-build stamps, started up to 9 us late).  A piece
 // is stored write-through, the wave drains its stores, and one lane adds 1 to
 // the slot's arrival count; a combining workgroup polls that count (device
 // scope), and every load of the pieces is a device-scope load (Guideline 16,
@@ -3335,11 +3252,12 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
 // order, so the pieces they wait for are already running: the launch always
 // drains.  (hot_waves is a multiple of 4: whole workgroups.)
 template <int LPR, int NV, int MODE>
-__global__ void __launch_bounds__(256, (NV == 1 && MODE != 1) ? 4 : 1) k_tri_combine(StepArgs a) {
+__global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
   __shared__ float4 red[NV * 256];
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
   int32_t* arrive = a.hot.arrive + (int64_t)a.t * a.hot.piece_stride;
+  STAMP(a.diag_launch, wave, 0);  // diagnostic builds: 1 piece, 2 / 3 combiner waited / done, 4 slot wave done
   if (wave < a.hot_waves) {
     const int hw = wave;
     constexpr int TEAM = 64 / LPR;
@@ -3366,10 +3284,17 @@ __global__ void __launch_bounds__(256, (NV == 1 && MODE != 1) ? 4 : 1) k_tri_com
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(arrive + pc.w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    STAMP(a.diag_launch, wave, 1);
     return;
   }
-  const int hb = (wave - a.hot_waves) >> 2;
-  if (hb < a.hot_blocks) {  // hot-slot combining workgroups (whole workgroups)
+  // then the small-slot waves [hot_waves, + slot_waves), then the combining
+  // workgroups (r05: the small slots first, so they do not queue behind
+  // workgroups that are waiting for pieces; 727M -> 747-763M triplets/s at
+  // configs[4] d = 64, same box)
+  const int w2 = wave - a.hot_waves;
+  if (w2 >= a.slot_waves) {  // hot-slot combining workgroups (whole workgroups)
+    const int hb = (w2 - a.slot_waves) >> 2;
+    if (hb >= a.hot_blocks) return;
     const int n = a.hot.cnt[a.t];
     const int4* hl = a.hot.list + (int64_t)a.t * a.hot.hot_stride;
     for (int hx = hb; hx < n; hx += a.hot_blocks) {
@@ -3389,15 +3314,13 @@ __global__ void __launch_bounds__(256, (NV == 1 && MODE != 1) ? 4 : 1) k_tri_com
         __hip_atomic_store(arrive + e.z, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __syncthreads();
+      if (hx == hb) STAMP(a.diag_launch, wave, 2);
       tri_hot_finish<LPR, NV, MODE>(a, e, red, pre);
     }
+    STAMP(a.diag_launch, wave, 3);
     return;
   }
-  const int sw = wave - a.hot_waves - 4 * a.hot_blocks;
-  if (sw >= a.slot_waves) {
-    if (MODE != 1 && a.tsel >= 2) tri_riders<LPR, NV>(a, sw - a.slot_waves, lane);
-    return;
-  }
+  const int sw = w2;
   const int ngroups = a.slot_waves * (64 / LPR), gid = sw * (64 / LPR) + g;
   const int n = a.slot_cnt[a.t];
   const int32_t* lst = a.slot_list + (int64_t)a.t * a.S;
@@ -3408,13 +3331,16 @@ __global__ void __launch_bounds__(256, (NV == 1 && MODE != 1) ? 4 : 1) k_tri_com
     tri_add_q<LPR, NV>(a, h, 0, h.count, 1, l, G);
     tri_finish<LPR, NV, MODE>(a, k, h, G, l);
   }
+  STAMP(a.diag_launch, wave, 4);
 }
 
 // k_tri_adv: 4 blocks (16 waves) per CU asked of the register allocator (d <= 256)
 template <int LPR, int NV>
 __global__ void __launch_bounds__(256, NV == 1 ? 4 : 1) k_tri_adv(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  STAMP(a.diag_launch, wave, 0);
   tri_triplets<LPR, NV, 2>(a, wave, threadIdx.x & 63);
+  STAMP(a.diag_launch, wave, 5);
 }
 
 // Flush the pending rows of batch t (wnew_cur) to the tables (end of a call):
@@ -3646,8 +3572,6 @@ struct acf_apr_ctx {
   int4 *uinfo = nullptr, *iinfo = nullptr;   // per unique row, see k_slot_info
   int32_t *iuniq = nullptr, *ioff = nullptr, *ibs = nullptr;
   OccRec* trec = nullptr;
-  int32_t* tlist = nullptr;  // [maxE] per-batch triplet lists of triplet-centric plans (tri_list_put)
-  int32_t* tcnt = nullptr;   // [2 maxNB] their counts: non-fused, fused
   OccRec *urec = nullptr, *irec = nullptr, *inl = nullptr;
   int32_t *err = nullptr, *gen_dev = nullptr;
   void* tmp = nullptr;
@@ -3670,7 +3594,6 @@ struct acf_apr_ctx {
   int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
-  int32_t riders = 1;   // fused triplets ride in the combine launches (acf_apr_set_step_overlap)
   int32_t plan_kind2 = 0;  // the plan encodes sources at every distance (k_prev_next)
   int32_t plan_kb = 1;     // slot bits of the plan's src encoding
   int32_t* nextt = nullptr;  // [maxNB][S] next batch touching each slot's row (k_prev_next)
@@ -3858,7 +3781,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->contrib, (size_t)4 * maxB * d);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
   A(&c->iinfo, 2 * maxE);
-  A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE); A(&c->tlist, maxE); A(&c->tcnt, 2 * maxNB);
+  A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
   A(&c->inl, (size_t)maxNB * S * c->R);
   A(&c->err, 4); A(&c->gen_dev, 4); A(&c->epoch, 4); A(&c->decide, 16 + 2 * 144);
   A(&c->g0, 2 * S * d); A(&c->delta, 2 * S * d);  // by batch parity
@@ -4126,7 +4049,6 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   const int64_t E = (int64_t)B * nb;
   const int32_t pb = hplan_pbits(B, ACF_HPLAN_PART);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));  // the other counters: k_hplan_keys
-  HIP_TRY(hipMemsetAsync(c->tcnt, 0, 2 * (size_t)nb * sizeof(int32_t), s));
   HPlanArgs p;
   p.user = user; p.ipos = ipos; p.ineg = ineg;
   p.U1 = c->U1; p.I1 = c->I1;
@@ -4145,7 +4067,6 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   p.pbase = c->hplan_ptot + ((size_t)c->maxNB << hplan_pbits(c->maxB, ACF_HPLAN_PART)) * ACF_HPLAN_TOT;
   p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
   p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
-  p.tlist = c->tlist; p.tcnt = c->tcnt;
   p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt; p.flush_cnt = c->flush_cnt;
   p.saux = c->flush_list;  // unused by in-place plans
   p.haux = c->hplan_haux;
@@ -4416,7 +4337,6 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
     // current (k_flush scans every slot of the batch).
     HIP_TRY(hipMemsetAsync(c->inl, 0, (size_t)nb * 3 * B * sizeof(OccRec), s));
   }
-  if (c->tri) HIP_TRY(hipMemsetAsync(c->tcnt, 0, 2 * (size_t)nb * sizeof(int32_t), s));
   if (packed) {  // k_records writes the slot flags of the slots it finds; the rest read 0
     HIP_TRY(hipMemsetAsync(c->key_in, 0, (size_t)3 * E * sizeof(uint64_t), s));
     HIP_TRY(hipMemsetAsync(c->hot.cnt, 0, 2 * (size_t)c->maxNB * sizeof(int32_t), s));
@@ -4426,8 +4346,7 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
                                         reinterpret_cast<const int4*>(c->tsl),
                                         reinterpret_cast<const int4*>(c->tpos), c->uinfo, c->iinfo,
                                         c->ubs, c->ibs, c->urec, c->irec, c->inl, c->trec, c->gen_dev,
-                                        packed ? c->key_in : nullptr, c->hot, c->tri ? c->tlist : nullptr,
-                                        c->tcnt);
+                                        packed ? c->key_in : nullptr, c->hot);
   HIP_TRY(hipGetLastError());
   c->task_lists = 0;
   if (all_dt) {  // streamed-step task lists
@@ -4511,8 +4430,6 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
   a.contrib = c->contrib;
   a.inplace = c->tri;
-  a.tlist = c->tlist; a.tcnt = c->tcnt;
-  a.tsel = a.rider_waves = 0;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
   a.clip_lo = hp->clip_lo; a.clip_hi = hp->clip_hi;
   a.adver = hp->adver; a.adv_mode = hp->adv_mode; a.zero_delta = hp->zero_delta; a.seed = hp->seed;
@@ -4534,7 +4451,6 @@ struct Kernels {
 };
 
 #define ACF_LIST_WAVES 4096  // slot waves of a list kernel
-#define ACF_TRI_RIDER_WAVES 2048  // rider waves after each combine's (tri_riders)
 #define ACF_TRI_COMB_WAVES 4096  // small-slot waves of k_tri_combine (512 / 1,024 slower: r04 A/B)
 #define ACF_TAIL_FLUSHERS 128    // workgroups of k_stream's tail write-back
 #define ACF_HOT_WAVES 2048   // piece waves of a list kernel (hot slots)
@@ -4838,11 +4754,6 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
     const int SWT = std::min(SW, ACF_TRI_COMB_WAVES);
     const int SW4 = (SWT + 3) & ~3, HW4 = (HW + 3) & ~3, HBT = std::min(HB, ACF_TRI_HOT_BLOCKS);
     const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);  // one lane-group per triplet
-    const int TW = (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv);
-    // riders (whole APR steps; see tri_riders): clean and adversarial passes over
-    // the non-fused triplets, the fused ones in RW waves after each combine's
-    const bool riders = hp->adver && tri_phases == 3 && c->riders;
-    const int RW = riders ? std::min(TW, ACF_TRI_RIDER_WAVES) : 0;
     for (int32_t t = first; t < first + n; ++t) {
       // every row is updated in its table (StepArgs.inplace): nothing pending from t-1
       StepArgs a = make_args(c, tb, hp, t, 0);
@@ -4859,27 +4770,17 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
       ac.hot_blocks = HBT;
       const int CW = SW4 + HW4 + 4 * HBT;
       (void)ah;
-      if (riders) {
-        a.tsel = at.tsel = 1;
-        StepArgs ar = ac;
-        ar.rider_waves = RW;
-        ar.tsel = 2;
-        ACF_RET(L(K.tri_clean, at, TW, 0));
-        ACF_RET(L(K.tri_comb[0], ar, CW + RW, 5));
-        ACF_RET(L(K.tri_adv, a, TW, 1));
-        ar.tsel = 3;
-        ACF_RET(L(K.tri_comb[2], ar, CW + RW, 5));
-      } else if (hp->adver) {
+      if (hp->adver) {
         if (tri_phases & 1) {
-          ACF_RET(L(K.tri_clean, at, TW, 0));
+          ACF_RET(L(K.tri_clean, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
           ACF_RET(L(K.tri_comb[0], ac, CW, 5));
         }
         if (tri_phases & 2) {
-          ACF_RET(L(K.tri_adv, a, TW, 1));
+          ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
           ACF_RET(L(K.tri_comb[2], ac, CW, 5));
         }
       } else if (tri_phases & 2) {
-        ACF_RET(L(K.tri_clean_bpr, at, TW, 0));
+        ACF_RET(L(K.tri_clean_bpr, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
         ACF_RET(L(K.tri_comb[1], ac, CW, 5));
       }
     }
@@ -5078,13 +4979,6 @@ extern "C" int acf_apr_set_fusion(acf_apr_ctx* c, int32_t on) {
   ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
   ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "fusion must be 0 or 1, got %d", on);
   c->fusion = on;
-  return ACF_OK;
-}
-
-extern "C" int acf_apr_set_step_overlap(acf_apr_ctx* c, int32_t on) {
-  ACF_CHECK(c, ACF_E_INVALID, "ctx is NULL");
-  ACF_CHECK(on == 0 || on == 1, ACF_E_INVALID, "step overlap must be 0 or 1, got %d", on);
-  c->riders = on;
   return ACF_OK;
 }
 

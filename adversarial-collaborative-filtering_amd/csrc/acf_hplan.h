@@ -64,8 +64,6 @@ struct HPlanArgs {
   OccRec* inl;
   OccRec* trec;
   int32_t* tpos;              // [E][4] CSR positions of the triplet's occurrences
-  int32_t* tlist;             // [nb][B] the batch's non-fused / fused triplets (tri_list_put)
-  int32_t* tcnt;              // [nb][2] (zeroed before k_hplan_trip)
   int32_t* slot_list;
   int32_t* slot_cnt;
   int32_t* flush_cnt;
@@ -489,7 +487,6 @@ __global__ void __launch_bounds__(256) k_hplan_trip(HPlanArgs p) {
   q.pb_slot = (int32_t)e;
   q.gen = p.gen;
   p.trec[e] = q;
-  tri_list_put(p.tlist, p.tcnt, B, t, b, su && si && sj);
 }
 
 // CSR position of occurrence id v (users: b; items: 2b + role) of batch t at sorted place x

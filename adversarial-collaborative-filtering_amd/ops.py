@@ -279,12 +279,6 @@ class APRContext:
         launch runs the whole batch range through tagged row versions."""
         call("acf_apr_set_stream", self._ptr, int(bool(on)))
 
-    def set_step_overlap(self, on: bool) -> None:
-        """Overlapped steps of large batches (default on; identical results either
-        way): the fused triplets' steps run beside the two combines, in their
-        launches, instead of in the adversarial pass."""
-        call("acf_apr_set_step_overlap", self._ptr, int(bool(on)))
-
     def set_failsafe(self, on: bool) -> None:
         """Verified streamed steps (default on): a streamed call stays asynchronous
         and is queued; if a hand-off wait gave up (k_stream needs all its waves
@@ -433,10 +427,6 @@ class PlanPipeline:
     def set_stream(self, on: bool) -> None:
         for c in self.ctx:
             c.set_stream(on)
-
-    def set_step_overlap(self, on: bool) -> None:
-        for c in self.ctx:
-            c.set_step_overlap(on)
 
     def step_errors(self) -> int:
         e = 0

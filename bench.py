@@ -283,7 +283,7 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
                                     "source": "out/janEval/ml-1m-sort_apr_..._11_56_42.out:54-55 (UCL CPU, TF1)"}}
 
 
-def large_batch_roofline(acf, ops, dev, ds, d=128, nb=256, chunk=32, step_overlap=True):
+def large_batch_roofline(acf, ops, dev, ds, d=128, nb=256, chunk=32, graph=True):
     """BASELINE configs[4] / SURVEY §8(d) "synthetic large" on one GPU: 10M users
     x 5M items (~200M interactions, Zipf items), batch 65,536, triplets from the
     device sampler with its alias-table negatives (equal weights: the reference's
@@ -302,12 +302,11 @@ def large_batch_roofline(acf, ops, dev, ds, d=128, nb=256, chunk=32, step_overla
     tabs = [torch.randn(U1, d, device=dev, generator=g) * 0.01, torch.randn(I1, d, device=dev, generator=g) * 0.01,
             torch.full((U1, d), 0.1, device=dev), torch.full((I1, d), 0.1, device=dev)]
     pipe = ops.PlanPipeline(U1, I1, d, B, chunk, dev)
-    pipe.set_step_overlap(step_overlap)  # the fused triplets ride in the combine launches (A/B)
     hp = ops.StepHParams(adver=1)
-    pipe.run(tabs, hp, u, i, j, 0, nb)  # warm (graph capture)
+    pipe.run(tabs, hp, u, i, j, 0, nb, graph=graph)  # warm (graph capture)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    pipe.run(tabs, hp, u, i, j, 0, nb)
+    pipe.run(tabs, hp, u, i, j, 0, nb, graph=graph)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     errors = pipe.step_errors()
@@ -323,7 +322,6 @@ def large_batch_roofline(acf, ops, dev, ds, d=128, nb=256, chunk=32, step_overla
     rl["step_bandwidth"] = step_bandwidth(d, B, st, nb * B / dt)
     rl["batch_stats"] = {k: round(v, 1) for k, v in st.items()}
     rl["step_errors"] = errors
-    rl["step_overlap"] = bool(step_overlap)
     rl["config"] = {"workload": "APR, synthetic large (BASELINE configs[4], one GPU)", "users": U1 - 1,
                     "items": I1 - 1, "interactions": len(ds), "dim": d, "batch": B, "batches": nb, "chunk": chunk,
                     "negatives": "device sampler, alias table of equal weights (uniform, APR.py:76-78)"}

@@ -182,20 +182,6 @@ int acf_apr_set_plan_mode(acf_apr_ctx* ctx, int32_t mode);
  * of the reference surface (tests and bench). */
 int acf_apr_plan_kind(const acf_apr_ctx* ctx);
 
-/* Overlapped APR steps of triplet-centric plans (one lane-group per slot with
- * fusion: batches of 4,096 triplets and more) in acf_apr_train_planned (1 = on,
- * the default; 0 = off; per context).  The batch's fused triplets (all three
- * rows occurring once in the batch) run their whole step beside the two
- * combines of the shared rows, in the same launches, instead of in the
- * adversarial pass; the clean and adversarial passes take the other triplets.
- * Every triplet's arithmetic is unchanged, so on and off give identical bits.
- * The two-phase API (acf_apr_delta_update / acf_apr_apply) always runs the
- * fused triplets in its adversarial pass.  Not part of the reference surface.
- * (r04's overlapped schedule of small batches, k_ovl, is gone: k_stream
- * replaced it; r05's k_tri_c2c, batch t's final combine beside batch t+1's
- * clean pass, was slower and is gone too.) */
-int acf_apr_set_step_overlap(acf_apr_ctx* ctx, int32_t on);
-
 /* Streamed APR steps in acf_apr_train_planned (1 = on, the default; 0 = off;
  * the setting is per context).  For plans with one wavefront
  * per slot and dim <= 256, ONE launch runs the whole batch range: every row a

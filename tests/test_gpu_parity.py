@@ -550,45 +550,6 @@ def _zipf_large(seed, U1, I1, d, B, nb, s=1.1):
     return P, Q, u, i, j
 
 
-@pytest.mark.parametrize("d", [64, 128])
-def test_tri_overlap_bit_identical(ops, dev, d):
-    """The overlapped triplet-centric step (r05 riders: the fused triplets' whole
-    steps run in the two combine launches, the clean and adversarial passes take
-    the others from the plan's per-batch lists) against the batch-order passes:
-    identical bits for tables, accumulators and both losses over 5 Zipf batches
-    of 32,768 (hot items shared by consecutive batches), whole range and
-    piecewise, graph and eager; no wait gave up; time_kernels sees four launches
-    per batch (clean, combine<0>, adv, combine<2>) and the closing flush."""
-    U1, I1, B, nb = 200_000, 100_000, 32768, 5
-    P, Q, u, i, j = _zipf_large(41 + d, U1, I1, d, B, nb)
-    j[::11] = i[::11]  # i == j occurrences (the trainList quirk)
-    hp = ops.StepHParams(adver=1, reg=0.01)
-    uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
-    runs = []
-    for ovl, pieces, graph in ((False, [(0, nb)], True), (True, [(0, nb)], True), (True, [(0, nb)], False),
-                               (True, [(0, 2), (2, nb - 2)], True), (True, [(0, 1), (1, nb - 1)], False)):
-        ctx = ops.APRContext(U1, I1, d, B, nb, dev)
-        ctx.set_step_overlap(ovl)
-        ctx.plan(uu, ii, jj, B)
-        assert ctx.plan_kind() == "hash"
-        tabs = _gpu_tables(P, Q, dev)
-        for first, n in pieces:
-            ctx.train_planned(tabs, hp, first, n, graph=graph)
-        lc, la = ctx.losses()
-        assert ctx.step_errors() == 0
-        runs.append(tabs + [lc.clone(), la.clone()])
-    torch.cuda.synchronize()
-    names = ("P", "Q", "accP", "accQ", "loss_clean", "loss_adv")
-    for k, other in enumerate(runs[1:]):
-        for x, y, n in zip(runs[0], other, names):
-            assert torch.equal(x, y), (k, n)
-    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
-    ctx.plan(uu, ii, jj, B)
-    t = ctx.time_kernels(_gpu_tables(P, Q, dev), hp)
-    assert {k: v[1] for k, v in t.items()} == {"clean": nb, "adv": nb, "flush": 1, "stream": 0, "hot": 2 * nb}
-    assert ctx.step_errors() == 0
-
-
 @pytest.mark.parametrize("d,adver", [(64, 1), (128, 1), (64, 0)])
 def test_hot_slots_large_batch_match_oracle(ops, oracle, dev, d, adver, fp32_parity):
     """B = 65,536 with Zipf positives: slots with more than ACF_HOT_MIN (8)

@@ -1,13 +1,10 @@
-# same-box A/B of two builds of libacf_apr.so on the large-batch lines (tools/ab/base.so vs tools/ab/new.so)
-set -e
+# Same-box A/B of the large-batch (configs[4]) lines: this build against an older
+# commit's library (tools/build_at.sh <rev> first; OLD=rev), interleaved.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/${OUT_TAG:-ab}
-mkdir -p $OUT
-LIB=adversarial-collaborative-filtering_amd/lib/libacf_apr.so
-for v in ${VARIANTS:-base new base new}; do
-  cp tools/ab/$v.so $LIB
-  timeout -k 10 300 python3 bench.py --no-sharded --no-neumf --no-cpu-baseline --no-eval --steps 20 --warmup 5 > $OUT/b_$v.json 2> $OUT/b_$v.err
-  python3 -c "
-import json;d=json.loads(open('$OUT/b_$v.json').read().strip().splitlines()[-1])
-print('$v', d['value'], *[(k[-3:], d[k]['avg_launch_us'], d[k]['frac'], d[k]['per_kernel_avg_us']['clean'], d[k]['per_kernel_avg_us']['hot'], round(d[k]['triplets_per_s']/1e6,1)) for k in ('roofline_large_batch','roofline_large_batch_d64')])"
+OUT=gpurun_out/${OUT_TAG:-ab_large}; mkdir -p $OUT
+OLD=${OLD:-82557ee}
+for k in 1 2; do
+  timeout -k 10 300 python3 tools/large_line.py ${LINES:-64 128} > $OUT/new$k.json 2> $OUT/new$k.err || { tail -20 $OUT/new$k.err; exit 1; }
+  ACF_LARGE_LINE_LIB=$PWD/tools/libacf_apr_$OLD.so timeout -k 10 300 python3 tools/large_line.py ${LINES:-64 128} > $OUT/old$k.json 2> $OUT/old$k.err || { tail -20 $OUT/old$k.err; exit 1; }
 done
+cut -c1-300 $OUT/new1.json $OUT/old1.json $OUT/new2.json $OUT/old2.json
