@@ -1326,6 +1326,11 @@ struct StepArgs {
   // other item slots' sums from g0 (no separate copy launch)
   float* xbuf;
   const int64_t* xmap;
+  // triplet-centric shard passes (r05): the owners' item deltas, row w's at
+  // xdelta[xdmap[w]] (the exchange rows acf_apr_shard_items_mapped dir 1 names),
+  // read by k_tri_adv in place of a copy into the delta slots
+  const float* xdelta;
+  const int64_t* xdmap;
   const int32_t* xubs;  // the plan's user / item slot bounds (one batch)
   const int32_t* xibs;
   int32_t xn, xblocks;
@@ -2900,6 +2905,11 @@ __device__ __forceinline__ float* tri_ci(const StepArgs& a) { return a.contrib +
 // PASS 0: APR clean (shared rows: clean contributions; single rows: nothing,
 // k_tri_adv recomputes their term); 1: BPR (single rows: Adagrad; shared:
 // contributions); 2: APR adversarial.
+// Shard mode (r05, distributed.ShardedAPR's local passes): an item's sum here is
+// a partial one for its owner, so a single item row is neither perturbed nor
+// stepped locally: its one product is its partial sum, stored straight to its
+// exchange row (the slot path's 0 + product), and pass 2 reads the owners'
+// item deltas from theirs; users are complete locally and step as above.
 template <int LPR, int NV, int PASS>
 __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, const RecV& r, const int4 ps) {
   if (b >= a.B) return;
@@ -2914,6 +2924,7 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
   const int32_t u = r.a.x, i = r.a.y, j = r.a.z;
   const int32_t ku = r.a.w, ki = r.b.x, kj = r.b.y;
   const bool su = (flags & TRI_SU) != 0, si = (flags & TRI_SI) != 0, sj = (flags & TRI_SJ) != 0;
+  const bool ai = si && !a.shard, aj = sj && !a.shard;  // single item rows stepped here
   RowV<NV> p, qi, qj;
   if (PASS == 2) {  // the tables are current (k_tri_clean wrote back batch t-1)
     p = load_row<LPR, NV>(a.P, u, d, l);
@@ -2927,13 +2938,18 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
   RowV<NV> cu, ci, cj, du, di, dj;  // Adagrad slots of the single rows, deltas of the shared ones
   if (PASS != 0) {
     if (su) cu = load_row<LPR, NV>(a.accP, u, d, l);
-    if (si) ci = load_row<LPR, NV>(a.accQ, i, d, l);
-    if (sj) cj = load_row<LPR, NV>(a.accQ, j, d, l);
+    if (ai) ci = load_row<LPR, NV>(a.accQ, i, d, l);
+    if (aj) cj = load_row<LPR, NV>(a.accQ, j, d, l);
   }
   if (PASS == 2) {  // issued with the row loads, not after the clean term
     if (!su) du = load_row<LPR, NV>(a.delta, ku, d, l);
-    if (!si) di = load_row<LPR, NV>(a.delta, ki, d, l);
-    if (!sj) dj = load_row<LPR, NV>(a.delta, kj, d, l);
+    if (a.shard) {  // items: the owners' deltas, straight from the exchange rows
+      di = load_row<LPR, NV>(a.xdelta, a.xdmap[i], d, l);
+      dj = load_row<LPR, NV>(a.xdelta, a.xdmap[j], d, l);
+    } else {
+      if (!si) di = load_row<LPR, NV>(a.delta, ki, d, l);
+      if (!sj) dj = load_row<LPR, NV>(a.delta, kj, d, l);
+    }
   }
   const int64_t lu = ps.x - (int64_t)a.t * a.B, li = ps.y - (int64_t)a.t * 2 * a.B,
                 lj = ps.z - (int64_t)a.t * 2 * a.B;
@@ -2948,7 +2964,9 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
       store_row<LPR, NV>(cuB, 2 * lu + 1, d, l, scale_row(qj, -g));
     }
     if (!si) store_row<LPR, NV>(ciB, li, d, l, scale_row(p, g));
+    else if (a.shard) store_row<LPR, NV>(a.xbuf, a.xmap[i], d, l, scale_row(p, g));
     if (!sj) store_row<LPR, NV>(ciB, lj, d, l, scale_row(p, -g));
+    else if (a.shard) store_row<LPR, NV>(a.xbuf, a.xmap[j], d, l, scale_row(p, -g));
     if (PASS == 0) return;
   }
   // the single rows' clean gradients (k_single's order)
@@ -2959,8 +2977,8 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
   axpy_row(Gj, -g, p);
   if (PASS == 2) {
     if (su) du = make_delta<LPR, NV>(a, Gu, 0, u, l);
-    if (si) di = make_delta<LPR, NV>(a, Gi, 1, i, l);
-    if (sj) dj = make_delta<LPR, NV>(a, Gj, 1, j, l);
+    if (ai) di = make_delta<LPR, NV>(a, Gi, 1, i, l);
+    if (aj) dj = make_delta<LPR, NV>(a, Gj, 1, j, l);
     const RowV<NV> pp = add_row(p, du), qip = add_row(qi, di), qjp = add_row(qj, dj);
     float ga, la;
     bpr_term(dot_row<LPR, NV>(pp, qip) - dot_row<LPR, NV>(pp, qjp), a.clip_lo, a.clip_hi, ga, la);
@@ -2970,19 +2988,21 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
       store_row<LPR, NV>(cuB, 2 * lu + 1, d, l, scale_row(qjp, -ga));
     }
     if (!si) store_row<LPR, NV>(ciB, li, d, l, scale_row(pp, ga));
+    else if (a.shard) store_row<LPR, NV>(a.xbuf, a.xmap[i], d, l, scale_row(pp, ga));
     if (!sj) store_row<LPR, NV>(ciB, lj, d, l, scale_row(pp, -ga));
+    else if (a.shard) store_row<LPR, NV>(a.xbuf, a.xmap[j], d, l, scale_row(pp, -ga));
     if (su) {
       RowV<NV> Au = zero_row<NV>();
       axpy_row(Au, ga, qip);
       axpy_row(Au, -ga, qjp);
       axpy_row(Gu, a.reg_adv, Au);
     }
-    if (si) {
+    if (ai) {
       RowV<NV> Ai = zero_row<NV>();
       axpy_row(Ai, ga, pp);
       axpy_row(Gi, a.reg_adv, Ai);
     }
-    if (sj) {
+    if (aj) {
       RowV<NV> Aj = zero_row<NV>();
       axpy_row(Aj, -ga, pp);
       axpy_row(Gj, a.reg_adv, Aj);
@@ -2995,13 +3015,13 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
     store_row<LPR, NV>(a.accP, u, d, l, cu);
     store_row<LPR, NV>((flags & 2) ? a.P : a.wnew_cur, (flags & 2) ? u : ku, d, l, w);
   }
-  if (si) {
+  if (ai) {
     RowV<NV> w;
     adagrad_row(a, Gi, qi, ci, 1, w);
     store_row<LPR, NV>(a.accQ, i, d, l, ci);
     store_row<LPR, NV>((flags & 4) ? a.Q : a.wnew_cur, (flags & 4) ? i : ki, d, l, w);
   }
-  if (sj) {
+  if (aj) {
     RowV<NV> w;
     adagrad_row(a, Gj, qj, cj, 1, w);
     store_row<LPR, NV>(a.accQ, j, d, l, cj);
@@ -3116,6 +3136,10 @@ __device__ __forceinline__ void tri_add_q(const StepArgs& a, const TriSlot& h, i
 template <int LPR, int NV, int MODE>
 __device__ __forceinline__ void tri_finish(const StepArgs& a, int k, const TriSlot& h, RowV<NV>& G, int l) {
   const int d = a.d;
+  if (a.shard && h.is_item) {  // shard mode: the partial item sum, straight to its exchange row
+    store_row<LPR, NV>(a.xbuf, a.xmap[h.row], d, l, G);
+    return;
+  }
   if (MODE == 0) {
     const RowV<NV> dl = make_delta<LPR, NV>(a, G, h.is_item, h.row, l);
     store_row<LPR, NV>(a.g0, k, d, l, G);
@@ -3179,12 +3203,12 @@ __device__ __forceinline__ TriHotPre<LPR, NV> tri_hot_prefetch(const StepArgs& a
   f.is_item = (r.meta() & ACF_ITEM_BIT) != 0;
   f.row = r.own_row();
   f.src = r.own_src();
-  if (MODE != 0) {
+  if (MODE != 0 && !(a.shard && f.is_item)) {
     f.acc = load_row<LPR, NV>(f.is_item ? a.accQ : a.accP, f.row, d, l);
     if (MODE == 1) f.own = load_at<LPR, NV>(row_src(a, f.is_item ? a.Q : a.P, f.row, f.src), d, l);
     else f.own = load_row<LPR, NV>(f.is_item ? a.Q : a.P, f.row, d, l);
   }
-  if (MODE == 2) f.g0 = load_row<LPR, NV>(a.g0, e.x, d, l);
+  if (MODE == 2 && !(a.shard && f.is_item)) f.g0 = load_row<LPR, NV>(a.g0, e.x, d, l);
   return f;
 }
 
@@ -3218,7 +3242,9 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
       T = add_row(T, o);
     }
     const int k = e.x;
-    if (MODE == 0) {
+    if (a.shard && f.is_item) {  // shard mode: the partial item sum, straight to its exchange row
+      store_row<LPR, NV>(a.xbuf, a.xmap[f.row], d, l, T);
+    } else if (MODE == 0) {
       const RowV<NV> dl = make_delta<LPR, NV>(a, T, f.is_item, f.row, l);
       store_row<LPR, NV>(a.g0, k, d, l, T);
       store_row<LPR, NV>(a.delta, k, d, l, dl);
@@ -3594,6 +3620,8 @@ struct acf_apr_ctx {
   int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
+  const float* xdelta = nullptr;    // triplet-centric shard passes: the owners' item deltas (acf_apr_shard_items_mapped)
+  const int64_t* xdmap = nullptr;
   int32_t plan_kind2 = 0;  // the plan encodes sources at every distance (k_prev_next)
   int32_t plan_kb = 1;     // slot bits of the plan's src encoding
   int32_t* nextt = nullptr;  // [maxNB][S] next batch touching each slot's row (k_prev_next)
@@ -4072,6 +4100,7 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   p.haux = c->hplan_haux;
   p.hl = c->hot;
   p.err = c->err; p.gen_ptr = c->gen_dev;
+  p.shard = c->shard;
   const unsigned tiles = (unsigned)(nb * p.tpb);
   k_hplan_keys<<<tiles, 256, 0, s>>>(p);
   HIP_TRY(hipGetLastError());
@@ -4085,8 +4114,10 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   k_hplan_bases<<<(unsigned)nb, 1024, 0, s>>>(p);
   k_hplan_emit<<<(unsigned)(nb << pb), 256, 0, s>>>(p);
   k_hplan_trip<<<(unsigned)((E + 255) / 256), 256, 0, s>>>(p);
-  k_hplan_rank_small<<<dim3(64, nb), 256, 0, s>>>(p);
-  k_hplan_rank_hot<<<dim3(64, nb), 256, (size_t)2 * ((2 * B + 31) / 32) * sizeof(uint32_t), s>>>(p);
+  // (a one-batch plan, the split step's, gets more workgroups per batch)
+  const unsigned rx = (unsigned)std::max(64, 1024 / nb);
+  k_hplan_rank_small<<<dim3(rx, nb), 256, 0, s>>>(p);
+  k_hplan_rank_hot<<<dim3(rx, nb), 256, (size_t)2 * ((2 * B + 31) / 32) * sizeof(uint32_t), s>>>(p);
   HIP_TRY(hipGetLastError());
   c->plan_R = 1;
   c->plan_kind2 = 0;
@@ -4254,8 +4285,8 @@ extern "C" int acf_apr_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* 
   if (c->shard && nb == 1 && B <= 1024 && c->plan_mode == 0 &&
       bits_for((uint64_t)std::max(c->U1, c->I1)) <= 30)
     return shard_plan_small(c, user, ipos, ineg, B, gen, check, s);
-  if (is_packed(c, B) && !c->shard && c->fusion && c->plan_mode == 0 && B <= ACF_HPLAN_MAXB &&
-      hplan_ready(c))
+  // triplet-centric plans (r05: in shard mode too, from B = 1,025)
+  if (is_packed(c, B) && c->fusion && c->plan_mode == 0 && B <= ACF_HPLAN_MAXB && hplan_ready(c))
     return hash_plan(c, user, ipos, ineg, B, nb, gen, (int32_t)bits_for((uint64_t)3 * B + 1), check, s);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
   // 32-bit keys (segment only, occurrence as the sort value) when they fit
@@ -4426,6 +4457,8 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.xmap = nullptr;
   a.xubs = a.xibs = nullptr;
   a.xn = a.xblocks = a.xflush = 0;
+  a.xdelta = c->xdelta;
+  a.xdmap = c->xdmap;
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
   a.contrib = c->contrib;
@@ -4520,7 +4553,7 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists, int tri) {
 
 static int get_kernels(const acf_apr_ctx* c, Kernels* k, int fused = 0) {
   return DISPATCH_GEOM(c->d, kernel_ptrs, k, is_packed(c, c->B), fused || c->shard, c->lists,
-                       c->tri && fused && !c->shard);
+                       c->tri && (fused || c->shard));
 }
 
 typedef void (*StepKernel)(StepArgs);
@@ -5033,6 +5066,38 @@ extern "C" int acf_apr_shard_pass_export(acf_apr_ctx* c, const acf_apr_tables* t
   const int SW = std::min((S + K.slots_per_wave - 1) / K.slots_per_wave, ACF_LIST_WAVES);
   const int HW = std::min(c->hot.piece_stride, ACF_HOT_WAVES);
   const int HB = std::min(c->hot.hot_stride, ACF_HOT_BLOCKS);
+  if (K.tri) {
+    // (r05) triplet-centric shard passes (hash plan): the triplet pass (a single
+    // item's product goes straight to its exchange row), then k_tri_combine,
+    // whose item slots store their partial sums there too and whose user slots
+    // finish as in the unsharded step (delta; Adagrad in place).  Pass 1 reads
+    // the owners' item deltas from the exchange rows (acf_apr_shard_items_mapped
+    // dir 1 names them).
+    ACF_CHECK(xbuf, ACF_E_INVALID, "triplet-centric shard passes export their item sums: xbuf is required");
+    ACF_CHECK(pass == 0 || c->xdelta, ACF_E_STATE, "pass 1 needs the owners' deltas (acf_apr_shard_items_mapped)");
+    const int SW4 = (std::min(SW, ACF_TRI_COMB_WAVES) + 3) & ~3, HW4 = (HW + 3) & ~3;
+    const int HBT = std::min(HB, ACF_TRI_HOT_BLOCKS);
+    const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);
+    const int TW = (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv);
+    StepArgs a = make_args(c, tb, hp, 0, 0);
+    a.use_single = 1;
+    a.xbuf = xbuf;
+    a.xmap = xmap;
+    a.xn = (int32_t)n_items;
+    StepArgs at = a, ac = a;
+    at.slot_waves = 0;
+    ac.slot_waves = SW4;
+    ac.hot_waves = HW4;
+    ac.hot_blocks = HBT;
+    if (pass == 0) {
+      ACF_RET(launch(hp->adver ? K.tri_clean : K.tri_clean_bpr, at, TW, s));
+      ACF_RET(launch(K.tri_comb[hp->adver ? 0 : 1], ac, SW4 + HW4 + 4 * HBT, s));
+    } else {
+      ACF_RET(launch(K.tri_adv, a, TW, s));
+      ACF_RET(launch(K.tri_comb[2], ac, SW4 + HW4 + 4 * HBT, s));
+    }
+    return ACF_OK;
+  }
   StepArgs a = make_args(c, tb, hp, 0, 0);
   a.use_single = 0;
   a.slot_waves = SW;
@@ -5098,6 +5163,12 @@ extern "C" int acf_apr_shard_items_mapped(acf_apr_ctx* c, int32_t dir, float* bu
   ACF_CHECK(dir == 0 || dir == 1, ACF_E_INVALID, "dir must be 0 or 1");
   ACF_CHECK(n_items >= 0 && n_items <= 2 * (int64_t)c->B, ACF_E_INVALID, "n_items %lld outside [0, 2B]",
             (long long)n_items);
+  if (c->tri) {  // triplet-centric shard passes read the deltas where they are (dir 1)
+    ACF_CHECK(dir == 1 && map, ACF_E_STATE, "triplet-centric shard plans take the owners' deltas by map (dir 1)");
+    c->xdelta = buf;
+    c->xdmap = map;
+    return ACF_OK;
+  }
   if (n_items == 0) return ACF_OK;
   hipStream_t s = static_cast<hipStream_t>(stream_);
   const int64_t n4 = n_items * (c->d / 4);

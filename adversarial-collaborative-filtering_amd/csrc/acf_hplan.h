@@ -55,6 +55,7 @@ struct HPlanArgs {
   int32_t* poff;              // its exclusive scan: where each (partition, tile) share starts
   int2* occ;                  // [nb][3B] occurrence -> {slot or -1 (single), CSR position}
   int4* claims;               // [nb][3B / 2] HClaim: a partition's shared keys from x0 / 2
+  int32_t shard;              // shard mode: no fused triplets (an item's single occurrence is a partial sum)
   int32_t* ptot;              // [nb << pb][6] partition totals
   int32_t* pbase;             // [nb << pb][6] their exclusive scans over the batch
   int32_t* csr;               // [nb][3B] occurrence ids by CSR position: users [0, B), items B + [0, 2B)
@@ -483,7 +484,7 @@ __global__ void __launch_bounds__(256) k_hplan_trip(HPlanArgs p) {
   q.own_row = u; q.own_src = i; q.meta = j; q.ovf = su ? 0 : su_.x;
   q.e_role = si ? 0 : si_.x; q.pa_row = sj ? 0 : sj_.x; q.pb_row = u; q.pa_src = i;
   q.pb_src = j;
-  q.pa_slot = ((su && si && sj) ? 1 : 0) | (su ? 2 + 16 : 0) | (si ? 4 + 32 : 0) | (sj ? 8 + 64 : 0);
+  q.pa_slot = ((su && si && sj && !p.shard) ? 1 : 0) | (su ? 2 + 16 : 0) | (si ? 4 + 32 : 0) | (sj ? 8 + 64 : 0);
   q.pb_slot = (int32_t)e;
   q.gen = p.gen;
   p.trec[e] = q;

@@ -84,6 +84,41 @@ def test_sharded_rccl_world1_matches_oracle(ops, oracle, dev, fp32_parity, shape
         fp32_parity(g, w, n)
 
 
+@pytest.mark.parametrize("adver,reg,routed", [(1, 0.0, False), (0, 0.01, False), (1, 0.0, True)])
+def test_sharded_triplet_centric_matches_slot_path(ops, dev, adver, reg, routed):
+    """(r05) Shard mode on the hash plan and the triplet-centric kernels (local
+    batches above 1,024 triplets with fusion on, the default: item occurrences
+    are never single, item slots export their partial sums straight to the
+    exchange rows, pass 1 reads the owners' deltas from theirs) against the sort
+    plan and the slot kernels (fusion off): identical bits for every table, on
+    Zipf batches of 32,768 with hot items, every exchange forced through a
+    one-rank RCCL group, eager (train) and captured (train_routed)."""
+    D_ = importlib.import_module(PKG + ".distributed")
+    U1, I1, d, B, nb = 300_000, 200_000, 64, 32768, 4
+    P, Q, u, i, j = _problem(21 + adver, U1, I1, d, B, nb, 1.1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    outs, kinds = [], []
+    try:
+        uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
+        for fusion in (False, True):
+            with D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, force_collectives=True,
+                               local_batch=B if routed else None) as sh:
+                for c in sh.local.ctxs:
+                    c.set_fusion(fusion)
+                hp = ops.StepHParams(adver=adver, reg=reg)
+                (sh.train_routed if routed else sh.train)(uu, ii, jj, hp, chunk=2)
+                torch.cuda.synchronize(dev)
+                assert sh.step_errors() == 0
+                kinds.append(sh.local.ctxs[0].plan_kind())
+                outs.append(sh.full_tables())
+    finally:
+        dist.destroy_process_group()
+    assert kinds == ["sort", "hash"], kinds
+    for g, e, n in zip(outs[1], outs[0], ("P", "Q", "accP", "accQ")):
+        assert torch.equal(g, e), n
+
+
 @pytest.mark.parametrize("exchange,adver,reg,routed", [("all_to_all", 1, 0.0, False), ("allgather", 1, 0.0, True),
                                                        ("all_to_all", 0, 0.01, False), ("all_to_all", 1, 0.0, True)])
 def test_sharded_graph_replay_bit_identical(ops, dev, exchange, adver, reg, routed):
