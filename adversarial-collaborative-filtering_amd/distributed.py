@@ -261,6 +261,7 @@ class ShardedAPR:
         if capture_collectives is None:  # default on (r05); ACF_SHARD_RCCL_GRAPH=0 keeps the steps eager
             capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "1") != "0"
         multi = self.G > 1 or self._force  # exchanges that are collectives
+        self._multi = multi
         self._cap_coll = bool(capture_collectives) and self.graph and multi
         self._C = 0   # per-peer block rows of the exchange buffers (only grows)
         self._T = 0   # steps the per-chunk maps hold
@@ -690,7 +691,8 @@ class ShardedAPR:
         the local passes allow it (_pipelined)."""
         # never across a segment cut (see the constructor): plans in line while
         # capturing segments; eager runs and whole-step graphs keep the pipeline
-        segments = self._rec is not None and not self._cap_coll
+        # (world 1 without forced collectives has no cut: one graph, pipelined)
+        segments = self._rec is not None and not self._cap_coll and self._multi
         pipe = self.device.type == "cuda" and self._pipelined() and not segments
         if pipe and getattr(self, "_plan_stream", None) is None:
             self._plan_stream = torch.cuda.Stream(self.device)

@@ -9,4 +9,4 @@ timeout -k 10 150 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smo
 timeout -k 10 250 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err
 timeout -k 10 250 python3 bench.py --steps 20 --warmup 5 > $OUT/bench_20.json 2> $OUT/bench_20.err
 python3 -c "import json;[print(f, json.loads(open('$OUT/'+f).read().strip().splitlines()[-1])['value']) for f in ('bench_default.json','bench_20.json')]"
-[ -n "$WITH_PROF" ] && bash tools/profile_bench.sh --no-sharded || true
+true
