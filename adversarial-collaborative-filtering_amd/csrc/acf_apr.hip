@@ -4489,6 +4489,8 @@ struct Kernels {
 #define ACF_HOT_WAVES 2048   // piece waves of a list kernel (hot slots)
 #define ACF_HOT_BLOCKS 1024  // workgroups of k_hot_combine
 #define ACF_TRI_HOT_BLOCKS 512  // hot-slot combining workgroups of k_tri_combine
+// (r05 same-box A/B: 2,048 / 8,192 small-slot waves, 256 / 1,024 combining
+// workgroups, 1,024 / 4,096 piece waves -- none faster; profiles/r05/combine_params_ab.json)
 
 template <int LPR, int NV, int TEAM>
 static void kernel_ptrs_team(Kernels* k, int fused) {

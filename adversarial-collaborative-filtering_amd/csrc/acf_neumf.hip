@@ -1314,6 +1314,8 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
   // while the adversarial k_nmf_inst writes its own
   A(&c->h0, 2 * B * 2 * dd); A(&c->a1, 2 * B * 2 * dd); A(&c->dz1, 2 * B * 2 * dd); A(&c->dz2, 2 * B * dd);
   A(&c->last_u, (size_t)U1); A(&c->last_i, (size_t)I1); A(&c->pend_u, (size_t)U1); A(&c->pend_i, (size_t)I1);
+  // (r05: the catch-up stream at the least stream priority measured the same, 7.17-7.19M
+  // instances/s either way, profiles/r05/neumf_side_priority_ab.txt)
   if (r == ACF_OK && (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
                       hipEventCreateWithFlags(&c->ev_next, hipEventDisableTiming) != hipSuccess ||
                       hipEventCreateWithFlags(&c->ev_rest, hipEventDisableTiming) != hipSuccess))
