@@ -770,7 +770,12 @@ __global__ void __launch_bounds__(256) k_nmf_wsum(NArgs a, int nslot, int npass,
 
 constexpr int MAX_Q = 2;   // d <= 128: each lane holds up to 2 of a row's elements
 constexpr int RCH = 2048;  // batch indices staged in LDS per round
-constexpr int RBATCH = 8;  // occurrences whose contributions are loaded together
+// occurrences whose contributions are loaded together (r05 same-box A/B, yelp
+// shape: 1 / 2 / 3 / 4 / 8 / 16 -> 7.40-7.50 / 7.47-7.49 / 7.44-7.48 / 7.43-7.58 /
+// 7.18-7.19 / 6.61-6.68M instances/s; most rows have few occurrences, and the
+// unrolled predicated loads of a wide batch cost more than the round trips save;
+// profiles/r05/neumf_rbatch_ab.txt)
+constexpr int RBATCH = 4;
 
 // One wave per (instance b, side s): s = 0 the user's MF_U / MLP_U rows, s = 1
 // the item's MF_I / MLP_I rows.  The first occurrence of the row in the batch

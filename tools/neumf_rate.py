@@ -10,6 +10,14 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 acf = importlib.import_module("adversarial-collaborative-filtering_amd")
+if os.environ.get("ACF_NEUMF_LIB"):  # another build (A/B), without the build-hash check
+    import ctypes
+    nat = importlib.import_module("adversarial-collaborative-filtering_amd._native")
+    lib = ctypes.CDLL(os.environ["ACF_NEUMF_LIB"])
+    for fname, (res, args) in nat.NEUMF_SIGNATURES.items():
+        fn = getattr(lib, fname)
+        fn.restype, fn.argtypes = res, args
+    nat._neumf = lib
 nm = importlib.import_module("adversarial-collaborative-filtering_amd.neumf")
 ds = acf.yelp_like()
 train = sp.coo_matrix((np.ones(len(ds.pair_user), np.float32), (ds.pair_user, ds.pair_item)),
