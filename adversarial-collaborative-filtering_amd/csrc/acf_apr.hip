@@ -2764,7 +2764,7 @@ __device__ __forceinline__ void hot_combine_slot(const StepArgs& a, const int4 e
     const float* own_tab = is_item ? a.Q : a.P;
     float* acc_tab = is_item ? a.accQ : a.accP;
     if (a.shard && is_item && a.xbuf)  // the owner's partial sum, straight to its exchange row
-      store_row<LPR, NV>(a.xbuf, a.xmap[k - (a.xubs[1] - a.xubs[0])], d, l, G);
+      store_row_wt<LPR, NV>(a.xbuf, a.xmap[k - (a.xubs[1] - a.xubs[0])], d, l, G);
     if (MODE != 0 && a.shard && is_item) {  // partial item sum for the owner
       store_row<LPR, NV>(a.g0, k, d, l, G);
     } else if (MODE == 0) {
@@ -2818,7 +2818,7 @@ __device__ __forceinline__ void shard_export_rest(const StepArgs& a, int bx) {
     const RecV r = load_rec(a.inl + ((int64_t)a.t * a.S + k) * a.R);
     const int cnt = r.meta() & ACF_COUNT_MASK;
     if (!(r.meta() & ACF_SINGLE_BIT) && cnt > ACF_HOT_MIN) continue;  // a hot slot: its combine exports it
-    store_row<LPR, NV>(a.xbuf, a.xmap[w], d, l, load_row<LPR, NV>(a.g0, k, d, l));
+    store_row_wt<LPR, NV>(a.xbuf, a.xmap[w], d, l, load_row<LPR, NV>(a.g0, k, d, l));
   }
 }
 
@@ -2971,9 +2971,9 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
       store_row_wt<LPR, NV>(cuB, 2 * lu + 1, d, l, scale_row(qj, -g));
     }
     if (!si) store_row_wt<LPR, NV>(ciB, li, d, l, scale_row(p, g));
-    else if (a.shard) store_row<LPR, NV>(a.xbuf, a.xmap[i], d, l, scale_row(p, g));
+    else if (a.shard) store_row_wt<LPR, NV>(a.xbuf, a.xmap[i], d, l, scale_row(p, g));
     if (!sj) store_row_wt<LPR, NV>(ciB, lj, d, l, scale_row(p, -g));
-    else if (a.shard) store_row<LPR, NV>(a.xbuf, a.xmap[j], d, l, scale_row(p, -g));
+    else if (a.shard) store_row_wt<LPR, NV>(a.xbuf, a.xmap[j], d, l, scale_row(p, -g));
     if (PASS == 0) return;
   }
   // the single rows' clean gradients (k_single's order)
@@ -2995,9 +2995,9 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
       store_row_wt<LPR, NV>(cuB, 2 * lu + 1, d, l, scale_row(qjp, -ga));
     }
     if (!si) store_row_wt<LPR, NV>(ciB, li, d, l, scale_row(pp, ga));
-    else if (a.shard) store_row<LPR, NV>(a.xbuf, a.xmap[i], d, l, scale_row(pp, ga));
+    else if (a.shard) store_row_wt<LPR, NV>(a.xbuf, a.xmap[i], d, l, scale_row(pp, ga));
     if (!sj) store_row_wt<LPR, NV>(ciB, lj, d, l, scale_row(pp, -ga));
-    else if (a.shard) store_row<LPR, NV>(a.xbuf, a.xmap[j], d, l, scale_row(pp, -ga));
+    else if (a.shard) store_row_wt<LPR, NV>(a.xbuf, a.xmap[j], d, l, scale_row(pp, -ga));
     if (su) {
       RowV<NV> Au = zero_row<NV>();
       axpy_row(Au, ga, qip);
@@ -3143,8 +3143,11 @@ __device__ __forceinline__ void tri_add_q(const StepArgs& a, const TriSlot& h, i
 template <int LPR, int NV, int MODE>
 __device__ __forceinline__ void tri_finish(const StepArgs& a, int k, const TriSlot& h, RowV<NV>& G, int l) {
   const int d = a.d;
+  // (the exchange rows are stored write-through: r05 same-box A/B, configs[4]
+  // split step 0.403-0.409 -> 0.398-0.401 ms; the owner kernels' outputs
+  // write-through were slower, 0.47 ms: profiles/r05/shard_writethrough_ab.json)
   if (a.shard && h.is_item) {  // shard mode: the partial item sum, straight to its exchange row
-    store_row<LPR, NV>(a.xbuf, a.xmap[h.row], d, l, G);
+    store_row_wt<LPR, NV>(a.xbuf, a.xmap[h.row], d, l, G);
     return;
   }
   if (MODE == 0) {
@@ -3250,7 +3253,7 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
     }
     const int k = e.x;
     if (a.shard && f.is_item) {  // shard mode: the partial item sum, straight to its exchange row
-      store_row<LPR, NV>(a.xbuf, a.xmap[f.row], d, l, T);
+      store_row_wt<LPR, NV>(a.xbuf, a.xmap[f.row], d, l, T);
     } else if (MODE == 0) {
       const RowV<NV> dl = make_delta<LPR, NV>(a, T, f.is_item, f.row, l);
       store_row<LPR, NV>(a.g0, k, d, l, T);

@@ -15,6 +15,16 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 acf = importlib.import_module(bench.PKG)
 ops = importlib.import_module(bench.PKG + ".ops")
+alt = os.environ.get("ACF_LARGE_LINE_LIB")  # another build of libacf_apr.so (A/B; see tools/large_line.py)
+if alt:
+    import ctypes
+    nat = importlib.import_module(bench.PKG + "._native")
+    lib = ctypes.CDLL(alt)
+    for fname, (res, args) in nat.SIGNATURES.items():
+        if hasattr(lib, fname):
+            fn = getattr(lib, fname)
+            fn.restype, fn.argtypes = res, args
+    nat._lib = lib
 big = acf.synthetic_large(device=dev)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 24
 print(json.dumps(bench.sharded_lines(acf, ops, dev, None, 1, 0, big, steps)))
