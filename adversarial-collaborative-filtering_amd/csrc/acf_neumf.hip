@@ -113,6 +113,11 @@ struct NArgs {
   float* wpart;          // [gridDim.x][nout] this pass's weight-gradient partials (one slot per workgroup)
   const float* delta;    // [B][4][d], rows written at their owner instance
   const int32_t* owner;  // [B][2] first occurrence of the instance's user / item
+  // rows in line (k_nmf_inst<.., .., true>, B <= FR_MAXB): arrivals at each row
+  // (users, then items; zero between passes), and the clean pass's delta
+  int32_t* rcnt;         // [U1 + I1]
+  int32_t with_delta;
+  float eps;
   float* pred;
   int32_t* err;
 };
@@ -124,6 +129,27 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MR = 16;        // instances per block = the MFMA tile height
 constexpr int NSLOT = 256;    // workgroups (= weight-gradient partial slots) per training pass, at most
 constexpr int DFAST = 64;     // the dimension with a compile-time specialisation of k_nmf_inst
+constexpr int MAX_Q = 2;      // d <= 128: each lane holds up to 2 of a row's elements
+// occurrences whose contributions are loaded together (r05 same-box A/B, yelp
+// shape: 1 / 2 / 3 / 4 / 8 / 16 -> 7.40-7.50 / 7.47-7.49 / 7.44-7.48 / 7.43-7.58 /
+// 7.18-7.19 / 6.61-6.68M instances/s; most rows have few occurrences, and the
+// unrolled predicated loads of a wide batch cost more than the round trips save;
+// profiles/r05/neumf_rbatch_ab.txt)
+constexpr int RBATCH = 4;
+// rows in line (k_nmf_inst<MODE, DC, true>) up to this batch: one block of MR
+// instances per workgroup, the batch's indices in LDS
+constexpr int FR_MAXB = 1024;
+
+// device-scope write-through store / load of one float (the contributions a row's
+// last arrival in another workgroup reads in the same launch; MI355X guide,
+// Guideline 16: no L2 write-back or invalidate)
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ float ld_dev(const float* p) {
+  return __uint_as_float(__hip_atomic_load((const __attribute__((address_space(1))) uint32_t*)p, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
 
 // Weight-gradient partial vector of one workgroup: the parameter buffer's tail from
 // S_W1 on, element for element -- W1 [2d][2d] | b1 [2d] | W2 [2d][d] | b2 [d] |
@@ -149,6 +175,13 @@ __host__ __device__ __forceinline__ WOut wout(int64_t d) {
 // W1 and W2 are staged in LDS (row stride +1 float: the transposed reads of the
 // backward products are then conflict-free) when they fit beside the activations
 __host__ __device__ __forceinline__ bool weights_in_lds(int d) { return d <= 64; }
+
+// k_nmf_inst's LDS in floats (the rows-in-line batch indices come after it)
+__host__ __device__ __forceinline__ int64_t inst_floats(int d) {
+  int64_t f = (int64_t)3 * MR * (2 * d + 1) + 3 * MR * (d + 1) + 2 * MR + 5 * d + 4;
+  if (weights_in_lds(d)) f += (int64_t)2 * d * (2 * d + 1) + (int64_t)2 * d * (d + 1);
+  return f;
+}
 
 // C[MR x N] = A[MR x K] . w(k, n) on v_mfma_f32_16x16x4_f32 (exact f32 products,
 // k-ordered fma chain).  A: LDS, row-major with leading dimension lda (padded so
@@ -378,6 +411,87 @@ __device__ __forceinline__ void wgrad_group(const NArgs& a, int w, int g, int ns
 
 static size_t wgrad_smem(int d) { return (size_t)MR * (3 * (2 * d + 1) + (d + 1)) * sizeof(float); }
 
+#ifndef ACF_SPIN_LIMIT
+#define ACF_SPIN_LIMIT (1 << 22)
+#endif
+
+// Rows in line (k_nmf_inst<MODE, DC, true>): the last arrival at a row (side s,
+// row r, first occurrence f; L = the side's clamped batch indices in LDS) sums
+// every occurrence's contribution in instance order -- k_nmf_rows' sum, bit for
+// bit -- adds it to the gradient rows and (with_delta) writes delta at f.  One wave.
+__device__ __forceinline__ void row_finish(const NArgs& a, const int32_t* L, int s, int32_t r, int f) {
+  const int lane = threadIdx.x & 63, B = a.B, d = a.d;
+  const int tA = s ? S_MF_I : S_MF_U, tB = s ? S_MLP_I : S_MLP_U;
+  float gA[MAX_Q], gB[MAX_Q], oA[MAX_Q], oB[MAX_Q];
+#pragma unroll
+  for (int q = 0; q < MAX_Q; ++q) {
+    const int k = lane + 64 * q;
+    gA[q] = gB[q] = 0.f;
+    oA[q] = k < d ? a.G[a.off[tA] + (int64_t)r * d + k] : 0.f;
+    oB[q] = k < d ? a.G[a.off[tB] + (int64_t)r * d + k] : 0.f;
+  }
+  for (int base = f & ~63; base < B; base += 64) {
+    const int j = base + lane;
+    uint64_t mask = __ballot(j < B && j >= f && L[j] == r);
+    while (mask) {
+      int js[RBATCH];
+#pragma unroll
+      for (int e = 0; e < RBATCH; ++e) {
+        js[e] = -1;
+        if (mask) {
+          js[e] = base + __ffsll((unsigned long long)mask) - 1;
+          mask &= mask - 1;
+        }
+      }
+      float va[RBATCH][MAX_Q], vb[RBATCH][MAX_Q];
+#pragma unroll
+      for (int e = 0; e < RBATCH; ++e)
+#pragma unroll
+        for (int q = 0; q < MAX_Q; ++q) {
+          const int k = lane + 64 * q;
+          const bool ok = js[e] >= 0 && k < d;
+          va[e][q] = ok ? ld_dev(a.contrib + ((int64_t)js[e] * 4 + tA) * d + k) : 0.f;
+          vb[e][q] = ok ? ld_dev(a.contrib + ((int64_t)js[e] * 4 + tB) * d + k) : 0.f;
+        }
+#pragma unroll
+      for (int e = 0; e < RBATCH; ++e)
+        if (js[e] >= 0)
+#pragma unroll
+          for (int q = 0; q < MAX_Q; ++q) {
+            gA[q] = gA[q] + va[e][q];
+            gB[q] = gB[q] + vb[e][q];
+          }
+    }
+  }
+  float ssA = 0.f, ssB = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAX_Q; ++q) {
+    const int k = lane + 64 * q;
+    if (k < d) {
+      a.G[a.off[tA] + (int64_t)r * d + k] = oA[q] + gA[q];
+      a.G[a.off[tB] + (int64_t)r * d + k] = oB[q] + gB[q];
+      ssA = ssA + gA[q] * gA[q];
+      ssB = ssB + gB[q] * gB[q];
+    }
+  }
+  if (!a.with_delta) return;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    ssA += __shfl_xor(ssA, m, 64);
+    ssB += __shfl_xor(ssB, m, 64);
+  }
+  const float invA = 1.0f / sqrtf(fmaxf(ssA, 1e-12f)), invB = 1.0f / sqrtf(fmaxf(ssB, 1e-12f));
+  float* delta = const_cast<float*>(a.delta);
+#pragma unroll
+  for (int q = 0; q < MAX_Q; ++q) {
+    const int k = lane + 64 * q;
+    if (k < d) {
+      delta[((int64_t)f * 4 + tA) * d + k] = gA[q] * invA * a.eps;
+      delta[((int64_t)f * 4 + tB) * d + k] = gB[q] * invB * a.eps;
+    }
+  }
+}
+
 #ifdef NMF_DIAG  // diagnostic build only: phase stamps (100 MHz) of workgroup 0, clean pass
 __device__ uint64_t g_nmf_stamps[16];
 __device__ uint64_t g_nmf_rstamps[8];  // k_nmf_rows, workgroup 0 wave 0 (owner of u[0]), clean pass
@@ -408,9 +522,84 @@ __device__ uint64_t g_nmf_rstamps[8];  // k_nmf_rows, workgroup 0 wave 0 (owner 
 // block's weight gradients accumulated into the workgroup's slot of a.wpart
 // (outer products on MFMA; bias / head / loss sums per owning thread).  MODE 2 is
 // prediction only.  DC = compile-time d (0: a.d at run time).
-template <int MODE, int DC>
+// FR (rows in line, B <= FR_MAXB: one block per workgroup): no k_nmf_rows launch
+// and no weight-gradient workgroups.  The block's weight-gradient tiles are taken
+// from LDS by the workgroup itself; once the block's contributions are out
+// (write-through) each (instance, side) counts its arrival at its row.  Workgroups
+// past inst_blocks are the row waves (row_wait_finish, a wave per (instance,
+// side) as in k_nmf_rows): the owner of a row waits for all its arrivals and sums
+// the row.  Same sums in the same order: bit-identical to the k_nmf_rows path
+// (test_neumf_rows_in_line_matches_rows_kernel).
+// Row waves of a rows-in-line launch (workgroup fb past the instance
+// workgroups): k_nmf_rows' wave per (instance, side) -- stage the batch's indices,
+// find the pair's first occurrence (the clean pass records it for the adversarial
+// pass's delta gathers) -- then the row's owner counts the row's occurrences,
+// waits until that many arrivals are in (no wave of the instance workgroups ever
+// waits for a row wave, and they are dispatched first), re-arms the counter and
+// sums the row (row_finish).
+template <int MODE>
+__device__ __forceinline__ void row_wait_finish(const NArgs& a, unsigned fb, int32_t* s_idx) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, B = a.B;
+  {
+    int32_t su[FR_MAXB / 256], si[FR_MAXB / 256];
+#pragma unroll
+    for (int q = 0; q < FR_MAXB / 256; ++q) {
+      const int x = tid + 256 * q;
+      su[q] = x < B ? a.u[x] : 0;
+      si[q] = x < B ? a.i[x] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < FR_MAXB / 256; ++q) {
+      const int x = tid + 256 * q;
+      if (x < B) {
+        s_idx[x] = clamp_idx(su[q], a.U1);
+        s_idx[B + x] = clamp_idx(si[q], a.I1);
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t item = (int64_t)fb * 4 + wave;
+  if (item >= 2 * (int64_t)B) return;
+  const int b = (int)(item >> 1), s = (int)(item & 1);
+  const int32_t* L = s_idx + s * B;
+  const int32_t r = L[b];
+  int first = b;
+  for (int base = 0; base <= b; base += 64) {
+    const int j = base + lane;
+    const uint64_t mask = __ballot(j <= b && L[j] == r);
+    if (mask) {
+      first = base + __ffsll((unsigned long long)mask) - 1;
+      break;
+    }
+  }
+  if (MODE == 0 && lane == 0) const_cast<int32_t*>(a.owner)[2 * b + s] = first;
+  if (first != b) return;
+  int cnt = 0;
+  for (int base = b & ~63; base < B; base += 64) {
+    const int j = base + lane;
+    cnt += __popcll(__ballot(j < B && j >= b && L[j] == r));
+  }
+  int32_t* ctr = a.rcnt + (s ? a.U1 : 0) + r;
+  for (int it = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cnt;) {
+    if (++it > ACF_SPIN_LIMIT) {
+      if (lane == 0) atomicOr(a.err, 512);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every arrival is in
+  row_finish(a, L, s, r, b);
+}
+
+template <int MODE, int DC, bool FR = false>
 __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned inst_blocks) {
   extern __shared__ float sm[];
+  if constexpr (FR) {
+    if (blockIdx.x >= inst_blocks) {
+      row_wait_finish<MODE>(a, blockIdx.x - inst_blocks, reinterpret_cast<int32_t*>(sm));
+      return;
+    }
+  }
   if (blockIdx.x >= inst_blocks) {  // the previous pass's weight-gradient workgroups
     const int x = (int)(blockIdx.x - inst_blocks), ns = (int)inst_blocks;
     if (wg.d % 16 == 0) wgrad_group<true>(wg, x % ns, x / ns, ns, sm);
@@ -495,6 +684,12 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
   if (blk < nblk) {
     gather_idx(blk);
     gather_rows(blk);
+  }
+  // FR: the row of the block's pair tid (instance tid >> 1; user, item), for its arrival
+  int32_t prow = 0;
+  if constexpr (FR) {
+    const int64_t b = blk * MR + (tid >> 1);
+    if (tid < 2 * MR && b < a.B) prow = (tid & 1) ? clamp_idx(a.i[b], a.I1) : clamp_idx(a.u[b], a.U1);
   }
   constexpr int Q1 = 64 * 64 * 4 / 4 / 256, Q2 = 64 * 64 * 2 / 4 / 256;  // weights_in_lds: d <= 64
   const int n1 = wl ? d2 * d2 / 4 : 0, n2 = wl ? d2 * d / 4 : 0;
@@ -623,8 +818,15 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
       s_dz2[t * L1 + k] = dz;
       if (t < nt) {
         const float dmf = dl * Wo[k];
-        a.contrib[((b0 + t) * 4 + S_MF_U) * d + k] = dmf * s_mi[t * L1 + k];
-        a.contrib[((b0 + t) * 4 + S_MF_I) * d + k] = dmf * s_mu[t * L1 + k];
+        float* cu = a.contrib + ((b0 + t) * 4 + S_MF_U) * d + k;
+        float* ci = a.contrib + ((b0 + t) * 4 + S_MF_I) * d + k;
+        if constexpr (FR) {
+          st_wt(cu, dmf * s_mi[t * L1 + k]);
+          st_wt(ci, dmf * s_mu[t * L1 + k]);
+        } else {
+          *cu = dmf * s_mi[t * L1 + k];
+          *ci = dmf * s_mu[t * L1 + k];
+        }
       }
     }
     if (tid < d2)
@@ -646,10 +848,34 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
     mfma_panel<true>(s_f, L2, W1, ld1, d2, d2, [&](int row, int col, float v) {
       if (row < nt) {
         const int tab = col < d ? S_MLP_U : S_MLP_I, kk = col < d ? col : col - d;
-        a.contrib[((b0 + row) * 4 + tab) * d + kk] = v;
+        float* cp = a.contrib + ((b0 + row) * 4 + tab) * d + kk;
+        if constexpr (FR) st_wt(cp, v);
+        else *cp = v;
       }
     });
     NSTAMP(8);
+    if constexpr (FR) {
+      if (tid < d2)
+        for (int t = 0; t < nt; ++t) acc_b1 = acc_b1 + s_f[t * L2 + tid];
+      if (tid < d)
+        for (int t = 0; t < nt; ++t) acc_b2 = acc_b2 + s_dz2[t * L1 + tid];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's contributions are out
+      __syncthreads();
+      if (tid < 2 * nt)  // arrival at the row (its owner's row wave waits for all of them)
+        __hip_atomic_fetch_add(a.rcnt + ((tid & 1) ? a.U1 : 0) + prow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nt < MR) {  // a partial block: rows past the batch zero, as wgrad_group stages them
+        for (int x = tid; x < (MR - nt) * L2; x += 256) {
+          s_a1[nt * L2 + x] = 0.f;
+          s_f[nt * L2 + x] = 0.f;
+        }
+        for (int x = tid; x < (MR - nt) * L1; x += 256) s_dz2[nt * L1 + x] = 0.f;
+        __syncthreads();
+      }
+      // the block's weight gradients into the slot (wgrad_group's tiles, from LDS)
+      if (d % 16 == 0) outer_tiles<false, true>(s_x, s_f, s_a1, s_dz2, d, slot + wo_.w1, slot + wo_.w2, 0, wtiles(d));
+      else outer_tiles<false, false>(s_x, s_f, s_a1, s_dz2, d, slot + wo_.w1, slot + wo_.w2, 0, wtiles(d));
+      continue;
+    }
     // the weight gradients' operands -> k_nmf_rows' gradient workgroups (W1 += h0^T dz1,
     // W2 += a1^T dz2 on MFMA there, beside the row sums); b1 += sum dz1, b2 += sum dz2 here
     for (int x = tid; x < MR * d2; x += 256) {
@@ -768,14 +994,7 @@ __global__ void __launch_bounds__(256) k_nmf_wsum(NArgs a, int nslot, int npass,
   wsum_one(a, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, nslot, npass, part, loss_out);
 }
 
-constexpr int MAX_Q = 2;   // d <= 128: each lane holds up to 2 of a row's elements
 constexpr int RCH = 2048;  // batch indices staged in LDS per round
-// occurrences whose contributions are loaded together (r05 same-box A/B, yelp
-// shape: 1 / 2 / 3 / 4 / 8 / 16 -> 7.40-7.50 / 7.47-7.49 / 7.44-7.48 / 7.43-7.58 /
-// 7.18-7.19 / 6.61-6.68M instances/s; most rows have few occurrences, and the
-// unrolled predicated loads of a wide batch cost more than the round trips save;
-// profiles/r05/neumf_rbatch_ab.txt)
-constexpr int RBATCH = 4;
 
 // One wave per (instance b, side s): s = 0 the user's MF_U / MLP_U rows, s = 1
 // the item's MF_I / MLP_I rows.  The first occurrence of the row in the batch
@@ -1241,6 +1460,8 @@ struct acf_neumf_ctx {
   float* wpart = nullptr;  // [2 passes][slots][weight-gradient outputs]
   int32_t nslot = 0;       // workgroups (slots) of a training pass at max_batch
   int32_t *owner = nullptr, *err = nullptr;
+  int32_t* rcnt = nullptr;  // rows in line: arrivals per row [U1 + I1]
+  int32_t rows_in_line = 1;  // B <= FR_MAXB: rows in line (acf_neumf_set_rows_in_line: 0 = k_nmf_rows)
   // acf_neumf_train's lazy Adam: each row's last iteration, the side stream and its events
   int32_t *last_u = nullptr, *last_i = nullptr, *pend_u = nullptr, *pend_i = nullptr;
   hipStream_t side = nullptr;
@@ -1276,6 +1497,12 @@ extern "C" int acf_neumf_param_offsets(int64_t U1, int64_t I1, int32_t d, int64_
   ACF_CHECK(off != nullptr, ACF_E_INVALID, "offsets pointer is NULL");
   const Layout L = make_layout(U1, I1, d);
   for (int k = 0; k < S_COUNT; ++k) off[k] = L.off[k];
+  return ACF_OK;
+}
+
+extern "C" int acf_neumf_set_rows_in_line(acf_neumf_ctx* c, int32_t on) {
+  ACF_CHECK(c != nullptr, ACF_E_INVALID, "ctx is NULL");
+  c->rows_in_line = on ? 1 : 0;
   return ACF_OK;
 }
 
@@ -1315,6 +1542,7 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
     *p = static_cast<std::remove_reference_t<decltype(*p)>>(q);
   };
   A(&c->contrib, B * 4 * dd); A(&c->delta, B * 4 * dd); A(&c->owner, 2 * B); A(&c->err, 4);
+  A(&c->rcnt, (size_t)(U1 + I1));
   // two sets (clean / adversarial pass): the clean pass's gradient workgroups read theirs
   // while the adversarial k_nmf_inst writes its own
   A(&c->h0, 2 * B * 2 * dd); A(&c->a1, 2 * B * 2 * dd); A(&c->dz1, 2 * B * 2 * dd); A(&c->dz2, 2 * B * dd);
@@ -1327,7 +1555,8 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
     r = set_error(ACF_E_HIP, "lazy-Adam setup failed");
   c->nslot = (int32_t)std::min<int64_t>(((int64_t)maxB + MR - 1) / MR, NSLOT);
   A(&c->wpart, 2 * (size_t)c->nslot * (size_t)wout(d).n);
-  if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipDeviceSynchronize() != hipSuccess))
+  if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->rcnt, 0, (size_t)(U1 + I1) * sizeof(int32_t)) != hipSuccess ||
+                      hipDeviceSynchronize() != hipSuccess))
     r = set_error(ACF_E_HIP, "hipMemset failed");
   if (r == ACF_OK) r = set_inst_smem_limit();
   if (r != ACF_OK) { acf_neumf_destroy(c); return r; }
@@ -1346,13 +1575,13 @@ static NArgs make_args(acf_neumf_ctx* c, const float* P, float* G, const int32_t
   a.contrib = c->contrib; a.wpart = c->wpart;
   a.h0 = c->h0; a.a1 = c->a1; a.dz1 = c->dz1; a.dz2 = c->dz2;
   a.delta = c->delta; a.owner = c->owner; a.pred = nullptr; a.err = c->err;
+  a.rcnt = c->rcnt; a.with_delta = 0; a.eps = 0.f;
   return a;
 }
 
-static size_t inst_smem(int d) {
-  size_t f = (size_t)3 * MR * (2 * d + 1) + 3 * MR * (d + 1) + 2 * MR + 5 * d + 4;
-  if (weights_in_lds(d)) f += (size_t)2 * d * (2 * d + 1) + (size_t)2 * d * (d + 1);
-  return f * sizeof(float);
+// fr_b: the batch of a rows-in-line launch (its row waves stage its indices), 0 otherwise
+static size_t inst_smem(int d, int fr_b = 0) {
+  return (size_t)std::max<int64_t>(inst_floats(d), 2 * (int64_t)fr_b) * sizeof(float);
 }
 
 // allow the large dynamic LDS of k_nmf_inst (gfx950: 160 KB per CU)
@@ -1365,7 +1594,11 @@ static int set_inst_smem_limit() {
                        reinterpret_cast<const void*>(&k_nmf_inst<2, 0>),
                        reinterpret_cast<const void*>(&k_nmf_inst<0, DFAST>),
                        reinterpret_cast<const void*>(&k_nmf_inst<1, DFAST>),
-                       reinterpret_cast<const void*>(&k_nmf_inst<2, DFAST>)};
+                       reinterpret_cast<const void*>(&k_nmf_inst<2, DFAST>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<0, 0, true>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<1, 0, true>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<0, DFAST, true>),
+                       reinterpret_cast<const void*>(&k_nmf_inst<1, DFAST, true>)};
   for (const void* f : fns) HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   // k_nmf_rows: 16 KB of indices + the gradient workgroups' operands (d = 128: 58 KB)
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_rows),
@@ -1379,27 +1612,31 @@ static int read_err(acf_neumf_ctx* c, hipStream_t s) {
   HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   ACF_CHECK(!(herr & 256), ACF_E_HIP, "lazy Adam: a row fell behind the learning-rate window (internal)");
+  ACF_CHECK(!(herr & 512), ACF_E_HIP, "rows in line: a row wave timed out waiting for its arrivals (internal)");
   ACF_CHECK(herr == 0, ACF_E_RANGE, "index out of range (%s%s)", (herr & 1) ? "user >= num_user_rows " : "",
             (herr & 2) ? "item >= num_item_rows" : "");
   return ACF_OK;
 }
 
 // grid = inst workgroups + (optional) the previous pass's weight-gradient workgroups (args wg)
-template <int MODE>
+template <int MODE, bool FR = false>
 static void launch_inst(const NArgs& a, unsigned inst_blocks, hipStream_t s, const NArgs* wg = nullptr,
                         unsigned wg_blocks = 0) {
   const NArgs& w = wg ? *wg : a;
-  const unsigned grid = inst_blocks + (wg ? wg_blocks : 0u);
+  // extra workgroups: the previous pass's weight-gradient workgroups (wg), or FR's row waves
+  const unsigned grid = inst_blocks + ((wg || FR) ? wg_blocks : 0u);
+  const size_t sm = inst_smem(a.d, FR ? a.B : 0);
   if (a.d == DFAST)
-    k_nmf_inst<MODE, DFAST><<<grid, 256, inst_smem(a.d), s>>>(a, w, inst_blocks);
+    k_nmf_inst<MODE, DFAST, FR><<<grid, 256, sm, s>>>(a, w, inst_blocks);
   else
-    k_nmf_inst<MODE, 0><<<grid, 256, inst_smem(a.d), s>>>(a, w, inst_blocks);
+    k_nmf_inst<MODE, 0, FR><<<grid, 256, sm, s>>>(a, w, inst_blocks);
 }
 
 // clean pass: k_nmf_inst<0> -> k_nmf_rows (owners, rows, delta; + the pass's
 // weight-gradient tiles); adversarial pass: k_nmf_inst<1> -> k_nmf_rows; then
 // k_nmf_wsum sums the passes' slots into G, unless the caller leaves that to
-// k_nmf_adam (acf_neumf_train)
+// k_nmf_adam (acf_neumf_train).  B <= FR_MAXB: one k_nmf_inst<.., true> per pass
+// (rows and weight-gradient tiles in line).
 static int launch_grad(acf_neumf_ctx* c, const float* P, float* G, const int32_t* u, const int32_t* i,
                        const float* y, int32_t B, const acf_neumf_hparams* hp, float* loss_out,
                        hipStream_t s, bool wsum = true) {
@@ -1410,21 +1647,34 @@ static int launch_grad(acf_neumf_ctx* c, const float* P, float* G, const int32_t
   const WOut o = wout(c->d);
   const int npass = hp->adver ? 2 : 1;
   NArgs a = make_args(c, P, G, u, i, y, B, 1.0f);
-  launch_inst<0>(a, gi, s);
-  // APR-style: the clean pass's gradient workgroups ride in the adversarial
-  // k_nmf_inst (32 workgroups at B = 512: the other CUs are idle); BPR-style
-  // (no adversary) in its k_nmf_rows
-  k_nmf_rows<<<gr + (hp->adver ? 0u : gw), 256, sw, s>>>(a, c->owner, c->delta, hp->adver ? 1 : 0, hp->eps, gr,
-                                                        (int)gi);
-  HIP_TRY(hipGetLastError());
-  if (hp->adver) {
-    NArgs b = make_args(c, P, G, u, i, y, B, hp->reg_adv);
-    b.wpart = c->wpart + (int64_t)gi * o.n;
-    const int64_t ab = (int64_t)c->maxB;  // the second activation buffer
-    b.h0 += ab * 2 * c->d; b.a1 += ab * 2 * c->d; b.dz1 += ab * 2 * c->d; b.dz2 += ab * c->d;
-    launch_inst<1>(b, gi, s, &a, gw);
-    k_nmf_rows<<<gr + gw, 256, sw, s>>>(b, c->owner, c->delta, 0, 0.f, gr, (int)gi);
+  if (B <= FR_MAXB && c->rows_in_line) {
+    a.with_delta = hp->adver ? 1 : 0;
+    a.eps = hp->eps;
+    launch_inst<0, true>(a, gi, s, nullptr, gr);
     HIP_TRY(hipGetLastError());
+    if (hp->adver) {
+      NArgs b = make_args(c, P, G, u, i, y, B, hp->reg_adv);
+      b.wpart = c->wpart + (int64_t)gi * o.n;
+      launch_inst<1, true>(b, gi, s, nullptr, gr);
+      HIP_TRY(hipGetLastError());
+    }
+  } else {
+    launch_inst<0>(a, gi, s);
+    // APR-style: the clean pass's gradient workgroups ride in the adversarial
+    // k_nmf_inst (32 workgroups at B = 512: the other CUs are idle); BPR-style
+    // (no adversary) in its k_nmf_rows
+    k_nmf_rows<<<gr + (hp->adver ? 0u : gw), 256, sw, s>>>(a, c->owner, c->delta, hp->adver ? 1 : 0, hp->eps, gr,
+                                                          (int)gi);
+    HIP_TRY(hipGetLastError());
+    if (hp->adver) {
+      NArgs b = make_args(c, P, G, u, i, y, B, hp->reg_adv);
+      b.wpart = c->wpart + (int64_t)gi * o.n;
+      const int64_t ab = (int64_t)c->maxB;  // the second activation buffer
+      b.h0 += ab * 2 * c->d; b.a1 += ab * 2 * c->d; b.dz1 += ab * 2 * c->d; b.dz2 += ab * c->d;
+      launch_inst<1>(b, gi, s, &a, gw);
+      k_nmf_rows<<<gr + gw, 256, sw, s>>>(b, c->owner, c->delta, 0, 0.f, gr, (int)gi);
+      HIP_TRY(hipGetLastError());
+    }
   }
   if (wsum) {
     k_nmf_wsum<<<(unsigned)((o.n + 255) / 256), 256, 0, s>>>(a, (int)gi, npass, c->wpart, loss_out);

@@ -103,6 +103,11 @@ class NeuMFContext:
         except Exception:
             pass
 
+    def set_rows_in_line(self, on: bool) -> None:
+        """Batches of <= 1,024 instances: rows summed inside the instance kernels
+        (default) or by the separate row-sum kernel (bit-identical; tests / A/B)."""
+        _native.call_neumf("acf_neumf_set_rows_in_line", self._ptr, int(bool(on)))
+
     @staticmethod
     def hparams(lr=0.001, beta1=0.9, beta2=0.999, adam_eps=1e-7, adver=0, eps=0.5, reg_adv=1.0):
         return _native.NeuMFHParams(lr, beta1, beta2, adam_eps, eps, reg_adv, int(bool(adver)), 0)

@@ -62,6 +62,12 @@ int acf_neumf_grad(acf_neumf_ctx* ctx, const float* params, float* grad, const i
                    const int32_t* item, const float* label, int32_t batch,
                    const acf_neumf_hparams* hp, float* loss_out, int32_t check, void* stream);
 
+/* Batches of at most 1,024 instances take the rows-in-line kernels (one launch
+ * per pass); on = 0 sends them through the row-sum kernel instead, as larger
+ * batches go (the same sums in the same order: bit-identical; for tests and
+ * same-box A/B).  Default 1. */
+int acf_neumf_set_rows_in_line(acf_neumf_ctx* ctx, int32_t on);
+
 /* Keras 2.2 Adam over the whole buffer, iteration t (1-based); zeroes grad. */
 int acf_neumf_adam(acf_neumf_ctx* ctx, float* params, float* grad, float* m, float* v,
                    int64_t t, const acf_neumf_hparams* hp, void* stream);

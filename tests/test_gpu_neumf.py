@@ -232,3 +232,37 @@ def test_yelp_shaped_grad_matches_oracle(nm, dev, adver):
         np.testing.assert_allclose(st.view(n, st.grad).cpu().numpy(), want[n], rtol=1e-4, atol=1e-6,
                                    err_msg=n)
     np.testing.assert_allclose(loss.cpu().numpy(), [lc, la], rtol=1e-5)
+
+
+@pytest.mark.parametrize("B,U1,I1,n,d", [
+    (512, 2000, 3000, 1500, 64),   # the bench's batch; Zipf items; a partial last batch (476)
+    (1024, 300, 200, 2048, 16),    # the largest rows-in-line batch, rows with many occurrences
+    (100, 41, 37, 300, 128),       # d = 128 (weights read from global), partial blocks
+])
+def test_neumf_rows_in_line_matches_rows_kernel(nm, dev, B, U1, I1, n, d):
+    """Batches of <= 1,024 instances sum their rows inside k_nmf_inst (the last
+    arrival at a row sums it, from write-through contributions; the block's
+    weight-gradient tiles from LDS): one gradient and one train epoch equal the
+    k_nmf_rows path's bit for bit (parameters, Adam moments, losses)."""
+    P = N.init_params(U1, I1, d, 31)
+    rng = np.random.default_rng(13)
+    u = rng.integers(0, U1, n).astype(np.int32)
+    i = ((rng.zipf(1.3, n) - 1) % I1).astype(np.int32)
+    y = (rng.random(n) < 0.5).astype(np.float32)
+    for adver in (0, 1):
+        a, b = _state(nm, P, dev), _state(nm, P, dev)
+        ca, cb = nm.NeuMFContext(a, B), nm.NeuMFContext(b, B)
+        cb.set_rows_in_line(False)
+        hp = ca.hparams(adver=adver, eps=0.5, reg_adv=0.7)
+        la, lb = torch.zeros(2, device=dev), torch.zeros(2, device=dev)
+        ca.grad(u[:B], i[:B], y[:B], hp, la)
+        cb.grad(u[:B], i[:B], y[:B], hp, lb)
+        torch.cuda.synchronize()
+        assert a.grad.any()
+        assert torch.equal(a.grad, b.grad) and torch.equal(la, lb)
+        a.grad.zero_()
+        b.grad.zero_()
+        ta, tb = ca.train(u, i, y, B, hp), cb.train(u, i, y, B, hp)
+        torch.cuda.synchronize()
+        assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+        assert torch.equal(ta, tb)

@@ -30,6 +30,8 @@ U = torch.as_tensor(x[0][perm], dtype=torch.int32, device="cuda")
 I = torch.as_tensor(x[1][perm], dtype=torch.int32, device="cuda")
 Y = torch.as_tensor(y[perm], dtype=torch.float32, device="cuda")
 ctx = r._context(B)
+if os.environ.get("ROWS_IN_LINE") == "0":  # A/B: the k_nmf_rows path
+    ctx.set_rows_in_line(False)
 hp = r.hparams()
 ctx.train(U[: 64 * B], I[: 64 * B], Y[: 64 * B], B, hp)
 torch.cuda.synchronize()
