@@ -418,8 +418,10 @@ static size_t wgrad_smem(int d) { return (size_t)MR * (3 * (2 * d + 1) + (d + 1)
 // Rows in line (k_nmf_inst<MODE, DC, true>): the last arrival at a row (side s,
 // row r, first occurrence f; L = the side's clamped batch indices in LDS) sums
 // every occurrence's contribution in instance order -- k_nmf_rows' sum, bit for
-// bit -- adds it to the gradient rows and (with_delta) writes delta at f.  One wave.
+// bit -- adds it to the gradient rows and (with_delta) writes delta at f.  One wave;
+// the contributions are loaded RB occurrences at a time.
 __device__ __forceinline__ void row_finish(const NArgs& a, const int32_t* L, int s, int32_t r, int f) {
+  constexpr int RB = RBATCH;
   const int lane = threadIdx.x & 63, B = a.B, d = a.d;
   const int tA = s ? S_MF_I : S_MF_U, tB = s ? S_MLP_I : S_MLP_U;
   float gA[MAX_Q], gB[MAX_Q], oA[MAX_Q], oB[MAX_Q];
@@ -430,22 +432,30 @@ __device__ __forceinline__ void row_finish(const NArgs& a, const int32_t* L, int
     oA[q] = k < d ? a.G[a.off[tA] + (int64_t)r * d + k] : 0.f;
     oB[q] = k < d ? a.G[a.off[tB] + (int64_t)r * d + k] : 0.f;
   }
-  for (int base = f & ~63; base < B; base += 64) {
-    const int j = base + lane;
-    uint64_t mask = __ballot(j < B && j >= f && L[j] == r);
-    while (mask) {
-      int js[RBATCH];
+  // occurrences in instance order, RB per round trip across 64-instance chunks
+  // (a row's occurrences are spread over the batch: one chunk at a time would be
+  // one round trip per chunk)
+  int base = f & ~63;
+  uint64_t mask = __ballot(base + lane < B && base + lane >= f && L[base + lane] == r);
+  while (true) {
+    int js[RB];
 #pragma unroll
-      for (int e = 0; e < RBATCH; ++e) {
-        js[e] = -1;
-        if (mask) {
-          js[e] = base + __ffsll((unsigned long long)mask) - 1;
-          mask &= mask - 1;
-        }
+    for (int e = 0; e < RB; ++e) {
+      while (!mask && base + 64 < B) {
+        base += 64;
+        mask = __ballot(base + lane < B && L[base + lane] == r);
       }
-      float va[RBATCH][MAX_Q], vb[RBATCH][MAX_Q];
+      js[e] = -1;
+      if (mask) {
+        js[e] = base + __ffsll((unsigned long long)mask) - 1;
+        mask &= mask - 1;
+      }
+    }
+    if (js[0] < 0) break;
+    {
+      float va[RB][MAX_Q], vb[RB][MAX_Q];
 #pragma unroll
-      for (int e = 0; e < RBATCH; ++e)
+      for (int e = 0; e < RB; ++e)
 #pragma unroll
         for (int q = 0; q < MAX_Q; ++q) {
           const int k = lane + 64 * q;
@@ -454,7 +464,7 @@ __device__ __forceinline__ void row_finish(const NArgs& a, const int32_t* L, int
           vb[e][q] = ok ? ld_dev(a.contrib + ((int64_t)js[e] * 4 + tB) * d + k) : 0.f;
         }
 #pragma unroll
-      for (int e = 0; e < RBATCH; ++e)
+      for (int e = 0; e < RB; ++e)
         if (js[e] >= 0)
 #pragma unroll
           for (int q = 0; q < MAX_Q; ++q) {
@@ -516,51 +526,16 @@ __device__ uint64_t g_nmf_rstamps[8];  // k_nmf_rows, workgroup 0 wave 0 (owner 
   } while (0)
 #endif
 
-// One workgroup per slot, looping over blocks of MR instances (blk = blockIdx.x,
-// + gridDim.x, ...): the MLP forward (and, MODE 0 / 1, the backward) of a block on
-// MFMA with every operand in LDS, the row contributions to global scratch, and the
-// block's weight gradients accumulated into the workgroup's slot of a.wpart
-// (outer products on MFMA; bias / head / loss sums per owning thread).  MODE 2 is
-// prediction only.  DC = compile-time d (0: a.d at run time).
-// FR (rows in line, B <= FR_MAXB: one block per workgroup): no k_nmf_rows launch
-// and no weight-gradient workgroups.  The block's weight-gradient tiles are taken
-// from LDS by the workgroup itself; once the block's contributions are out
-// (write-through) each (instance, side) counts its arrival at its row.  Workgroups
-// past inst_blocks are the row waves (row_wait_finish, a wave per (instance,
-// side) as in k_nmf_rows): the owner of a row waits for all its arrivals and sums
-// the row.  Same sums in the same order: bit-identical to the k_nmf_rows path
-// (test_neumf_rows_in_line_matches_rows_kernel).
-// Row waves of a rows-in-line launch (workgroup fb past the instance
-// workgroups): k_nmf_rows' wave per (instance, side) -- stage the batch's indices,
-// find the pair's first occurrence (the clean pass records it for the adversarial
-// pass's delta gathers) -- then the row's owner counts the row's occurrences,
-// waits until that many arrivals are in (no wave of the instance workgroups ever
-// waits for a row wave, and they are dispatched first), re-arms the counter and
-// sums the row (row_finish).
+// Row waves of a rows-in-line launch (k_nmf_inst workgroups past the instance
+// workgroups): k_nmf_rows' wave per (instance, side) -- find the pair's first
+// occurrence (the clean pass records it for the adversarial pass's delta
+// gathers) -- then the row's owner counts the row's occurrences, waits until that
+// many arrivals are in (no wave of the instance workgroups ever waits for a row
+// wave, and they are dispatched first), re-arms the counter and sums the row
+// (row_finish).
 template <int MODE>
-__device__ __forceinline__ void row_wait_finish(const NArgs& a, unsigned fb, int32_t* s_idx) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, B = a.B;
-  {
-    int32_t su[FR_MAXB / 256], si[FR_MAXB / 256];
-#pragma unroll
-    for (int q = 0; q < FR_MAXB / 256; ++q) {
-      const int x = tid + 256 * q;
-      su[q] = x < B ? a.u[x] : 0;
-      si[q] = x < B ? a.i[x] : 0;
-    }
-#pragma unroll
-    for (int q = 0; q < FR_MAXB / 256; ++q) {
-      const int x = tid + 256 * q;
-      if (x < B) {
-        s_idx[x] = clamp_idx(su[q], a.U1);
-        s_idx[B + x] = clamp_idx(si[q], a.I1);
-      }
-    }
-  }
-  __syncthreads();
-  const int64_t item = (int64_t)fb * 4 + wave;
-  if (item >= 2 * (int64_t)B) return;
-  const int b = (int)(item >> 1), s = (int)(item & 1);
+__device__ __forceinline__ void row_wait_finish_one(const NArgs& a, const int32_t* s_idx, int b, int s) {
+  const int lane = threadIdx.x & 63, B = a.B;
   const int32_t* L = s_idx + s * B;
   const int32_t r = L[b];
   int first = b;
@@ -588,9 +563,53 @@ __device__ __forceinline__ void row_wait_finish(const NArgs& a, unsigned fb, int
     __builtin_amdgcn_s_sleep(8);
   }
   if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every arrival is in
+  // (r05 same-box A/B: hot rows' contributions 8 or 16 at a time measured the same
+  // as RBATCH, 8.35-8.61M instances/s, profiles/r05/neumf_rows_in_line_ab.txt)
   row_finish(a, L, s, r, b);
 }
 
+// a row workgroup: the batch's indices into LDS, then its waves' pairs (strided
+// over the row workgroups)
+template <int MODE>
+__device__ __forceinline__ void row_wait_finish(const NArgs& a, unsigned fb, int32_t* s_idx) {
+  const int tid = threadIdx.x, wave = tid >> 6, B = a.B;
+  {
+    int32_t su[FR_MAXB / 256], si[FR_MAXB / 256];
+#pragma unroll
+    for (int q = 0; q < FR_MAXB / 256; ++q) {
+      const int x = tid + 256 * q;
+      su[q] = x < B ? a.u[x] : 0;
+      si[q] = x < B ? a.i[x] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < FR_MAXB / 256; ++q) {
+      const int x = tid + 256 * q;
+      if (x < B) {
+        s_idx[x] = clamp_idx(su[q], a.U1);
+        s_idx[B + x] = clamp_idx(si[q], a.I1);
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t nrow = gridDim.x - (blockIdx.x - fb);  // row workgroups
+  for (int64_t item = (int64_t)fb * 4 + wave; item < 2 * (int64_t)B; item += 4 * nrow)
+    row_wait_finish_one<MODE>(a, s_idx, (int)(item >> 1), (int)(item & 1));
+}
+
+// One workgroup per slot, looping over blocks of MR instances (blk = blockIdx.x,
+// + gridDim.x, ...): the MLP forward (and, MODE 0 / 1, the backward) of a block on
+// MFMA with every operand in LDS, the row contributions to global scratch, and the
+// block's weight gradients accumulated into the workgroup's slot of a.wpart
+// (outer products on MFMA; bias / head / loss sums per owning thread).  MODE 2 is
+// prediction only.  DC = compile-time d (0: a.d at run time).
+// FR (rows in line, B <= FR_MAXB: one block per workgroup): no k_nmf_rows launch
+// and no weight-gradient workgroups.  The block's weight-gradient tiles are taken
+// from LDS by the workgroup itself; once the block's contributions are out
+// (write-through) each (instance, side) counts its arrival at its row.  Workgroups
+// past inst_blocks are the row waves (row_wait_finish, a wave per (instance,
+// side) as in k_nmf_rows): the owner of a row waits for all its arrivals and sums
+// the row.  Same sums in the same order: bit-identical to the k_nmf_rows path
+// (test_neumf_rows_in_line_matches_rows_kernel).
 template <int MODE, int DC, bool FR = false>
 __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned inst_blocks) {
   extern __shared__ float sm[];
@@ -1650,6 +1669,9 @@ static int launch_grad(acf_neumf_ctx* c, const float* P, float* G, const int32_t
   if (B <= FR_MAXB && c->rows_in_line) {
     a.with_delta = hp->adver ? 1 : 0;
     a.eps = hp->eps;
+    // a row wave per (instance, side); half as many (two pairs per wave) or as many as
+    // fit beside the instance workgroups measured 1-3% slower (same box,
+    // profiles/r05/neumf_rows_in_line_ab.txt)
     launch_inst<0, true>(a, gi, s, nullptr, gr);
     HIP_TRY(hipGetLastError());
     if (hp->adver) {
