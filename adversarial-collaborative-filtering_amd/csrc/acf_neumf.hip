@@ -118,6 +118,10 @@ struct NArgs {
   int32_t* rcnt;         // [U1 + I1]
   int32_t with_delta;
   float eps;
+  // both passes in one launch (k_nmf_step): per row, (gen << 32 | its first
+  // occurrence) once the clean pass's owner has stored the row's delta and gradient
+  unsigned long long* rdone;  // [U1 + I1]
+  int32_t gen;
   float* pred;
   int32_t* err;
 };
@@ -420,6 +424,9 @@ static size_t wgrad_smem(int d) { return (size_t)MR * (3 * (2 * d + 1) + (d + 1)
 // every occurrence's contribution in instance order -- k_nmf_rows' sum, bit for
 // bit -- adds it to the gradient rows and (with_delta) writes delta at f.  One wave;
 // the contributions are loaded RB occurrences at a time.
+// MG (both passes in one launch): the clean pass stores the row write-through and
+// then publishes it (rdone); the adversarial pass reads the gradient row that way.
+template <int MODE, bool MG>
 __device__ __forceinline__ void row_finish(const NArgs& a, const int32_t* L, int s, int32_t r, int f) {
   constexpr int RB = RBATCH;
   const int lane = threadIdx.x & 63, B = a.B, d = a.d;
@@ -429,8 +436,10 @@ __device__ __forceinline__ void row_finish(const NArgs& a, const int32_t* L, int
   for (int q = 0; q < MAX_Q; ++q) {
     const int k = lane + 64 * q;
     gA[q] = gB[q] = 0.f;
-    oA[q] = k < d ? a.G[a.off[tA] + (int64_t)r * d + k] : 0.f;
-    oB[q] = k < d ? a.G[a.off[tB] + (int64_t)r * d + k] : 0.f;
+    const float* pA = a.G + a.off[tA] + (int64_t)r * d + k;
+    const float* pB = a.G + a.off[tB] + (int64_t)r * d + k;
+    oA[q] = k < d ? (MG && MODE == 1 ? ld_dev(pA) : *pA) : 0.f;
+    oB[q] = k < d ? (MG && MODE == 1 ? ld_dev(pB) : *pB) : 0.f;
   }
   // occurrences in instance order, RB per round trip across 64-instance chunks
   // (a row's occurrences are spread over the batch: one chunk at a time would be
@@ -478,8 +487,15 @@ __device__ __forceinline__ void row_finish(const NArgs& a, const int32_t* L, int
   for (int q = 0; q < MAX_Q; ++q) {
     const int k = lane + 64 * q;
     if (k < d) {
-      a.G[a.off[tA] + (int64_t)r * d + k] = oA[q] + gA[q];
-      a.G[a.off[tB] + (int64_t)r * d + k] = oB[q] + gB[q];
+      float* pA = a.G + a.off[tA] + (int64_t)r * d + k;
+      float* pB = a.G + a.off[tB] + (int64_t)r * d + k;
+      if (MG && MODE == 0) {
+        st_wt(pA, oA[q] + gA[q]);
+        st_wt(pB, oB[q] + gB[q]);
+      } else {
+        *pA = oA[q] + gA[q];
+        *pB = oB[q] + gB[q];
+      }
       ssA = ssA + gA[q] * gA[q];
       ssB = ssB + gB[q] * gB[q];
     }
@@ -496,9 +512,22 @@ __device__ __forceinline__ void row_finish(const NArgs& a, const int32_t* L, int
   for (int q = 0; q < MAX_Q; ++q) {
     const int k = lane + 64 * q;
     if (k < d) {
-      delta[((int64_t)f * 4 + tA) * d + k] = gA[q] * invA * a.eps;
-      delta[((int64_t)f * 4 + tB) * d + k] = gB[q] * invB * a.eps;
+      float* dA = delta + ((int64_t)f * 4 + tA) * d + k;
+      float* dB = delta + ((int64_t)f * 4 + tB) * d + k;
+      if (MG) {
+        st_wt(dA, gA[q] * invA * a.eps);
+        st_wt(dB, gB[q] * invB * a.eps);
+      } else {
+        *dA = gA[q] * invA * a.eps;
+        *dB = gB[q] * invB * a.eps;
+      }
     }
+  }
+  if (MG && MODE == 0) {  // the row is out: publish it to the adversarial pass
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(a.rdone + (s ? a.U1 : 0) + r, ((unsigned long long)(uint32_t)a.gen << 32) | (uint32_t)f,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -533,7 +562,7 @@ __device__ uint64_t g_nmf_rstamps[8];  // k_nmf_rows, workgroup 0 wave 0 (owner 
 // many arrivals are in (no wave of the instance workgroups ever waits for a row
 // wave, and they are dispatched first), re-arms the counter and sums the row
 // (row_finish).
-template <int MODE>
+template <int MODE, bool MG>
 __device__ __forceinline__ void row_wait_finish_one(const NArgs& a, const int32_t* s_idx, int b, int s) {
   const int lane = threadIdx.x & 63, B = a.B;
   const int32_t* L = s_idx + s * B;
@@ -565,13 +594,13 @@ __device__ __forceinline__ void row_wait_finish_one(const NArgs& a, const int32_
   if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every arrival is in
   // (r05 same-box A/B: hot rows' contributions 8 or 16 at a time measured the same
   // as RBATCH, 8.35-8.61M instances/s, profiles/r05/neumf_rows_in_line_ab.txt)
-  row_finish(a, L, s, r, b);
+  row_finish<MODE, MG>(a, L, s, r, b);
 }
 
 // a row workgroup: the batch's indices into LDS, then its waves' pairs (strided
 // over the row workgroups)
-template <int MODE>
-__device__ __forceinline__ void row_wait_finish(const NArgs& a, unsigned fb, int32_t* s_idx) {
+template <int MODE, bool MG>
+__device__ __forceinline__ void row_wait_finish(const NArgs& a, unsigned fb, unsigned nrow, int32_t* s_idx) {
   const int tid = threadIdx.x, wave = tid >> 6, B = a.B;
   {
     int32_t su[FR_MAXB / 256], si[FR_MAXB / 256];
@@ -591,9 +620,8 @@ __device__ __forceinline__ void row_wait_finish(const NArgs& a, unsigned fb, int
     }
   }
   __syncthreads();
-  const int64_t nrow = gridDim.x - (blockIdx.x - fb);  // row workgroups
-  for (int64_t item = (int64_t)fb * 4 + wave; item < 2 * (int64_t)B; item += 4 * nrow)
-    row_wait_finish_one<MODE>(a, s_idx, (int)(item >> 1), (int)(item & 1));
+  for (int64_t item = (int64_t)fb * 4 + wave; item < 2 * (int64_t)B; item += 4 * (int64_t)nrow)
+    row_wait_finish_one<MODE, MG>(a, s_idx, (int)(item >> 1), (int)(item & 1));
 }
 
 // One workgroup per slot, looping over blocks of MR instances (blk = blockIdx.x,
@@ -610,21 +638,11 @@ __device__ __forceinline__ void row_wait_finish(const NArgs& a, unsigned fb, int
 // side) as in k_nmf_rows): the owner of a row waits for all its arrivals and sums
 // the row.  Same sums in the same order: bit-identical to the k_nmf_rows path
 // (test_neumf_rows_in_line_matches_rows_kernel).
-template <int MODE, int DC, bool FR = false>
-__global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned inst_blocks) {
-  extern __shared__ float sm[];
-  if constexpr (FR) {
-    if (blockIdx.x >= inst_blocks) {
-      row_wait_finish<MODE>(a, blockIdx.x - inst_blocks, reinterpret_cast<int32_t*>(sm));
-      return;
-    }
-  }
-  if (blockIdx.x >= inst_blocks) {  // the previous pass's weight-gradient workgroups
-    const int x = (int)(blockIdx.x - inst_blocks), ns = (int)inst_blocks;
-    if (wg.d % 16 == 0) wgrad_group<true>(wg, x % ns, x / ns, ns, sm);
-    else wgrad_group<false>(wg, x % ns, x / ns, ns, sm);
-    return;
-  }
+// (instance workgroup bx of the pass; MG: the clean and adversarial passes share
+// one launch, k_nmf_step)
+template <int MODE, int DC, bool FR, bool MG>
+__device__ __forceinline__ void inst_block(const NArgs& a, unsigned bx, unsigned inst_blocks, float* sm) {
+  __shared__ int32_t s_own[MG && MODE == 1 ? 2 * MR : 1];  // the block's pairs' owners (first occurrences)
   NSTAMP(0);
   const int d = DC ? DC : a.d, d2 = 2 * d, tid = threadIdx.x;
   const int L2 = d2 + 1, L1 = d + 1;  // padded leading dimensions
@@ -664,7 +682,10 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
       const int64_t b = b0 + ((x < MR * d && t < nt) ? t : 0);
       uu[q] = a.u[b];
       ii[q] = a.i[b];
-      if (MODE == 1) {
+      if (MODE == 1 && MG) {
+        ou[q] = s_own[2 * (b - b0)];
+        oi[q] = s_own[2 * (b - b0) + 1];
+      } else if (MODE == 1) {
         ou[q] = a.owner[2 * b];
         oi[q] = a.owner[2 * b + 1];
       }
@@ -687,10 +708,17 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
         if (MODE == 1) {
           const float* du = a.delta + (int64_t)ou[q] * 4 * d;
           const float* di = a.delta + (int64_t)oi[q] * 4 * d;
-          v0 = v0 + du[0 * d + k];
-          v1_ = v1_ + di[1 * d + k];
-          v2_ = v2_ + du[2 * d + k];
-          v3 = v3 + di[3 * d + k];
+          if (MG) {  // stored in this launch (write-through)
+            v0 = v0 + ld_dev(du + 0 * d + k);
+            v1_ = v1_ + ld_dev(di + 1 * d + k);
+            v2_ = v2_ + ld_dev(du + 2 * d + k);
+            v3 = v3 + ld_dev(di + 3 * d + k);
+          } else {
+            v0 = v0 + du[0 * d + k];
+            v1_ = v1_ + di[1 * d + k];
+            v2_ = v2_ + du[2 * d + k];
+            v3 = v3 + di[3 * d + k];
+          }
         }
         g[q][0] = ok ? v0 : 0.f;
         g[q][1] = ok ? v1_ : 0.f;
@@ -699,16 +727,16 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
       }
     }
   };
-  int64_t blk = blockIdx.x;
-  if (blk < nblk) {
-    gather_idx(blk);
-    gather_rows(blk);
-  }
+  int64_t blk = bx;
   // FR: the row of the block's pair tid (instance tid >> 1; user, item), for its arrival
   int32_t prow = 0;
   if constexpr (FR) {
     const int64_t b = blk * MR + (tid >> 1);
     if (tid < 2 * MR && b < a.B) prow = (tid & 1) ? clamp_idx(a.i[b], a.I1) : clamp_idx(a.u[b], a.U1);
+  }
+  if (!(MG && MODE == 1) && blk < nblk) {
+    gather_idx(blk);
+    gather_rows(blk);
   }
   constexpr int Q1 = 64 * 64 * 4 / 4 / 256, Q2 = 64 * 64 * 2 / 4 / 256;  // weights_in_lds: d <= 64
   const int n1 = wl ? d2 * d2 / 4 : 0, n2 = wl ? d2 * d / 4 : 0;
@@ -756,6 +784,34 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
       dst[0] = v2[q].x; dst[1] = v2[q].y; dst[2] = v2[q].z; dst[3] = v2[q].w;
     }
   }
+  if constexpr (MG && MODE == 1) {
+    // the adversarial pass beside the clean one: the block's rows wait for their
+    // clean owners (delta and gradient stored, owner index in the flag), then gather
+    if (tid < 2 * MR) {
+      const int64_t b = blk * MR + (tid >> 1);
+      int32_t own = 0;
+      if (b < a.B) {
+        unsigned long long* fl = a.rdone + ((tid & 1) ? a.U1 : 0) + prow;
+        unsigned long long v = 0;
+        for (int it = 0;; ++it) {
+          v = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((int32_t)(v >> 32) == a.gen) break;
+          if (it > ACF_SPIN_LIMIT) {
+            atomicOr(a.err, 512);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
+        }
+        own = (int32_t)(v & 0xFFFFFFFFull);
+      }
+      s_own[tid] = own;
+    }
+    __syncthreads();
+    if (blk < nblk) {
+      gather_idx(blk);
+      gather_rows(blk);
+    }
+  }
   NSTAMP(1);
   const float* W1 = wl ? s_w1 : a.P + a.off[S_W1];
   const float* W2 = wl ? s_w2 : a.P + a.off[S_W2];
@@ -764,7 +820,7 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
   const float* b1 = s_b1;
   const float* b2 = s_b2;
   const WOut wo_ = wout(d);
-  float* slot = MODE == 2 ? nullptr : a.wpart + (int64_t)blockIdx.x * wo_.n;
+  float* slot = MODE == 2 ? nullptr : a.wpart + (int64_t)bx * wo_.n;
   // vector partials owned by threads across the workgroup's blocks
   float acc_wo = 0.f, acc_b1 = 0.f, acc_b2 = 0.f, acc_bo = 0.f, acc_ls = 0.f;
   for (; blk < nblk; blk += inst_blocks) {
@@ -930,6 +986,40 @@ __global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned in
     }
   }
   if (bad) atomicOr(a.err, bad);
+}
+
+template <int MODE, int DC, bool FR = false>
+__global__ void __launch_bounds__(256) k_nmf_inst(NArgs a, NArgs wg, unsigned inst_blocks) {
+  extern __shared__ float sm[];
+  if (FR && blockIdx.x >= inst_blocks) {  // the pass's row waves
+    row_wait_finish<MODE, false>(a, blockIdx.x - inst_blocks, gridDim.x - inst_blocks, reinterpret_cast<int32_t*>(sm));
+    return;
+  }
+  if (blockIdx.x >= inst_blocks) {  // the previous pass's weight-gradient workgroups
+    const int x = (int)(blockIdx.x - inst_blocks), ns = (int)inst_blocks;
+    if (wg.d % 16 == 0) wgrad_group<true>(wg, x % ns, x / ns, ns, sm);
+    else wgrad_group<false>(wg, x % ns, x / ns, ns, sm);
+    return;
+  }
+  inst_block<MODE, DC, FR, false>(a, blockIdx.x, inst_blocks, sm);
+}
+
+// Both passes of an adversarial rows-in-line step in ONE launch, in dispatch
+// order: the clean instance workgroups (a), the clean row waves, the adversarial
+// instance workgroups (b: each waits for its rows' clean owners, rdone), the
+// adversarial row waves.  Every wait is on workgroups earlier in the grid, and
+// the first ones never wait.  Bit-identical to the two launches.
+template <int DC>
+__global__ void __launch_bounds__(256) k_nmf_step(NArgs a, NArgs b, unsigned gi, unsigned gr) {
+  extern __shared__ float sm[];
+  unsigned x = blockIdx.x;
+  if (x < gi) return inst_block<0, DC, true, true>(a, x, gi, sm);
+  x -= gi;
+  if (x < gr) return row_wait_finish<0, true>(a, x, gr, reinterpret_cast<int32_t*>(sm));
+  x -= gr;
+  if (x < gi) return inst_block<1, DC, true, true>(b, x, gi, sm);
+  x -= gi;
+  row_wait_finish<1, true>(b, x, gr, reinterpret_cast<int32_t*>(sm));
 }
 
 // Weight gradients of the step: slot element x summed over the passes' slots
@@ -1479,7 +1569,9 @@ struct acf_neumf_ctx {
   float* wpart = nullptr;  // [2 passes][slots][weight-gradient outputs]
   int32_t nslot = 0;       // workgroups (slots) of a training pass at max_batch
   int32_t *owner = nullptr, *err = nullptr;
-  int32_t* rcnt = nullptr;  // rows in line: arrivals per row [U1 + I1]
+  int32_t* rcnt = nullptr;  // rows in line: arrivals per row [2][U1 + I1] (clean, adversarial)
+  unsigned long long* rdone = nullptr;  // [U1 + I1] k_nmf_step's published rows
+  int32_t gen = 0;                      // k_nmf_step launches so far
   int32_t rows_in_line = 1;  // B <= FR_MAXB: rows in line (acf_neumf_set_rows_in_line: 0 = k_nmf_rows)
   // acf_neumf_train's lazy Adam: each row's last iteration, the side stream and its events
   int32_t *last_u = nullptr, *last_i = nullptr, *pend_u = nullptr, *pend_i = nullptr;
@@ -1561,7 +1653,7 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
     *p = static_cast<std::remove_reference_t<decltype(*p)>>(q);
   };
   A(&c->contrib, B * 4 * dd); A(&c->delta, B * 4 * dd); A(&c->owner, 2 * B); A(&c->err, 4);
-  A(&c->rcnt, (size_t)(U1 + I1));
+  A(&c->rcnt, 2 * (size_t)(U1 + I1)); A(&c->rdone, (size_t)(U1 + I1));
   // two sets (clean / adversarial pass): the clean pass's gradient workgroups read theirs
   // while the adversarial k_nmf_inst writes its own
   A(&c->h0, 2 * B * 2 * dd); A(&c->a1, 2 * B * 2 * dd); A(&c->dz1, 2 * B * 2 * dd); A(&c->dz2, 2 * B * dd);
@@ -1574,7 +1666,8 @@ extern "C" int acf_neumf_create(acf_neumf_ctx** out, int64_t U1, int64_t I1, int
     r = set_error(ACF_E_HIP, "lazy-Adam setup failed");
   c->nslot = (int32_t)std::min<int64_t>(((int64_t)maxB + MR - 1) / MR, NSLOT);
   A(&c->wpart, 2 * (size_t)c->nslot * (size_t)wout(d).n);
-  if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->rcnt, 0, (size_t)(U1 + I1) * sizeof(int32_t)) != hipSuccess ||
+  if (r == ACF_OK && (hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->rcnt, 0, 2 * (size_t)(U1 + I1) * sizeof(int32_t)) != hipSuccess ||
+                      hipMemset(c->rdone, 0, (size_t)(U1 + I1) * sizeof(unsigned long long)) != hipSuccess ||
                       hipDeviceSynchronize() != hipSuccess))
     r = set_error(ACF_E_HIP, "hipMemset failed");
   if (r == ACF_OK) r = set_inst_smem_limit();
@@ -1594,7 +1687,7 @@ static NArgs make_args(acf_neumf_ctx* c, const float* P, float* G, const int32_t
   a.contrib = c->contrib; a.wpart = c->wpart;
   a.h0 = c->h0; a.a1 = c->a1; a.dz1 = c->dz1; a.dz2 = c->dz2;
   a.delta = c->delta; a.owner = c->owner; a.pred = nullptr; a.err = c->err;
-  a.rcnt = c->rcnt; a.with_delta = 0; a.eps = 0.f;
+  a.rcnt = c->rcnt; a.with_delta = 0; a.eps = 0.f; a.rdone = c->rdone; a.gen = 0;
   return a;
 }
 
@@ -1617,7 +1710,9 @@ static int set_inst_smem_limit() {
                        reinterpret_cast<const void*>(&k_nmf_inst<0, 0, true>),
                        reinterpret_cast<const void*>(&k_nmf_inst<1, 0, true>),
                        reinterpret_cast<const void*>(&k_nmf_inst<0, DFAST, true>),
-                       reinterpret_cast<const void*>(&k_nmf_inst<1, DFAST, true>)};
+                       reinterpret_cast<const void*>(&k_nmf_inst<1, DFAST, true>),
+                       reinterpret_cast<const void*>(&k_nmf_step<0>),
+                       reinterpret_cast<const void*>(&k_nmf_step<DFAST>)};
   for (const void* f : fns) HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   // k_nmf_rows: 16 KB of indices + the gradient workgroups' operands (d = 128: 58 KB)
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nmf_rows),
@@ -1666,7 +1761,21 @@ static int launch_grad(acf_neumf_ctx* c, const float* P, float* G, const int32_t
   const WOut o = wout(c->d);
   const int npass = hp->adver ? 2 : 1;
   NArgs a = make_args(c, P, G, u, i, y, B, 1.0f);
-  if (B <= FR_MAXB && c->rows_in_line) {
+  // both passes in one launch (r05 same-box A/B against one launch per pass:
+  // 8.52-8.96M vs 8.38-8.40M instances/s, profiles/r05/neumf_rows_in_line_ab.txt)
+  if (B <= FR_MAXB && c->rows_in_line && hp->adver) {
+    a.with_delta = 1;
+    a.eps = hp->eps;
+    a.gen = ++c->gen;
+    NArgs b = make_args(c, P, G, u, i, y, B, hp->reg_adv);
+    b.wpart = c->wpart + (int64_t)gi * o.n;
+    b.rcnt = c->rcnt + (c->U1 + c->I1);
+    b.gen = a.gen;
+    const size_t sm = inst_smem(c->d, B);
+    if (c->d == DFAST) k_nmf_step<DFAST><<<2 * (gi + gr), 256, sm, s>>>(a, b, gi, gr);
+    else k_nmf_step<0><<<2 * (gi + gr), 256, sm, s>>>(a, b, gi, gr);
+    HIP_TRY(hipGetLastError());
+  } else if (B <= FR_MAXB && c->rows_in_line) {
     a.with_delta = hp->adver ? 1 : 0;
     a.eps = hp->eps;
     // a row wave per (instance, side); half as many (two pairs per wave) or as many as
