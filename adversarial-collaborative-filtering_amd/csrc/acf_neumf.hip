@@ -1373,8 +1373,10 @@ constexpr int LAZY_W = 32;  // lr_t window (> the catch-up period)
 // workgroups of a step's catch-up slice, beside the step's kernels (r03, period
 // 8: 32 WGs 3.9M instances/s (the slice outlasts the step), 64 5.6M, 96 7.55M,
 // 128 7.3M, 192 7.45M, 256 7.35M; r04, period 16: 48 5.1M, 64 5.8-6.0M, 96 7.10M,
-// 128 7.10-7.15M, 192 7.16-7.18M, 256 7.13M)
-constexpr int64_t CATCHUP_WG = 192;
+// 128 7.10-7.15M, 192 7.16-7.18M, 256 7.13M; r05 beside the one-launch step
+// (k_nmf_step), same box: 96 6.83-6.84M, 128 7.49-7.67M, 192 8.35M, 384 8.82-8.85M,
+// profiles/r05/neumf_catchup_wg_ab.txt)
+constexpr int64_t CATCHUP_WG = 384;
 static_assert(LAZY_W > LAZY_S, "lr window");
 
 struct AdamLazy {
