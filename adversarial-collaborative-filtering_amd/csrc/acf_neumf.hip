@@ -1374,9 +1374,10 @@ constexpr int LAZY_W = 32;  // lr_t window (> the catch-up period)
 // 8: 32 WGs 3.9M instances/s (the slice outlasts the step), 64 5.6M, 96 7.55M,
 // 128 7.3M, 192 7.45M, 256 7.35M; r04, period 16: 48 5.1M, 64 5.8-6.0M, 96 7.10M,
 // 128 7.10-7.15M, 192 7.16-7.18M, 256 7.13M; r05 beside the one-launch step
-// (k_nmf_step), same box: 96 6.83-6.84M, 128 7.49-7.67M, 192 8.35M, 384 8.82-8.85M,
+// (k_nmf_step), same box: 96 6.83-6.84M, 128 7.49-7.67M, 192 8.35M, 384 8.82-8.85M;
+// another box: 192 8.19-8.32M, 384 8.83-8.85M, 512 9.03-9.05M, 768 9.01-9.06M,
 // profiles/r05/neumf_catchup_wg_ab.txt)
-constexpr int64_t CATCHUP_WG = 384;
+constexpr int64_t CATCHUP_WG = 512;
 static_assert(LAZY_W > LAZY_S, "lr window");
 
 struct AdamLazy {
