@@ -19,6 +19,12 @@
 //                       step's last k_nmf_rows launch also sums the weight-
 //                       gradient slots in slot order (deterministic, no atomics)
 //   (adver) k_nmf_inst<ADV>, k_nmf_rows on the perturbed rows, scaled by reg_adv
+//
+// Batches of <= FR_MAXB instances (r05) sum their rows in line instead: one
+// k_nmf_step launch per adversarial step (k_nmf_inst<MODE, DC, true> per pass
+// otherwise) holds the instance workgroups, which take their weight-gradient
+// tiles from LDS and count arrivals at their rows, and the row waves, whose
+// owners wait for the arrivals and sum the rows in k_nmf_rows' order.
 //   k_nmf_adam          Keras 2.2 Adam over the WHOLE flat parameter buffer
 //                       (Keras densifies the embedding IndexedSlices, so every
 //                       row's moments decay and every row moves): one HBM
