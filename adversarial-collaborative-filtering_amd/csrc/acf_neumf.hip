@@ -1373,8 +1373,11 @@ __global__ void __launch_bounds__(256) k_nmf_adam(float4* __restrict__ p, float4
 // rows, so a longer period is a smaller slice beside each step (r04, yelp shape,
 // d 64, B 512, one box: period 8 6.47M instances/s, 16 7.10-7.15M, 24 6.91M, 31 6.74M;
 // r05, same-box A/B with the workgroups below: 16 x 192 7.24M, 24 x 128 6.96-7.06M,
-// 31 x 192 6.84-6.86M, 31 x 96 6.75-6.88M -- the env knobs of those A/Bs are gone)
-constexpr int LAZY_S = 16;
+// 31 x 192 6.84-6.86M, 31 x 96 6.75-6.88M -- the env knobs of those A/Bs are gone;
+// r05 beside the one-launch step with 512 workgroups, same box: 8 9.33-9.40M,
+// 16 9.12-9.19M, 24 8.84M; another box: 4 9.08-9.11M, 8 9.35-9.38M, 16 9.13-9.14M,
+// profiles/r05/neumf_catchup_wg_ab.txt)
+constexpr int LAZY_S = 8;
 constexpr int LAZY_W = 32;  // lr_t window (> the catch-up period)
 // workgroups of a step's catch-up slice, beside the step's kernels (r03, period
 // 8: 32 WGs 3.9M instances/s (the slice outlasts the step), 64 5.6M, 96 7.55M,
