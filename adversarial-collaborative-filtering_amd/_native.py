@@ -191,6 +191,9 @@ NEUMF_SIGNATURES = {
     "acf_neumf_create": (ctypes.c_int, [ctypes.POINTER(_P), _I64, _I64, _I32, _I32]),
     "acf_neumf_destroy": (ctypes.c_int, [_P]),
     "acf_neumf_set_rows_in_line": (ctypes.c_int, [_P, _I32]),
+    "acf_neumf_set_spin_limit": (ctypes.c_int, [_P, _I32]),
+    "acf_neumf_set_failsafe": (ctypes.c_int, [_P, _I32]),
+    "acf_neumf_recoveries": (ctypes.c_int, [_P, ctypes.POINTER(_I64)]),
     "acf_neumf_grad": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, ctypes.POINTER(NeuMFHParams), _P,
                                       _I32, _P]),
     "acf_neumf_adam": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, ctypes.POINTER(NeuMFHParams), _P]),

@@ -48,6 +48,7 @@
 #include <map>
 #include <string>
 #include <thread>
+#include <mutex>
 #include <vector>
 
 #include "acf_apr.h"
@@ -3582,16 +3583,24 @@ struct FailGroup {
 };
 // every live group, for acf_apr_resolve_all (readers outside a group: evaluation,
 // forward, checkpoints)
+// (ctypes releases the GIL around native calls, so contexts may be created,
+// destroyed and resolved from several threads: the list is guarded; recursive,
+// because acf_apr_resolve_all holds it across resolve())
 static std::vector<FailGroup*> g_groups;
+static std::recursive_mutex g_groups_mu;
 static FailGroup* new_group() {
   FailGroup* g = new FailGroup();
   g->refs = 1;
+  std::lock_guard<std::recursive_mutex> lk(g_groups_mu);
   g_groups.push_back(g);
   return g;
 }
 static void drop_group(FailGroup* g) {
   if (g->gate) (void)hipFree(g->gate);
-  g_groups.erase(std::find(g_groups.begin(), g_groups.end(), g));
+  {
+    std::lock_guard<std::recursive_mutex> lk(g_groups_mu);
+    g_groups.erase(std::find(g_groups.begin(), g_groups.end(), g));
+  }
   delete g;
 }
 
@@ -3661,7 +3670,7 @@ struct acf_apr_ctx {
   int32_t task_lists = 0, task_stride = 0;
   // batch-local plan (k_bplan_sort / k_bplan_build)
   int32_t plan_mode = 0;     // 0 auto (batch-local plan where it applies), 1 always the sort plan
-  // hash plan of triplet-centric steps (k_hplan_*); ACF_HASH_PLAN=0 keeps the sort plan (A/B)
+  // hash plan of triplet-centric steps (k_hplan_*); acf_apr_set_plan_mode(ctx, 1) keeps the sort plan (A/B)
   int32_t plan_kind = -1;    // acf_apr_plan_kind
   int32_t hplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   int2* hplan_occ = nullptr;   // [3 maxE] occurrence -> {slot or -1, CSR position}
@@ -3985,6 +3994,7 @@ extern "C" int acf_apr_share_failsafe(acf_apr_ctx* c, acf_apr_ctx* peer) {
 }
 
 extern "C" int acf_apr_resolve_all(void) {
+  std::lock_guard<std::recursive_mutex> lk(g_groups_mu);
   for (size_t k = 0; k < g_groups.size(); ++k)
     if (!g_groups[k]->q.empty()) ACF_RET(resolve(g_groups[k]->q.front().c, 2));
   return ACF_OK;

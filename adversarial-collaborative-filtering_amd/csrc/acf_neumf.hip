@@ -128,6 +128,9 @@ struct NArgs {
   // occurrence) once the clean pass's owner has stored the row's delta and gradient
   unsigned long long* rdone;  // [U1 + I1]
   int32_t gen;
+  // polls a rows-in-line wait makes before it gives up (err bit 512; 0: give up at
+  // once -- acf_neumf_set_spin_limit, the failsafe's forcing test)
+  int32_t spin;
   float* pred;
   int32_t* err;
 };
@@ -590,8 +593,12 @@ __device__ __forceinline__ void row_wait_finish_one(const NArgs& a, const int32_
     cnt += __popcll(__ballot(j < B && j >= b && L[j] == r));
   }
   int32_t* ctr = a.rcnt + (s ? a.U1 : 0) + r;
+  // a give-up leaves the launch's results undefined (never its addresses: every
+  // index is clamped) and its counters stale: the host resets them and, with the
+  // failsafe on, replays the call on the row-sum path (acf_neumf_train / _grad)
+  if (a.spin == 0 && lane == 0) atomicOr(a.err, 512);  // forced: every owner reports a give-up
   for (int it = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cnt;) {
-    if (++it > ACF_SPIN_LIMIT) {
+    if (++it > a.spin) {
       if (lane == 0) atomicOr(a.err, 512);
       break;
     }
@@ -802,7 +809,7 @@ __device__ __forceinline__ void inst_block(const NArgs& a, unsigned bx, unsigned
         for (int it = 0;; ++it) {
           v = __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((int32_t)(v >> 32) == a.gen) break;
-          if (it > ACF_SPIN_LIMIT) {
+          if (it >= a.spin) {
             atomicOr(a.err, 512);
             break;
           }
@@ -1593,6 +1600,14 @@ struct acf_neumf_ctx {
   hipEvent_t ev_next = nullptr, ev_rest = nullptr;
   int32_t lazy_s = LAZY_S;           // catch-up period (< LAZY_W)
   int64_t catchup_wg = CATCHUP_WG;   // workgroups of a catch-up slice
+  // rows-in-line failure safety (acf_neumf_set_spin_limit / _set_failsafe): a give-up
+  // (err bit 512) is replayed from a snapshot of the call's inputs on the row-sum path
+  int32_t spin = ACF_SPIN_LIMIT;
+  int32_t failsafe = 1;
+  int64_t recoveries = 0;     // calls replayed
+  bool unchecked_fr = false;  // an unchecked rows-in-line grad has not been verified yet
+  float* snap = nullptr;      // [P | G | m | v] of the call being verified (allocated at first use)
+  size_t snap_n = 0;          // floats in snap
   std::vector<void*> allocs;
 };
 
@@ -1631,10 +1646,30 @@ extern "C" int acf_neumf_set_rows_in_line(acf_neumf_ctx* c, int32_t on) {
   return ACF_OK;
 }
 
+extern "C" int acf_neumf_set_spin_limit(acf_neumf_ctx* c, int32_t polls) {
+  ACF_CHECK(c != nullptr, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(polls >= 0, ACF_E_INVALID, "spin limit must be >= 0, got %d", polls);
+  c->spin = polls;
+  return ACF_OK;
+}
+
+extern "C" int acf_neumf_set_failsafe(acf_neumf_ctx* c, int32_t on) {
+  ACF_CHECK(c != nullptr, ACF_E_INVALID, "ctx is NULL");
+  c->failsafe = on ? 1 : 0;
+  return ACF_OK;
+}
+
+extern "C" int acf_neumf_recoveries(acf_neumf_ctx* c, int64_t* out) {
+  ACF_CHECK(c != nullptr && out != nullptr, ACF_E_INVALID, "NULL argument");
+  *out = c->recoveries;
+  return ACF_OK;
+}
+
 extern "C" int acf_neumf_destroy(acf_neumf_ctx* c) {
   if (!c) return ACF_OK;
   if (c->side) (void)hipStreamSynchronize(c->side);
   for (void* p : c->allocs) (void)hipFree(p);
+  if (c->snap) (void)hipFree(c->snap);
   if (c->ev_next) (void)hipEventDestroy(c->ev_next);
   if (c->ev_rest) (void)hipEventDestroy(c->ev_rest);
   if (c->side) (void)hipStreamDestroy(c->side);
@@ -1701,7 +1736,7 @@ static NArgs make_args(acf_neumf_ctx* c, const float* P, float* G, const int32_t
   a.contrib = c->contrib; a.wpart = c->wpart;
   a.h0 = c->h0; a.a1 = c->a1; a.dz1 = c->dz1; a.dz2 = c->dz2;
   a.delta = c->delta; a.owner = c->owner; a.pred = nullptr; a.err = c->err;
-  a.rcnt = c->rcnt; a.with_delta = 0; a.eps = 0.f; a.rdone = c->rdone; a.gen = 0;
+  a.rcnt = c->rcnt; a.with_delta = 0; a.eps = 0.f; a.rdone = c->rdone; a.gen = 0; a.spin = c->spin;
   return a;
 }
 
@@ -1735,14 +1770,82 @@ static int set_inst_smem_limit() {
   return ACF_OK;
 }
 
-static int read_err(acf_neumf_ctx* c, hipStream_t s) {
-  int32_t herr = 0;
-  HIP_TRY(hipMemcpyAsync(&herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+static int fetch_err(acf_neumf_ctx* c, hipStream_t s, int32_t* herr) {
+  *herr = 0;
+  HIP_TRY(hipMemcpyAsync(herr, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  return ACF_OK;
+}
+
+static int check_err(int32_t herr) {
   ACF_CHECK(!(herr & 256), ACF_E_HIP, "lazy Adam: a row fell behind the learning-rate window (internal)");
-  ACF_CHECK(!(herr & 512), ACF_E_HIP, "rows in line: a row wave timed out waiting for its arrivals (internal)");
+  ACF_CHECK(!(herr & 512), ACF_E_HIP, "rows in line: a row wave timed out waiting for its arrivals "
+            "(failsafe off: the call's results are undefined)");
   ACF_CHECK(herr == 0, ACF_E_RANGE, "index out of range (%s%s)", (herr & 1) ? "user >= num_user_rows " : "",
             (herr & 2) ? "item >= num_item_rows" : "");
+  return ACF_OK;
+}
+
+static int read_err(acf_neumf_ctx* c, hipStream_t s) {
+  int32_t herr = 0;
+  int r = fetch_err(c, s, &herr);
+  return r != ACF_OK ? r : check_err(herr);
+}
+
+// After a give-up: late arrivals may have landed after their owner re-armed its
+// counter, so every arrival counter is zeroed (the stream is idle: fetch_err
+// synchronised it) before anything else runs on this context.  rdone needs no
+// reset: its entries carry the launch generation.
+static int reset_row_counters(acf_neumf_ctx* c, hipStream_t s) {
+  HIP_TRY(hipMemsetAsync(c->rcnt, 0, 2 * (size_t)(c->U1 + c->I1) * sizeof(int32_t), s));
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ACF_OK;
+}
+
+// An unchecked acf_neumf_grad on the rows-in-line path is verified by the next
+// call that reads the error word (grad with check, train, predict) before that
+// call clears it: a give-up there cannot be replayed any more (the caller may have
+// consumed the gradient), so it is reported, never dropped.
+static int settle_unchecked(acf_neumf_ctx* c, hipStream_t s) {
+  if (!c->unchecked_fr) return ACF_OK;
+  int32_t herr = 0;
+  int r = fetch_err(c, s, &herr);
+  if (r != ACF_OK) return r;
+  c->unchecked_fr = false;
+  if (herr & 512) {
+    r = reset_row_counters(c, s);
+    if (r != ACF_OK) return r;
+    return set_error(ACF_E_HIP, "rows in line: an earlier unchecked acf_neumf_grad call timed out waiting for "
+                     "its arrivals; the gradient it added is undefined");
+  }
+  return ACF_OK;
+}
+
+// the failsafe's snapshot of the buffers a call writes (nbuf of P, G, m, v: each
+// L.total floats), taken on the call's stream before its first launch
+static int take_snapshot(acf_neumf_ctx* c, hipStream_t s, float* const* bufs, int nbuf) {
+  const size_t n = (size_t)c->L.total;
+  if (c->snap_n < 4 * n) {
+    if (c->snap) HIP_TRY(hipFree(c->snap));
+    c->snap = nullptr;
+    c->snap_n = 0;
+    if (hipMalloc(&c->snap, 4 * n * sizeof(float)) != hipSuccess) {
+      (void)hipGetLastError();
+      c->snap = nullptr;
+      return set_error(ACF_E_NOMEM, "failsafe snapshot: hipMalloc of %zu bytes failed", 4 * n * sizeof(float));
+    }
+    c->snap_n = 4 * n;
+  }
+  for (int k = 0; k < nbuf; ++k)
+    HIP_TRY(hipMemcpyAsync(c->snap + k * n, bufs[k], n * sizeof(float), hipMemcpyDeviceToDevice, s));
+  return ACF_OK;
+}
+
+static int restore_snapshot(acf_neumf_ctx* c, hipStream_t s, float* const* bufs, int nbuf) {
+  const size_t n = (size_t)c->L.total;
+  for (int k = 0; k < nbuf; ++k)
+    HIP_TRY(hipMemcpyAsync(bufs[k], c->snap + k * n, n * sizeof(float), hipMemcpyDeviceToDevice, s));
   return ACF_OK;
 }
 
@@ -1834,11 +1937,34 @@ extern "C" int acf_neumf_grad(acf_neumf_ctx* c, const float* P, float* G, const 
   ACF_CHECK(c && P && G && u && i && y && hp, ACF_E_INVALID, "NULL argument");
   ACF_CHECK(B > 0 && B <= c->maxB, ACF_E_INVALID, "batch %d outside (0, %d]", B, c->maxB);
   hipStream_t s = static_cast<hipStream_t>(stream_);
-  if (check) HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
-  int r = launch_grad(c, P, G, u, i, y, B, hp, loss_out, s);
+  const bool fr = B <= FR_MAXB && c->rows_in_line;
+  if (!check) {  // verified by the next checking call (settle_unchecked)
+    int r = launch_grad(c, P, G, u, i, y, B, hp, loss_out, s);
+    if (r == ACF_OK && fr) c->unchecked_fr = true;
+    return r;
+  }
+  int r = settle_unchecked(c, s);
   if (r != ACF_OK) return r;
-  if (check) return read_err(c, s);
-  return ACF_OK;
+  HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
+  float* bufs[1] = {G};
+  const bool snap = fr && c->failsafe;
+  if (snap && (r = take_snapshot(c, s, bufs, 1)) != ACF_OK) return r;
+  if ((r = launch_grad(c, P, G, u, i, y, B, hp, loss_out, s)) != ACF_OK) return r;
+  int32_t herr = 0;
+  if ((r = fetch_err(c, s, &herr)) != ACF_OK) return r;
+  if ((herr & 512) && fr) {
+    if ((r = reset_row_counters(c, s)) != ACF_OK) return r;
+    if (!snap) return check_err(herr);
+    // the exact replay: G as the call found it, the row-sum path (same bits)
+    if ((r = restore_snapshot(c, s, bufs, 1)) != ACF_OK) return r;
+    c->rows_in_line = 0;
+    r = launch_grad(c, P, G, u, i, y, B, hp, loss_out, s);
+    c->rows_in_line = 1;
+    if (r != ACF_OK) return r;
+    ++c->recoveries;
+    if ((r = fetch_err(c, s, &herr)) != ACF_OK) return r;
+  }
+  return check_err(herr);
 }
 
 // lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t), evaluated in float32 as Keras does
@@ -1866,14 +1992,9 @@ extern "C" int acf_neumf_adam(acf_neumf_ctx* c, float* P, float* G, float* m, fl
   return launch_adam(c, P, G, m, v, t, hp, static_cast<hipStream_t>(stream_));
 }
 
-extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, float* v,
-                               const int32_t* u, const int32_t* i, const float* y, int64_t n,
-                               int32_t batch, int64_t t_first, const acf_neumf_hparams* hp,
-                               float* losses, void* stream_) {
-  ACF_CHECK(c && P && G && m && v && u && i && y && hp, ACF_E_INVALID, "NULL argument");
-  ACF_CHECK(batch > 0 && batch <= c->maxB, ACF_E_INVALID, "batch %d outside (0, %d]", batch, c->maxB);
-  ACF_CHECK(n >= 0 && t_first >= 1, ACF_E_INVALID, "bad instance count or Adam iteration");
-  hipStream_t s = static_cast<hipStream_t>(stream_);
+static int train_launches(acf_neumf_ctx* c, float* P, float* G, float* m, float* v, const int32_t* u,
+                          const int32_t* i, const float* y, int64_t n, int32_t batch, int64_t t_first,
+                          const acf_neumf_hparams* hp, float* losses, hipStream_t s) {
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
   float4 *P4 = reinterpret_cast<float4*>(P), *G4 = reinterpret_cast<float4*>(G);
   float4 *m4 = reinterpret_cast<float4*>(m), *v4 = reinterpret_cast<float4*>(v);
@@ -1956,7 +2077,44 @@ extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, f
     k_nmf_adam_catchup<<<rows_grid(nrows, 256 * 16), 256, 0, s>>>(P4, G4, m4, v4, ak, z, 0, nrows);
     HIP_TRY(hipGetLastError());
   }
-  return read_err(c, s);
+  return ACF_OK;
+}
+
+// The call is verified once, at its end (it synchronises there anyway).  With the
+// rows-in-line step and the failsafe on, P, G, m, v are copied first (4 x the
+// parameter bytes, D2D: ~40 us for the yelp shape against a ~150 ms epoch); a
+// give-up (err bit 512) restores them and replays the whole call on the row-sum
+// path, which gives the same bits (test_neumf_give_up_replays_exactly).
+extern "C" int acf_neumf_train(acf_neumf_ctx* c, float* P, float* G, float* m, float* v,
+                               const int32_t* u, const int32_t* i, const float* y, int64_t n,
+                               int32_t batch, int64_t t_first, const acf_neumf_hparams* hp,
+                               float* losses, void* stream_) {
+  ACF_CHECK(c && P && G && m && v && u && i && y && hp, ACF_E_INVALID, "NULL argument");
+  ACF_CHECK(batch > 0 && batch <= c->maxB, ACF_E_INVALID, "batch %d outside (0, %d]", batch, c->maxB);
+  ACF_CHECK(n >= 0 && t_first >= 1, ACF_E_INVALID, "bad instance count or Adam iteration");
+  hipStream_t s = static_cast<hipStream_t>(stream_);
+  int r = settle_unchecked(c, s);
+  if (r != ACF_OK) return r;
+  const bool fr = n > 0 && std::min<int64_t>(batch, n) <= FR_MAXB && c->rows_in_line;
+  float* bufs[4] = {P, G, m, v};
+  const bool snap = fr && c->failsafe;
+  if (snap && (r = take_snapshot(c, s, bufs, 4)) != ACF_OK) return r;
+  r = train_launches(c, P, G, m, v, u, i, y, n, batch, t_first, hp, losses, s);
+  if (r != ACF_OK) return r;
+  int32_t herr = 0;
+  if ((r = fetch_err(c, s, &herr)) != ACF_OK) return r;
+  if ((herr & 512) && fr) {
+    if ((r = reset_row_counters(c, s)) != ACF_OK) return r;
+    if (!snap) return check_err(herr);
+    if ((r = restore_snapshot(c, s, bufs, 4)) != ACF_OK) return r;
+    c->rows_in_line = 0;
+    r = train_launches(c, P, G, m, v, u, i, y, n, batch, t_first, hp, losses, s);
+    c->rows_in_line = 1;
+    if (r != ACF_OK) return r;
+    ++c->recoveries;
+    if ((r = fetch_err(c, s, &herr)) != ACF_OK) return r;
+  }
+  return check_err(herr);
 }
 
 #ifdef NMF_DIAG
@@ -1974,6 +2132,8 @@ extern "C" int acf_neumf_predict(acf_neumf_ctx* c, const float* P, const int32_t
   ACF_CHECK(c && P && u && i && out, ACF_E_INVALID, "NULL argument");
   ACF_CHECK(n >= 0, ACF_E_INVALID, "negative count");
   hipStream_t s = static_cast<hipStream_t>(stream_);
+  int r = settle_unchecked(c, s);
+  if (r != ACF_OK) return r;
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));
   const int64_t chunk = 1 << 28;
   for (int64_t o = 0; o < n; o += chunk) {

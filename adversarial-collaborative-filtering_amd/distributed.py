@@ -47,20 +47,23 @@ chunk's steps are captured as hipGraphs once and replayed:
 
   * world 1: the exchanges are the identity (no collective), the whole chunk is
     ONE graph;
-  * world > 1: the fixed-size RCCL all_to_all / all_gather calls are captured
-    INSIDE the graph too (``capture_collectives``, default on since r05;
-    ACF_SHARD_RCCL_GRAPH=0 turns it off), after a one-off capture + replay of an
-    all_reduce at construction that every rank must pass, so a chunk is again
-    ONE graph with no host round trip
-    per exchange.  A graph holding captured RCCL work keeps the communicator
-    busy, so the graphs are dropped before the process group goes: ``close()``,
-    the with-block, the object's collection or, failing all three, the
-    interpreter's exit (a weakref.finalize; tools/rccl_capture_probe.py checks
-    the orders).  Without captured collectives (the check failed on some rank,
-    or ACF_SHARD_RCCL_GRAPH=0) a chunk is captured as SEGMENTS cut at every
-    collective, the collectives host-issued between the segment replays, with
-    the plans in line while capturing (r04's pipelined plan straddled the cuts:
-    the capture failed -- the "allocator assertion" of r04).
+  * world > 1: a chunk is captured as SEGMENTS cut at every collective, the
+    fixed-size RCCL all_to_all / all_gather calls host-issued between the
+    segment replays (the default since r06), with the plans in line while
+    capturing (r04's pipelined plan straddled the cuts: the capture failed --
+    the "allocator assertion" of r04).  ``capture_collectives=True``
+    (or ACF_SHARD_RCCL_GRAPH=1) captures the collectives INSIDE the graph too,
+    after a one-off capture + replay of an all_reduce at construction that every
+    rank must pass, so a chunk is again ONE graph with no host round trip per
+    exchange.  That form is rehearsed only as a one-rank RCCL self-exchange on
+    one GPU (RCCL refuses two ranks on one GPU), never at world > 1 on several
+    GPUs, so it is opt-in.  A graph holding captured RCCL work keeps
+    the communicator busy, so the graphs are dropped before the process group
+    goes: ``close()``, the with-block, the object's collection or, failing all
+    three, the interpreter's exit (a weakref.finalize; tools/rccl_capture_probe.py
+    checks the orders).  The recorded collectives of a segment capture hold the
+    tensors and the group, never the object, so a dropped object is collected in
+    both forms.
     ``force_collectives`` routes the
     exchanges through the process group even at world 1 (an RCCL self-exchange):
     the one-GPU rehearsal of the captured collectives
@@ -157,6 +160,19 @@ class _Chunk:
 class _Buffers:
     """Persistent per-chunk maps and per-step exchange buffers (fixed addresses, so
     captured step graphs stay valid from one chunk to the next)."""
+
+
+def _a2a_op(G, force, stage, group, out, inp, out_splits=None, in_splits=None) -> None:
+    """One all_to_all_single of `inp` into `out` (a copy at world 1 unless forced;
+    host-staged over gloo for device tensors: the one-GPU rehearsal of several ranks)."""
+    if G == 1 and not force:
+        out.copy_(inp)
+    elif stage:
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
 def _hp_key(hp) -> tuple:
@@ -258,8 +274,8 @@ class ShardedAPR:
         self.local = local(me) if local is not None else HipLocal(me)
         can_graph = (self.device.type == "cuda" and not self._stage and getattr(self.local, "graphable", False))
         self.graph = (True if graph is None else bool(graph)) and can_graph
-        if capture_collectives is None:  # default on (r05); ACF_SHARD_RCCL_GRAPH=0 keeps the steps eager
-            capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "1") != "0"
+        if capture_collectives is None:  # default off (r06): opt in with ACF_SHARD_RCCL_GRAPH=1
+            capture_collectives = os.environ.get("ACF_SHARD_RCCL_GRAPH", "0") == "1"
         multi = self.G > 1 or self._force  # exchanges that are collectives
         self._multi = multi
         self._cap_coll = bool(capture_collectives) and self.graph and multi
@@ -391,14 +407,7 @@ class ShardedAPR:
         return agree(ok)
 
     def _a2a(self, out, inp, out_splits=None, in_splits=None):
-        if self.G == 1 and not self._force:  # one rank: the exchange is a copy
-            out.copy_(inp)
-        elif self._stage:  # gloo with device tensors (rehearsal of several ranks on one GPU)
-            o = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
-            out.copy_(o)
-        else:
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        _a2a_op(self.G, self._force, self._stage, self.group, out, inp, out_splits, in_splits)
 
     def _exchange(self, out, inp):
         """Fixed-size exchange of G blocks of C rows (block o to / from rank o);
@@ -406,7 +415,11 @@ class ShardedAPR:
         if self.G == 1 and not self._force:
             return inp
         n = self.G * self._C
-        self._collective(lambda: self._a2a(out[:n], inp[:n]))
+        # the closure holds the tensors and the group, never self: a segment
+        # recorder keeps it, and the finalizer's graphs must not keep this object
+        # alive
+        G, force, stage, group, o, x = self.G, self._force, self._stage, self.group, out[:n], inp[:n]
+        self._collective(lambda: _a2a_op(G, force, stage, group, o, x))
         return out
 
     def _gather_q(self):
@@ -415,14 +428,15 @@ class ShardedAPR:
         if self.G == 1 and not self._force:
             return self._Qst
         self._qpad[: self.ni] = self.Q
+        G, stage, group, qall, qpad, cap, d = self.G, self._stage, self.group, self._qall, self._qpad, self._qcap, self.d
 
-        def gather():
-            if self._stage:
-                parts = [torch.empty(self._qcap, self.d) for _ in range(self.G)]
-                dist.all_gather(parts, self._qpad.cpu(), group=self.group)
-                self._qall.copy_(torch.cat(parts))
+        def gather():  # no reference to self (see _exchange)
+            if stage:
+                parts = [torch.empty(cap, d) for _ in range(G)]
+                dist.all_gather(parts, qpad.cpu(), group=group)
+                qall.copy_(torch.cat(parts))
             else:
-                dist.all_gather_into_tensor(self._qall, self._qpad, group=self.group)
+                dist.all_gather_into_tensor(qall, qpad, group=group)
         self._collective(gather)
         return self._qall
 

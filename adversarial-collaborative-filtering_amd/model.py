@@ -109,7 +109,17 @@ class MF:
     # -- state ----------------------------------------------------------------
     @property
     def tables(self):
+        """The four tables for a READER: every queued streamed call is settled
+        first (its lazy verification, ops.settle_tables)."""
         ops.settle_tables()
+        return self.launch_tables
+
+    @property
+    def launch_tables(self):
+        """The four tables for a training LAUNCH, without settling: a launch on
+        them is ordered after the queued calls on the stream, and the native
+        failure-safe gate covers the rest (settling here blocked the
+        host on every queued call at each epoch)."""
         return (self.embedding_P, self.embedding_Q, self.accumulator_P, self.accumulator_Q)
 
     def hparams(self, adver=None) -> ops.StepHParams:
@@ -157,7 +167,7 @@ class MF:
     def delta_update(self, u, i, j):
         """sess.run([update_P, update_Q], feed) — utils.py:117-118."""
         ctx = self._plan_feed(u, i, j)
-        ctx.delta_update(self.tables, self.hparams(adver=1), 0)
+        ctx.delta_update(self.launch_tables, self.hparams(adver=1), 0)
         self._delta_feed = (u, i, j)
 
     def optimizer_step(self, u, i, j):
@@ -170,7 +180,7 @@ class MF:
             ctx = self._ctx
         elif not self.adver:
             ctx = self._plan_feed(u, i, j)
-        ctx.optimizer_step(self.tables, self.hparams(), 0)
+        ctx.optimizer_step(self.launch_tables, self.hparams(), 0)
         self._delta_feed = None
 
     def scores(self, users, items):

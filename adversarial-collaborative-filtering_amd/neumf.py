@@ -108,6 +108,21 @@ class NeuMFContext:
         (default) or by the separate row-sum kernel (bit-identical; tests / A/B)."""
         _native.call_neumf("acf_neumf_set_rows_in_line", self._ptr, int(bool(on)))
 
+    def set_spin_limit(self, polls: int) -> None:
+        """Polls a rows-in-line wait makes before it gives up (0: at once; tests)."""
+        _native.call_neumf("acf_neumf_set_spin_limit", self._ptr, int(polls))
+
+    def set_failsafe(self, on: bool) -> None:
+        """On (default): a give-up is replayed exactly on the row-sum path;
+        off: it raises RuntimeError."""
+        _native.call_neumf("acf_neumf_set_failsafe", self._ptr, int(bool(on)))
+
+    def recoveries(self) -> int:
+        """Calls replayed after a rows-in-line give-up."""
+        out = ctypes.c_int64()
+        _native.call_neumf("acf_neumf_recoveries", self._ptr, ctypes.byref(out))
+        return int(out.value)
+
     @staticmethod
     def hparams(lr=0.001, beta1=0.9, beta2=0.999, adam_eps=1e-7, adver=0, eps=0.5, reg_adv=1.0):
         return _native.NeuMFHParams(lr, beta1, beta2, adam_eps, eps, reg_adv, int(bool(adver)), 0)

@@ -622,8 +622,12 @@ def _unique_exclusions(off: torch.Tensor, ex: torch.Tensor, n_users: int) -> tor
     host sync; the lengths stay as given."""
     if ex.numel() < 2:
         return ex
-    seg = torch.repeat_interleave(torch.arange(n_users, device=ex.device), off[1:] - off[:-1],
-                                  output_size=ex.numel())
+    # each list's segment id by a search over the offsets (no assumption that
+    # off[0] == 0 or off[-1] == len(ex); entries outside every list get -1 and
+    # are left alone; ADVICE r05)
+    pos = torch.arange(ex.numel(), device=ex.device, dtype=off.dtype)
+    seg = torch.searchsorted(off[1:].contiguous(), pos, right=True)
+    seg = torch.where((pos >= off[0]) & (seg < n_users), seg, torch.full_like(seg, -1))
     wide = int(2 ** 31)
     key = seg * wide + ex.long().clamp(-1, wide - 2) + 1
     skey, perm = torch.sort(key)

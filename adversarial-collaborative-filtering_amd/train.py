@@ -72,7 +72,7 @@ def training_batch(model, sess, batches, adver=False, graph=True):
         B, nb = ep.batch_size, ep.n_batches
         hp = model.hparams(adver=int(bool(adver)))
         pipe = model.pipeline(B, min(nb, plan_chunk(B)))
-        pipe.run(model.tables, hp, ep.user, ep.item_pos, ep.item_neg, graph=graph, check=True)
+        pipe.run(model.launch_tables, hp, ep.user, ep.item_pos, ep.item_neg, graph=graph, check=True)
         errs = pipe.step_errors()  # one stream sync per epoch
         if errs:
             raise ops.StepWaitError(errs)
@@ -90,8 +90,8 @@ def training_batch(model, sess, batches, adver=False, graph=True):
         ctx = model.context(uu.numel(), 1)
         ctx.plan(uu, item_input_pos[k], sel, uu.numel())
         if hp.adver:
-            ctx.delta_update(model.tables, hp, 0)
-        ctx.optimizer_step(model.tables, hp, 0)
+            ctx.delta_update(model.launch_tables, hp, 0)
+        ctx.optimizer_step(model.launch_tables, hp, 0)
         negs.append(sel.cpu().numpy().reshape(-1, 1))
     return user_input, item_input_pos, negs
 

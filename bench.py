@@ -13,6 +13,9 @@ tables) already resident in HBM.  value = triplets/s over all ranks.
 --gpus N (torchrun, one rank per GPU): N independent APR jobs (replicas, weak
 scaling) — the reference's experiments are independent single-process runs and a
 B = 512 step has no data-parallel split worth an exchange.
+An unaided `bench.py --gpus N` (no WORLD_SIZE in the environment) starts torchrun
+with N ranks itself as a child process; a WORLD_SIZE that differs from --gpus is
+an error.
 
 Extra fields: "roofline" (dominant kernel, HIP-event kernel times),
 "cpu_baseline" (the reference's CPU hot loop restated in torch-CPU on every
@@ -74,6 +77,48 @@ def parse():
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def launch_command(argv, gpus: int, port: int) -> list:
+    """The child command `--gpus N` (N > 1) runs when no launcher started this
+    process: torchrun with one rank per GPU, every flag passed through unchanged
+    (the ranks see WORLD_SIZE = N and run the multi-rank path)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def check_world(gpus: int, env) -> str:
+    """What `--gpus` asks of this process, decided before anything touches the GPU:
+      "run"    -- this process is a rank (or the whole job at N = 1);
+      "launch" -- N > 1 and no WORLD_SIZE: start N ranks as a child (launch_command);
+    a WORLD_SIZE that disagrees with --gpus is an error (SystemExit 2), so a job can
+    never report an n_gpus other than the one it was asked for."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus}: must be >= 1")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {gpus}")
+    return "run"
+
+
+def launch_ranks(a) -> int:
+    """The parent of an unaided `bench.py --gpus N`: it never initialises the GPU
+    (a process that has must not start another program in its place), checks that
+    N devices exist (or --rehearse-one-gpu: every rank on cuda:0), runs torchrun as
+    a child process whose rank 0 prints the one JSON line on the inherited stdout,
+    and returns the child's exit status."""
+    import subprocess
+    if not a.rehearse_one_gpu:
+        n = torch.cuda.device_count()  # counts devices without initialising HIP
+        if n < a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but {n} GPU(s) visible "
+                             f"(--rehearse-one-gpu puts every rank on cuda:0 over gloo)")
+    port = 29500 + os.getpid() % 2000
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launch_command(sys.argv[1:], a.gpus, port), env=env)
 
 
 def batch_stats(u, i, j, B, nb, U1, I1):
@@ -577,6 +622,8 @@ def eval_bench(acf, dev, reps=5):
 
 def main():
     a = parse()
+    if check_world(a.gpus, os.environ) == "launch":
+        sys.exit(launch_ranks(a))
     # RCCL prints its version banner on stdout at init: keep fd 1 for the one JSON line
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
@@ -673,6 +720,11 @@ def main():
         "step_errors": step_errors,
         "stream_recoveries": recoveries,
         "step_stream": roof["kernel"].startswith("k_stream"),
+        # the process group this line was measured in: ranks, backend, and how many
+        # of them talk over RCCL (0 for the one-GPU gloo rehearsal)
+        "world": {"ranks": world, "backend": None if dist is None else dist.get_backend(),
+                  "rccl_ranks": world if dist is not None and dist.get_backend() == "nccl" else 0,
+                  "gpus_flag": a.gpus, "rehearsal": bool(a.rehearse_one_gpu)},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cb = cpu_baseline(u, i, j, P0, Q0, B, a.cpu_batches)

@@ -68,6 +68,20 @@ int acf_neumf_grad(acf_neumf_ctx* ctx, const float* params, float* grad, const i
  * same-box A/B).  Default 1. */
 int acf_neumf_set_rows_in_line(acf_neumf_ctx* ctx, int32_t on);
 
+/* Failure safety of the rows-in-line kernels (no reference counterpart: Keras has
+ * no cross-workgroup waits).  Their row owners wait, bounded, for the other
+ * workgroups' contributions; a wait that gives up after `polls` polls (default
+ * 2^22; 0 = give up at once, for tests) leaves the launch's results undefined.
+ * With the failsafe on (default) acf_neumf_train and a checked acf_neumf_grad
+ * snapshot the buffers they write first (train: params, grad, m, v; grad: grad)
+ * and, on a give-up, restore them and replay the call on the row-sum kernels:
+ * the same bits as a call that never gave up.  Failsafe off: ACF_E_HIP.  An
+ * unchecked grad that gave up is reported (ACF_E_HIP) by the next grad with
+ * check, train or predict on the context.  acf_neumf_recoveries: calls replayed. */
+int acf_neumf_set_spin_limit(acf_neumf_ctx* ctx, int32_t polls);
+int acf_neumf_set_failsafe(acf_neumf_ctx* ctx, int32_t on);
+int acf_neumf_recoveries(acf_neumf_ctx* ctx, int64_t* count);
+
 /* Keras 2.2 Adam over the whole buffer, iteration t (1-based); zeroes grad. */
 int acf_neumf_adam(acf_neumf_ctx* ctx, float* params, float* grad, float* m, float* v,
                    int64_t t, const acf_neumf_hparams* hp, void* stream);

@@ -155,14 +155,15 @@ def test_sharded_collectives_captured_in_graph_world1(ops, dev, exchange, routed
     """The RCCL collectives of the split step captured INSIDE the step graph
     (capture_collectives), rehearsed on one GPU: force_collectives issues every
     exchange through a one-rank nccl group (an RCCL self-exchange) instead of the
-    world-1 identity.  On the DEFAULT settings (capture_collectives=None, r05) the
-    constructor's capture check passes, a chunk is ONE graph, and eager /
-    collectives-in-graph runs give identical bits (pinterest-20 shape,
-    configs[2]); with the collectives kept out of graphs (capture_collectives=
-    False) a chunk is captured as segments cut at every collective (the plans in
-    line while capturing: r04's pipelined plan straddled the cuts) and gives the
-    same bits.  The captured object is then dropped without close(): its
-    finalizer releases the graphs before the process group is destroyed."""
+    world-1 identity.  With capture_collectives=True the constructor's capture
+    check passes, a chunk is ONE graph, and eager / collectives-in-graph runs give
+    identical bits (pinterest-20 shape, configs[2]); with the collectives kept out
+    of graphs (capture_collectives=False, and the default since r06: ADVICE r05)
+    a chunk is captured as segments cut at every collective (the plans in line
+    while capturing: r04's pipelined plan straddled the cuts) and gives the same
+    bits.  Both captured objects are then dropped without close(): the finalizer
+    releases the graphs before the process group is destroyed -- in segment mode
+    too, whose recorded collectives hold no reference to the object."""
     D_ = importlib.import_module(PKG + ".distributed")
     U1, I1, d, B, nb = 55_188, 9_917, 64, 512, 12
     P, Q, u, i, j = _problem(9, U1, I1, d, B, nb)
@@ -171,10 +172,10 @@ def test_sharded_collectives_captured_in_graph_world1(ops, dev, exchange, routed
     outs, segs = [], []
     try:
         uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
-        for graph, cap in ((False, False), (True, False), (None, None)):
+        for graph, cap in ((False, False), (None, None), (True, True)):
             sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, item_exchange=exchange, graph=graph,
                                local_batch=B if routed else None, force_collectives=True, capture_collectives=cap)
-            on = cap is None  # the defaults capture the collectives
+            on = bool(cap)  # the default (None) keeps the collectives between segments
             assert sh._cap_coll == on and sh.graph == (graph is not False)
             hp = ops.StepHParams(adver=1)
             (sh.train_routed if routed else sh.train)(uu, ii, jj, hp, chunk=4)
@@ -184,7 +185,7 @@ def test_sharded_collectives_captured_in_graph_world1(ops, dev, exchange, routed
             segs.append([len(r.segs) for r in sh._graphs.values()])
             assert (sh.stats["graph_replays"] >= 1) == (graph is not False)
             graphs = sh._graphs
-            if on:
+            if graph is not False:
                 assert graphs
                 del sh  # no close(): the finalizer drops the graphs
                 if graphs:  # never expected; drop them before the group goes (a hang otherwise)

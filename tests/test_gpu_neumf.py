@@ -240,10 +240,11 @@ def test_yelp_shaped_grad_matches_oracle(nm, dev, adver):
     (100, 41, 37, 300, 128),       # d = 128 (weights read from global), partial blocks
 ])
 def test_neumf_rows_in_line_matches_rows_kernel(nm, dev, B, U1, I1, n, d):
-    """Batches of <= 1,024 instances sum their rows inside k_nmf_inst (the last
-    arrival at a row sums it, from write-through contributions; the block's
-    weight-gradient tiles from LDS): one gradient and one train epoch equal the
-    k_nmf_rows path's bit for bit (parameters, Adam moments, losses)."""
+    """Batches of <= 1,024 instances sum their rows inside the instance launch
+    (each row's first occurrence owns it: its row wave waits for the row's
+    arrival count, then adds the write-through contributions in instance order;
+    the block's weight-gradient tiles from LDS): one gradient and one train epoch
+    equal the k_nmf_rows path's bit for bit (parameters, Adam moments, losses)."""
     P = N.init_params(U1, I1, d, 31)
     rng = np.random.default_rng(13)
     u = rng.integers(0, U1, n).astype(np.int32)
@@ -266,3 +267,55 @@ def test_neumf_rows_in_line_matches_rows_kernel(nm, dev, B, U1, I1, n, d):
         torch.cuda.synchronize()
         assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
         assert torch.equal(ta, tb)
+
+
+@pytest.mark.parametrize("B,U1,I1,n,d", [(512, 2000, 3000, 1500, 64), (100, 41, 37, 300, 128)])
+def test_neumf_give_up_replays_exactly(nm, dev, B, U1, I1, n, d):
+    """ Spin limit 0 makes every rows-in-line wait give up at
+    once.  With the failsafe on, acf_neumf_train and a checked acf_neumf_grad
+    restore what they wrote from their snapshot and replay on the row-sum path:
+    the bits of set_rows_in_line(False), one recovery per call, and the context
+    is sound afterwards (the stale arrival counters were zeroed: a normal call
+    then matches too).  Failsafe off: the give-up raises; an unchecked grad's
+    give-up is raised by the next checking call."""
+    P = N.init_params(U1, I1, d, 47)
+    rng = np.random.default_rng(19)
+    u = rng.integers(0, U1, n).astype(np.int32)
+    i = ((rng.zipf(1.3, n) - 1) % I1).astype(np.int32)
+    y = (rng.random(n) < 0.5).astype(np.float32)
+    for adver in (1, 0):
+        a, b = _state(nm, P, dev), _state(nm, P, dev)
+        ca, cb = nm.NeuMFContext(a, B), nm.NeuMFContext(b, B)
+        cb.set_rows_in_line(False)
+        hp = ca.hparams(adver=adver, eps=0.5, reg_adv=0.7)
+        ca.set_spin_limit(0)
+        la, lb = torch.zeros(2, device=dev), torch.zeros(2, device=dev)
+        ca.grad(u[:B], i[:B], y[:B], hp, la)
+        cb.grad(u[:B], i[:B], y[:B], hp, lb)
+        torch.cuda.synchronize()
+        assert ca.recoveries() == 1
+        assert torch.equal(a.grad, b.grad) and torch.equal(la, lb)
+        a.grad.zero_()
+        b.grad.zero_()
+        ta, tb = ca.train(u, i, y, B, hp), cb.train(u, i, y, B, hp)
+        torch.cuda.synchronize()
+        assert ca.recoveries() == 2
+        assert torch.equal(a.params, b.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+        assert torch.equal(ta, tb)
+        # back to the default limit: the next call runs in line and still matches
+        ca.set_spin_limit(1 << 22)
+        ta, tb = ca.train(u, i, y, B, hp), cb.train(u, i, y, B, hp)
+        torch.cuda.synchronize()
+        assert ca.recoveries() == 2
+        assert torch.equal(a.params, b.params) and torch.equal(ta, tb)
+        # failsafe off: reported, and the context recovers for the next call
+        ca.set_failsafe(False)
+        ca.set_spin_limit(0)
+        with pytest.raises(RuntimeError, match="timed out"):
+            ca.train(u, i, y, B, hp)
+        # an unchecked grad that gives up is raised by the next checking call
+        ca.grad(u[:B], i[:B], y[:B], hp, None, check=False)
+        ca.set_spin_limit(1 << 22)
+        with pytest.raises(RuntimeError, match="earlier unchecked"):
+            ca.predict(u[:8], i[:8])
+        ca.predict(u[:8], i[:8])  # reported once
