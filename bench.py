@@ -282,8 +282,9 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
     """BASELINE.md §2 / SURVEY §8(d): the reference's CPU hot loop restated, timed
     on this box's host over ONE full ml-1m-shaped epoch (nb batches of B) of the
     APR phase with the reference's dense delta work (APR.py:183-191).  `value` is
-    the STRONGEST faithful restatement measured: today the C
-    oracle (oracle/apr_oracle.c, dense mode, one thread).  Beside it: the TF graph
+    the STRONGEST faithful restatement measured: the C
+    oracle (oracle/apr_oracle.c, dense mode) on one thread and on every host
+    thread this job may use (OMP_NUM_THREADS: 16 on the GPU box).  Beside it: the TF graph
     op for op in torch-CPU fp32 on every host thread (TF's CPU kernels run on its
     intra-op pool) for the APR phase, the BPR phase and a touched-rows-only APR
     variant.  Sampling and evaluation are excluded (APR.py:261-263)."""
@@ -304,13 +305,24 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
     apr_dense, bpr, apr_sparse = run(True, True), run(False, True), run(True, False)
     o = COracle()
     Pn, Qn = P0.cpu().numpy().copy(), Q0.cpu().numpy().copy()
+    Un, In, Jn = U.int().numpy(), I.int().numpy(), J.int().numpy()
     t0 = time.perf_counter()
-    o.apr_train(Pn, Qn, np.full_like(Pn, 0.1), np.full_like(Qn, 0.1), U.int().numpy(), I.int().numpy(),
-                J.int().numpy(), B, HParams(adver=1), dense=True)
+    o.apr_train(Pn, Qn, np.full_like(Pn, 0.1), np.full_like(Qn, 0.1), Un, In, Jn, B, HParams(adver=1), dense=True)
     c1 = nb * B / (time.perf_counter() - t0)
-    nthr = torch.get_num_threads()
+    # the same restatement on every host thread this job may use (rows partitioned
+    # by thread, sums in the one-thread order: the same bits)
+    nthr = threads()
+    Pm, Qm = P0.cpu().numpy().copy(), Q0.cpu().numpy().copy()
+    t0 = time.perf_counter()
+    o.apr_train_mt(Pm, Qm, np.full_like(Pm, 0.1), np.full_like(Qm, 0.1), Un, In, Jn, B, HParams(adver=1),
+                   dense=True, threads=nthr)
+    cm = nb * B / (time.perf_counter() - t0)
+    same = bool(np.array_equal(Pm, Pn) and np.array_equal(Qm, Qn))
     variants = {"c_oracle_dense": (c1, 1, "oracle/apr_oracle.c (dense mode), the TF graph's arithmetic in C, "
                                           "one thread"),
+                "c_oracle_dense_threads": (cm, nthr, f"oracle/apr_oracle.c (dense mode, oracle_apr_train_mt), the "
+                                                     f"TF graph's arithmetic in C on {nthr} OpenMP threads, the "
+                                                     f"one-thread result bit for bit"),
                 "torch_cpu_dense": (apr_dense, nthr, f"oracle/apr_torch_cpu.py, the TF graph op for op in "
                                                      f"torch-CPU fp32 on {nthr} threads")}
     best = max(variants, key=lambda k: variants[k][0])
@@ -321,6 +333,7 @@ def cpu_baseline(u, i, j, P0, Q0, B, nb):
                       f"delta densify/normalise/assign per batch (APR.py:183-191): {what}; the strongest of "
                       f"the CPU restatements measured here",
             "c_oracle_1thread_apr_dense": round(c1, 1),
+            "c_oracle_threads_apr_dense": {"value": round(cm, 1), "cores": nthr, "bits_equal_1thread": same},
             "torch_cpu_apr_dense": {"value": round(apr_dense, 1), "cores": nthr},
             "torch_cpu_bpr_phase": round(bpr, 1),
             "torch_cpu_apr_touched_rows_only": round(apr_sparse, 1),

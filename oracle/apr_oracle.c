@@ -401,3 +401,193 @@ int oracle_eval_positions_list(const float* P, const float* Q, int d, const int3
   }
   return 0;
 }
+
+/* ---- the CPU baseline on every host core (bench.py cpu_baseline) ----
+ * oracle_apr_train with the batch's work split over `nthreads` OpenMP threads,
+ * every sum kept in the single-thread order, so the result is bit-identical to
+ * oracle_apr_train (tests/test_oracle.py::test_threaded_oracle_bit_identical):
+ *   per-triplet terms (clean / adversarial forward)      split by triplet;
+ *   per-row sums (IndexedSlices, reg, adversarial terms)  split by row slot
+ *     (slot % T): each thread walks every occurrence in the batch's order and
+ *     adds only its own rows' terms, so a row's additions keep their order;
+ *   the dense delta work (APR.py:183-191: zero, scatter, l2-normalise every
+ *     row of both tables, gather) and the Adagrad apply   split by row.
+ * Finding the batch's unique rows (first-touch order) stays on one thread. */
+#include <omp.h>
+
+int oracle_apr_train_mt(float* P, float* Q, float* accP, float* accQ, int64_t U1, int64_t I1, int d,
+                        const int32_t* u0, const int32_t* ip0, const int32_t* in0, int B, int n_batches,
+                        const oracle_hparams* hp, int nthreads) {
+  for (int64_t e = 0; e < (int64_t)B * n_batches; ++e)
+    if (u0[e] < 0 || u0[e] >= U1 || ip0[e] < 0 || ip0[e] >= I1 || in0[e] < 0 || in0[e] >= I1) return -2;
+  rowset RU, RI;
+  if (rowset_init(&RU, U1, B, d) || rowset_init(&RI, I1, 2 * B, d)) return -1;
+  float* g = (float*)malloc(sizeof(float) * B);
+  float* ga = (float*)malloc(sizeof(float) * B);
+  int32_t* su = (int32_t*)malloc(sizeof(int32_t) * B);   /* triplet -> user slot */
+  int32_t* si = (int32_t*)malloc(sizeof(int32_t) * B);   /* -> positive item slot */
+  int32_t* sj = (int32_t*)malloc(sizeof(int32_t) * B);   /* -> negative item slot */
+  float* dU = (float*)calloc((size_t)B * d, sizeof(float));
+  float* dI = (float*)calloc((size_t)2 * B * d, sizeof(float));
+  float* G0U = (float*)calloc((size_t)B * d, sizeof(float));
+  float* G0I = (float*)calloc((size_t)2 * B * d, sizeof(float));
+  float* denseU = hp->dense ? (float*)malloc(sizeof(float) * (size_t)U1 * d) : NULL;
+  float* denseI = hp->dense ? (float*)malloc(sizeof(float) * (size_t)I1 * d) : NULL;
+  if (!g || !ga || !su || !si || !sj || !dU || !dI || !G0U || !G0I || (hp->dense && (!denseU || !denseI)))
+    return -1;
+  const float lam = hp->reg_adv;
+  const float coef = (2.0f * hp->reg / ((float)B * (float)d)) * (hp->adver ? 2.0f : 1.0f);
+#pragma omp parallel num_threads(nthreads)
+  {
+    const int tid = omp_get_thread_num(), T = omp_get_num_threads();
+    float* pp = (float*)malloc(sizeof(float) * d);
+    float* qi = (float*)malloc(sizeof(float) * d);
+    float* qj = (float*)malloc(sizeof(float) * d);
+    oracle_hparams h = *hp;
+    for (int t = 0; t < n_batches; ++t) {
+      const int32_t *u = u0 + (int64_t)t * B, *ip = ip0 + (int64_t)t * B, *in = in0 + (int64_t)t * B;
+      h.t = hp->t + t;
+#pragma omp for schedule(static)
+      for (int b = 0; b < B; ++b) { /* 1. clean forward */
+        const float* p = P + (int64_t)u[b] * d;
+        float x = dotp(p, Q + (int64_t)ip[b] * d, d) - dotp(p, Q + (int64_t)in[b] * d, d);
+        float l;
+        bpr_term(x, h.clip_lo, h.clip_hi, &g[b], &l);
+      }
+#pragma omp single
+      {
+        for (int b = 0; b < B; ++b) RU.count[su[b] = rowset_touch(&RU, u[b])]++;
+        for (int b = 0; b < B; ++b) RI.count[si[b] = rowset_touch(&RI, ip[b])]++;
+        for (int b = 0; b < B; ++b) RI.count[sj[b] = rowset_touch(&RI, in[b])]++;
+      } /* (rowset_touch zeroes each new slot's acc row) */
+      if (h.adver) {
+        /* 2. clean gradient segment sums, each slot in occurrence order */
+#pragma omp for schedule(static)
+        for (int s = 0; s < 2 * B; ++s) {
+          if (s < B) memset(G0U + (size_t)s * d, 0, sizeof(float) * d);
+          memset(G0I + (size_t)s * d, 0, sizeof(float) * d);
+        }
+        for (int b = 0; b < B; ++b) {
+          if (su[b] % T == tid) axpy(G0U + (size_t)su[b] * d, g[b], Q + (int64_t)ip[b] * d, d);
+          if (si[b] % T == tid) axpy(G0I + (size_t)si[b] * d, g[b], P + (int64_t)u[b] * d, d);
+        }
+        for (int b = 0; b < B; ++b) {
+          if (su[b] % T == tid) axpy(G0U + (size_t)su[b] * d, -g[b], Q + (int64_t)in[b] * d, d);
+          if (sj[b] % T == tid) axpy(G0I + (size_t)sj[b] * d, -g[b], P + (int64_t)u[b] * d, d);
+        }
+#pragma omp barrier
+        /* 3. delta = eps * l2_normalize(grad) */
+        if (h.dense) {
+#pragma omp for schedule(static)
+          for (int64_t r = 0; r < U1 + I1; ++r)
+            memset(r < U1 ? denseU + r * d : denseI + (r - U1) * d, 0, sizeof(float) * d);
+#pragma omp for schedule(static)
+          for (int s = 0; s < RU.n + RI.n; ++s) {
+            if (s < RU.n) memcpy(denseU + (int64_t)RU.rows[s] * d, G0U + (size_t)s * d, sizeof(float) * d);
+            else memcpy(denseI + (int64_t)RI.rows[s - RU.n] * d, G0I + (size_t)(s - RU.n) * d, sizeof(float) * d);
+          }
+#pragma omp for schedule(static)
+          for (int64_t r = 0; r < U1 + I1; ++r) {
+            float* x = r < U1 ? denseU + r * d : denseI + (r - U1) * d;
+            float ss = 0.f;
+            for (int k = 0; k < d; ++k) ss = ss + x[k] * x[k];
+            float inv = 1.0f / sqrtf(ss > 1e-12f ? ss : 1e-12f);
+            for (int k = 0; k < d; ++k) x[k] = h.zero_delta ? 0.f : (x[k] * inv) * h.eps;
+          }
+#pragma omp for schedule(static)
+          for (int s = 0; s < RU.n + RI.n; ++s) {
+            if (s < RU.n) memcpy(dU + (size_t)s * d, denseU + (int64_t)RU.rows[s] * d, sizeof(float) * d);
+            else memcpy(dI + (size_t)(s - RU.n) * d, denseI + (int64_t)RI.rows[s - RU.n] * d, sizeof(float) * d);
+          }
+        } else {
+#pragma omp for schedule(static)
+          for (int s = 0; s < RU.n + RI.n; ++s) {
+            const float* x = s < RU.n ? G0U + (size_t)s * d : G0I + (size_t)(s - RU.n) * d;
+            float* y = s < RU.n ? dU + (size_t)s * d : dI + (size_t)(s - RU.n) * d;
+            float ss = 0.f;
+            for (int k = 0; k < d; ++k) ss = ss + x[k] * x[k];
+            float inv = 1.0f / sqrtf(ss > 1e-12f ? ss : 1e-12f);
+            for (int k = 0; k < d; ++k) y[k] = h.zero_delta ? 0.f : (x[k] * inv) * h.eps;
+          }
+        }
+        if (h.adv_mode == 1 && !h.zero_delta) {
+#pragma omp for schedule(static)
+          for (int s = 0; s < RU.n + RI.n; ++s) {
+            if (s < RU.n) random_delta(&h, 0, RU.rows[s], d, dU + (size_t)s * d);
+            else random_delta(&h, 1, RI.rows[s - RU.n], d, dI + (size_t)(s - RU.n) * d);
+          }
+        }
+        /* 4. adversarial forward */
+#pragma omp for schedule(static)
+        for (int b = 0; b < B; ++b) {
+          const float *du = dU + (size_t)su[b] * d, *di = dI + (size_t)si[b] * d, *dj = dI + (size_t)sj[b] * d;
+          const float* p = P + (int64_t)u[b] * d;
+          for (int k = 0; k < d; ++k) {
+            pp[k] = p[k] + du[k];
+            qi[k] = Q[(int64_t)ip[b] * d + k] + di[k];
+            qj[k] = Q[(int64_t)in[b] * d + k] + dj[k];
+          }
+          float x = dotp(pp, qi, d) - dotp(pp, qj, d);
+          float l;
+          bpr_term(x, h.clip_lo, h.clip_hi, &ga[b], &l);
+        }
+      }
+      /* 5. the optimizer's deduplicated gradient, each slot in the single-thread order */
+      for (int b = 0; b < B; ++b) {
+        if (su[b] % T == tid) axpy(RU.acc + (size_t)su[b] * d, g[b], Q + (int64_t)ip[b] * d, d);
+        if (si[b] % T == tid) axpy(RI.acc + (size_t)si[b] * d, g[b], P + (int64_t)u[b] * d, d);
+      }
+      for (int b = 0; b < B; ++b) {
+        if (su[b] % T == tid) axpy(RU.acc + (size_t)su[b] * d, -g[b], Q + (int64_t)in[b] * d, d);
+        if (sj[b] % T == tid) axpy(RI.acc + (size_t)sj[b] * d, -g[b], P + (int64_t)u[b] * d, d);
+      }
+      if (h.reg != 0.f) {
+        for (int s = tid; s < RU.n; s += T)
+          axpy(RU.acc + (size_t)s * d, coef * (float)RU.count[s], P + (int64_t)RU.rows[s] * d, d);
+        for (int s = tid; s < RI.n; s += T)
+          axpy(RI.acc + (size_t)s * d, coef * (float)RI.count[s], Q + (int64_t)RI.rows[s] * d, d);
+      }
+      if (h.adver)
+        for (int pass = 0; pass < 2; ++pass)
+          for (int b = 0; b < B; ++b) {
+            const int32_t sq = pass == 0 ? si[b] : sj[b];
+            const int mine_u = su[b] % T == tid, mine_i = sq % T == tid;
+            if (!mine_u && !mine_i) continue;
+            const float* du = dU + (size_t)su[b] * d;
+            const float* p = P + (int64_t)u[b] * d;
+            const int item = pass == 0 ? ip[b] : in[b];
+            const float* dq = dI + (size_t)sq * d;
+            const float* q = Q + (int64_t)item * d;
+            const float sgn = pass == 0 ? 1.f : -1.f;
+            for (int k = 0; k < d; ++k) { pp[k] = p[k] + du[k]; qi[k] = q[k] + dq[k]; }
+            if (mine_u) axpy(RU.acc + (size_t)su[b] * d, lam * sgn * ga[b], qi, d);
+            if (mine_i) axpy(RI.acc + (size_t)sq * d, lam * sgn * ga[b], pp, d);
+          }
+#pragma omp barrier
+      /* 6. SparseApplyAdagrad on the unique rows */
+#pragma omp for schedule(static)
+      for (int s = 0; s < RU.n + RI.n; ++s) {
+        const int side = s >= RU.n, x = side ? s - RU.n : s;
+        const rowset* R = side ? &RI : &RU;
+        float* w = (side ? Q : P) + (int64_t)R->rows[x] * d;
+        float* a = (side ? accQ : accP) + (int64_t)R->rows[x] * d;
+        const float* gr = R->acc + (size_t)x * d;
+        for (int k = 0; k < d; ++k) {
+          a[k] = a[k] + gr[k] * gr[k];
+          w[k] = w[k] - (h.lr * gr[k]) * (1.0f / sqrtf(a[k]));
+        }
+      }
+#pragma omp single
+      {
+        rowset_clear(&RU);
+        rowset_clear(&RI);
+      }
+    }
+    free(pp); free(qi); free(qj);
+  }
+  rowset_free(&RU);
+  rowset_free(&RI);
+  free(g); free(ga); free(su); free(si); free(sj);
+  free(dU); free(dI); free(G0U); free(G0I); free(denseU); free(denseI);
+  return 0;
+}

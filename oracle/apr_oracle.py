@@ -92,6 +92,9 @@ class COracle:
         L.oracle_apr_train.restype = ctypes.c_int
         L.oracle_apr_train.argtypes = [P, P, P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                        P, P, P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_OHP)]
+        L.oracle_apr_train_mt.restype = ctypes.c_int
+        L.oracle_apr_train_mt.argtypes = [P, P, P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                          P, P, P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_OHP), ctypes.c_int]
         L.oracle_bpr_forward.restype = ctypes.c_int
         L.oracle_bpr_forward.argtypes = [P, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, P, P, P,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
@@ -135,6 +138,19 @@ class COracle:
                                       _c(i), _c(j), batch_size, nb, ctypes.byref(h))
         if r:
             raise ValueError(f"oracle_apr_train failed ({r})")
+
+    def apr_train_mt(self, P, Q, accP, accQ, u, i, j, batch_size, hp: HParams, dense=False, threads=None):
+        """apr_train on `threads` OpenMP threads (default: every core of this
+        process's affinity mask): the same bits (apr_oracle.c, oracle_apr_train_mt)."""
+        nb = len(u) // batch_size
+        h = self._hp(hp, dense)
+        nt = int(threads or len(os.sched_getaffinity(0)))
+        r = self.lib.oracle_apr_train_mt(P.ctypes.data, Q.ctypes.data, accP.ctypes.data,
+                                         accQ.ctypes.data, P.shape[0], Q.shape[0], P.shape[1], _c(u),
+                                         _c(i), _c(j), batch_size, nb, ctypes.byref(h), nt)
+        if r:
+            raise ValueError(f"oracle_apr_train_mt failed ({r})")
+        return nt
 
     def bpr_forward(self, P, Q, u, i, j, batch_size, clip_lo=-80.0, clip_hi=1e8):
         nb = len(u) // batch_size

@@ -16,8 +16,10 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if force or not os.path.exists(LIB) or os.path.getmtime(SRC) > os.path.getmtime(LIB):
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
         tmp = LIB + ".tmp"
-        cmd = ["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", SRC, "-o", tmp,
-               "-lm"]
+        # -fopenmp: oracle_apr_train_mt (the threaded CPU baseline); the other
+        # functions have no OpenMP pragmas and run on the calling thread
+        cmd = ["gcc", "-O3", "-std=c11", "-ffp-contract=off", "-fopenmp", "-fPIC", "-shared", "-Wall", SRC, "-o",
+               tmp, "-lm"]
         if verbose:
             print("[build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -261,3 +261,32 @@ def test_torch_cpu_baseline_matches_c_oracle(oracle, adver, dense):
                  adver=bool(adver), dense=dense)
     for g, w in zip(tabs, (rP, rQ, aP, aQ)):
         np.testing.assert_allclose(g.numpy(), w, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("adver,reg,dense,adv,threads", [(1, 0.0, True, "grad", 8), (1, 0.01, False, "grad", 3),
+                                                         (0, 0.01, True, "grad", 5), (1, 0.0, False, "random", 4)])
+def test_threaded_oracle_bit_identical(oracle, adver, reg, dense, adv, threads):
+    """oracle_apr_train_mt (bench.py's CPU baseline on every host core, VERDICT
+    r05 #7) gives the bits of the one-thread oracle_apr_train: per-triplet terms
+    split by triplet, per-row sums split by row slot in occurrence order, a hot
+    row and i == j triplets included."""
+    rng = np.random.default_rng(11 + adver)
+    U1, I1, d, B, nb = 61, 53, 16, 64, 6
+    P = (rng.standard_normal((U1, d)) * 0.1).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.1).astype(np.float32)
+    u = rng.integers(0, U1, nb * B).astype(np.int32)
+    i = rng.integers(0, I1, nb * B).astype(np.int32)
+    j = rng.integers(0, I1, nb * B).astype(np.int32)
+    i[::5] = 7
+    j[::9] = i[::9]
+    hp = HParams(adver=adver, reg=reg, adv=adv, seed=3)
+    outs = []
+    for mt in (False, True):
+        t = [P.copy(), Q.copy(), np.full_like(P, 0.1), np.full_like(Q, 0.1)]
+        if mt:
+            assert oracle.apr_train_mt(*t, u, i, j, B, hp, dense=dense, threads=threads) == threads
+        else:
+            oracle.apr_train(*t, u, i, j, B, hp, dense=dense)
+        outs.append(t)
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
