@@ -513,8 +513,9 @@ def neumf_bench(acf, dev):
     yelp-sort-shaped synthetic data, d = 64, batch 512 (run.py --bs default), one
     epoch of Keras-style training (libacf_neumf.so).  The epoch (acf_neumf_train)
     runs Keras's dense Adam lazily (bit-identical) and is a
-    latency-bound chain of small launches; the roofline is the dense Adam kernel
-    of the stepwise API (acf_neumf_adam: 8 x 4 B per parameter per step)."""
+    latency-bound chain of small launches; the roofline is its dominant kernel,
+    k_nmf_step, and the dense Adam of the stepwise API is
+    reported beside it."""
     import scipy.sparse as sp
     nm = importlib.import_module(PKG + ".neumf")
     ds = acf.yelp_like()
@@ -550,10 +551,40 @@ def neumf_bench(acf, dev):
         torch.cuda.synchronize(dev)
         return e0.elapsed_time(e1) * 1e3 / reps
 
+    # the timed path's dominant kernel: k_nmf_step (both passes of a step in one
+    # launch), timed through unchecked acf_neumf_grad calls on the
+    # same batches (each call = k_nmf_step + the small k_nmf_wsum launch, so the
+    # figure is an upper bound for the kernel); grad is restored afterwards
+    reps = 200
+    gsave = st.grad.clone()
+    lb = torch.zeros(2, device=dev)
+    for k in range(8):
+        s_ = slice(k * B, (k + 1) * B)
+        ctx.grad(U[s_], I[s_], Y[s_], hp, lb, check=False)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for k in range(reps):
+        s_ = slice((k % 64) * B, (k % 64 + 1) * B)
+        ctx.grad(U[s_], I[s_], Y[s_], hp, lb, check=False)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    step_us = e0.elapsed_time(e1) * 1e3 / reps
+    ctx.predict(U[:8], I[:8])  # verifies the unchecked calls (a give-up would raise here)
+    st.grad.copy_(gsave)
+    del gsave
+    d4 = 4 * d
+    # algorithmic bytes of one step: the 4 embedding rows of every instance gathered
+    # by the clean and by the adversarial pass, the adversarial pass's 4 delta rows,
+    # and the MLP/head weights read once per instance workgroup (B / 16 of them per pass)
+    nwg = -(-B // 16)
+    wbytes = 4 * (2 * d * 2 * d + 2 * d + 2 * d * d + d + 2 * d + 1)
+    step_bytes = 2 * B * 4 * d4 + B * 4 * d4 + 2 * nwg * wbytes
+    step_gbs = step_bytes / (step_us * 1e-6) / 1e9
+
     # the yelp-shaped buffer (212 MB of p, g, m, v) stays in the 256 MB Infinity
-    # Cache between steps: its Adam rate is not an HBM rate.  The roofline is
-    # taken on the same kernel over a 1.2 GB buffer (262,144 user rows), which
-    # streams from HBM; the yelp-shaped rate is reported beside it.
+    # Cache between steps: its Adam rate is not an HBM rate.  The dense Adam's
+    # rate is taken on the same kernel over a 1.2 GB buffer (262,144 user rows),
+    # which streams from HBM; the yelp-shaped rate is reported beside it.
     adam_us_mall = adam_time(ctx)
     nparam = st.params.numel()
     big = nm.NeuMFState(262_144, ds.num_items + 1, d, dev)
@@ -570,11 +601,24 @@ def neumf_bench(acf, dev):
                                    "weight 1, Keras Adam lr 0.001, batch 512", "dim": d, "batch": B,
                        "instances": n, "params": nparam},
             "final_loss": round(float(losses[-1, 0]), 5),
-            "roofline": {"bound": "hbm", "kernel": "k_nmf_adam", "achieved": round(achieved, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "bytes_per_launch": 8 * 4 * nbig, "avg_launch_us": round(adam_us, 3),
-                         "buffer": "1.2 GB (262,144 user rows: beyond the 256 MB Infinity Cache)",
+            "recoveries": ctx.recoveries(),
+            "roofline": {"bound": "latency", "kernel": "k_nmf_step", "achieved": round(step_gbs, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 5),
+                         "bytes_per_launch": int(step_bytes), "avg_launch_us": round(step_us, 3),
+                         "bytes_formula": "2 passes x B x 4 embedding rows x 4d B + B x 4 delta rows x 4d B "
+                                          "+ 2 x (B/16 workgroups) x MLP/head weights",
+                         "timing": f"HIP events over {reps} unchecked acf_neumf_grad calls on the bench's "
+                                   "batches (k_nmf_step + k_nmf_wsum each): an upper bound for the kernel",
+                         "note": "one step is a dependent chain (gather -> 4 MFMA layers -> weight "
+                                 "gradients -> row sums -> adversarial pass) on 64 workgroups at B = 512: "
+                                 "latency-bound, far from any bandwidth or MFMA limit",
                          "traffic": None},
+            "adam_dense": {"kernel": "k_nmf_adam", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                           "bytes_per_launch": 8 * 4 * nbig, "avg_launch_us": round(adam_us, 3),
+                           "buffer": "1.2 GB (262,144 user rows: beyond the 256 MB Infinity Cache)",
+                           "note": "the stepwise API's dense Adam; acf_neumf_train runs it lazily "
+                                   "(k_nmf_adam_next + catch-up)"},
             "adam_yelp_shape": {"bytes_per_launch": 8 * 4 * nparam, "avg_launch_us": round(adam_us_mall, 3),
                                 "achieved_GBs": round(8 * 4 * nparam / (adam_us_mall * 1e-6) / 1e9, 2),
                                 "note": "212 MB buffer resident in the Infinity Cache between steps",
