@@ -1341,6 +1341,13 @@ struct StepArgs {
   int32_t xflush;
   // triplet-centric list step (k_tri_*): per-occurrence contributions of shared rows
   const int4* tpos;    // [E] CSR positions of a triplet's three occurrences
+  // hash plans (r06): [nb] fused triplets of each batch, placed first in trec /
+  // tpos (the clean pass starts past them); null: plans in triplet order
+  const int32_t* tri_nf;
+  // k_tri_cadv (r06): per shared slot of the batch, (call counter << 32 | t) once
+  // its clean sum and delta are stored (the adversarial triplets of the same
+  // launch wait for it)
+  unsigned long long* ready;
   float* contrib;      // users [B][2][d] (positive, negative branch), then items [2B][d]
   int32_t inplace;     // triplet-centric plans: every row is updated in its table (no W scratch)
   float lr, eps, reg, reg_adv, clip_lo, clip_hi;
@@ -2907,6 +2914,14 @@ __global__ void __launch_bounds__(256) k_adv_list(StepArgs a) {
 #define TRI_SI 32
 #define TRI_SJ 64
 
+// the tag k_tri_cadv's finishers publish per slot and its triplets wait for:
+// unique per call (the call counter, bumped by the flush at the end of every
+// call) and batch
+__device__ __forceinline__ unsigned long long ready_tag(const StepArgs& a) {
+  return ((unsigned long long)*a.epoch << 32) | (uint32_t)a.t;
+}
+
+
 __device__ __forceinline__ float* tri_cu(const StepArgs& a) { return a.contrib; }
 __device__ __forceinline__ float* tri_ci(const StepArgs& a) { return a.contrib + (int64_t)2 * a.B * a.d; }
 
@@ -2918,11 +2933,11 @@ __device__ __forceinline__ float* tri_ci(const StepArgs& a) { return a.contrib +
 // stepped locally: its one product is its partial sum, stored straight to its
 // exchange row (the slot path's 0 + product), and pass 2 reads the owners'
 // item deltas from theirs; users are complete locally and step as above.
-template <int LPR, int NV, int PASS>
+template <int LPR, int NV, int PASS, bool MERGED = false>
 __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, const RecV& r, const int4 ps) {
   if (b >= a.B) return;
-  const int64_t e = (int64_t)a.t * a.B + b;
   if (r.c.w != *a.gen_ptr) return;
+  const int64_t e = r.c.z;  // the triplet (its losses); b is its place in the plan (hash plans: fused first)
   const int flags = r.c.y;
   // a fused triplet (all three rows single) takes the same code as the others
   // (k_single's operation sequence), so a wave's lane-groups do not diverge
@@ -2950,13 +2965,15 @@ __device__ __forceinline__ void tri_triplet_r(const StepArgs& a, int b, int l, c
     if (aj) cj = load_row<LPR, NV>(a.accQ, j, d, l);
   }
   if (PASS == 2) {  // issued with the row loads, not after the clean term
-    if (!su) du = load_row<LPR, NV>(a.delta, ku, d, l);
+    // (MERGED, k_tri_cadv: the deltas were stored in this launch by other
+    // workgroups -- device-scope loads, after their tags, tri_wait_ready)
+    if (!su) du = load_piece<LPR, NV, MERGED>(a.delta, ku, d, l);
     if (a.shard) {  // items: the owners' deltas, straight from the exchange rows
       di = load_row<LPR, NV>(a.xdelta, a.xdmap[i], d, l);
       dj = load_row<LPR, NV>(a.xdelta, a.xdmap[j], d, l);
     } else {
-      if (!si) di = load_row<LPR, NV>(a.delta, ki, d, l);
-      if (!sj) dj = load_row<LPR, NV>(a.delta, kj, d, l);
+      if (!si) di = load_piece<LPR, NV, MERGED>(a.delta, ki, d, l);
+      if (!sj) dj = load_piece<LPR, NV, MERGED>(a.delta, kj, d, l);
     }
   }
   const int64_t lu = ps.x - (int64_t)a.t * a.B, li = ps.y - (int64_t)a.t * 2 * a.B,
@@ -3054,16 +3071,70 @@ __device__ __forceinline__ void tri_rec(const StepArgs& a, int b, RecV& r, int4&
 // many wave rounds
 __host__ __device__ constexpr int tri_gpw(int nv) { return nv == 1 ? 2 : 1; }
 
-template <int LPR, int NV, int PASS>
-__device__ __forceinline__ void tri_triplets(const StepArgs& a, int tw, int lane) {
+// k_tri_cadv: the wave's triplets wait until the shared slots whose deltas they
+// read carry this batch's tag (finished by the combine part of the launch,
+// dispatched before every triplet wave, so the wait always ends); a lane-group's
+// lanes poll its triplets' (up to) 3 x GPW slots.  All-single (fused) triplets
+// wait for nothing.  Bounded: a give-up sets step_err bit 0.
+template <int LPR, int GPW>
+__device__ __forceinline__ void tri_wait_ready(const StepArgs& a, const int* bs, const RecV* r, int l) {
+  const unsigned long long tag = ready_tag(a);
+  const int32_t gen = *a.gen_ptr;
+  constexpr int NQ = (3 * GPW + LPR - 1) / LPR;
+  int32_t slot[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) slot[q] = -1;
+  // candidate c = 3x + which (x: the wave's group, which: u / i / j) goes to lane
+  // c % LPR, entry c / LPR -- every index a compile-time constant (no scratch)
+#pragma unroll
+  for (int x = 0; x < GPW; ++x) {
+    const bool live = bs[x] < a.B && r[x].c.w == gen;
+    const int flags = r[x].c.y;
+#pragma unroll
+    for (int which = 0; which < 3; ++which) {
+      const int c = 3 * x + which;
+      if (l != c % LPR || !live) continue;
+      const int mask = which == 0 ? TRI_SU : which == 1 ? TRI_SI : TRI_SJ;
+      const int32_t k = which == 0 ? r[x].a.w : which == 1 ? r[x].b.x : r[x].b.y;
+      if (!(flags & mask)) slot[c / LPR] = k;
+    }
+  }
+  bool need = false;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) need |= slot[q] >= 0;
+  if (!__any(need)) return;
+  for (int it = 0;; ++it) {
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      if (slot[q] >= 0 && __hip_atomic_load(a.ready + slot[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag)
+        ok = false;
+    if (__all(ok)) return;
+    if (it >= a.spin_limit) {
+      if ((threadIdx.x & 63) == 0) atomicOr(a.step_err, 1);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// triplets at places [boff + tw * GPW * OPW, ...) below bend (default: the batch)
+template <int LPR, int NV, int PASS, bool MERGED = false>
+__device__ __forceinline__ void tri_triplets(const StepArgs& a, int tw, int lane, int boff = 0, int bend = -1) {
   constexpr int OPW = 64 / LPR, GPW = tri_gpw(NV);
-  const int b0 = tw * GPW * OPW + lane / LPR;
+  const int b0 = boff + tw * GPW * OPW + lane / LPR;
   RecV r[GPW];
   int4 ps[GPW];
+  int bs[GPW];
 #pragma unroll
-  for (int x = 0; x < GPW; ++x) tri_rec(a, b0 + x * OPW, r[x], ps[x]);
+  for (int x = 0; x < GPW; ++x) {
+    bs[x] = b0 + x * OPW;
+    if (bend >= 0 && bs[x] >= bend) bs[x] = a.B;  // past the range: no triplet
+    tri_rec(a, bs[x], r[x], ps[x]);
+  }
+  if (MERGED) tri_wait_ready<LPR, GPW>(a, bs, r, lane & (LPR - 1));
 #pragma unroll
-  for (int x = 0; x < GPW; ++x) tri_triplet_r<LPR, NV, PASS>(a, b0 + x * OPW, lane & (LPR - 1), r[x], ps[x]);
+  for (int x = 0; x < GPW; ++x) tri_triplet_r<LPR, NV, PASS, MERGED>(a, bs[x], lane & (LPR - 1), r[x], ps[x]);
 }
 
 // header of shared slot k: count, side, own row, source, local CSR base
@@ -3180,7 +3251,9 @@ __global__ void __launch_bounds__(256) k_tri_clean(StepArgs a) {
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
   if (wave >= a.slot_waves) {
     STAMP(a.diag_launch, wave, 0);
-    tri_triplets<LPR, NV, BPR ? 1 : 0>(a, wave - a.slot_waves, lane);
+    // APR clean pass: fused triplets have no clean work; a hash plan places them first
+    const int boff = (!BPR && a.tri_nf) ? a.tri_nf[a.t] : 0;
+    tri_triplets<LPR, NV, BPR ? 1 : 0>(a, wave - a.slot_waves, lane, boff);
     STAMP(a.diag_launch, wave, 5);
     return;
   }
@@ -3223,7 +3296,7 @@ __device__ __forceinline__ TriHotPre<LPR, NV> tri_hot_prefetch(const StepArgs& a
   return f;
 }
 
-template <int LPR, int NV, int MODE>
+template <int LPR, int NV, int MODE, bool READY = false>
 __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, float4* __restrict__ red,
                                                TriHotPre<LPR, NV>& f) {
   constexpr int NG = 256 / LPR, FG = 64 / LPR;
@@ -3257,8 +3330,15 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
       store_row_wt<LPR, NV>(a.xbuf, a.xmap[f.row], d, l, T);
     } else if (MODE == 0) {
       const RowV<NV> dl = make_delta<LPR, NV>(a, T, f.is_item, f.row, l);
-      store_row<LPR, NV>(a.g0, k, d, l, T);
-      store_row<LPR, NV>(a.delta, k, d, l, dl);
+      if (READY) {  // read in this launch: write-through, drained, then the tag
+        store_row_wt<LPR, NV>(a.g0, k, d, l, T);
+        store_row_wt<LPR, NV>(a.delta, k, d, l, dl);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (l == 0) __hip_atomic_store(a.ready + k, ready_tag(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        store_row<LPR, NV>(a.g0, k, d, l, T);
+        store_row<LPR, NV>(a.delta, k, d, l, dl);
+      }
     } else {
       RowV<NV> wout;
       if (MODE == 1) {
@@ -3288,10 +3368,9 @@ __device__ __forceinline__ void tri_hot_finish(const StepArgs& a, const int4 e, 
 // row 1).  The combining workgroups come after every piece wave in dispatch
 // order, so the pieces they wait for are already running: the launch always
 // drains.  (hot_waves is a multiple of 4: whole workgroups.)
-template <int LPR, int NV, int MODE>
-__global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
-  __shared__ float4 red[NV * 256];
-  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+// (READY: k_tri_cadv's combine part -- the finished slots publish their tags)
+template <int LPR, int NV, int MODE, bool READY>
+__device__ __forceinline__ void tri_combine_wave(const StepArgs& a, const int wave, float4* __restrict__ red) {
   const int lane = threadIdx.x & 63, g = lane / LPR, l = lane & (LPR - 1);
   int32_t* arrive = a.hot.arrive + (int64_t)a.t * a.hot.piece_stride;
   STAMP(a.diag_launch, wave, 0);  // diagnostic builds: 1 piece, 2 / 3 combiner waited / done, 4 slot wave done
@@ -3352,7 +3431,7 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
       }
       __syncthreads();
       if (hx == hb) STAMP(a.diag_launch, wave, 2);
-      tri_hot_finish<LPR, NV, MODE>(a, e, red, pre);
+      tri_hot_finish<LPR, NV, MODE, READY>(a, e, red, pre);
     }
     STAMP(a.diag_launch, wave, 3);
     return;
@@ -3367,8 +3446,19 @@ __global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
     RowV<NV> G = zero_row<NV>();
     tri_add_q<LPR, NV>(a, h, 0, h.count, 1, l, G);
     tri_finish<LPR, NV, MODE>(a, k, h, G, l);
+    if (READY) {  // g0 and delta went out write-through: drained, then the tag
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (l == 0) __hip_atomic_store(a.ready + k, ready_tag(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   STAMP(a.diag_launch, wave, 4);
+}
+
+template <int LPR, int NV, int MODE>
+__global__ void __launch_bounds__(256) k_tri_combine(StepArgs a) {
+  __shared__ float4 red[NV * 256];
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  tri_combine_wave<LPR, NV, MODE, false>(a, wave, red);
 }
 
 // k_tri_adv: 4 blocks (16 waves) per CU asked of the register allocator (d <= 256)
@@ -3377,6 +3467,32 @@ __global__ void __launch_bounds__(256, NV == 1 ? 4 : 1) k_tri_adv(StepArgs a) {
   const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
   STAMP(a.diag_launch, wave, 0);
   tri_triplets<LPR, NV, 2>(a, wave, threadIdx.x & 63);
+  STAMP(a.diag_launch, wave, 5);
+}
+
+// (r06) The clean combine and the adversarial pass of a batch in ONE launch:
+// the combine's piece waves, small-slot waves and combining workgroups first
+// (k_tri_combine<0>'s, each finished slot publishing its tag after write-through
+// stores of g0 / delta), then the triplet waves of k_tri_adv.  The hash plan
+// places each batch's fused triplets first (k_hplan_trip): they read no delta
+// and run while the combine's chains finish; the other triplets wait for their
+// shared slots' tags (tri_wait_ready).  Every wait is on work dispatched earlier
+// in the grid, so the launch always drains.  No launch boundary between the two
+// passes, and the combine's idle tail is filled: configs[4] d = 64 727-736M ->
+// 752-760M triplets/s, d = 128 +1.5% (same box, profiles/r06/tri_cadv_v1_ab.json).
+// (Dispatching the fused triplets before the small-slot waves instead was slower,
+// 715M: the small slots queued behind them, profiles/r06/tri_cadv_v2_layout_ab.json.)
+template <int LPR, int NV>
+__global__ void __launch_bounds__(256, NV == 1 ? 4 : 1) k_tri_cadv(StepArgs a) {
+  __shared__ float4 red[NV * 256];
+  const int wave = (int)((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6);
+  const int cw = a.hot_waves + a.slot_waves + 4 * a.hot_blocks;  // whole workgroups
+  if (wave < cw) {
+    tri_combine_wave<LPR, NV, 0, true>(a, wave, red);
+    return;
+  }
+  STAMP(a.diag_launch, wave, 0);
+  tri_triplets<LPR, NV, 2, true>(a, wave - cw, threadIdx.x & 63);
   STAMP(a.diag_launch, wave, 5);
 }
 
@@ -3636,6 +3752,7 @@ struct acf_apr_ctx {
   int32_t shard = 0;            // shard mode (acf_apr_set_shard_mode): item rows are partial sums
   int32_t tri = 0;              // the plan is triplet-centric (packed, not shard: k_tri_*)
   float* contrib = nullptr;     // [4 maxB, d] per-occurrence contributions of shared rows (k_tri_*)
+  unsigned long long* ready = nullptr;  // [3 maxB] k_tri_cadv's per-slot tags (zeroed: never a tag)
   int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
@@ -3681,6 +3798,9 @@ struct acf_apr_ctx {
   size_t hplan_tmp_bytes = 0;
   int32_t* hplan_cnt = nullptr;  // [3][maxNB] shared slots, user / item CSR positions
   int32_t* hplan_haux = nullptr;  // [maxNB][hot_stride] CSR base | item of each hot-list entry
+  int32_t* hplan_perm = nullptr;  // [maxE] triplet -> its place (fused first, r06)
+  int32_t* hplan_tcnt = nullptr;  // [maxNB] fused triplets per batch
+  int32_t* hplan_ttc = nullptr;   // [maxNB * tiles + 1] fused triplets per tile of 256, then its scan
   int32_t bplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   unsigned long long* bmask[2] = {nullptr, nullptr};
   size_t bmask_words = 0;
@@ -3826,6 +3946,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   A(&c->hot.paux, (size_t)maxNB * c->hot.piece_stride);
   A(&c->hot_part, (size_t)c->hot.piece_stride * d);
   A(&c->contrib, (size_t)4 * maxB * d);
+  A(&c->ready, (size_t)3 * maxB);
   A(&c->iuniq, 2 * maxE); A(&c->ioff, 2 * maxE + 1); A(&c->ibs, maxNB + 1);
   A(&c->iinfo, 2 * maxE);
   A(&c->urec, maxE); A(&c->irec, 2 * maxE); A(&c->trec, maxE);
@@ -3866,6 +3987,7 @@ extern "C" int acf_apr_create(acf_apr_ctx** out, int64_t U1, int64_t I1, int32_t
   if (hipMemset(c->inl, 0, (size_t)maxNB * S * c->R * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->trec, 0, (size_t)maxE * sizeof(OccRec)) != hipSuccess ||
       hipMemset(c->err, 0, 16) != hipSuccess || hipMemset(c->gen_dev, 0, 16) != hipSuccess ||
+      hipMemset(c->ready, 0, (size_t)3 * maxB * sizeof(unsigned long long)) != hipSuccess ||
       hipMemset(c->decide, 0, (16 + 2 * 144) * 8) != hipSuccess ||
       hipMemcpy(c->epoch, &kOne, sizeof(kOne), hipMemcpyHostToDevice) != hipSuccess || hipMemset(c->nextt, 0, 3 * maxE * sizeof(int32_t)) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
@@ -4057,8 +4179,10 @@ static bool hplan_ready(acf_apr_ctx* c) {
   if (pb + (int32_t)bits_for((uint64_t)c->maxNB) > 32) return false;
   const size_t n3 = (size_t)3 * c->maxE;
   const size_t ncnt = ((size_t)c->maxNB << pb) * (((size_t)3 * c->maxB + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE);
+  const size_t ntt = (size_t)c->maxNB * ((c->maxB + 255) / 256) + 1;  // triplet tiles (+ a zero)
   size_t tb = 0;
-  if (rocprim::exclusive_scan(nullptr, tb, c->flag, c->inc, 0, ncnt, rocprim::plus<int32_t>()) != hipSuccess)
+  if (rocprim::exclusive_scan(nullptr, tb, c->flag, c->inc, 0, std::max(ncnt, ntt), rocprim::plus<int32_t>()) !=
+      hipSuccess)
     return false;
   std::vector<void*> got;
   auto A = [&](auto** p, size_t m) -> bool {
@@ -4068,7 +4192,9 @@ static bool hplan_ready(acf_apr_ctx* c) {
   };
   bool ok = A(&c->hplan_occ, n3) && A(&c->hplan_pcnt, 2 * ncnt) && A(&c->hplan_claims, n3 / 2 + 1) &&
             A(&c->hplan_ptot, ((size_t)c->maxNB << pb) * 2 * ACF_HPLAN_TOT) &&
-            A(&c->hplan_cnt, (size_t)3 * c->maxNB) && A(&c->hplan_haux, (size_t)c->maxNB * c->hot.hot_stride);
+            A(&c->hplan_cnt, (size_t)3 * c->maxNB) && A(&c->hplan_haux, (size_t)c->maxNB * c->hot.hot_stride) &&
+            A(&c->hplan_perm, (size_t)c->maxE) && A(&c->hplan_tcnt, (size_t)c->maxNB) &&
+            A(&c->hplan_ttc, 2 * ntt);
   c->hplan_tmp_bytes = tb;
   if (ok && tb > c->tmp_bytes) ok = A(reinterpret_cast<char**>(&c->hplan_tmp), tb);
   if (!ok) {
@@ -4083,6 +4209,9 @@ static bool hplan_ready(acf_apr_ctx* c) {
     c->hplan_ptot = nullptr;
     c->hplan_cnt = nullptr;
     c->hplan_haux = nullptr;
+    c->hplan_perm = nullptr;
+    c->hplan_tcnt = nullptr;
+    c->hplan_ttc = nullptr;
     c->hplan_tmp = nullptr;
     return false;
   }
@@ -4094,7 +4223,6 @@ static bool hplan_ready(acf_apr_ctx* c) {
 // tri branch, slot ids and CSR ranges numbered in allocation order
 static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, const int32_t* ineg, int32_t B,
                      int32_t nb, int32_t gen, int32_t kb, int32_t check, hipStream_t s) {
-  const int64_t E = (int64_t)B * nb;
   const int32_t pb = hplan_pbits(B, ACF_HPLAN_PART);
   HIP_TRY(hipMemsetAsync(c->err, 0, sizeof(int32_t), s));  // the other counters: k_hplan_keys
   HPlanArgs p;
@@ -4115,6 +4243,10 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   p.pbase = c->hplan_ptot + ((size_t)c->maxNB << hplan_pbits(c->maxB, ACF_HPLAN_PART)) * ACF_HPLAN_TOT;
   p.scnt = c->hplan_cnt; p.ucsr = c->hplan_cnt + c->maxNB; p.icsr = c->hplan_cnt + 2 * c->maxNB;
   p.inl = c->inl; p.trec = c->trec; p.tpos = c->tpos;
+  p.perm = c->hplan_perm; p.tcnt = c->hplan_tcnt;
+  p.ttiles = (B + 255) / 256;
+  p.ttc = c->hplan_ttc;
+  p.tto = c->hplan_ttc + (size_t)c->maxNB * ((c->maxB + 255) / 256) + 1;
   p.slot_list = c->slot_list; p.slot_cnt = c->slot_cnt; p.flush_cnt = c->flush_cnt;
   p.saux = c->flush_list;  // unused by in-place plans
   p.haux = c->hplan_haux;
@@ -4133,7 +4265,14 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
   k_hplan_dedup<ACF_HPLAN_BUCKETS><<<(unsigned)(nb << pb), 256, 0, s>>>(p);
   k_hplan_bases<<<(unsigned)nb, 1024, 0, s>>>(p);
   k_hplan_emit<<<(unsigned)(nb << pb), 256, 0, s>>>(p);
-  k_hplan_trip<<<(unsigned)((E + 255) / 256), 256, 0, s>>>(p);
+  {  // the triplets' places (fused first): per-tile counts, their scan, the records
+    const unsigned ttl = (unsigned)(nb * p.ttiles);
+    k_hplan_tcount<<<ttl, 256, 0, s>>>(p);
+    void* tmp = c->hplan_tmp ? c->hplan_tmp : c->tmp;
+    size_t tb = c->hplan_tmp ? c->hplan_tmp_bytes : c->tmp_bytes;
+    HIP_TRY(rocprim::exclusive_scan(tmp, tb, p.ttc, p.tto, 0, (size_t)ttl + 1, rocprim::plus<int32_t>(), s));
+    k_hplan_trip<<<ttl, 256, 0, s>>>(p);
+  }
   // (a one-batch plan, the split step's, gets more workgroups per batch)
   const unsigned rx = (unsigned)std::max(64, 1024 / nb);
   k_hplan_rank_small<<<dim3(rx, nb), 256, 0, s>>>(p);
@@ -4481,6 +4620,8 @@ static StepArgs make_args(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_ap
   a.xdmap = c->xdmap;
   a.reg_B = c->reg_batch > 0 ? c->reg_batch : c->B;
   a.tpos = reinterpret_cast<const int4*>(c->tpos);
+  a.tri_nf = c->plan_kind == 3 ? c->hplan_tcnt : nullptr;
+  a.ready = c->ready;
   a.contrib = c->contrib;
   a.inplace = c->tri;
   a.lr = hp->lr; a.eps = hp->eps; a.reg = hp->reg; a.reg_adv = hp->reg_adv;
@@ -4497,6 +4638,7 @@ struct Kernels {
   void *hot_clean = nullptr, *hot_bpr = nullptr, *hot_adv = nullptr;  // k_hot_combine (list kernels)
   // triplet-centric list step (tri plans with fusion): clean (APR / BPR), combine (MODE 0/1/2), adversarial
   void *tri_clean = nullptr, *tri_clean_bpr = nullptr, *tri_adv = nullptr;
+  void* tri_cadv = nullptr;  // the clean combine + adversarial pass in one launch (hash plans, r06)
   void* tri_comb[3] = {nullptr, nullptr, nullptr};
   int tri = 0;
   int slots_per_wave = 1;
@@ -4534,6 +4676,7 @@ static void kernel_ptrs(Kernels* k, int packed, int fused, int lists, int tri) {
     k->tri_clean = reinterpret_cast<void*>(&k_tri_clean<LPR, NV, false>);
     k->tri_clean_bpr = reinterpret_cast<void*>(&k_tri_clean<LPR, NV, true>);
     k->tri_adv = reinterpret_cast<void*>(&k_tri_adv<LPR, NV>);
+    k->tri_cadv = reinterpret_cast<void*>(&k_tri_cadv<LPR, NV>);
     k->tri_comb[0] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 0>);
     k->tri_comb[1] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 1>);
     k->tri_comb[2] = reinterpret_cast<void*>(&k_tri_combine<LPR, NV, 2>);
@@ -4825,13 +4968,17 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
       ac.hot_blocks = HBT;
       const int CW = SW4 + HW4 + 4 * HBT;
       (void)ah;
+      // hash plans (fused triplets placed first), a whole step, not shard mode: the
+      // clean combine rides at the head of the adversarial launch (k_tri_cadv)
+      const bool merged = tri_phases == 3 && !c->shard && c->plan_kind == 3 && K.tri_cadv;
       if (hp->adver) {
         if (tri_phases & 1) {
           ACF_RET(L(K.tri_clean, at, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 0));
-          ACF_RET(L(K.tri_comb[0], ac, CW, 5));
+          if (!merged) ACF_RET(L(K.tri_comb[0], ac, CW, 5));
         }
         if (tri_phases & 2) {
-          ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
+          if (merged) ACF_RET(L(K.tri_cadv, ac, CW + (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
+          else ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
           ACF_RET(L(K.tri_comb[2], ac, CW, 5));
         }
       } else if (tri_phases & 2) {

@@ -24,7 +24,8 @@
 //     shared ones enter their CSR range (in LDS-atomic order).  A partition with
 //     more distinct keys than the table holds is split by further hash bits and
 //     done in rounds (terminates: the hash is a bijection of 32-bit keys);
-//  3. k_hplan_trip: per triplet its record (coalesced reads of step 2's output);
+//  3. k_hplan_trip: per triplet its record (coalesced reads of step 2's output),
+//     at its place: the batch's fused triplets first (r06);
 //  4. k_hplan_rank_small / k_hplan_rank_hot: each CSR range put in occurrence
 //     order -- <= 8 entries by one thread, <= 64 by a wave (all-pairs ranks), more
 //     by a workgroup (an LDS bitmap of the side's occurrence ids and its prefix
@@ -64,7 +65,15 @@ struct HPlanArgs {
   int32_t* icsr;              // [nb] item CSR positions taken
   OccRec* inl;
   OccRec* trec;
-  int32_t* tpos;              // [E][4] CSR positions of the triplet's occurrences
+  int32_t* tpos;              // [E][4] CSR positions of the triplet's occurrences (at its place, perm)
+  // (r06) triplet places: each batch's fused triplets first, the others after them
+  // (k_hplan_trip), so the step's waves are all-fused or all-shared and the clean
+  // pass starts past the fused ones
+  int32_t* perm;              // [E] triplet e -> its place t * B + x (trec / tpos index)
+  int32_t* tcnt;              // [nb] fused triplets of each batch (placed first)
+  int32_t ttiles;             // tiles of 256 triplets per batch (k_hplan_tcount / k_hplan_trip)
+  int32_t* ttc;               // [nb * ttiles + 1] fused triplets per tile (+ a zero)
+  int32_t* tto;               // its exclusive scan: fused triplets before each tile (the last: all)
   int32_t* slot_list;
   int32_t* slot_cnt;
   int32_t* flush_cnt;
@@ -466,18 +475,74 @@ __global__ void __launch_bounds__(256) k_hplan_emit(HPlanArgs p) {
   }
 }
 
+// (r06) triplet places: per tile of 256 triplets of a batch its fused triplets
+// (k_hplan_tcount), their exclusive scan over the tiles (rocPRIM), then
+// k_hplan_trip writes every triplet at its place -- the batch's fused triplets
+// first, in triplet order, then the others in triplet order.  Deterministic; any
+// order would give the same bits (a triplet's arithmetic and the CSR order of its
+// contributions do not depend on its place).  (A first form took places from two
+// per-batch counters with one atomic per wave: ~1,000 same-address returning
+// atomics per counter and batch serialised at the memory side and slowed the
+// plan beside the step, configs[4] d = 64 737M -> 662M.)
+__device__ __forceinline__ bool hplan_fused(const HPlanArgs& p, int32_t t, int32_t b) {
+  const int64_t ob = (int64_t)t * 3 * p.B;
+  return !p.shard && p.occ[ob + b].x < 0 && p.occ[ob + p.B + 2 * b].x < 0 && p.occ[ob + p.B + 2 * b + 1].x < 0;
+}
+
+// fused triplets before lane `lane` among the workgroup's, and the workgroup total
+__device__ __forceinline__ int32_t block_rank(bool f, int32_t* s_w, int32_t& total) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const unsigned long long m = __ballot(f);
+  if (lane == 0) s_w[wave] = __popcll(m);
+  __syncthreads();
+  int32_t before = 0;
+  total = 0;
+  for (int w = 0; w < 4; ++w) {
+    if (w < wave) before += s_w[w];
+    total += s_w[w];
+  }
+  return before + __popcll(m & ((1ull << lane) - 1ull));
+}
+
+__global__ void __launch_bounds__(256) k_hplan_tcount(HPlanArgs p) {
+  __shared__ int32_t s_w[4];
+  const int32_t t = blockIdx.x / p.ttiles, tile = blockIdx.x - t * p.ttiles, b = tile * 256 + threadIdx.x;
+  const bool f = b < p.B && hplan_fused(p, t, b);
+  int32_t tot = 0;
+  (void)block_rank(f, s_w, tot);
+  if (threadIdx.x == 0) p.ttc[blockIdx.x] = tot;
+  if (blockIdx.x == 0 && threadIdx.x == 0) p.ttc[p.nb * p.ttiles] = 0;
+}
+
 __global__ void __launch_bounds__(256) k_hplan_trip(HPlanArgs p) {
-  const int64_t e = blockIdx.x * 256ll + threadIdx.x;
+  __shared__ int32_t s_w[4];
   const int B = p.B, S3 = 3 * B;
+  const int32_t t = blockIdx.x / p.ttiles, tile = blockIdx.x - t * p.ttiles, b = tile * 256 + threadIdx.x;
+  const int64_t e = (int64_t)t * B + b;
   if (e == 0) *p.gen_ptr = p.gen;
-  if (e >= (int64_t)p.nb * B) return;
-  const int32_t t = (int32_t)(e / B), b = (int32_t)(e - (int64_t)t * B);
+  const bool valid = b < B;
   const int64_t ob = (int64_t)t * S3;
-  const int2 su_ = p.occ[ob + b], si_ = p.occ[ob + B + 2 * b], sj_ = p.occ[ob + B + 2 * b + 1];
+  int2 su_ = make_int2(-1, 0), si_ = su_, sj_ = su_;
+  if (valid) {
+    su_ = p.occ[ob + b];
+    si_ = p.occ[ob + B + 2 * b];
+    sj_ = p.occ[ob + B + 2 * b + 1];
+  }
+  const int32_t f0 = p.tto[(int64_t)t * p.ttiles], fb = p.tto[blockIdx.x] - f0,
+                nf = p.tto[(int64_t)(t + 1) * p.ttiles] - f0;
+  const bool su = su_.x < 0, si = si_.x < 0, sj = sj_.x < 0;
+  const bool fz = valid && su && si && sj && !p.shard;
+  int32_t tot = 0;
+  const int32_t rf = block_rank(fz, s_w, tot);
+  if (tile == 0 && threadIdx.x == 0) p.tcnt[t] = nf;
+  if (!valid) return;
+  // fused: after the batch's fused triplets of earlier tiles; the others after all
+  // fused ones and the earlier tiles' others
+  const int32_t x = fz ? fb + rf : nf + (tile * 256 - fb) + ((int32_t)threadIdx.x - rf);
+  const int64_t at = (int64_t)t * B + x;
   int err = 0;
   const int32_t u = (int32_t)hplan_key(p, t, b, err), i = (int32_t)(hplan_key(p, t, B + 2 * b, err) & 0x7FFFFFFFu),
                 j = (int32_t)(hplan_key(p, t, B + 2 * b + 1, err) & 0x7FFFFFFFu);
-  const bool su = su_.x < 0, si = si_.x < 0, sj = sj_.x < 0;
   // fused-triplet record layout (see records_one): a = {u, i, j, slot u}, b = {slot i,
   // slot j, src u, src i}, c = {src j, flags, e, gen}; in place: sources are the rows
   OccRec q;
@@ -485,17 +550,18 @@ __global__ void __launch_bounds__(256) k_hplan_trip(HPlanArgs p) {
   q.e_role = si ? 0 : si_.x; q.pa_row = sj ? 0 : sj_.x; q.pb_row = u; q.pa_src = i;
   q.pb_src = j;
   q.pa_slot = ((su && si && sj && !p.shard) ? 1 : 0) | (su ? 2 + 16 : 0) | (si ? 4 + 32 : 0) | (sj ? 8 + 64 : 0);
-  q.pb_slot = (int32_t)e;
+  q.pb_slot = (int32_t)e;  // the triplet itself (its losses' index)
   q.gen = p.gen;
-  p.trec[e] = q;
+  p.trec[at] = q;
+  p.perm[e] = (int32_t)at;
 }
 
 // CSR position of occurrence id v (users: b; items: 2b + role) of batch t at sorted place x
 __device__ __forceinline__ void hplan_put(const HPlanArgs& p, int32_t t, bool item, int32_t base, int32_t v,
                                           int32_t x) {
   const int B = p.B;
-  if (!item) p.tpos[((int64_t)t * B + v) * 4] = t * B + base + x;
-  else p.tpos[((int64_t)t * B + (v >> 1)) * 4 + 1 + (v & 1)] = t * 2 * B + base + x;
+  if (!item) p.tpos[(int64_t)p.perm[(int64_t)t * B + v] * 4] = t * B + base + x;
+  else p.tpos[(int64_t)p.perm[(int64_t)t * B + (v >> 1)] * 4 + 1 + (v & 1)] = t * 2 * B + base + x;
 }
 
 // shared slots of <= ACF_HOT_MIN occurrences: one thread each, a fixed

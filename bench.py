@@ -183,8 +183,8 @@ def step_kernel_name(kind: str, d: int, B: int) -> str:
         lpr <<= 1
     nv = (d4 + lpr - 1) // lpr
     if B >= 4096:  # packed mapping with fusion: the triplet-centric list step
-        if kind == "adv":
-            return f"k_tri_adv<{lpr}, {nv}>"
+        if kind == "adv":  # (r06) hash plans: the clean combine rides in the adversarial launch
+            return f"k_tri_cadv<{lpr}, {nv}>"
         if kind == "clean":
             return f"k_tri_clean<{lpr}, {nv}, false>"
         return "k_flush"

@@ -553,8 +553,9 @@ def _zipf_large(seed, U1, I1, d, B, nb, s=1.1):
 @pytest.mark.parametrize("d,adver", [(64, 1), (128, 1), (64, 0)])
 def test_hot_slots_large_batch_match_oracle(ops, oracle, dev, d, adver, fp32_parity):
     """B = 65,536 with Zipf positives: slots with more than ACF_HOT_MIN (8)
-    occurrences run as pieces + a combine of the pieces (inside k_tri_combine; the
-    top item has ~3,000 occurrences per batch).  Tables and losses vs the oracle, and the hot path
+    occurrences run as pieces + a combine of the pieces (inside k_tri_combine, or
+    for the clean pass at the head of k_tri_cadv; the top item has ~3,000
+    occurrences per batch).  Tables and losses vs the oracle, and the hot path
     really ran (kind 'hot' launches)."""
     U1, I1, B, nb = 300_000, 200_000, 65536, 2
     P, Q, u, i, j = _zipf_large(d + adver, U1, I1, d, B, nb)
@@ -564,7 +565,11 @@ def test_hot_slots_large_batch_match_oracle(ops, oracle, dev, d, adver, fp32_par
     ctx = ops.APRContext(U1, I1, d, B, nb, dev)
     ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
     t = ctx.time_kernels(tabs, ops.StepHParams(adver=adver))
-    assert t["hot"][1] == nb * (2 if adver else 1)  # one tri combine per pass, hot slots combined inside
+    # one combine launch per pass, hot slots combined inside; (r06) on the hash plan
+    # the clean pass's combine rides in the adversarial launch (k_tri_cadv)
+    assert ctx.plan_kind() == "hash"
+    assert t["hot"][1] == nb  # APR: the adversarial combine; BPR: its one combine
+    assert t["adv"][1] == (nb if adver else 0)
     lc, la = ctx.losses()
     for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
         fp32_parity(g, w, n)
