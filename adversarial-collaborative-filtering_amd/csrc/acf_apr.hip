@@ -3800,7 +3800,7 @@ struct acf_apr_ctx {
   int32_t* hplan_haux = nullptr;  // [maxNB][hot_stride] CSR base | item of each hot-list entry
   int32_t* hplan_perm = nullptr;  // [maxE] triplet -> its place (fused first, r06)
   int32_t* hplan_tcnt = nullptr;  // [maxNB] fused triplets per batch
-  int32_t* hplan_ttc = nullptr;   // [maxNB * tiles + 1] fused triplets per tile of 256, then its scan
+  unsigned long long* hplan_ttc = nullptr;  // [maxNB * tiles + 1] triplet classes per tile of 256, then its scan
   int32_t bplan_ok = -1;     // -1 unknown, 0 unavailable, 1 buffers allocated
   unsigned long long* bmask[2] = {nullptr, nullptr};
   size_t bmask_words = 0;
@@ -4181,9 +4181,12 @@ static bool hplan_ready(acf_apr_ctx* c) {
   const size_t ncnt = ((size_t)c->maxNB << pb) * (((size_t)3 * c->maxB + ACF_HPLAN_PTILE - 1) / ACF_HPLAN_PTILE);
   const size_t ntt = (size_t)c->maxNB * ((c->maxB + 255) / 256) + 1;  // triplet tiles (+ a zero)
   size_t tb = 0;
-  if (rocprim::exclusive_scan(nullptr, tb, c->flag, c->inc, 0, std::max(ncnt, ntt), rocprim::plus<int32_t>()) !=
-      hipSuccess)
+  size_t tb2 = 0;
+  if (rocprim::exclusive_scan(nullptr, tb, c->flag, c->inc, 0, ncnt, rocprim::plus<int32_t>()) != hipSuccess ||
+      rocprim::exclusive_scan(nullptr, tb2, (unsigned long long*)nullptr, (unsigned long long*)nullptr, 0ull, ntt,
+                              rocprim::plus<unsigned long long>()) != hipSuccess)
     return false;
+  tb = std::max(tb, tb2);
   std::vector<void*> got;
   auto A = [&](auto** p, size_t m) -> bool {
     if (dalloc(c, p, m) != ACF_OK) return false;
@@ -4270,7 +4273,8 @@ static int hash_plan(acf_apr_ctx* c, const int32_t* user, const int32_t* ipos, c
     k_hplan_tcount<<<ttl, 256, 0, s>>>(p);
     void* tmp = c->hplan_tmp ? c->hplan_tmp : c->tmp;
     size_t tb = c->hplan_tmp ? c->hplan_tmp_bytes : c->tmp_bytes;
-    HIP_TRY(rocprim::exclusive_scan(tmp, tb, p.ttc, p.tto, 0, (size_t)ttl + 1, rocprim::plus<int32_t>(), s));
+    HIP_TRY(rocprim::exclusive_scan(tmp, tb, p.ttc, p.tto, 0ull, (size_t)ttl + 1, rocprim::plus<unsigned long long>(),
+                                    s));
     k_hplan_trip<<<ttl, 256, 0, s>>>(p);
   }
   // (a one-batch plan, the split step's, gets more workgroups per batch)
@@ -4651,6 +4655,13 @@ struct Kernels {
 #define ACF_HOT_WAVES 2048   // piece waves of a list kernel (hot slots)
 #define ACF_HOT_BLOCKS 1024  // workgroups of k_hot_combine
 #define ACF_TRI_HOT_BLOCKS 512  // hot-slot combining workgroups of k_tri_combine
+// the same two inside k_tri_cadv (the clean combine at the head of the adversarial launch)
+#ifndef ACF_CADV_SLOT_WAVES
+#define ACF_CADV_SLOT_WAVES 4096
+#endif
+#ifndef ACF_CADV_HOT_BLOCKS
+#define ACF_CADV_HOT_BLOCKS 512
+#endif
 // (r05 same-box A/B: 2,048 / 8,192 small-slot waves, 256 / 1,024 combining
 // workgroups, 1,024 / 4,096 piece waves -- none faster; profiles/r05/combine_params_ab.json)
 
@@ -4977,7 +4988,13 @@ static int run_loop(acf_apr_ctx* c, const acf_apr_tables* tb, const acf_apr_hpar
           if (!merged) ACF_RET(L(K.tri_comb[0], ac, CW, 5));
         }
         if (tri_phases & 2) {
-          if (merged) ACF_RET(L(K.tri_cadv, ac, CW + (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
+          if (merged) {
+            StepArgs am = ac;
+            am.slot_waves = (std::min(SW, ACF_CADV_SLOT_WAVES) + 3) & ~3;
+            am.hot_blocks = std::min(HB, ACF_CADV_HOT_BLOCKS);
+            const int CWm = am.slot_waves + HW4 + 4 * am.hot_blocks;
+            ACF_RET(L(K.tri_cadv, am, CWm + (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
+          }
           else ACF_RET(L(K.tri_adv, a, (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv), 1));
           ACF_RET(L(K.tri_comb[2], ac, CW, 5));
         }

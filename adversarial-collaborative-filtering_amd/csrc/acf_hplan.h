@@ -36,7 +36,8 @@
 // returning atomics serialising at the memory side on the Zipf-popular items;
 // tile-aggregated, still 0.48 ms: slower than the sort plan.)
 // ---------------------------------------------------------------------------
-#define ACF_HPLAN_MAXB 65536  // the hot-rank bitmap: 2B bits of LDS per workgroup
+#define ACF_HPLAN_MAXB 65536
+#define ACF_OCC_HOT 0x40000000  // occ[].x: the slot is hot (more than ACF_HOT_MIN occurrences)  // the hot-rank bitmap: 2B bits of LDS per workgroup
 // partitions of ~384 occurrences, 1,024 LDS buckets (~768 / 2,048 was 0.5% slower at
 // configs[4], r04 A/B); a round takes at most 3/4 of the buckets
 #define ACF_HPLAN_PART 384
@@ -72,8 +73,8 @@ struct HPlanArgs {
   int32_t* perm;              // [E] triplet e -> its place t * B + x (trec / tpos index)
   int32_t* tcnt;              // [nb] fused triplets of each batch (placed first)
   int32_t ttiles;             // tiles of 256 triplets per batch (k_hplan_tcount / k_hplan_trip)
-  int32_t* ttc;               // [nb * ttiles + 1] fused triplets per tile (+ a zero)
-  int32_t* tto;               // its exclusive scan: fused triplets before each tile (the last: all)
+  unsigned long long* ttc;    // [nb * ttiles + 1] per tile: fused | plain << 32 (+ a zero)
+  unsigned long long* tto;    // its exclusive scan: both counts before each tile (the last: all)
   int32_t* slot_list;
   int32_t* slot_cnt;
   int32_t* flush_cnt;
@@ -470,76 +471,109 @@ __global__ void __launch_bounds__(256) k_hplan_emit(HPlanArgs p) {
     const int32_t o = (int32_t)(v & 0x3FFFFull), lpos = (int32_t)((v >> 18) & 0x3FFFFull), j = (int32_t)(v >> 36);
     const bool item = o >= B;
     const int32_t pos = (item ? base[2] : base[1]) + lpos;
-    p.occ[(int64_t)t * S3 + o] = make_int2(base[0] + j, pos);
+    // a hot slot's occurrences carry ACF_OCC_HOT (k_hplan_trip places their triplets last)
+    const bool hot = claims[j].count > ACF_HOT_MIN;
+    p.occ[(int64_t)t * S3 + o] = make_int2((base[0] + j) | (hot ? ACF_OCC_HOT : 0), pos);
     p.csr[(int64_t)t * S3 + (item ? B : 0) + pos] = item ? o - B : o;
   }
 }
 
-// (r06) triplet places: per tile of 256 triplets of a batch its fused triplets
-// (k_hplan_tcount), their exclusive scan over the tiles (rocPRIM), then
-// k_hplan_trip writes every triplet at its place -- the batch's fused triplets
-// first, in triplet order, then the others in triplet order.  Deterministic; any
-// order would give the same bits (a triplet's arithmetic and the CSR order of its
-// contributions do not depend on its place).  (A first form took places from two
-// per-batch counters with one atomic per wave: ~1,000 same-address returning
-// atomics per counter and batch serialised at the memory side and slowed the
-// plan beside the step, configs[4] d = 64 737M -> 662M.)
-__device__ __forceinline__ bool hplan_fused(const HPlanArgs& p, int32_t t, int32_t b) {
-  const int64_t ob = (int64_t)t * 3 * p.B;
-  return !p.shard && p.occ[ob + b].x < 0 && p.occ[ob + p.B + 2 * b].x < 0 && p.occ[ob + p.B + 2 * b + 1].x < 0;
+// (r06) triplet places, in three classes: the batch's fused triplets (all rows
+// single), then the "plain" ones (shared rows, none of them hot), then those
+// with a hot row -- each class in triplet order.  k_tri_cadv runs them in that
+// order: the fused ones need no delta, and the hot slots' deltas (the longest
+// chains of the combine at the head of the launch) are needed last.  Per tile of
+// 256 triplets the two counts (k_hplan_tcount), their exclusive scan over the
+// tiles (rocPRIM, packed fused | plain << 32), then k_hplan_trip writes every
+// triplet at its place.  Deterministic; any place gives the same bits (a
+// triplet's arithmetic and the CSR order of its contributions do not depend on
+// it).  (A first form took places from two per-batch counters with one atomic
+// per wave: ~1,000 same-address returning atomics per counter and batch
+// serialised at the memory side and slowed the plan beside the step, configs[4]
+// d = 64 737M -> 662M.)
+// class of triplet b of batch t: 0 fused, 1 plain, 2 hot (occ rows as k_hplan_emit left them)
+__device__ __forceinline__ int hplan_class(const HPlanArgs& p, int2 su, int2 si, int2 sj) {
+  if (su.x < 0 && si.x < 0 && sj.x < 0 && !p.shard) return 0;
+  const bool hot = (su.x >= 0 && (su.x & ACF_OCC_HOT)) || (si.x >= 0 && (si.x & ACF_OCC_HOT)) ||
+                   (sj.x >= 0 && (sj.x & ACF_OCC_HOT));
+  return hot ? 2 : 1;
 }
 
-// fused triplets before lane `lane` among the workgroup's, and the workgroup total
-__device__ __forceinline__ int32_t block_rank(bool f, int32_t* s_w, int32_t& total) {
+// ranks of the workgroup's lanes among those with f0 / with f1 (lanes in order),
+// and the workgroup totals
+__device__ __forceinline__ int2 block_rank2(bool f0, bool f1, int32_t* s_w, int2& total) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const unsigned long long m = __ballot(f);
-  if (lane == 0) s_w[wave] = __popcll(m);
-  __syncthreads();
-  int32_t before = 0;
-  total = 0;
-  for (int w = 0; w < 4; ++w) {
-    if (w < wave) before += s_w[w];
-    total += s_w[w];
+  const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1);
+  if (lane == 0) {
+    s_w[wave] = __popcll(m0);
+    s_w[4 + wave] = __popcll(m1);
   }
-  return before + __popcll(m & ((1ull << lane) - 1ull));
+  __syncthreads();
+  int2 before = make_int2(0, 0);
+  total = make_int2(0, 0);
+  for (int w = 0; w < 4; ++w) {
+    if (w < wave) {
+      before.x += s_w[w];
+      before.y += s_w[4 + w];
+    }
+    total.x += s_w[w];
+    total.y += s_w[4 + w];
+  }
+  const unsigned long long below = (1ull << lane) - 1ull;
+  return make_int2(before.x + __popcll(m0 & below), before.y + __popcll(m1 & below));
+}
+
+__device__ __forceinline__ void hplan_occ3(const HPlanArgs& p, int32_t t, int32_t b, int2& su, int2& si, int2& sj) {
+  const int64_t ob = (int64_t)t * 3 * p.B;
+  su = p.occ[ob + b];
+  si = p.occ[ob + p.B + 2 * b];
+  sj = p.occ[ob + p.B + 2 * b + 1];
 }
 
 __global__ void __launch_bounds__(256) k_hplan_tcount(HPlanArgs p) {
-  __shared__ int32_t s_w[4];
+  __shared__ int32_t s_w[8];
   const int32_t t = blockIdx.x / p.ttiles, tile = blockIdx.x - t * p.ttiles, b = tile * 256 + threadIdx.x;
-  const bool f = b < p.B && hplan_fused(p, t, b);
-  int32_t tot = 0;
-  (void)block_rank(f, s_w, tot);
-  if (threadIdx.x == 0) p.ttc[blockIdx.x] = tot;
-  if (blockIdx.x == 0 && threadIdx.x == 0) p.ttc[p.nb * p.ttiles] = 0;
+  int cls = 3;
+  if (b < p.B) {
+    int2 su, si, sj;
+    hplan_occ3(p, t, b, su, si, sj);
+    cls = hplan_class(p, su, si, sj);
+  }
+  int2 tot;
+  (void)block_rank2(cls == 0, cls == 1, s_w, tot);
+  if (threadIdx.x == 0) p.ttc[blockIdx.x] = (unsigned long long)(uint32_t)tot.x | ((unsigned long long)tot.y << 32);
+  if (blockIdx.x == 0 && threadIdx.x == 0) p.ttc[p.nb * p.ttiles] = 0ull;
 }
 
 __global__ void __launch_bounds__(256) k_hplan_trip(HPlanArgs p) {
-  __shared__ int32_t s_w[4];
-  const int B = p.B, S3 = 3 * B;
+  __shared__ int32_t s_w[8];
+  const int B = p.B;
   const int32_t t = blockIdx.x / p.ttiles, tile = blockIdx.x - t * p.ttiles, b = tile * 256 + threadIdx.x;
   const int64_t e = (int64_t)t * B + b;
   if (e == 0) *p.gen_ptr = p.gen;
   const bool valid = b < B;
-  const int64_t ob = (int64_t)t * S3;
   int2 su_ = make_int2(-1, 0), si_ = su_, sj_ = su_;
-  if (valid) {
-    su_ = p.occ[ob + b];
-    si_ = p.occ[ob + B + 2 * b];
-    sj_ = p.occ[ob + B + 2 * b + 1];
-  }
-  const int32_t f0 = p.tto[(int64_t)t * p.ttiles], fb = p.tto[blockIdx.x] - f0,
-                nf = p.tto[(int64_t)(t + 1) * p.ttiles] - f0;
-  const bool su = su_.x < 0, si = si_.x < 0, sj = sj_.x < 0;
-  const bool fz = valid && su && si && sj && !p.shard;
-  int32_t tot = 0;
-  const int32_t rf = block_rank(fz, s_w, tot);
+  if (valid) hplan_occ3(p, t, b, su_, si_, sj_);
+  const unsigned long long o0 = p.tto[(int64_t)t * p.ttiles], ob_ = p.tto[blockIdx.x],
+                           o1 = p.tto[(int64_t)(t + 1) * p.ttiles];
+  const int32_t fb = (int32_t)((uint32_t)ob_ - (uint32_t)o0), pbf = (int32_t)((ob_ >> 32) - (o0 >> 32));
+  const int32_t nf = (int32_t)((uint32_t)o1 - (uint32_t)o0), np = (int32_t)((o1 >> 32) - (o0 >> 32));
+  const int cls = valid ? hplan_class(p, su_, si_, sj_) : 3;
+  int2 tot;
+  const int2 rk = block_rank2(cls == 0, cls == 1, s_w, tot);
   if (tile == 0 && threadIdx.x == 0) p.tcnt[t] = nf;
   if (!valid) return;
-  // fused: after the batch's fused triplets of earlier tiles; the others after all
-  // fused ones and the earlier tiles' others
-  const int32_t x = fz ? fb + rf : nf + (tile * 256 - fb) + ((int32_t)threadIdx.x - rf);
+  // fused: after the batch's fused triplets of earlier tiles; plain: after every
+  // fused one and the earlier tiles' plain ones; hot: after both classes and the
+  // earlier tiles' hot ones (earlier tiles are full: 256 triplets each)
+  const int32_t x = cls == 0   ? fb + rk.x
+                    : cls == 1 ? nf + pbf + rk.y
+                               : nf + np + (tile * 256 - fb - pbf) + ((int32_t)threadIdx.x - rk.x - rk.y);
   const int64_t at = (int64_t)t * B + x;
+  su_.x = su_.x < 0 ? su_.x : (su_.x & ~ACF_OCC_HOT);
+  si_.x = si_.x < 0 ? si_.x : (si_.x & ~ACF_OCC_HOT);
+  sj_.x = sj_.x < 0 ? sj_.x : (sj_.x & ~ACF_OCC_HOT);
+  const bool su = su_.x < 0, si = si_.x < 0, sj = sj_.x < 0;
   int err = 0;
   const int32_t u = (int32_t)hplan_key(p, t, b, err), i = (int32_t)(hplan_key(p, t, B + 2 * b, err) & 0x7FFFFFFFu),
                 j = (int32_t)(hplan_key(p, t, B + 2 * b + 1, err) & 0x7FFFFFFFu);
