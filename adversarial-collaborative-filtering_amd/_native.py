@@ -88,6 +88,7 @@ SIGNATURES = {
     "acf_alias_build": (ctypes.c_int, [_P, _I64, _P, _P]),
     "acf_dns_select": (ctypes.c_int, [_P, _P, _I64, _I64, _I32, _P, _P, _I64, _I32, _P, _P]),
     "acf_apr_set_shard_mode": (ctypes.c_int, [_P, _I32, _I32]),
+    "acf_apr_set_shard_batch": (ctypes.c_int, [_P, _I32]),
     "acf_apr_shard_pass": (ctypes.c_int, [_P, ctypes.POINTER(Tables), ctypes.POINTER(HParams), _I32, _P]),
     "acf_apr_shard_items": (ctypes.c_int, [_P, _I32, _P, _I64, _P]),
     "acf_apr_shard_items_mapped": (ctypes.c_int, [_P, _I32, _P, _P, _I64, _P]),

@@ -3754,6 +3754,7 @@ struct acf_apr_ctx {
   float* contrib = nullptr;     // [4 maxB, d] per-occurrence contributions of shared rows (k_tri_*)
   unsigned long long* ready = nullptr;  // [3 maxB] k_tri_cadv's per-slot tags (zeroed: never a tag)
   int32_t reg_batch = 0;        // batch size of the reg mean (0: the planned batch size)
+  int32_t shard_t = 0;          // the batch shard passes use (acf_apr_set_shard_batch)
   float* hot_part = nullptr;    // their piece sums
   int32_t fusion = 1;   // fused triplets in train_planned / time_kernels
   const float* xdelta = nullptr;    // triplet-centric shard passes: the owners' item deltas (acf_apr_shard_items_mapped)
@@ -5229,6 +5230,17 @@ extern "C" int acf_apr_set_shard_mode(acf_apr_ctx* c, int32_t on, int32_t reg_ba
   c->shard = on != 0;
   c->reg_batch = reg_batch;
   c->nb = 0;  // re-plan: the records depend on the mode
+  c->shard_t = 0;
+  return ACF_OK;
+}
+
+// (r06) the batch of a multi-batch triplet-centric shard plan that the next
+// shard pass / item map calls use (distributed.ShardedAPR plans a chunk of
+// steps at once)
+extern "C" int acf_apr_set_shard_batch(acf_apr_ctx* c, int32_t t) {
+  ACF_CHECK(c != nullptr, ACF_E_INVALID, "ctx is NULL");
+  ACF_CHECK(t >= 0 && t < c->maxNB, ACF_E_INVALID, "batch %d outside [0, %d)", t, c->maxNB);
+  c->shard_t = t;
   return ACF_OK;
 }
 
@@ -5237,8 +5249,9 @@ extern "C" int acf_apr_shard_pass_export(acf_apr_ctx* c, const acf_apr_tables* t
                                          void* stream_) {
   ACF_RET(check_step(c, tb, hp, 0));
   ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
-  ACF_CHECK(c->shard && c->lists && c->nb == 1, ACF_E_STATE,
-            "shard pass needs shard mode and a one-batch plan");
+  ACF_CHECK(c->shard && c->lists && (c->nb == 1 || (c->tri && c->nb > 1)), ACF_E_STATE,
+            "shard pass needs shard mode and a one-batch plan (or a triplet-centric plan of several)");
+  ACF_CHECK(c->shard_t < c->nb, ACF_E_STATE, "shard batch %d outside the plan's %d", c->shard_t, c->nb);
   ACF_CHECK(pass == 0 || (pass == 1 && hp->adver), ACF_E_INVALID, "pass must be 0, or 1 for APR");
   ACF_CHECK(hp->adv_mode == 0, ACF_E_INVALID, "shard mode supports adv = grad only");
   ACF_CHECK((xbuf == nullptr) == (xmap == nullptr), ACF_E_INVALID, "xbuf and xmap go together");
@@ -5265,7 +5278,7 @@ extern "C" int acf_apr_shard_pass_export(acf_apr_ctx* c, const acf_apr_tables* t
     const int HBT = std::min(HB, ACF_TRI_HOT_BLOCKS);
     const int TWT = (c->B + 64 / c->lpr - 1) / (64 / c->lpr);
     const int TW = (TWT + tri_gpw(c->nv) - 1) / tri_gpw(c->nv);
-    StepArgs a = make_args(c, tb, hp, 0, 0);
+    StepArgs a = make_args(c, tb, hp, c->shard_t, 0);  // batch shard_t of the plan
     a.use_single = 1;
     a.xbuf = xbuf;
     a.xmap = xmap;
@@ -5284,6 +5297,7 @@ extern "C" int acf_apr_shard_pass_export(acf_apr_ctx* c, const acf_apr_tables* t
     }
     return ACF_OK;
   }
+  ACF_CHECK(c->nb == 1 && c->shard_t == 0, ACF_E_STATE, "slot-kernel shard passes take one-batch plans");
   StepArgs a = make_args(c, tb, hp, 0, 0);
   a.use_single = 0;
   a.slot_waves = SW;
@@ -5345,7 +5359,8 @@ extern "C" int acf_apr_shard_items_mapped(acf_apr_ctx* c, int32_t dir, float* bu
                                           int64_t n_items, void* stream_) {
   ACF_CHECK(c && (buf || n_items == 0), ACF_E_INVALID, "NULL argument");
   ACF_RET(resolve(c, 2));  // settle queued streamed calls first (FailGroup)
-  ACF_CHECK(c->shard && c->nb == 1, ACF_E_STATE, "shard items need shard mode and a one-batch plan");
+  ACF_CHECK(c->shard && (c->nb == 1 || (c->tri && c->nb > 1)), ACF_E_STATE,
+            "shard items need shard mode and a one-batch plan (or a triplet-centric plan of several)");
   ACF_CHECK(dir == 0 || dir == 1, ACF_E_INVALID, "dir must be 0 or 1");
   ACF_CHECK(n_items >= 0 && n_items <= 2 * (int64_t)c->B, ACF_E_INVALID, "n_items %lld outside [0, 2B]",
             (long long)n_items);
@@ -5356,6 +5371,7 @@ extern "C" int acf_apr_shard_items_mapped(acf_apr_ctx* c, int32_t dir, float* bu
     return ACF_OK;
   }
   if (n_items == 0) return ACF_OK;
+  ACF_CHECK(c->nb == 1, ACF_E_STATE, "slot-plan shard items take one-batch plans");
   hipStream_t s = static_cast<hipStream_t>(stream_);
   const int64_t n4 = n_items * (c->d / 4);
   k_shard_items<<<grid_for(n4), 256, 0, s>>>(c->g0, c->delta, c->ubs, buf, map, n4, c->d / 4, dir);

@@ -105,6 +105,10 @@ class HipLocal:
 
     graphable = True  # every call is a fixed-shape launch sequence (no host sync)
     pipelined = True  # plan_into / use: the next step's plan beside this step
+    # (r06) plan_chunk / use_batch: a chunk of equal local batches over 1,024
+    # triplets (the hash plan) planned at once, each step one batch of it --
+    # one plan's launches per chunk instead of one plan beside every step
+    chunk_planned = True
 
     def __init__(self, sh: "ShardedAPR"):
         from . import ops
@@ -114,6 +118,7 @@ class HipLocal:
         for c in self.ctxs:
             c.set_shard_mode(True, reg_batch=sh.B)
         self.ctx = self.ctxs[0]  # the context the passes below use
+        self.cctx, self._cT = None, 0  # the chunk plan's context (plan_chunk), sized for _cT steps
         # the fetched item rows are never updated locally; their Adagrad slots are unused
         self.accQc = torch.full((sh.max_items, sh.d), 0.1, device=sh.device)
 
@@ -129,6 +134,27 @@ class HipLocal:
 
     def plan(self, u_rows, wi, wj):
         self.ctx.plan(u_rows, wi, wj, u_rows.numel(), check=False)
+
+    def plan_chunk(self, u_rows, wi, wj):
+        """[T, b] local rows of T steps, planned as ONE T-batch plan (b > 1,024:
+        the triplet-centric hash plan, whose batches are independent); the
+        passes then take batch t of it (use_batch)."""
+        sh, (T, b) = self.sh, tuple(u_rows.shape)
+        if self.cctx is None or self._cT < T:
+            self.cctx = None  # free the smaller one first
+            self.cctx = self.ops.APRContext(sh.P.shape[0], sh.max_items, sh.d, sh.b_max, T, sh.device)
+            self.cctx.set_shard_mode(True, reg_batch=sh.B)
+            self._cT = T
+        self.ctx = self.cctx
+        self.cctx.plan(u_rows.reshape(-1), wi.reshape(-1), wj.reshape(-1), b, check=False)
+
+    def use_batch(self, t: int) -> None:
+        self.cctx.set_shard_batch(t)
+
+    def chunk_ok(self) -> bool:
+        """Chunk plans are triplet-centric (hash) plans: fusion must be on (a
+        fusion-off plan is the sort plan, whose shard passes take one batch)."""
+        return getattr(self.ctxs[0], "fusion", True)
 
     def clean(self, hp, out, rows):
         """pass 0; working-set entry w's partial clean sum -> out[rows[w]]"""
@@ -150,7 +176,8 @@ class HipLocal:
                                     reg_batch=self.sh.B)
 
     def step_errors(self) -> int:
-        return self.ctxs[0].step_errors() | self.ctxs[1].step_errors()
+        e = self.ctxs[0].step_errors() | self.ctxs[1].step_errors()
+        return e | (self.cctx.step_errors() if self.cctx is not None else 0)
 
 
 class _Chunk:
@@ -645,7 +672,7 @@ class ShardedAPR:
             ev.record(torch.cuda.current_stream(self.device))
             self._free[t & 1] = ev
 
-    def _step(self, m, t: int, nb: list, hp, count: bool, pipe: bool = False) -> None:
+    def _step(self, m, t: int, nb: list, hp, count: bool, pipe: bool = False, chunk: bool = False) -> None:
         """Step t of a chunk routed into map set m (fixed shapes: every size is the buffers')."""
         b = nb[t]
         bf = self._buf
@@ -659,7 +686,10 @@ class ShardedAPR:
             torch.index_select(self._exchange(bf.R1, bf.S1), 0, m.wsrc[t], out=self.Qc)
         rows = m.wsrc[t, : 2 * b]  # working-set entry -> its exchange row
         if b:
-            self._plan_step(m, t, nb, pipe)
+            if chunk:  # batch t of the chunk's plan (_run_steps)
+                self.local.use_batch(t)
+            else:
+                self._plan_step(m, t, nb, pipe)
             self.local.clean(hp, bf.S, rows)
             if not hp.adver:
                 self._release(t, pipe)
@@ -707,12 +737,20 @@ class ShardedAPR:
         # capturing segments; eager runs and whole-step graphs keep the pipeline
         # (world 1 without forced collectives has no cut: one graph, pipelined)
         segments = self._rec is not None and not self._cap_coll and self._multi
-        pipe = self.device.type == "cuda" and self._pipelined() and not segments
+        # (r06) equal local batches over 1,024 triplets: the whole chunk in ONE plan,
+        # in line at its start (the one-batch hash plans beside every step cost
+        # ~150 us of GPU time per configs[4] step)
+        chunk = (getattr(self.local, "chunk_planned", False) and len(nb) > 1 and len(set(nb)) == 1
+                 and nb[0] > 1024 and self.local.chunk_ok())
+        pipe = self.device.type == "cuda" and self._pipelined() and not segments and not chunk
         if pipe and getattr(self, "_plan_stream", None) is None:
             self._plan_stream = torch.cuda.Stream(self.device)
         self._planned, self._free = [None, None], [None, None]
+        if chunk:
+            T, b = len(nb), nb[0]
+            self.local.plan_chunk(m.u_rows[:T, :b], m.wi[:T, :b], m.wj[:T, :b])
         for t in range(len(nb)):
-            self._step(m, t, nb, hp, count, pipe)
+            self._step(m, t, nb, hp, count, pipe, chunk)
         self._planned, self._free = [None, None], [None, None]
 
     def _capture(self, m, T: int, b: int, hp, count: bool) -> _SegmentRecorder:

@@ -256,6 +256,7 @@ class APRContext:
         made with fusion on is triplet-centric and updates every row in place, and
         training it with fusion off raises."""
         call("acf_apr_set_fusion", self._ptr, int(bool(on)))
+        self.fusion = bool(on)
 
     def time_kernels(self, tables, hp: StepHParams, first: int = 0, n: int | None = None):
         """Per-kernel-kind device time (ms) and launch counts over planned batches,
@@ -315,6 +316,11 @@ class APRContext:
         fusion, one-batch plans); reg_batch = the global batch of the reg mean."""
         call("acf_apr_set_shard_mode", self._ptr, int(bool(on)), int(reg_batch))
         self.batch_size = self.n_batches = 0
+
+    def set_shard_batch(self, t: int) -> None:
+        """The plan's batch the next shard passes step (a triplet-centric shard
+        plan may hold a chunk of steps; 0 otherwise)."""
+        call("acf_apr_set_shard_batch", self._ptr, int(t))
 
     def shard_pass(self, tables, hp: StepHParams, pass_: int) -> None:
         """pass 0: clean sums (users: delta; items: partial sums); pass 1 (APR):

@@ -243,6 +243,12 @@ int acf_apr_share_failsafe(acf_apr_ctx* ctx, acf_apr_ctx* peer);
  * reg * mean(w^2) terms divide by (0 = the planned batch size). */
 int acf_apr_set_shard_mode(acf_apr_ctx* ctx, int32_t on, int32_t reg_batch);
 
+/* (r06) Which batch of the plan the next shard pass / item map calls step: a
+ * triplet-centric shard plan (batches over 1,024 triplets) may hold a chunk of
+ * steps planned at once (distributed.ShardedAPR); slot-kernel shard plans are
+ * one batch (0).  Reset to 0 by acf_apr_set_shard_mode. */
+int acf_apr_set_shard_batch(acf_apr_ctx* ctx, int32_t batch);
+
 /* pass 0: clean sums (users complete: delta; items: partial sums in the item
  * slots' rows; BPR also updates the users); pass 1 (APR): adversarial sums
  * (users: Adagrad + write-back to the user shard; items: partial sums).  The

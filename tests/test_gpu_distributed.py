@@ -110,7 +110,7 @@ def test_sharded_triplet_centric_matches_slot_path(ops, dev, adver, reg, routed)
                 (sh.train_routed if routed else sh.train)(uu, ii, jj, hp, chunk=2)
                 torch.cuda.synchronize(dev)
                 assert sh.step_errors() == 0
-                kinds.append(sh.local.ctxs[0].plan_kind())
+                kinds.append(sh.local.ctx.plan_kind())  # the context the passes used (r06: the chunk plan's)
                 outs.append(sh.full_tables())
     finally:
         dist.destroy_process_group()

@@ -25,6 +25,9 @@ if alt:
             fn = getattr(lib, fname)
             fn.restype, fn.argtypes = res, args
     nat._lib = lib
+if "--per-step-plans" in sys.argv:  # A/B: r05's one-batch plan beside every step
+    sys.argv.remove("--per-step-plans")
+    importlib.import_module(bench.PKG + ".distributed").HipLocal.chunk_planned = False
 big = acf.synthetic_large(device=dev)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 24
 print(json.dumps(bench.sharded_lines(acf, ops, dev, None, 1, 0, big, steps)))
