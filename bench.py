@@ -363,10 +363,15 @@ def large_batch_roofline(acf, ops, dev, ds, d=128, nb=256, chunk=32, graph=True)
     hp = ops.StepHParams(adver=1)
     pipe.run(tabs, hp, u, i, j, 0, nb, graph=graph)  # warm (graph capture)
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    pipe.run(tabs, hp, u, i, j, 0, nb, graph=graph)
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
+    # three timed passes over the same nb batches: the line is their median, with
+    # min / max beside it, so box-to-box noise can be told from a change
+    dts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        pipe.run(tabs, hp, u, i, j, 0, nb, graph=graph)
+        torch.cuda.synchronize(dev)
+        dts.append(time.perf_counter() - t0)
+    dt = sorted(dts)[1]
     errors = pipe.step_errors()
     st = batch_stats(u, i, j, B, nb, U1, I1)
     # the dominant kernel timed alone, then with the next chunk's plan beside it
@@ -377,6 +382,8 @@ def large_batch_roofline(acf, ops, dev, ds, d=128, nb=256, chunk=32, graph=True)
     rl["alone"] = {"avg_launch_us": alone["avg_launch_us"], "frac": alone["frac"],
                    "per_kernel_avg_us": alone["per_kernel_avg_us"]}
     rl["triplets_per_s"] = round(nb * B / dt, 1)
+    rl["triplets_per_s_passes"] = {"median": round(nb * B / dt, 1), "min": round(nb * B / max(dts), 1),
+                                   "max": round(nb * B / min(dts), 1), "passes": len(dts)}
     rl["step_bandwidth"] = step_bandwidth(d, B, st, nb * B / dt)
     rl["batch_stats"] = {k: round(v, 1) for k, v in st.items()}
     rl["step_errors"] = errors
