@@ -24,10 +24,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nb", type=int, default=20)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--lib", default=os.path.join(REPO, "tools", "libacf_apr_diag.so"))
     a = ap.parse_args()
     native = importlib.import_module(PKG + "._native")
-    lib = native.load(os.path.join(REPO, "tools", "libacf_apr_diag.so"))
     import ctypes
+    lib = ctypes.CDLL(a.lib)  # a -DACF_DIAG build: no build-hash check (as tools/bench_lib.py)
+    for fname, (res_t, args) in native.SIGNATURES.items():
+        if hasattr(lib, fname):
+            fn = getattr(lib, fname)
+            fn.restype, fn.argtypes = res_t, args
+    native._lib = lib
     lib.acf_diag_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     acf = importlib.import_module(PKG)
     ops = importlib.import_module(PKG + ".ops")
@@ -56,6 +62,7 @@ def main():
     for st in res:
         so = st[:, :8, :5]  # [nb][waves][phase]
         bo = st[:, 16:32, :7]
+        b7 = st[:, 16:32, 7]
         live_s = so[:, :, 0] > 0
         live_b = bo[:, :, 0] > 0
         for t in range(nb):
@@ -64,6 +71,9 @@ def main():
                 acc["sort_" + sort_ph[k]].append(ws[:, k + 1].max() - ws[:, k].max())
             for k in range(6):
                 acc["build_" + build_ph[k]].append(wb[:, k + 1].max() - wb[:, k].max())
+            w7 = b7[t][live_b[t]]
+            if (w7 > 0).all():  # optional stamp 7: after the first task-list scan
+                acc.setdefault("build_task_list_first_scan", []).append(w7.max() - wb[:, 4].max())
         s0, s1 = so[:, :, 0][live_s].min(), so[:, :, 4][live_s].max()
         b0, b1 = bo[:, :, 0][live_b].min(), bo[:, :, 6][live_b].max()
         acc["sort_span"].append(s1 - s0)
