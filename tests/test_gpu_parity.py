@@ -1026,3 +1026,49 @@ def test_pipeline_failed_chunks_gate_and_replay(ops, acf, dev):
     assert pipe.stream_recoveries() == nb // chunk and pipe.step_errors() == 0
     for x, y in zip(ref, got):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("case", ["one_per_batch", "identical", "identical_large", "edge_rows"])
+@pytest.mark.parametrize("stream", [False, True])
+def test_degenerate_batches_match_oracle(ops, oracle, dev, case, stream):
+    """Edge cases of the batch shape against the oracle: one triplet per batch;
+    batches of B identical triplets (one user slot and one or two item slots with
+    B occurrences each; in the first batch the negative IS the positive, so the
+    item's contributions cancel pair by pair); the same at B = 4,096 (hash plan,
+    hot-slot pieces); only the first and last rows of both tables."""
+    U1, I1, d = 37, 29, 64
+    rng = np.random.default_rng(len(case))
+    if case == "one_per_batch":
+        B, nb = 1, 6
+        u, i, j = rng.integers(0, U1, nb), rng.integers(0, I1, nb), rng.integers(0, I1, nb)
+    elif case.startswith("identical"):
+        B, nb = (4096, 2) if case == "identical_large" else (256, 3)
+        u = np.full(nb * B, 3)
+        i = np.full(nb * B, 5)
+        j = np.full(nb * B, 7)
+        j[:B] = 5
+    else:
+        B, nb = 64, 4
+        u = rng.choice([0, U1 - 1], nb * B)
+        i, j = rng.choice([0, I1 - 1], nb * B), rng.choice([0, I1 - 1], nb * B)
+    u, i, j = (x.astype(np.int32) for x in (u, i, j))
+    P = (rng.standard_normal((U1, d)) * 0.3).astype(np.float32)
+    Q = (rng.standard_normal((I1, d)) * 0.3).astype(np.float32)
+    want, lc_w, la_w, _ = _oracle_run(oracle, P, Q, u, i, j, B, HParams(adver=1))
+    tabs = _gpu_tables(P, Q, dev)
+    ctx = ops.APRContext(U1, I1, d, B, nb, dev)
+    ctx.set_stream(stream)
+    ctx.plan(torch.tensor(u, device=dev), torch.tensor(i, device=dev), torch.tensor(j, device=dev), B)
+    ctx.train_planned(tabs, ops.StepHParams(adver=1))
+    lc, la = ctx.losses()
+    torch.cuda.synchronize()
+    assert ctx.step_errors() == 0
+    # a row's sum over n occurrences in another order (lane-group teams, hot-slot
+    # pieces): Higham's bound 2 n u, relative to the row's scale, as test_hot_slots_*
+    n_terms = max(2 * np.bincount(u[:B]).max(), np.bincount(np.concatenate([i[:B], j[:B]])).max())
+    rtol = max(RTOL, 2 * n_terms * 2.0 ** -24)
+    for g, w, n in zip(tabs, want, ("P", "Q", "accP", "accQ")):
+        atol = max(ATOL, rtol * float(np.abs(w).max()))
+        np.testing.assert_allclose(g.cpu().numpy(), w, rtol=rtol, atol=atol, err_msg=n)
+    np.testing.assert_allclose(lc.cpu().numpy(), lc_w, rtol=rtol, atol=ATOL)
+    np.testing.assert_allclose(la.cpu().numpy(), la_w, rtol=rtol, atol=ATOL)
