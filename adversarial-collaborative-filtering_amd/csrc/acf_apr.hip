@@ -458,8 +458,12 @@ __device__ __forceinline__ OccRec item_rec(const int4& own, const int4& oth, con
 // hot_part, and k_hot_combine adds a slot's pieces in piece order (fixed order:
 // deterministic bits).  Each plan appends a batch's hot slots and their pieces
 // with atomics; the order of the lists changes nothing but which wave does what.
+#ifndef ACF_HOT_MIN
 #define ACF_HOT_MIN 8
+#endif
+#ifndef ACF_HOT_PIECE
 #define ACF_HOT_PIECE 16
+#endif
 #define ACF_HOT_MAXP 256
 
 __host__ __device__ __forceinline__ int32_t hot_pieces(int32_t count) {
