@@ -105,10 +105,13 @@ class HipLocal:
 
     graphable = True  # every call is a fixed-shape launch sequence (no host sync)
     pipelined = True  # plan_into / use: the next step's plan beside this step
-    # (r06) plan_chunk / use_batch: a chunk of equal local batches over 1,024
-    # triplets (the hash plan) planned at once, each step one batch of it --
-    # one plan's launches per chunk instead of one plan beside every step
+    # (r06) plan_chunk / use_batch: a chunk of equal local batches (the hash
+    # plan) planned at once, each step one batch of it -- one plan's launches per
+    # chunk instead of one plan beside every step
     chunk_planned = True
+    # ... for local batches larger than this: every size (configs[2]'s 512-triplet
+    # batches too: 0.055 -> 0.045 ms per step, profiles/r06/shard_chunk_small_ab.json)
+    chunk_min = 0
 
     def __init__(self, sh: "ShardedAPR"):
         from . import ops
@@ -136,8 +139,8 @@ class HipLocal:
         self.ctx.plan(u_rows, wi, wj, u_rows.numel(), check=False)
 
     def plan_chunk(self, u_rows, wi, wj):
-        """[T, b] local rows of T steps, planned as ONE T-batch plan (b > 1,024:
-        the triplet-centric hash plan, whose batches are independent); the
+        """[T, b] local rows of T steps, planned as ONE T-batch plan (shard mode,
+        T > 1: the triplet-centric hash plan, whose batches are independent); the
         passes then take batch t of it (use_batch)."""
         sh, (T, b) = self.sh, tuple(u_rows.shape)
         if self.cctx is None or self._cT < T:
@@ -153,8 +156,9 @@ class HipLocal:
 
     def chunk_ok(self) -> bool:
         """Chunk plans are triplet-centric (hash) plans: fusion must be on (a
-        fusion-off plan is the sort plan, whose shard passes take one batch)."""
-        return getattr(self.ctxs[0], "fusion", True)
+        fusion-off plan is the sort plan, whose shard passes take one batch), and
+        the step contexts' plan mode the default (mode 1 asks for the sort plan)."""
+        return getattr(self.ctxs[0], "fusion", True) and getattr(self.ctxs[0], "plan_mode", 0) == 0
 
     def clean(self, hp, out, rows):
         """pass 0; working-set entry w's partial clean sum -> out[rows[w]]"""
@@ -737,11 +741,11 @@ class ShardedAPR:
         # capturing segments; eager runs and whole-step graphs keep the pipeline
         # (world 1 without forced collectives has no cut: one graph, pipelined)
         segments = self._rec is not None and not self._cap_coll and self._multi
-        # (r06) equal local batches over 1,024 triplets: the whole chunk in ONE plan,
-        # in line at its start (the one-batch hash plans beside every step cost
-        # ~150 us of GPU time per configs[4] step)
+        # (r06) equal local batches: the whole chunk in ONE plan, in line at its
+        # start (the one-batch plans beside every step cost ~150 us of GPU time per
+        # configs[4] step; at configs[2] k_shard_plan's ~22 us per step)
         chunk = (getattr(self.local, "chunk_planned", False) and len(nb) > 1 and len(set(nb)) == 1
-                 and nb[0] > 1024 and self.local.chunk_ok())
+                 and nb[0] > getattr(self.local, "chunk_min", 1024) and self.local.chunk_ok())
         pipe = self.device.type == "cuda" and self._pipelined() and not segments and not chunk
         if pipe and getattr(self, "_plan_stream", None) is None:
             self._plan_stream = torch.cuda.Stream(self.device)

@@ -240,6 +240,7 @@ class APRContext:
         write identical plans; 'sort' is for A/B and the equivalence test."""
         m = {"auto": 0, "sort": 1}.get(mode, mode)
         call("acf_apr_set_plan_mode", self._ptr, int(m))
+        self.plan_mode = int(m)
 
     PLAN_KINDS = {-1: None, 0: "sort", 1: "batch", 2: "shard", 3: "hash"}
 

@@ -84,18 +84,27 @@ def test_sharded_rccl_world1_matches_oracle(ops, oracle, dev, fp32_parity, shape
         fp32_parity(g, w, n)
 
 
-@pytest.mark.parametrize("adver,reg,routed", [(1, 0.0, False), (0, 0.01, False), (1, 0.0, True)])
-def test_sharded_triplet_centric_matches_slot_path(ops, dev, adver, reg, routed):
+@pytest.mark.parametrize("adver,reg,routed,shape", [(1, 0.0, False, "zipf"), (0, 0.01, False, "zipf"),
+                                                    (1, 0.0, True, "zipf"), (1, 0.0, False, "pinterest"),
+                                                    (1, 0.0, True, "pinterest")])
+def test_sharded_triplet_centric_matches_slot_path(ops, dev, adver, reg, routed, shape):
     """(r05) Shard mode on the hash plan and the triplet-centric kernels (local
     batches above 1,024 triplets with fusion on, the default: item occurrences
     are never single, item slots export their partial sums straight to the
     exchange rows, pass 1 reads the owners' deltas from theirs) against the sort
     plan and the slot kernels (fusion off): identical bits for every table, on
     Zipf batches of 32,768 with hot items, every exchange forced through a
-    one-rank RCCL group, eager (train) and captured (train_routed)."""
+    one-rank RCCL group, eager (train) and captured (train_routed).  (r06)
+    "pinterest": configs[2]'s 512-triplet local batches, a chunk of them on one
+    hash plan too (HipLocal.chunk_min 0)."""
     D_ = importlib.import_module(PKG + ".distributed")
-    U1, I1, d, B, nb = 300_000, 200_000, 64, 32768, 4
-    P, Q, u, i, j = _problem(21 + adver, U1, I1, d, B, nb, 1.1)
+    if shape == "zipf":
+        U1, I1, d, B, nb = 300_000, 200_000, 64, 32768, 4
+        P, Q, u, i, j = _problem(21 + adver, U1, I1, d, B, nb, 1.1)
+    else:
+        U1, I1, d, B, nb = 55_188, 9_917, 64, 512, 8
+        P, Q, u, i, j = _problem(23 + adver, U1, I1, d, B, nb)
+        i[::5] = 17  # a hot item in every batch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     outs, kinds = [], []
@@ -107,14 +116,14 @@ def test_sharded_triplet_centric_matches_slot_path(ops, dev, adver, reg, routed)
                 for c in sh.local.ctxs:
                     c.set_fusion(fusion)
                 hp = ops.StepHParams(adver=adver, reg=reg)
-                (sh.train_routed if routed else sh.train)(uu, ii, jj, hp, chunk=2)
+                (sh.train_routed if routed else sh.train)(uu, ii, jj, hp, chunk=2 if shape == "zipf" else 4)
                 torch.cuda.synchronize(dev)
                 assert sh.step_errors() == 0
                 kinds.append(sh.local.ctx.plan_kind())  # the context the passes used (r06: the chunk plan's)
                 outs.append(sh.full_tables())
     finally:
         dist.destroy_process_group()
-    assert kinds == ["sort", "hash"], kinds
+    assert kinds == ["sort" if shape == "zipf" else "shard", "hash"], kinds
     for g, e, n in zip(outs[1], outs[0], ("P", "Q", "accP", "accQ")):
         assert torch.equal(g, e), n
 
@@ -220,6 +229,7 @@ def test_shard_plan_small_matches_sort_plan(ops, dev, adver):
         uu, ii, jj = (torch.tensor(x, device=dev) for x in (u, i, j))
         for mode in (0, 1):
             sh = D_.ShardedAPR(U1, I1, d, B, device=dev, init_P=P, init_Q=Q, graph=False)
+            sh.local.chunk_min = 1 << 30  # one plan per step (r06: chunks of equal batches take one hash plan)
             for c in sh.local.ctxs:  # both step contexts (the next step is planned beside this one)
                 c.set_plan_mode(mode)
             sh.train(uu, ii, jj, ops.StepHParams(adver=adver), chunk=3)

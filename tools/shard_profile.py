@@ -28,6 +28,10 @@ if alt:
 if "--per-step-plans" in sys.argv:  # A/B: r05's one-batch plan beside every step
     sys.argv.remove("--per-step-plans")
     importlib.import_module(bench.PKG + ".distributed").HipLocal.chunk_planned = False
+if "--chunk-min" in sys.argv:  # A/B: chunk plans from this local batch size up
+    k = sys.argv.index("--chunk-min")
+    importlib.import_module(bench.PKG + ".distributed").HipLocal.chunk_min = int(sys.argv[k + 1])
+    del sys.argv[k:k + 2]
 big = acf.synthetic_large(device=dev)
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 24
 print(json.dumps(bench.sharded_lines(acf, ops, dev, None, 1, 0, big, steps)))
