@@ -586,8 +586,11 @@ class ShardedAPR:
         # owner reduction segments: per (step, row), positions in requester order;
         # non-head entries write to the maps' dump element (no compaction, no sync)
         key = (t_e * (ni + 1) + rows) * G + o_e
-        skey, sp = torch.sort(key.to(torch.int32) if T * (ni + 1) * G < 2 ** 31 else key)
-        skey = skey.long()
+        if G == 1:  # the requests are the working sets, already in (step, row) order: no sort
+            skey, sp = key, torch.arange(Rn, device=dev)
+        else:
+            skey, sp = torch.sort(key.to(torch.int32) if T * (ni + 1) * G < 2 ** 31 else key)
+            skey = skey.long()
         srow = skey // G
         head = torch.ones_like(srow, dtype=torch.bool)
         if srow.numel() > 1:
